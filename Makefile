@@ -1,0 +1,38 @@
+# Builds the MI355X (gfx950) library in-tree: usnetd_amd/libusn.so
+# and the CPU oracle (test infrastructure) oracle/build/liboracle.so.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+CSRC := usnetd_amd/csrc
+LIB := usnetd_amd/libusn.so
+OBJS := build/usn_device.o build/usn_host.o
+
+all: $(LIB) oracle
+
+build/usn_device.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/usn_host.o: $(CSRC)/usn_host.cpp $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+# kernel resource usage (VGPR/SGPR/LDS/occupancy) for DESIGN.md
+resources: $(CSRC)/usn_device.hip
+	$(HIPCC) $(HIPFLAGS) -c -o /dev/null $< -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E 'Function Name|VGPRs:|SGPRs:|Occupancy|LDS Size|ScratchSize'
+
+asm: $(CSRC)/usn_device.hip
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -S --offload-device-only -o build/usn_device.s $<
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean resources asm

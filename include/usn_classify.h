@@ -1,0 +1,241 @@
+/*
+ * usn_classify.h -- C ABI of the MI355X-native usnetd match path.
+ *
+ * This is the drop-in boundary for usnetd's per-frame decision path.  The
+ * reference has no FFI; the path is internal Rust and is called once per
+ * received frame:
+ *
+ *   Endpoint::forward (drain loop)       /root/reference/src/endpoint.rs:114-171
+ *     -> Endpoint::find_forward          /root/reference/src/endpoint.rs:172-296
+ *        -> extract_pkt_info             /root/reference/src/pkt.rs:158-218
+ *        -> get_endpoint                 /root/reference/src/endpoint.rs:307-338
+ *        -> mirror_to_all (FLOOD)        /root/reference/src/endpoint.rs:340-363
+ *
+ * Here a drained rx ring is one batch resident in HBM and one call classifies
+ * all of it.  The state the reference keeps in `main` and in each `Endpoint`
+ * (match_register, innerl2bridge, fragmentation_map, listening, last_pkt,
+ * last_pkt_dst, next_dhcp_endpoint) lives in a usn_ctx; the rule-registry
+ * operations keep the reference's semantics so a host (Rust over this ABI,
+ * see INTEGRATION.md, or the C++ control plane) can drive it directly.
+ *
+ * Conventions: every function returns int status (0 = ok, negative = error,
+ * see USN_E*), never throws, never aborts.  Pointers named dev_* or documented
+ * "device" are HIP device pointers on the ctx's device.  Nothing here takes
+ * or returns a torch type.
+ */
+#ifndef USN_CLASSIFY_H
+#define USN_CLASSIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define USN_ABI_VERSION 1
+#define USN_WINDOW 64     /* header bytes read per frame (ports beyond it: slow path) */
+#define USN_TILE 1024     /* frames per tile of the per-endpoint order output */
+#define USN_MAX_ENDPOINTS 1021 /* endpoint ids 0..1020 (bins = endpoints + NIC + FLOOD + DROP) */
+
+/* status codes */
+#define USN_OK 0
+#define USN_EINVAL (-22)
+#define USN_ENOMEM (-12)
+#define USN_EEXIST (-17)
+#define USN_ENOENT (-2)
+#define USN_EPERM (-1)
+#define USN_EHIP (-5)        /* HIP runtime error; usn_last_hip_error() */
+#define USN_ENODEV (-19)     /* no gfx950 device */
+#define USN_ERANGE (-34)
+
+/* ---- decision word (u32), one per frame --------------------------------
+ *   [15:0]  endpoint id (0xFFFF = none)            Target::Endpoint/EndpointRef
+ *   [19:16] class                                  Option<Target>
+ *   [23:20] drop reason (informational, exact)
+ *   [31:24] flags (informational)
+ * Parity with the reference is defined on bits [23:0]. */
+#define USN_CLS_DROP 0u    /* None: endpoint.rs:207, 275, 293 */
+#define USN_CLS_EP 1u      /* Target::Endpoint / EndpointRef / Last->endpoint */
+#define USN_CLS_NIC 2u     /* Target::Nic (endpoint id = the source's NIC) */
+#define USN_CLS_FLOOD 3u   /* mirror_to_all: every endpoint except the source */
+#define USN_R_NONE 0u
+#define USN_R_PARSE 1u     /* extract_pkt_info -> None */
+#define USN_R_LOOPBACK 2u  /* endpoint.rs:205-208 */
+#define USN_R_NOMATCH 3u   /* endpoint.rs:274-277 */
+#define USN_R_EXCLUDED 4u  /* get_endpoint hit a NIC or the source (endpoint.rs:328-336) */
+#define USN_R_FRAGMISS 5u  /* later fragment without a remembered first (pkt.rs:172-176) */
+#define USN_R_DHCP_NONE 6u /* DHCP answer, no rule, no next_dhcp (endpoint.rs:269-272) */
+#define USN_F_CACHE (1u << 24)   /* decision taken from the 1-entry cache (endpoint.rs:186-191) */
+#define USN_F_FRAG1 (1u << 25)   /* first fragment: remembered in the fragment map */
+#define USN_F_FRAGN (1u << 26)   /* later fragment: resolved through the fragment map */
+#define USN_F_DHCP (1u << 27)    /* DHCP steering involved */
+#define USN_F_HOST (1u << 28)    /* resolved by the ordered host stage (usn_finalize) */
+#define USN_F_LEARN (1u << 29)   /* tx: this frame learned a MAC or an answer rule */
+#define USN_DEC_CLASS(d) (((d) >> 16) & 0xFu)
+#define USN_DEC_EP(d) ((d) & 0xFFFFu)
+#define USN_DEC_REASON(d) (((d) >> 20) & 0xFu)
+#define USN_PARITY_MASK 0x00FFFFFFu
+
+/* ---- endpoints (all_devices entries; devices.rs:14-25) ------------------ */
+#define USN_EP_NIC 0   /* NicNetmap / NicMacVtap: get_nic().is_some() */
+#define USN_EP_HOST 1  /* HostRing / HostTap */
+#define USN_EP_PIPE 2  /* UserNetmap */
+#define USN_EP_UDS 3   /* UserUnixDomainSocket */
+
+/* ---- rule key: Want (pkt.rs:220-227) ------------------------------------ */
+#define USN_WANT_DPORT 1u  /* dst_port is Some */
+#define USN_WANT_SRC 2u    /* src_addr is Some */
+#define USN_WANT_SPORT 4u  /* src_port is Some */
+typedef struct {
+  uint32_t dst_addr;   /* IPv4 a.b.c.d as (a<<24)|(b<<16)|(c<<8)|d */
+  uint32_t src_addr;
+  uint16_t dst_port;
+  uint16_t src_port;
+  uint8_t protocol;
+  uint8_t present;     /* USN_WANT_* bits; absent fields are ignored */
+  uint16_t _reserved;
+} usn_want;
+
+/* ---- batch of frames (one drained rx ring of one source endpoint) -------- */
+typedef struct {
+  const uint8_t *frames;   /* device: frame i starts at frames + i*stride or frames + offsets[i];
+                              16-byte aligned, USN_WINDOW readable bytes at every start */
+  uint64_t stride;         /* > 0 selects the fixed-stride layout (netmap-slot like) */
+  const uint64_t *offsets; /* device, or NULL when stride > 0 */
+  const uint16_t *lens;    /* device: frame lengths (netmap_slot.len) */
+  uint64_t n;              /* frames in the batch */
+  uint16_t src_endpoint;   /* the endpoint whose ring was drained */
+  uint16_t _reserved[3];
+} usn_batch;
+
+/* Tile header: one per USN_TILE frames (written by the tile's workgroup only,
+ * so no device-wide atomics and no per-batch memset are needed). */
+typedef struct {
+  uint16_t n_frames;       /* frames in this tile */
+  uint16_t n_runs;         /* entries of runs[] used by this tile */
+  uint16_t n_host;         /* frames of this tile listed for the ordered host stage */
+  uint16_t _reserved;
+  uint16_t class_count[4]; /* frames per decision class (before host fix-ups) */
+  uint32_t last_state;     /* internal: 1-entry cache state after this tile */
+  uint32_t last_dst;
+  uint32_t last_idx;
+  uint32_t last_info[4];
+  uint32_t _pad;
+} usn_tile_hdr;            /* 48 bytes */
+
+/* Batch summary (device), written by workgroup 0 and by usn_finalize. */
+typedef struct {
+  uint32_t flags;          /* USN_S_* */
+  uint32_t first_break;    /* stale mode: first frame that ends the stale prefix */
+  uint32_t n_frames;
+  uint32_t n_tiles;
+  uint32_t cin_state, cin_dst, cin_info[4];   /* carried-in cache as resolved on device */
+  uint32_t cout_state, cout_dst, cout_info[4];/* carried-out override (finalize) */
+} usn_summary;             /* 64 bytes */
+#define USN_S_STALE 1u         /* carried cache entry disagrees with the current table */
+#define USN_S_STALE_EXTENDS 2u /* stale prefix may continue past tile 0 */
+#define USN_S_COUT 8u          /* cout_* is authoritative (set by finalize) */
+
+/* Result buffers (device), carved by usn_result_bind from one allocation. */
+typedef struct {
+  uint32_t *decisions;     /* n decision words */
+  uint16_t *order;         /* n: per tile, tile-local frame indices stably sorted by bin */
+  uint32_t *runs;          /* per tile USN_TILE slots: (bin << 16) | start, n_runs used */
+  usn_tile_hdr *tiles;     /* ceil(n / USN_TILE) */
+  usn_summary *summary;    /* 1 */
+  uint32_t *host_list;     /* per tile USN_TILE slots: frames for the ordered host stage */
+  uint64_t n;
+} usn_result;
+
+/* Per-batch outcome of the ordered host stage. */
+typedef struct {
+  uint32_t n_host;         /* frames resolved on the host */
+  uint32_t n_patched;      /* decisions changed by the host stage */
+  uint32_t n_learned;      /* tx: MACs + answer rules learned */
+  uint32_t flags;          /* summary flags seen */
+  uint32_t class_count[4]; /* final per-class frame counts */
+} usn_finalize_info;
+
+/* ---- context --------------------------------------------------------------- */
+typedef struct usn_ctx usn_ctx;
+
+int usn_abi_version(void);
+const char *usn_strerror(int status);
+int usn_last_hip_error(void);
+
+/* Binds to HIP device `hip_device` (must be gfx950).  Replaces the daemon
+ * state set up in main() (main.rs:447-449: fragmentation_map, match_register,
+ * innerl2bridge). */
+int usn_ctx_create(int hip_device, usn_ctx **out);
+void usn_ctx_destroy(usn_ctx *ctx);
+
+/* Endpoints::add / EntryChange::Add (main.rs:151-166).  for_nic = -1 iff NIC. */
+int usn_endpoint_add(usn_ctx *ctx, uint16_t id, int kind, int32_t for_nic);
+/* EntryChange::Remove (main.rs:1058-1069): drops the endpoint and its rules.
+ * Cached decisions that name it stay (as in the reference). */
+int usn_endpoint_remove(usn_ctx *ctx, uint16_t id);
+
+/* add_listening_match (main.rs:266-298): 1 inserted, 0 key exists ("ER"),
+ * USN_EPERM owner is a NIC (the reference panics). Clears the owner's NIC
+ * decision cache and records the listening triple. */
+int usn_add_match(usn_ctx *ctx, const usn_want *w, uint16_t owner, int sticky);
+/* act_on RemoveMatch (main.rs:608-625): 1 removed, 0 absent, USN_EPERM if
+ * requester is not the owner.  Does NOT clear any cache (as the reference). */
+int usn_remove_match(usn_ctx *ctx, const usn_want *w, uint16_t requester);
+/* QueryUsedPorts / introspection: number of rules, and a copy of them. */
+int usn_rule_count(usn_ctx *ctx);
+int usn_rules_get(usn_ctx *ctx, usn_want *w, uint16_t *owner, uint8_t *sticky, uint32_t cap);
+/* Owner of an exact key, or USN_ENOENT. */
+int usn_lookup(usn_ctx *ctx, const usn_want *w);
+
+/* ADD_MACS prefill (main.rs:450-462): appends to the inner L2 bridge. */
+int usn_bridge_add(usn_ctx *ctx, const uint8_t mac[6]);
+int usn_bridge_count(usn_ctx *ctx);
+/* 90 s cleanup: fragmentation_map.clear() (main.rs Cleanup handler). */
+int usn_frag_clear(usn_ctx *ctx);
+
+/* ---- the hot path ------------------------------------------------------------ */
+size_t usn_result_bytes(uint64_t n);
+int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
+
+/* Classify one batch on `hip_stream` (hipStream_t; NULL = default stream).
+ * Asynchronous: writes decisions, per-tile order/runs and the summary.
+ * Consecutive batches of one source may be enqueued back to back; the 1-entry
+ * decision cache is carried on the device from the previous batch's result,
+ * which must stay allocated until this call's work has been enqueued. */
+int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream);
+
+/* Ordered host stage for one classified batch (synchronises the stream).
+ * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
+ * frame order and patches decisions/order on the device.  Must be called
+ * before the next usn_classify of the same source whenever the summary has
+ * n_host > 0 or flags != 0; calling it always is allowed. */
+int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
+                 usn_finalize_info *info);
+
+/* Forget the carried decision cache of one endpoint (last_pkt = None). */
+int usn_cache_clear(usn_ctx *ctx, uint16_t endpoint);
+
+/* ---- device plumbing for hosts without their own HIP bindings -------------------- */
+int usn_dev_alloc(usn_ctx *ctx, size_t bytes, void **dev);
+int usn_dev_free(usn_ctx *ctx, void *dev);
+int usn_host_alloc_pinned(usn_ctx *ctx, size_t bytes, void **host);
+int usn_host_free_pinned(usn_ctx *ctx, void *host);
+int usn_memcpy_h2d(usn_ctx *ctx, void *dev, const void *host, size_t bytes, void *hip_stream);
+int usn_memcpy_d2h(usn_ctx *ctx, void *host, const void *dev, size_t bytes, void *hip_stream);
+int usn_memset_d(usn_ctx *ctx, void *dev, int value, size_t bytes, void *hip_stream);
+int usn_stream_create(usn_ctx *ctx, void **stream);
+int usn_stream_destroy(usn_ctx *ctx, void *stream);
+int usn_stream_sync(usn_ctx *ctx, void *stream);
+int usn_device_sync(usn_ctx *ctx);
+/* Events: elapsed milliseconds between two recorded events. */
+int usn_event_create(usn_ctx *ctx, void **ev);
+int usn_event_destroy(usn_ctx *ctx, void *ev);
+int usn_event_record(usn_ctx *ctx, void *ev, void *hip_stream);
+int usn_event_elapsed_ms(usn_ctx *ctx, void *ev_start, void *ev_end, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* USN_CLASSIFY_H */

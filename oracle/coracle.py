@@ -148,3 +148,13 @@ class Oracle:
         self.L.uso_forward_batch(self.h, src, frames.ctypes.data, stride, offp,
                                  lens.ctypes.data, n, out.ctypes.data)
         return out
+
+
+def install_oracle(o: "Oracle", cfg) -> None:
+    """Install a usnetd_amd.traffic.Config (endpoints, rules, bridge) into an oracle."""
+    for eid, kind, for_nic in cfg.endpoints:
+        o.add_endpoint(eid, kind, -1 if for_nic is None else for_nic)
+    for w, owner, sticky in cfg.rules:
+        o.add_match(make_want(w["dst"], w["proto"], w["dport"], w["src"], w["sport"]), owner, sticky)
+    for m in cfg.bridge:
+        o.bridge_add(m)

@@ -56,8 +56,8 @@ def test_batch_api_matches_single():
     cfg = traffic.config("c2", n=4096)
     o1, o2 = coracle.Oracle(), coracle.Oracle()
     for o in (o1, o2):
-        traffic.install_oracle(o, cfg)
+        coracle.install_oracle(o, cfg)
     d1 = o1.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
-    d2 = np.array([o2.forward(cfg.src, bytes(cfg.frames[i * cfg.stride:i * cfg.stride + cfg.lens[i]]))
+    d2 = np.array([o2.forward(cfg.src, cfg.window(i))
                    for i in range(cfg.n)], dtype=np.uint32)
     assert (d1 == d2).all()

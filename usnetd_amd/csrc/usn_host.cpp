@@ -1,0 +1,933 @@
+/*
+ * usn_host.cpp -- C ABI implementation: context, rule registry, device table
+ * build, batch launch and the ordered host stage (usn_finalize).
+ *
+ * State model (all from /root/reference):
+ *   match_register  HashMap<Want, (bool sticky, Rc<endpoint>)>   main.rs:448
+ *   innerl2bridge   Vec<EthernetAddress>                         main.rs:449
+ *   fragmentation_map HashMap<FragmentationKey, (PacketInfo,..)> main.rs:447
+ *   Endpoint { listening, next_dhcp_endpoint, last_pkt, last_pkt_dst, for_nic }
+ *                                                                endpoint.rs:19-29
+ * The device sees an immutable snapshot of match_register (rebuilt when the
+ * registry changes) and the bridge; the 1-entry decision cache of each source
+ * is carried on the device from batch to batch (see usn_device.hip).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "usn_internal.h"
+#include "usn_kernels.h"
+
+using usn::ClassifyArgs;
+
+namespace {
+
+thread_local int g_last_hip = 0;
+
+int hip_fail(hipError_t e) {
+  g_last_hip = (int)e;
+  return USN_EHIP;
+}
+#define HIPCHK(x)                              \
+  do {                                         \
+    hipError_t _e = (x);                       \
+    if (_e != hipSuccess) return hip_fail(_e); \
+  } while (0)
+
+struct WantKey {
+  uint32_t dst, src;
+  uint16_t dport, sport;
+  uint8_t proto, present;
+  bool operator==(const WantKey &o) const {
+    return dst == o.dst && src == o.src && dport == o.dport && sport == o.sport &&
+           proto == o.proto && present == o.present;
+  }
+};
+struct WantHash {
+  size_t operator()(const WantKey &k) const {
+    return usn_key_hash(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
+                        usn_key_meta(k.proto, k.present));
+  }
+};
+/* canonical key: absent Option fields are zero (derive(Hash, Eq) on Want) */
+WantKey canon(const usn_want &w) {
+  WantKey k;
+  k.present = w.present & 7u;
+  k.dst = w.dst_addr;
+  k.proto = w.protocol;
+  k.dport = (k.present & USN_WANT_DPORT) ? w.dst_port : 0;
+  k.src = (k.present & USN_WANT_SRC) ? w.src_addr : 0;
+  k.sport = (k.present & USN_WANT_SPORT) ? w.src_port : 0;
+  return k;
+}
+
+struct Rule {
+  uint16_t owner;
+  uint8_t sticky;
+};
+
+struct Listen {
+  uint32_t dst;
+  uint8_t proto, has_port;
+  uint16_t port;
+};
+
+struct Info {   // PacketInfo words (usn_internal.h)
+  uint32_t w[4];
+  bool operator==(const Info &o) const {
+    return w[0] == o.w[0] && w[1] == o.w[1] && w[2] == o.w[2] && w[3] == o.w[3];
+  }
+  uint32_t kind() const { return w[0] & 0xFFu; }
+  uint32_t proto() const { return (w[0] >> 8) & 0xFFu; }
+  bool has_ports() const { return (w[0] >> 16) & 1u; }
+  uint32_t src() const { return w[1]; }
+  uint32_t dst() const { return w[2]; }
+  uint32_t sport() const { return w[3] & 0xFFFFu; }
+  uint32_t dport() const { return w[3] >> 16; }
+};
+
+struct FragKey {
+  uint16_t id;
+  uint8_t proto;
+  uint32_t src, dst;
+  uint64_t smac, dmac;
+  bool operator==(const FragKey &o) const {
+    return id == o.id && proto == o.proto && src == o.src && dst == o.dst && smac == o.smac &&
+           dmac == o.dmac;
+  }
+};
+struct FragHash {
+  size_t operator()(const FragKey &k) const {
+    uint64_t h = k.smac * 0x9E3779B97F4A7C15ull ^ (k.dmac + 0x632BE59BD9B4E019ull);
+    h ^= ((uint64_t)k.src << 32 | k.dst) * 0xC2B2AE3D27D4EB4Full;
+    h ^= ((uint64_t)k.id << 8 | k.proto) * 0x165667B19E3779F9ull;
+    return (size_t)(h ^ (h >> 29));
+  }
+};
+struct FragVal {
+  Info info;
+  uint64_t smac, dmac;
+};
+
+struct Ep {
+  bool used = false;
+  int kind = 0;
+  int for_nic = -1;
+  std::vector<Listen> listening;
+  int next_dhcp = -1;
+};
+
+/* carried decision cache of one source endpoint */
+struct Chain {
+  bool device_chain = false;        // previous result on the device is authoritative
+  const usn_tile_hdr *tiles = nullptr;
+  uint32_t ntiles = 0;
+  const usn_summary *summary = nullptr;
+  uint32_t state = 0, dst = 0;      // explicit state when !device_chain
+  uint32_t info[4] = {0, 0, 0, 0};
+};
+
+struct ParsedH {   // host-side extract_pkt_info result
+  int status;      // 0 fail (reason in `reason`), 1 ok
+  uint32_t reason;
+  Info info;
+  uint64_t smac, dmac;
+};
+
+}  // namespace
+
+struct usn_ctx {
+  int device = 0;
+  int n_cu = 0;
+  std::mutex mu;
+  std::vector<Ep> eps = std::vector<Ep>(USN_MAX_ENDPOINTS);
+  uint32_t n_ep = 0;   // max id + 1
+  std::unordered_map<WantKey, Rule, WantHash> rules;
+  std::vector<uint64_t> bridge;
+  std::unordered_map<FragKey, FragVal, FragHash> frags;
+  std::vector<Chain> chains = std::vector<Chain>(USN_MAX_ENDPOINTS);
+  /* device table snapshot */
+  bool table_dirty = true;
+  uint4 *d_table = nullptr;
+  size_t d_table_cap = 0;
+  uint32_t table_slots = 0, bucket_mask = 0;
+  bool bridge_dirty = true;
+  uint64_t *d_bridge = nullptr;
+  size_t d_bridge_cap = 0;
+};
+
+namespace {
+
+uint32_t next_pow2(uint32_t v) {
+  uint32_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+int rebuild_table(usn_ctx *c) {
+  const uint32_t n = (uint32_t)c->rules.size();
+  uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
+  std::vector<uint4> img((size_t)nb * 4);
+  std::memset(img.data(), 0, img.size() * sizeof(uint4));
+  for (const auto &kv : c->rules) {
+    const WantKey &k = kv.first;
+    const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
+    const uint32_t meta = usn_key_meta(k.proto, k.present);
+    uint32_t b = usn_key_hash(k.dst, k.src, z, meta) & (nb - 1);
+    for (;;) {
+      uint4 *s = &img[(size_t)b * 4];
+      int free_slot = -1;
+      for (int j = 0; j < 4; ++j)
+        if (!(s[j].w & USN_SLOT_VALID)) { free_slot = j; break; }
+      if (free_slot >= 0) {
+        const uint16_t owner = kv.second.owner;
+        const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
+        s[free_slot] = make_uint4(k.dst, k.src, z,
+                                  meta | (nic ? USN_SLOT_NICOWNER : 0u) | ((uint32_t)owner << 16));
+        break;
+      }
+      b = (b + 1) & (nb - 1);
+    }
+  }
+  const size_t bytes = img.size() * sizeof(uint4);
+  HIPCHK(hipDeviceSynchronize());   // no in-flight batch may read the old snapshot
+  if (bytes > c->d_table_cap) {
+    if (c->d_table) HIPCHK(hipFree(c->d_table));
+    c->d_table = nullptr;
+    HIPCHK(hipMalloc(&c->d_table, bytes));
+    c->d_table_cap = bytes;
+  }
+  HIPCHK(hipMemcpy(c->d_table, img.data(), bytes, hipMemcpyHostToDevice));
+  c->table_slots = nb * 4;
+  c->bucket_mask = nb - 1;
+  c->table_dirty = false;
+  return USN_OK;
+}
+
+int rebuild_bridge(usn_ctx *c) {
+  const size_t bytes = std::max<size_t>(8, c->bridge.size() * 8);
+  HIPCHK(hipDeviceSynchronize());
+  if (bytes > c->d_bridge_cap) {
+    if (c->d_bridge) HIPCHK(hipFree(c->d_bridge));
+    c->d_bridge = nullptr;
+    HIPCHK(hipMalloc(&c->d_bridge, bytes));
+    c->d_bridge_cap = bytes;
+  }
+  if (!c->bridge.empty())
+    HIPCHK(hipMemcpy(c->d_bridge, c->bridge.data(), c->bridge.size() * 8, hipMemcpyHostToDevice));
+  c->bridge_dirty = false;
+  return USN_OK;
+}
+
+void cache_clear(usn_ctx *c, int ep) {
+  if (ep < 0 || ep >= USN_MAX_ENDPOINTS) return;
+  Chain &ch = c->chains[ep];
+  ch = Chain();   // last_pkt = None
+}
+
+/* ---- host restatement of the per-frame path for the ordered stage -------- */
+uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+uint64_t mac48(const uint8_t *p) {
+  uint64_t m = 0;
+  for (int i = 0; i < 6; ++i) m |= (uint64_t)p[i] << (8 * i);
+  return m;
+}
+
+/* extract_pkt_info (pkt.rs:158-218) including the fragment map side effects */
+ParsedH host_parse(usn_ctx *c, const uint8_t *b, uint32_t len) {
+  ParsedH r{};
+  r.status = 0;
+  r.reason = USN_R_PARSE;
+  if (len < 14) return r;
+  r.dmac = mac48(b);
+  r.smac = mac48(b + 6);
+  const uint16_t et = be16(b + 12);
+  if (et == 0x0806) { r.status = 1; r.info.w[0] = USN_INFO_ARP; return r; }
+  if (et == 0x888E) { r.status = 1; r.info.w[0] = USN_INFO_EAPOL; return r; }
+  if (et != 0x0800) return r;
+  const uint8_t *p = b + 14;
+  const uint32_t n = len - 14;
+  if (n < 20) return r;
+  const uint32_t hl = (p[0] & 0x0Fu) * 4, tl = be16(p + 2);
+  if (n < hl || hl > tl || n < tl) return r;
+  const uint16_t ff = be16(p + 6);
+  FragKey fk{be16(p + 4), p[9], be32(p + 12), be32(p + 16), r.smac, r.dmac};
+  if (ff & 0x1FFF) {
+    auto it = c->frags.find(fk);
+    if (it == c->frags.end()) { r.reason = USN_R_FRAGMISS; return r; }
+    r.status = 1;
+    r.info = it->second.info;
+    r.smac = it->second.smac;
+    r.dmac = it->second.dmac;
+    return r;
+  }
+  const uint32_t proto = p[9];
+  const bool pp = proto == 6 || proto == 17 || proto == 0x21 || proto == 0x84 || proto == 0x88;
+  const bool ports = pp && (tl - hl) > 4;
+  r.info.w[0] = USN_INFO_IPV4 | (proto << 8) | ((ports ? 1u : 0u) << 16);
+  r.info.w[1] = be32(p + 12);
+  r.info.w[2] = be32(p + 16);
+  r.info.w[3] = ports ? ((uint32_t)be16(p + hl) | ((uint32_t)be16(p + hl + 2) << 16)) : 0u;
+  r.status = 1;
+  if (!(ff & 0x4000) && (ff & 0x2000)) c->frags[fk] = FragVal{r.info, r.smac, r.dmac};
+  return r;
+}
+
+int registry_get(const usn_ctx *c, const WantKey &k) {
+  auto it = c->rules.find(k);
+  return it == c->rules.end() ? -1 : (int)it->second.owner;
+}
+
+bool bridge_has(const usn_ctx *c, uint64_t mac) {
+  return std::find(c->bridge.begin(), c->bridge.end(), mac) != c->bridge.end();
+}
+
+struct CacheState {
+  bool valid = false;
+  Info info{};
+  uint32_t dst = 0;
+};
+
+/* find_forward (endpoint.rs:172-296) for one frame; updates registry, bridge,
+ * fragment map, next_dhcp and the source's cache state. */
+uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, CacheState &st,
+                   bool &learned) {
+  learned = false;
+  Ep &S = c->eps[src];
+  const bool incoming = S.kind == USN_EP_NIC;
+  ParsedH p = host_parse(c, frame, len);
+  if (!p.status) return usn_mkdec(USN_CLS_DROP, p.reason, 0xFFFF);
+  if (st.valid && st.info == p.info) return st.dst | USN_F_CACHE;
+  st.valid = false;
+  if (!incoming && !(p.smac & 1) && !bridge_has(c, p.smac)) {
+    c->bridge.push_back(p.smac);
+    c->bridge_dirty = true;
+    learned = true;
+  }
+  const uint32_t kind = p.info.kind();
+  if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) return usn_mkdec(USN_CLS_FLOOD, 0, 0xFFFF);
+  if ((p.info.dst() >> 24) == 127) return usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFF);
+  st.valid = true;
+  st.info = p.info;
+  const bool ports = p.info.has_ports();
+  const uint32_t proto = p.info.proto();
+  if (!incoming) {
+    WantKey w;   // to_want (pkt.rs:78-95)
+    w.dst = p.info.src();
+    w.src = p.info.dst();
+    w.proto = (uint8_t)proto;
+    w.present = USN_WANT_SRC | (ports ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0);
+    w.dport = ports ? (uint16_t)p.info.sport() : 0;
+    w.sport = ports ? (uint16_t)p.info.dport() : 0;
+    bool listening = false;
+    for (const Listen &l : S.listening)
+      if (l.dst == w.dst && l.proto == w.proto && l.has_port == (ports ? 1 : 0) &&
+          (!ports || l.port == w.dport)) { listening = true; break; }
+    if (!listening) {
+      const bool dhcp_req = proto == 17 && p.info.src() == 0 && ports && p.info.sport() == 68 &&
+                            p.info.dport() == 67 && (p.info.dst() & 0xFF) == 255;
+      if (dhcp_req) {
+        if (S.for_nic >= 0) {
+          c->eps[S.for_nic].next_dhcp = src;
+          cache_clear(c, S.for_nic);
+          st.valid = false;
+        }
+      } else if (!c->rules.count(w)) {
+        if (S.for_nic >= 0) cache_clear(c, S.for_nic);
+        c->rules[w] = Rule{(uint16_t)src, 0};
+        c->table_dirty = true;
+        learned = true;
+      }
+    }
+  }
+  uint32_t d;
+  if (!incoming && !bridge_has(c, p.dmac)) {
+    d = usn_mkdec(USN_CLS_NIC, 0, (uint32_t)S.for_nic);
+  } else {
+    WantKey k1;
+    k1.dst = p.info.dst();
+    k1.src = p.info.src();
+    k1.proto = (uint8_t)proto;
+    k1.present = USN_WANT_SRC | (ports ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0);
+    k1.dport = ports ? (uint16_t)p.info.dport() : 0;
+    k1.sport = ports ? (uint16_t)p.info.sport() : 0;
+    int e = registry_get(c, k1);
+    if (e < 0) {
+      WantKey k2 = k1;
+      k2.src = 0;
+      k2.sport = 0;
+      k2.present = ports ? USN_WANT_DPORT : 0;
+      e = registry_get(c, k2);
+    }
+    bool excl = false;
+    if (e >= 0 && (c->eps[e].kind == USN_EP_NIC || e == src)) { excl = true; e = -1; }
+    if (e >= 0) {
+      d = usn_mkdec(USN_CLS_EP, 0, (uint32_t)e);
+    } else if (proto == 17 && ports && p.info.sport() == 67 && p.info.dport() == 68) {
+      if (S.next_dhcp >= 0) {
+        d = usn_mkdec(USN_CLS_EP, 0, (uint32_t)S.next_dhcp) | USN_F_DHCP;
+        S.next_dhcp = -1;
+        st.valid = false;
+      } else {
+        d = usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFF);
+      }
+    } else {
+      d = usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFF);
+    }
+  }
+  st.dst = d & USN_PARITY_MASK;
+  return d;
+}
+
+}  // namespace
+
+/* ========================================================================== */
+extern "C" {
+
+int usn_abi_version(void) { return USN_ABI_VERSION; }
+int usn_last_hip_error(void) { return g_last_hip; }
+
+const char *usn_strerror(int s) {
+  switch (s) {
+    case USN_OK: return "ok";
+    case USN_EINVAL: return "invalid argument";
+    case USN_ENOMEM: return "out of memory";
+    case USN_EEXIST: return "exists";
+    case USN_ENOENT: return "not found";
+    case USN_EPERM: return "not permitted";
+    case USN_EHIP: return "HIP runtime error";
+    case USN_ENODEV: return "no gfx950 device";
+    case USN_ERANGE: return "out of range";
+    default: return "unknown";
+  }
+}
+
+int usn_ctx_create(int hip_device, usn_ctx **out) {
+  if (!out) return USN_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (hip_device < 0 || hip_device >= ndev) return USN_ENODEV;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, hip_device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return USN_ENODEV;
+  HIPCHK(hipSetDevice(hip_device));
+  usn_ctx *c = new (std::nothrow) usn_ctx();
+  if (!c) return USN_ENOMEM;
+  c->device = hip_device;
+  c->n_cu = prop.multiProcessorCount;
+  *out = c;
+  return USN_OK;
+}
+
+void usn_ctx_destroy(usn_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  if (c->d_table) (void)hipFree(c->d_table);
+  if (c->d_bridge) (void)hipFree(c->d_bridge);
+  delete c;
+}
+
+int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
+  if (!c || id >= USN_MAX_ENDPOINTS || kind < USN_EP_NIC || kind > USN_EP_UDS) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->eps[id].used) return USN_EEXIST;
+  if ((kind == USN_EP_NIC) != (for_nic < 0)) return USN_EINVAL;   // main.rs:157-159
+  if (for_nic >= 0 && (for_nic >= USN_MAX_ENDPOINTS || !c->eps[for_nic].used ||
+                       c->eps[for_nic].kind != USN_EP_NIC))
+    return USN_EINVAL;
+  Ep &e = c->eps[id];
+  e = Ep();
+  e.used = true;
+  e.kind = kind;
+  e.for_nic = for_nic;
+  c->n_ep = std::max<uint32_t>(c->n_ep, (uint32_t)id + 1);
+  c->chains[id] = Chain();
+  return USN_OK;
+}
+
+int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
+  if (!c || id >= USN_MAX_ENDPOINTS) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->eps[id].used) return USN_ENOENT;
+  for (auto it = c->rules.begin(); it != c->rules.end();) {   // match_register.retain
+    if (it->second.owner == id) { it = c->rules.erase(it); c->table_dirty = true; }
+    else ++it;
+  }
+  c->eps[id] = Ep();
+  c->chains[id] = Chain();
+  return USN_OK;
+}
+
+int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
+  if (!c || !w || owner >= USN_MAX_ENDPOINTS) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  Ep &e = c->eps[owner];
+  if (!e.used) return USN_ENOENT;
+  const WantKey k = canon(*w);
+  if (c->rules.count(k)) return 0;                                   // main.rs:272-274
+  e.listening.push_back(Listen{k.dst, k.proto, (uint8_t)((k.present & USN_WANT_DPORT) ? 1 : 0),
+                               k.dport});                            // main.rs:276-279
+  if (e.for_nic < 0) return USN_EPERM;                                // main.rs:287-289 panics
+  cache_clear(c, e.for_nic);                                          // main.rs:280-286
+  c->rules[k] = Rule{owner, (uint8_t)(sticky ? 1 : 0)};
+  c->table_dirty = true;
+  return 1;
+}
+
+int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
+  if (!c || !w) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  const WantKey k = canon(*w);
+  auto it = c->rules.find(k);
+  if (it == c->rules.end()) return 0;
+  if (it->second.owner != requester) return USN_EPERM;               // main.rs:612-616
+  c->rules.erase(it);
+  c->table_dirty = true;
+  return 1;
+}
+
+int usn_rule_count(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return (int)c->rules.size();
+}
+
+int usn_rules_get(usn_ctx *c, usn_want *w, uint16_t *owner, uint8_t *sticky, uint32_t cap) {
+  if (!c) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  uint32_t n = 0;
+  for (const auto &kv : c->rules) {
+    if (n >= cap) break;
+    if (w) {
+      usn_want &o = w[n];
+      std::memset(&o, 0, sizeof o);
+      o.dst_addr = kv.first.dst;
+      o.src_addr = kv.first.src;
+      o.dst_port = kv.first.dport;
+      o.src_port = kv.first.sport;
+      o.protocol = kv.first.proto;
+      o.present = kv.first.present;
+    }
+    if (owner) owner[n] = kv.second.owner;
+    if (sticky) sticky[n] = kv.second.sticky;
+    ++n;
+  }
+  return (int)n;
+}
+
+int usn_lookup(usn_ctx *c, const usn_want *w) {
+  if (!c || !w) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  const int e = registry_get(c, canon(*w));
+  return e < 0 ? USN_ENOENT : e;
+}
+
+int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
+  if (!c || !mac) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->bridge.push_back(mac48(mac));
+  c->bridge_dirty = true;
+  return USN_OK;
+}
+
+int usn_bridge_count(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return (int)c->bridge.size();
+}
+
+int usn_frag_clear(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->frags.clear();
+  return USN_OK;
+}
+
+int usn_cache_clear(usn_ctx *c, uint16_t ep) {
+  if (!c || ep >= USN_MAX_ENDPOINTS) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  cache_clear(c, ep);
+  return USN_OK;
+}
+
+/* ---- result layout ------------------------------------------------------- */
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct Layout {
+  size_t dec, order, runs, tiles, summary, host, total;
+};
+static Layout layout_for(uint64_t n) {
+  const uint64_t nt = (n + USN_TILE - 1) / USN_TILE;
+  Layout L;
+  size_t off = 0;
+  L.dec = off; off = align256(off + n * 4);
+  L.order = off; off = align256(off + nt * USN_TILE * 2);
+  L.runs = off; off = align256(off + nt * USN_TILE * 4);
+  L.tiles = off; off = align256(off + nt * sizeof(usn_tile_hdr));
+  L.summary = off; off = align256(off + sizeof(usn_summary));
+  L.host = off; off = align256(off + nt * USN_TILE * 4);
+  L.total = off;
+  return L;
+}
+
+size_t usn_result_bytes(uint64_t n) { return layout_for(n).total; }
+
+int usn_result_bind(void *mem, size_t bytes, uint64_t n, usn_result *out) {
+  if (!mem || !out || n == 0) return USN_EINVAL;
+  const Layout L = layout_for(n);
+  if (bytes < L.total) return USN_ERANGE;
+  uint8_t *b = static_cast<uint8_t *>(mem);
+  out->decisions = reinterpret_cast<uint32_t *>(b + L.dec);
+  out->order = reinterpret_cast<uint16_t *>(b + L.order);
+  out->runs = reinterpret_cast<uint32_t *>(b + L.runs);
+  out->tiles = reinterpret_cast<usn_tile_hdr *>(b + L.tiles);
+  out->summary = reinterpret_cast<usn_summary *>(b + L.summary);
+  out->host_list = reinterpret_cast<uint32_t *>(b + L.host);
+  out->n = n;
+  return USN_OK;
+}
+
+/* ---- the hot path ----------------------------------------------------------- */
+static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, ClassifyArgs &a) {
+  std::memset(&a, 0, sizeof a);
+  a.frames = b->frames;
+  a.stride = b->stride;
+  a.offsets = b->offsets;
+  a.lens = b->lens;
+  a.n = b->n;
+  a.ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
+  a.decisions = r->decisions;
+  a.order = r->order;
+  a.runs = r->runs;
+  a.tiles = r->tiles;
+  a.summary = r->summary;
+  a.host_list = r->host_list;
+  a.table = c->d_table;
+  a.bucket_mask = c->bucket_mask;
+  a.table_slots = c->table_slots;
+  a.bridge = c->d_bridge;
+  a.n_bridge = (uint32_t)c->bridge.size();
+  const Ep &S = c->eps[b->src_endpoint];
+  a.src = b->src_endpoint;
+  a.src_is_nic = S.kind == USN_EP_NIC;
+  a.for_nic = S.for_nic < 0 ? 0xFFFFu : (uint32_t)S.for_nic;
+  a.n_ep = c->n_ep;
+  a.nbins = c->n_ep + 3;
+  return USN_OK;
+}
+
+int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
+  if (!c || !b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
+  if ((b->stride == 0) == (b->offsets == nullptr)) return USN_EINVAL;
+  if (b->stride && (b->stride % 16 != 0 || b->stride < USN_WINDOW)) return USN_EINVAL;
+  if (((uintptr_t)b->frames & 15) != 0) return USN_EINVAL;
+  if (b->n > 0xFFFFFFFFull) return USN_ERANGE;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (b->src_endpoint >= USN_MAX_ENDPOINTS || !c->eps[b->src_endpoint].used) return USN_EINVAL;
+  if (c->eps[b->src_endpoint].kind != USN_EP_NIC) return USN_EINVAL;   // tx: not yet on device
+  HIPCHK(hipSetDevice(c->device));
+  if (c->table_dirty) { int s = rebuild_table(c); if (s) return s; }
+  if (c->bridge_dirty) { int s = rebuild_bridge(c); if (s) return s; }
+  ClassifyArgs a;
+  fill_args(c, b, r, a);
+  Chain &ch = c->chains[b->src_endpoint];
+  if (ch.device_chain) {
+    a.carry_mode = usn::CARRY_CHAIN;
+    a.prev_tiles = ch.tiles;
+    a.prev_ntiles = ch.ntiles;
+    a.prev_summary = ch.summary;
+  } else {
+    a.carry_mode = usn::CARRY_EXPLICIT;
+    a.cin_state = ch.state;
+    a.cin_dst = ch.dst;
+    std::memcpy(a.cin_info, ch.info, sizeof ch.info);
+  }
+  HIPCHK(usn::launch_classify(a, (hipStream_t)stream));
+  ch.device_chain = true;
+  ch.tiles = r->tiles;
+  ch.ntiles = a.ntiles;
+  ch.summary = r->summary;
+  return USN_OK;
+}
+
+/* ---- ordered host stage --------------------------------------------------- */
+namespace {
+
+struct HostView {   // lazily fetched device data of one batch
+  usn_ctx *c;
+  const usn_batch *b;
+  const usn_result *r;
+  hipStream_t s;
+  std::vector<uint32_t> dec;     // decisions (fetched whole on first need)
+  std::vector<uint16_t> lens;
+  bool have_dec = false, have_lens = false;
+
+  int fetch_dec() {
+    if (have_dec) return USN_OK;
+    dec.resize(b->n);
+    HIPCHK(hipMemcpy(dec.data(), r->decisions, b->n * 4, hipMemcpyDeviceToHost));
+    have_dec = true;
+    return USN_OK;
+  }
+  int fetch_lens() {
+    if (have_lens) return USN_OK;
+    lens.resize(b->n);
+    HIPCHK(hipMemcpy(lens.data(), b->lens, b->n * 2, hipMemcpyDeviceToHost));
+    have_lens = true;
+    return USN_OK;
+  }
+  /* frame bytes [0, max(64, min(len, 80))) of frame i */
+  int frame(uint64_t i, std::vector<uint8_t> &buf, uint32_t &len) {
+    int s = fetch_lens();
+    if (s) return s;
+    len = lens[i];
+    uint64_t off;
+    if (b->offsets) HIPCHK(hipMemcpy(&off, b->offsets + i, 8, hipMemcpyDeviceToHost));
+    else off = i * b->stride;
+    const uint32_t want = std::max<uint32_t>(USN_WINDOW, std::min<uint32_t>(len, 80));
+    buf.assign(want, 0);
+    HIPCHK(hipMemcpy(buf.data(), b->frames + off, want, hipMemcpyDeviceToHost));
+    return USN_OK;
+  }
+};
+
+bool touches(uint32_t d) {
+  return !(USN_DEC_CLASS(d) == USN_CLS_DROP &&
+           (USN_DEC_REASON(d) == USN_R_PARSE || USN_DEC_REASON(d) == USN_R_FRAGMISS));
+}
+bool retains(uint32_t d) {
+  return USN_DEC_CLASS(d) != USN_CLS_FLOOD && USN_DEC_REASON(d) != USN_R_LOOPBACK;
+}
+
+}  // namespace
+
+int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
+                 usn_finalize_info *info) {
+  if (!c || !b || !r || b->n == 0) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
+  usn_summary sum;
+  HIPCHK(hipMemcpy(&sum, r->summary, sizeof sum, hipMemcpyDeviceToHost));
+  std::vector<usn_tile_hdr> th(ntiles);
+  HIPCHK(hipMemcpy(th.data(), r->tiles, ntiles * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+  usn_finalize_info fi;
+  std::memset(&fi, 0, sizeof fi);
+  fi.flags = sum.flags;
+  std::vector<uint32_t> hosts;
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
+    if (th[t].n_host) {
+      const size_t at = hosts.size();
+      hosts.resize(at + th[t].n_host);
+      HIPCHK(hipMemcpy(hosts.data() + at, r->host_list + (size_t)t * USN_TILE,
+                       th[t].n_host * 4, hipMemcpyDeviceToHost));
+    }
+  }
+  const bool stale_walk = (sum.flags & USN_S_STALE) && sum.first_break < b->n;
+  if (hosts.empty() && !stale_walk && !(sum.flags & USN_S_STALE_EXTENDS)) {
+    if (info) *info = fi;
+    return USN_OK;   // device results are final; the device chain carries the cache
+  }
+  const int src = b->src_endpoint;
+  HostView hv{c, b, r, s, {}, {}, false, false};
+  int st = hv.fetch_dec();
+  if (st) return st;
+  std::vector<uint8_t> buf;
+  uint32_t len = 0;
+  std::vector<char> dirty(ntiles, 0);
+  CacheState cs;
+  cs.valid = sum.cin_state & USN_CS_VALID;
+  cs.dst = sum.cin_dst;
+  std::memcpy(cs.info.w, sum.cin_info, 16);
+  const CacheState carried = cs;
+  uint64_t pos = 0;   // cache state `cs` is the state just before frame `pos`
+
+  /* advance cs over device-final frames [pos, j) */
+  auto advance = [&](uint64_t j) -> int {
+    for (uint64_t k = j; k > pos; --k) {
+      const uint32_t d = hv.dec[k - 1];
+      if (!touches(d)) continue;
+      if (!retains(d)) { cs.valid = false; break; }
+      int e = hv.frame(k - 1, buf, len);
+      if (e) return e;
+      ParsedH p = host_parse(c, buf.data(), len);   // no map side effect: not a first fragment
+      cs.valid = true;
+      cs.info = p.info;
+      cs.dst = d & USN_PARITY_MASK;
+      break;
+    }
+    pos = j;
+    return USN_OK;
+  };
+  auto resolve = [&](uint64_t j) -> int {
+    int e = advance(j);
+    if (e) return e;
+    e = hv.frame(j, buf, len);
+    if (e) return e;
+    bool learned;
+    const uint32_t d = host_step(c, src, buf.data(), len, cs, learned) | USN_F_HOST;
+    const uint32_t old = hv.dec[j];
+    if ((old & USN_PARITY_MASK) != (d & USN_PARITY_MASK)) {
+      fi.n_patched++;
+      fi.class_count[USN_DEC_CLASS(old)]--;
+      fi.class_count[USN_DEC_CLASS(d)]++;
+      dirty[j / USN_TILE] = 1;
+    }
+    if (old != d) {
+      hv.dec[j] = d;
+      HIPCHK(hipMemcpy(r->decisions + j, &d, 4, hipMemcpyHostToDevice));
+    }
+    fi.n_host++;
+    pos = j + 1;
+    return USN_OK;
+  };
+
+  std::sort(hosts.begin(), hosts.end());
+  size_t hi = 0;
+  /* stale prefix that the device could not close inside tile 0 */
+  if (stale_walk || (sum.flags & USN_S_STALE_EXTENDS)) {
+    uint64_t j = (sum.flags & USN_S_STALE_EXTENDS) ? std::min<uint64_t>(USN_TILE, b->n)
+                                                   : sum.first_break;
+    // frames before j are final (device override or host frames among them)
+    while (hi < hosts.size() && hosts[hi] < j) {
+      st = resolve(hosts[hi++]);
+      if (st) return st;
+    }
+    st = advance(j);
+    if (st) return st;
+    // walk while the stale entry is still the cached one
+    while (j < b->n && cs.valid && cs.info == carried.info && cs.dst == carried.dst) {
+      if (hi < hosts.size() && hosts[hi] == j) ++hi;
+      st = resolve(j);
+      if (st) return st;
+      ++j;
+    }
+  }
+  while (hi < hosts.size()) {
+    st = resolve(hosts[hi++]);
+    if (st) return st;
+  }
+  st = advance(b->n);
+  if (st) return st;
+  /* patched tiles: rebuild their order / runs / counts */
+  ClassifyArgs a;
+  fill_args(c, b, r, a);
+  for (uint32_t t = 0; t < ntiles;) {
+    if (!dirty[t]) { ++t; continue; }
+    uint32_t e = t;
+    while (e < ntiles && dirty[e]) ++e;
+    HIPCHK(usn::launch_resort(a, t, e, s));
+    t = e;
+  }
+  /* carried-out cache: authoritative from now on */
+  usn_summary out = sum;
+  out.flags |= USN_S_COUT;
+  out.cout_state = cs.valid ? USN_CS_VALID : 0u;
+  out.cout_dst = cs.dst;
+  std::memcpy(out.cout_info, cs.info.w, 16);
+  HIPCHK(hipMemcpy(r->summary, &out, sizeof out, hipMemcpyHostToDevice));
+  HIPCHK(hipStreamSynchronize(s));
+  if (info) *info = fi;
+  return USN_OK;
+}
+
+/* ---- device plumbing ------------------------------------------------------- */
+int usn_dev_alloc(usn_ctx *c, size_t bytes, void **p) {
+  if (!c || !p) return USN_EINVAL;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMalloc(p, bytes));
+  return USN_OK;
+}
+int usn_dev_free(usn_ctx *c, void *p) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipFree(p));
+  return USN_OK;
+}
+int usn_host_alloc_pinned(usn_ctx *c, size_t bytes, void **p) {
+  if (!c || !p) return USN_EINVAL;
+  HIPCHK(hipHostMalloc(p, bytes, hipHostMallocDefault));
+  return USN_OK;
+}
+int usn_host_free_pinned(usn_ctx *c, void *p) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipHostFree(p));
+  return USN_OK;
+}
+int usn_memcpy_h2d(usn_ctx *c, void *d, const void *h, size_t n, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, (hipStream_t)s));
+  return USN_OK;
+}
+int usn_memcpy_d2h(usn_ctx *c, void *h, const void *d, size_t n, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, (hipStream_t)s));
+  return USN_OK;
+}
+int usn_memset_d(usn_ctx *c, void *d, int v, size_t n, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipMemsetAsync(d, v, n, (hipStream_t)s));
+  return USN_OK;
+}
+int usn_stream_create(usn_ctx *c, void **s) {
+  if (!c || !s) return USN_EINVAL;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st;
+  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  *s = st;
+  return USN_OK;
+}
+int usn_stream_destroy(usn_ctx *c, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipStreamDestroy((hipStream_t)s));
+  return USN_OK;
+}
+int usn_stream_sync(usn_ctx *c, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  return USN_OK;
+}
+int usn_device_sync(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipDeviceSynchronize());
+  return USN_OK;
+}
+int usn_event_create(usn_ctx *c, void **ev) {
+  if (!c || !ev) return USN_EINVAL;
+  hipEvent_t e;
+  HIPCHK(hipEventCreate(&e));
+  *ev = e;
+  return USN_OK;
+}
+int usn_event_destroy(usn_ctx *c, void *ev) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipEventDestroy((hipEvent_t)ev));
+  return USN_OK;
+}
+int usn_event_record(usn_ctx *c, void *ev, void *s) {
+  if (!c) return USN_EINVAL;
+  HIPCHK(hipEventRecord((hipEvent_t)ev, (hipStream_t)s));
+  return USN_OK;
+}
+int usn_event_elapsed_ms(usn_ctx *c, void *a, void *b, float *ms) {
+  if (!c || !ms) return USN_EINVAL;
+  HIPCHK(hipEventSynchronize((hipEvent_t)b));
+  HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+  return USN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+/*
+ * usn_internal.h -- layouts shared by the HIP kernels and the C++ host.
+ *
+ * Rule table in HBM/LDS: open addressing over 64-byte buckets of four 16-byte
+ * slots (one cache line per probe).  A slot is the exact Want key of
+ * /root/reference/src/pkt.rs:220-227 packed into three words plus a meta word:
+ *   x = dst_addr
+ *   y = src_addr          (0 when absent)
+ *   z = dst_port | src_port << 16   (absent ports are 0)
+ *   w = protocol | present << 8 | VALID | owner_is_nic << 12 | owner << 16
+ * The key compare is (x, y, z, w & KEY_META_MASK); `present` makes
+ * Option::None differ from Some(0) exactly as derive(Eq) on Want does.
+ * The table is rebuilt from the host registry on every change (no
+ * tombstones), so a probe ends at the first bucket that has a free slot.
+ *
+ * PacketInfo (pkt.rs:11-22) as 4 words, compared whole for the 1-entry
+ * decision cache (endpoint.rs:186-191, derive(PartialEq)):
+ *   i0 = kind | proto << 8 | has_ports << 16     kind: 1 Ipv4, 2 Arp, 3 Eapol
+ *   i1 = src_addr, i2 = dst_addr                 (0 for Arp/Eapol)
+ *   i3 = has_ports ? src_port | dst_port << 16 : 0
+ */
+#ifndef USN_INTERNAL_H
+#define USN_INTERNAL_H
+
+#include <stdint.h>
+
+#define USN_SLOT_VALID (1u << 11)
+#define USN_SLOT_NICOWNER (1u << 12)
+#define USN_KEY_META_MASK 0x0FFFu
+
+#define USN_INFO_IPV4 1u
+#define USN_INFO_ARP 2u
+#define USN_INFO_EAPOL 3u
+
+/* tile header last_state bits */
+#define USN_TS_HAS 1u       /* a frame in the tile touched the cache */
+#define USN_TS_RETAINED 2u  /* ...and left last_pkt = Some(info) */
+#define USN_TS_UNKNOWN 4u   /* ...but it is a later fragment (host resolves) */
+
+/* summary cin/cout state bits */
+#define USN_CS_VALID 1u     /* last_pkt is Some(info) */
+
+/* bins of the per-tile order: endpoints 0..E-1, then NIC, FLOOD, DROP */
+#define USN_BIN_NIC(E) (E)
+#define USN_BIN_FLOOD(E) ((E) + 1)
+#define USN_BIN_DROP(E) ((E) + 2)
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define USN_HD __host__ __device__ __forceinline__
+#else
+#define USN_HD static inline
+#endif
+
+USN_HD uint32_t usn_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+/* Bucket hash of a packed key.  Shared bit-for-bit by host build and device probe. */
+USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
+  uint32_t h = x * 0x9E3779B1u;
+  h ^= usn_rotl32(y * 0x85EBCA77u, 13);
+  h ^= usn_rotl32(z * 0xC2B2AE3Du, 7);
+  h ^= meta * 0x27D4EB2Fu;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+
+USN_HD uint32_t usn_key_meta(uint32_t proto, uint32_t present) {
+  return (proto & 0xFFu) | ((present & 7u) << 8) | USN_SLOT_VALID;
+}
+
+USN_HD uint32_t usn_mkdec(uint32_t cls, uint32_t reason, uint32_t ep) {
+  return (ep & 0xFFFFu) | (cls << 16) | (reason << 20);
+}
+
+#endif

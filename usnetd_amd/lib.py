@@ -1,0 +1,378 @@
+"""ctypes binding of the C ABI in include/usn_classify.h (usnetd_amd/libusn.so).
+
+This is thin plumbing for tests, bench.py and the control plane; the product is
+the native library.  Loading fails loudly when the library is missing or when
+no gfx950 device is present: there is no CPU fallback for the match path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libusn.so")
+
+USN_TILE = 1024
+USN_WINDOW = 64
+USN_MAX_ENDPOINTS = 1021
+PARITY_MASK = 0x00FFFFFF
+EP_NIC, EP_HOST, EP_PIPE, EP_UDS = 0, 1, 2, 3
+CLS_DROP, CLS_EP, CLS_NIC, CLS_FLOOD = 0, 1, 2, 3
+F_CACHE, F_FRAG1, F_FRAGN, F_DHCP, F_HOST, F_LEARN = (1 << 24, 1 << 25, 1 << 26, 1 << 27,
+                                                      1 << 28, 1 << 29)
+S_STALE, S_STALE_EXTENDS, S_COUT = 1, 2, 8
+STATUS = {0: "ok", -22: "EINVAL", -12: "ENOMEM", -17: "EEXIST", -2: "ENOENT", -1: "EPERM",
+          -5: "EHIP", -19: "ENODEV", -34: "ERANGE"}
+
+
+class UsnError(RuntimeError):
+    pass
+
+
+class Want(C.Structure):
+    _fields_ = [("dst_addr", C.c_uint32), ("src_addr", C.c_uint32), ("dst_port", C.c_uint16),
+                ("src_port", C.c_uint16), ("protocol", C.c_uint8), ("present", C.c_uint8),
+                ("_reserved", C.c_uint16)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("stride", C.c_uint64), ("offsets", C.c_void_p),
+                ("lens", C.c_void_p), ("n", C.c_uint64), ("src_endpoint", C.c_uint16),
+                ("_reserved", C.c_uint16 * 3)]
+
+
+class Result(C.Structure):
+    _fields_ = [("decisions", C.c_void_p), ("order", C.c_void_p), ("runs", C.c_void_p),
+                ("tiles", C.c_void_p), ("summary", C.c_void_p), ("host_list", C.c_void_p),
+                ("n", C.c_uint64)]
+
+
+class FinalizeInfo(C.Structure):
+    _fields_ = [("n_host", C.c_uint32), ("n_patched", C.c_uint32), ("n_learned", C.c_uint32),
+                ("flags", C.c_uint32), ("class_count", C.c_uint32 * 4)]
+
+
+TILE_HDR_DTYPE = np.dtype([("n_frames", "<u2"), ("n_runs", "<u2"), ("n_host", "<u2"),
+                           ("_r", "<u2"), ("class_count", "<u2", (4,)), ("last_state", "<u4"),
+                           ("last_dst", "<u4"), ("last_idx", "<u4"), ("last_info", "<u4", (4,)),
+                           ("_pad", "<u4")])
+SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames", "<u4"),
+                          ("n_tiles", "<u4"), ("cin_state", "<u4"), ("cin_dst", "<u4"),
+                          ("cin_info", "<u4", (4,)), ("cout_state", "<u4"), ("cout_dst", "<u4"),
+                          ("cout_info", "<u4", (4,))])
+assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 64
+
+_lib = None
+
+
+def load():
+    """Load libusn.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise UsnError("%s is missing: run `make` (or __graft_entry__.build()) first; "
+                       "the match path has no CPU fallback" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    P, I, U16, U32, U64, SZ = C.c_void_p, C.c_int, C.c_uint16, C.c_uint32, C.c_uint64, C.c_size_t
+    sig = {
+        "usn_abi_version": ([], I), "usn_strerror": ([I], C.c_char_p),
+        "usn_last_hip_error": ([], I),
+        "usn_ctx_create": ([I, C.POINTER(P)], I), "usn_ctx_destroy": ([P], None),
+        "usn_endpoint_add": ([P, U16, I, C.c_int32], I), "usn_endpoint_remove": ([P, U16], I),
+        "usn_add_match": ([P, C.POINTER(Want), U16, I], I),
+        "usn_remove_match": ([P, C.POINTER(Want), U16], I),
+        "usn_rule_count": ([P], I),
+        "usn_rules_get": ([P, P, P, P, U32], I),
+        "usn_lookup": ([P, C.POINTER(Want)], I),
+        "usn_bridge_add": ([P, C.c_char_p], I), "usn_bridge_count": ([P], I),
+        "usn_frag_clear": ([P], I), "usn_cache_clear": ([P, U16], I),
+        "usn_result_bytes": ([U64], SZ),
+        "usn_result_bind": ([P, SZ, U64, C.POINTER(Result)], I),
+        "usn_classify": ([P, C.POINTER(Batch), C.POINTER(Result), P], I),
+        "usn_finalize": ([P, C.POINTER(Batch), C.POINTER(Result), P, C.POINTER(FinalizeInfo)], I),
+        "usn_dev_alloc": ([P, SZ, C.POINTER(P)], I), "usn_dev_free": ([P, P], I),
+        "usn_host_alloc_pinned": ([P, SZ, C.POINTER(P)], I), "usn_host_free_pinned": ([P, P], I),
+        "usn_memcpy_h2d": ([P, P, P, SZ, P], I), "usn_memcpy_d2h": ([P, P, P, SZ, P], I),
+        "usn_memset_d": ([P, P, I, SZ, P], I),
+        "usn_stream_create": ([P, C.POINTER(P)], I), "usn_stream_destroy": ([P, P], I),
+        "usn_stream_sync": ([P, P], I), "usn_device_sync": ([P], I),
+        "usn_event_create": ([P, C.POINTER(P)], I), "usn_event_destroy": ([P, P], I),
+        "usn_event_record": ([P, P, P], I),
+        "usn_event_elapsed_ms": ([P, P, P, C.POINTER(C.c_float)], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_create",
+            "usn_ctx_destroy", "usn_endpoint_add", "usn_endpoint_remove", "usn_add_match",
+            "usn_remove_match", "usn_rule_count", "usn_rules_get", "usn_lookup", "usn_bridge_add",
+            "usn_bridge_count", "usn_frag_clear", "usn_cache_clear", "usn_result_bytes",
+            "usn_result_bind", "usn_classify", "usn_finalize", "usn_dev_alloc", "usn_dev_free",
+            "usn_host_alloc_pinned", "usn_host_free_pinned", "usn_memcpy_h2d", "usn_memcpy_d2h",
+            "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
+            "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
+            "usn_event_elapsed_ms"]
+
+
+def check(rc, what=""):
+    if rc < 0:
+        L = load()
+        extra = ""
+        if rc == -5:
+            extra = " (hipError %d)" % L.usn_last_hip_error()
+        raise UsnError("%s failed: %s%s" % (what, STATUS.get(rc, rc), extra))
+    return rc
+
+
+def ip2int(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def make_want(dst, proto, dport=None, src=None, sport=None) -> Want:
+    w = Want()
+    w.dst_addr = ip2int(dst)
+    w.protocol = proto
+    p = 0
+    if dport is not None:
+        p |= 1
+        w.dst_port = dport
+    if src is not None:
+        p |= 2
+        w.src_addr = ip2int(src)
+    if sport is not None:
+        p |= 4
+        w.src_port = sport
+    w.present = p
+    return w
+
+
+def want_from_dict(d) -> Want:
+    return make_want(d["dst"], d["proto"], d.get("dport"), d.get("src"), d.get("sport"))
+
+
+class DevBuf:
+    """A device allocation owned by a Ctx."""
+
+    def __init__(self, ctx: "Ctx", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(ctx.L.usn_dev_alloc(ctx.h, max(self.nbytes, 16), C.byref(p)), "usn_dev_alloc")
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            self.ctx.L.usn_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def upload(self, arr: np.ndarray, stream=None, offset=0):
+        arr = np.ascontiguousarray(arr)
+        assert offset + arr.nbytes <= self.nbytes
+        check(self.ctx.L.usn_memcpy_h2d(self.ctx.h, self.ptr + offset, arr.ctypes.data,
+                                        arr.nbytes, stream), "h2d")
+        if stream is None:
+            self.ctx.sync()
+
+    def download(self, dtype, count, offset=0, stream=None) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        check(self.ctx.L.usn_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr + offset,
+                                        out.nbytes, stream), "d2h")
+        self.ctx.sync(stream)
+        return out
+
+
+class Ctx:
+    """One usn_ctx bound to one gfx950 device (the daemon's match state)."""
+
+    def __init__(self, device: int = 0):
+        self.L = load()
+        h = C.c_void_p()
+        check(self.L.usn_ctx_create(device, C.byref(h)), "usn_ctx_create")
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.L.usn_ctx_destroy(self.h)
+            self.h = None
+
+    # --- control plane --------------------------------------------------------
+    def endpoint_add(self, eid, kind, for_nic=None):
+        return check(self.L.usn_endpoint_add(self.h, eid, kind, -1 if for_nic is None else for_nic),
+                     "usn_endpoint_add")
+
+    def endpoint_remove(self, eid):
+        return check(self.L.usn_endpoint_remove(self.h, eid), "usn_endpoint_remove")
+
+    def add_match(self, want: Want, owner: int, sticky=False) -> int:
+        rc = self.L.usn_add_match(self.h, C.byref(want), owner, int(bool(sticky)))
+        return rc if rc in (0, 1) else check(rc, "usn_add_match")
+
+    def remove_match(self, want: Want, requester: int) -> int:
+        rc = self.L.usn_remove_match(self.h, C.byref(want), requester)
+        return -1 if rc == -1 else check(rc, "usn_remove_match")
+
+    def rule_count(self):
+        return check(self.L.usn_rule_count(self.h), "usn_rule_count")
+
+    def rules(self):
+        n = self.rule_count()
+        ws = (Want * max(n, 1))()
+        owners = np.zeros(max(n, 1), np.uint16)
+        sticky = np.zeros(max(n, 1), np.uint8)
+        got = check(self.L.usn_rules_get(self.h, C.cast(ws, C.c_void_p), owners.ctypes.data,
+                                         sticky.ctypes.data, n), "usn_rules_get")
+        return [(ws[i], int(owners[i]), bool(sticky[i])) for i in range(got)]
+
+    def lookup(self, want: Want) -> int:
+        rc = self.L.usn_lookup(self.h, C.byref(want))
+        return -1 if rc == -2 else check(rc, "usn_lookup")
+
+    def bridge_add(self, mac: bytes):
+        check(self.L.usn_bridge_add(self.h, bytes(mac)), "usn_bridge_add")
+
+    def frag_clear(self):
+        check(self.L.usn_frag_clear(self.h), "usn_frag_clear")
+
+    def cache_clear(self, eid):
+        check(self.L.usn_cache_clear(self.h, eid), "usn_cache_clear")
+
+    # --- plumbing ---------------------------------------------------------------
+    def alloc(self, nbytes) -> DevBuf:
+        return DevBuf(self, nbytes)
+
+    def sync(self, stream=None):
+        if stream is None:
+            check(self.L.usn_device_sync(self.h), "usn_device_sync")
+        else:
+            check(self.L.usn_stream_sync(self.h, stream), "usn_stream_sync")
+
+    def stream(self):
+        s = C.c_void_p()
+        check(self.L.usn_stream_create(self.h, C.byref(s)), "usn_stream_create")
+        return s.value
+
+    def event(self):
+        e = C.c_void_p()
+        check(self.L.usn_event_create(self.h, C.byref(e)), "usn_event_create")
+        return e.value
+
+    def record(self, ev, stream):
+        check(self.L.usn_event_record(self.h, ev, stream), "usn_event_record")
+
+    def elapsed_ms(self, a, b) -> float:
+        ms = C.c_float()
+        check(self.L.usn_event_elapsed_ms(self.h, a, b, C.byref(ms)), "usn_event_elapsed_ms")
+        return ms.value
+
+    # --- hot path -----------------------------------------------------------------
+    def classify(self, batch: "DeviceBatch", result: "DeviceResult", stream=None):
+        check(self.L.usn_classify(self.h, C.byref(batch.desc), C.byref(result.desc), stream),
+              "usn_classify")
+
+    def finalize(self, batch: "DeviceBatch", result: "DeviceResult", stream=None) -> FinalizeInfo:
+        info = FinalizeInfo()
+        check(self.L.usn_finalize(self.h, C.byref(batch.desc), C.byref(result.desc), stream,
+                                  C.byref(info)), "usn_finalize")
+        return info
+
+
+class DeviceBatch:
+    """Frames + lengths resident in HBM (one drained rx ring)."""
+
+    def __init__(self, ctx: Ctx, frames: np.ndarray, lens: np.ndarray, src: int,
+                 stride: int = 0, offsets: np.ndarray | None = None, pad: int = USN_WINDOW):
+        frames = np.ascontiguousarray(frames, dtype=np.uint8).reshape(-1)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        self.n = int(lens.shape[0])
+        self.buf = ctx.alloc(frames.nbytes + pad)
+        self.buf.upload(frames)
+        self.lbuf = ctx.alloc(lens.nbytes)
+        self.lbuf.upload(lens)
+        self.obuf = None
+        self.desc = Batch()
+        self.desc.frames = self.buf.ptr
+        self.desc.lens = self.lbuf.ptr
+        self.desc.n = self.n
+        self.desc.src_endpoint = src
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            self.obuf = ctx.alloc(offsets.nbytes)
+            self.obuf.upload(offsets)
+            self.desc.offsets = self.obuf.ptr
+            self.desc.stride = 0
+        else:
+            self.desc.stride = stride
+
+    def set_src(self, src):
+        self.desc.src_endpoint = src
+
+    def free(self):
+        for b in (self.buf, self.lbuf, self.obuf):
+            if b is not None:
+                b.free()
+
+
+class DeviceResult:
+    def __init__(self, ctx: Ctx, n: int):
+        self.ctx = ctx
+        self.n = int(n)
+        nbytes = ctx.L.usn_result_bytes(self.n)
+        self.buf = ctx.alloc(nbytes)
+        self.desc = Result()
+        check(ctx.L.usn_result_bind(self.buf.ptr, nbytes, self.n, C.byref(self.desc)),
+              "usn_result_bind")
+        self.ntiles = (self.n + USN_TILE - 1) // USN_TILE
+
+    def _off(self, ptr):
+        return ptr - self.buf.ptr
+
+    def decisions(self, n=None) -> np.ndarray:
+        return self.buf.download(np.uint32, n or self.n, self._off(self.desc.decisions))
+
+    def order(self) -> np.ndarray:
+        return self.buf.download(np.uint16, self.ntiles * USN_TILE, self._off(self.desc.order))
+
+    def runs(self) -> np.ndarray:
+        return self.buf.download(np.uint32, self.ntiles * USN_TILE, self._off(self.desc.runs))
+
+    def tiles(self) -> np.ndarray:
+        raw = self.buf.download(np.uint8, self.ntiles * TILE_HDR_DTYPE.itemsize,
+                                self._off(self.desc.tiles))
+        return raw.view(TILE_HDR_DTYPE)
+
+    def summary(self) -> np.ndarray:
+        raw = self.buf.download(np.uint8, SUMMARY_DTYPE.itemsize, self._off(self.desc.summary))
+        return raw.view(SUMMARY_DTYPE)[0]
+
+    def free(self):
+        self.buf.free()
+
+
+def per_endpoint_lists(order: np.ndarray, runs: np.ndarray, tiles: np.ndarray, n: int):
+    """Expand the per-tile (order, runs) output into {bin: global frame indices}."""
+    out: dict[int, list] = {}
+    for t in range(tiles.shape[0]):
+        nr = int(tiles[t]["n_runs"])
+        nf = int(tiles[t]["n_frames"])
+        r = runs[t * USN_TILE:t * USN_TILE + nr]
+        starts = (r & 0xFFFF).astype(np.int64)
+        bins = (r >> 16).astype(np.int64)
+        ends = np.append(starts[1:], nf)
+        o = order[t * USN_TILE:t * USN_TILE + nf].astype(np.int64) + t * USN_TILE
+        for b, s, e in zip(bins, starts, ends):
+            out.setdefault(int(b), []).append(o[s:e])
+    return {b: np.concatenate(v) for b, v in out.items()}

@@ -1,0 +1,244 @@
+"""Synthetic workloads of the BASELINE.json configurations (numpy, vectorized).
+
+  c1  4-rule table (DEBUG_PORTS TCP:22 + 3 static pipes, eval/enp6s0f0config),
+      64 B UDP to 169.254.137.191:3333 (eval/Makefile:18); variants "fixed"
+      (pkt-gen: one 5-tuple) and "rand" (random source port)
+  c2  64 B IPv4/UDP, 16 listening rules, 90 % hit                (bench workload)
+  c3  IMIX 64/576/1500 B (7:4:1), TCP/UDP/ICMP 45/45/10, 1024 rules
+      (512 listening + 512 connected), 2048 B stride (netmap slots)
+  c4  IPv4 70 % / IPv6 10 % / ARP 10 % / 802.1Q 10 %, 4096 rules
+  c5  64 B, 65536 rules (16 IPs x 2048 listening ports + 32768 connected)
+
+Frames are generated directly into their HBM layout (fixed stride); every
+frame start has 64 readable bytes.  Data is synthetic (no captures).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+LOCAL = 0xA9FE89BF            # 169.254.137.191 (eval/Makefile:18)
+NICMAC = bytes.fromhex("001b214b508c")
+REMMAC = bytes.fromhex("001b214b508d")
+EP_NIC, EP_HOST, EP_PIPE = 0, 1, 2
+TCP, UDP, ICMP = 6, 17, 1
+
+
+@dataclasses.dataclass
+class Config:
+    name: str
+    n: int
+    frames: np.ndarray        # flat uint8, n * stride (+ 64 pad)
+    lens: np.ndarray          # uint16
+    stride: int
+    src: int                  # source endpoint (0 = the NIC: rx direction)
+    endpoints: list           # (id, kind, for_nic)
+    rules: list               # (want dict, owner, sticky)
+    bridge: list = dataclasses.field(default_factory=list)
+
+    def window(self, i):
+        return bytes(self.frames[i * self.stride:i * self.stride + int(self.lens[i])])
+
+
+def _want(dst, proto, dport=None, src=None, sport=None):
+    return {"dst": int(dst), "proto": int(proto), "dport": dport, "src": src, "sport": sport}
+
+
+def _u16be(H, col, v):
+    v = np.asarray(v, dtype=np.uint32)
+    H[:, col] = (v >> 8) & 0xFF
+    H[:, col + 1] = v & 0xFF
+
+
+def _u32be(H, col, v):
+    v = np.asarray(v, dtype=np.uint64)
+    for k in range(4):
+        H[:, col + k] = (v >> (24 - 8 * k)) & 0xFF
+
+
+def _layout(H, lens, stride, pad=64):
+    n = H.shape[0]
+    buf = np.zeros(n * stride + pad, dtype=np.uint8)
+    view = buf[:n * stride].reshape(n, stride)
+    view[:, :H.shape[1]] = H
+    return buf
+
+
+def build_ipv4(n, dst, src, proto, sport, dport, lens, ident=None, ff=0x4000, rng=None,
+               dmac=NICMAC, smac=REMMAC, hdr=64):
+    """IPv4 frames: header window (n, hdr) with TCP/UDP ports where proto has them."""
+    H = np.zeros((n, hdr), dtype=np.uint8)
+    H[:, 0:6] = np.frombuffer(dmac, np.uint8)
+    H[:, 6:12] = np.frombuffer(smac, np.uint8)
+    _u16be(H, 12, 0x0800)
+    H[:, 14] = 0x45
+    tl = np.asarray(lens, dtype=np.uint32) - 14
+    _u16be(H, 16, tl)
+    _u16be(H, 18, np.arange(n, dtype=np.uint32) & 0xFFFF if ident is None else ident)
+    _u16be(H, 20, ff)
+    H[:, 22] = 64
+    H[:, 23] = np.asarray(proto, dtype=np.uint8) if np.ndim(proto) else proto
+    _u32be(H, 26, src)
+    _u32be(H, 30, dst)
+    proto_a = np.broadcast_to(np.asarray(proto), (n,))
+    has = (proto_a == TCP) | (proto_a == UDP)
+    _u16be(H, 34, np.where(has, sport, 0x0800))          # ICMP: type 8 code 0
+    _u16be(H, 36, np.where(has, dport, 0))
+    is_udp = proto_a == UDP
+    _u16be(H, 38, np.where(is_udp, tl - 20, 0))
+    is_tcp = proto_a == TCP
+    H[:, 46] = np.where(is_tcp, 0x50, H[:, 46])
+    H[:, 47] = np.where(is_tcp, 0x10, H[:, 47])
+    return H
+
+
+def _base_endpoints(n_pipes):
+    eps = [(0, EP_NIC, None), (1, EP_HOST, 0)]
+    eps += [(2 + k, EP_PIPE, 0) for k in range(n_pipes)]
+    return eps
+
+
+def c1(n=1 << 16, variant="rand", seed=1):
+    rng = np.random.default_rng(seed)
+    rules = [(_want(LOCAL, TCP, 22), 1, True), (_want(LOCAL, UDP, 3333), 2, True),
+             (_want(LOCAL, UDP, 3334), 3, True), (_want(LOCAL, UDP, 3335), 4, True)]
+    sport = np.full(n, 1234, np.uint32) if variant == "fixed" else rng.integers(1024, 65536, n)
+    lens = np.full(n, 64, np.uint16)
+    src = np.full(n, 0xA9FE89BE, np.uint64)   # 169.254.137.190
+    H = build_ipv4(n, LOCAL, src, UDP, sport, 3333, lens,
+                   ident=np.zeros(n, np.uint32) if variant == "fixed" else None)
+    return Config("c1-" + variant, n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(3), rules)
+
+
+def c2(n=1 << 20, seed=2):
+    """1M x 64 B IPv4/UDP, 16 rules (UDP 3333..3348 -> pipes 2..17), 90 % hit."""
+    rng = np.random.default_rng(seed)
+    rules = [(_want(LOCAL, UDP, 3333 + k), 2 + k, False) for k in range(16)]
+    hit = rng.random(n) < 0.9
+    dport = np.where(hit, 3333 + rng.integers(0, 16, n), rng.integers(20000, 30000, n))
+    sport = rng.integers(1024, 65536, n)
+    src = (10 << 24) | rng.integers(0, 1 << 16, n).astype(np.uint64)
+    lens = np.full(n, 64, np.uint16)
+    H = build_ipv4(n, LOCAL, src, UDP, sport, dport, lens)
+    return Config("c2", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(16), rules)
+
+
+def _listen_conn_rules(rng, n_listen, n_conn, n_ips, n_ep, protos=(TCP, UDP), icmp=True):
+    ips = LOCAL - np.arange(n_ips, dtype=np.int64)
+    rules, listen, conn = [], [], []
+    seen = set()
+    if icmp:
+        for j in range(n_ips):
+            rules.append((_want(ips[j], ICMP), 2 + (j % n_ep), False))
+    k = 0
+    while len(listen) < n_listen:
+        ip = int(ips[k % n_ips])
+        proto = protos[(k // n_ips) % len(protos)]
+        port = 1000 + k // (n_ips * len(protos))
+        k += 1
+        key = (ip, proto, port)
+        if key in seen:
+            continue
+        seen.add(key)
+        listen.append(key)
+        rules.append((_want(ip, proto, port), 2 + int(rng.integers(0, n_ep)), False))
+    while len(conn) < n_conn:
+        ip = int(ips[rng.integers(0, n_ips)])
+        proto = protos[int(rng.integers(0, len(protos)))]
+        port = int(rng.integers(40000, 50000))
+        rsrc = (10 << 24) | int(rng.integers(0, 1 << 20))
+        rsport = int(rng.integers(1024, 65536))
+        key = (ip, proto, port, rsrc, rsport)
+        if key in seen:
+            continue
+        seen.add(key)
+        conn.append(key)
+        rules.append((_want(ip, proto, port, rsrc, rsport), 2 + int(rng.integers(0, n_ep)), False))
+    return ips, rules, listen, conn
+
+
+def _ipv4_mix(rng, n, ips, listen, conn, p_icmp, hit_rate=0.9):
+    """Per-frame (dst, src, proto, sport, dport) hitting listen/conn rules at hit_rate."""
+    listen = np.array(listen, dtype=np.int64).reshape(-1, 3)
+    conn = np.array(conn, dtype=np.int64).reshape(-1, 5)
+    kind = rng.random(n)
+    icmp = kind < p_icmp
+    hit = rng.random(n) < hit_rate
+    use_conn = rng.random(n) < (len(conn) / max(1, len(conn) + len(listen)))
+    li = rng.integers(0, max(1, len(listen)), n)
+    ci = rng.integers(0, max(1, len(conn)), n)
+    dst = np.where(use_conn, conn[ci, 0], listen[li, 0]).astype(np.uint64)
+    proto = np.where(use_conn, conn[ci, 1], listen[li, 1]).astype(np.uint32)
+    dport = np.where(use_conn, conn[ci, 2], listen[li, 2]).astype(np.uint32)
+    src = np.where(use_conn, conn[ci, 3], (10 << 24) | rng.integers(0, 1 << 20, n)).astype(np.uint64)
+    sport = np.where(use_conn, conn[ci, 4], rng.integers(1024, 65536, n)).astype(np.uint32)
+    miss = ~hit
+    dport = np.where(miss, rng.integers(20000, 30000, n), dport).astype(np.uint32)
+    proto = np.where(icmp, ICMP, proto).astype(np.uint32)
+    dst = np.where(icmp, ips[rng.integers(0, len(ips), n)], dst).astype(np.uint64)
+    return dst, src, proto, sport, dport
+
+
+def c3(n=1 << 18, seed=3, stride=2048):
+    rng = np.random.default_rng(seed)
+    ips, rules, listen, conn = _listen_conn_rules(rng, 504, 512, 8, 64)
+    dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.10)
+    sizes = rng.choice(np.array([64, 576, 1500]), size=n, p=[7 / 12, 4 / 12, 1 / 12])
+    lens = sizes.astype(np.uint16)
+    H = build_ipv4(n, dst, src, proto, sport, dport, lens)
+    return Config("c3", n, _layout(H, lens, stride), lens, stride, 0, _base_endpoints(64), rules)
+
+
+def c4(n=1 << 18, seed=4):
+    rng = np.random.default_rng(seed)
+    ips, rules, listen, conn = _listen_conn_rules(rng, 2048 - 32, 2048, 32, 256)
+    dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.1)
+    lens = np.full(n, 64, np.uint16)
+    H = build_ipv4(n, dst, src, proto, sport, dport, lens)
+    kind = rng.random(n)
+    v6 = (kind >= 0.70) & (kind < 0.80)
+    arp = (kind >= 0.80) & (kind < 0.90)
+    vlan = kind >= 0.90
+    H[v6, 12], H[v6, 13] = 0x86, 0xDD
+    H[v6, 14] = 0x60
+    H[arp, 12], H[arp, 13] = 0x08, 0x06
+    H[arp, 0:6] = 0xFF
+    # 802.1Q: tag then the IPv4 packet shifted by 4 bytes
+    if vlan.any():
+        inner = H[vlan, 12:60].copy()
+        H[vlan, 12], H[vlan, 13] = 0x81, 0x00
+        H[vlan, 14], H[vlan, 15] = 0x00, 0x05
+        H[vlan, 16:64] = inner
+    return Config("c4", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(256), rules)
+
+
+def c5(n=1 << 23, seed=5):
+    rng = np.random.default_rng(seed)
+    ips, rules, listen, conn = _listen_conn_rules(rng, 16 * 2048, 32768, 16, 1000, icmp=False)
+    dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.0)
+    lens = np.full(n, 64, np.uint16)
+    H = build_ipv4(n, dst, src, proto, sport, dport, lens)
+    return Config("c5", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(1000), rules)
+
+
+CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
+
+
+def config(name, n=None, seed=None, **kw):
+    f = CONFIGS[name]
+    if n is not None:
+        kw["n"] = n
+    if seed is not None:
+        kw["seed"] = seed
+    return f(**kw)
+
+
+def install_ctx(ctx, cfg: Config):
+    from .lib import make_want
+    for eid, kind, for_nic in cfg.endpoints:
+        ctx.endpoint_add(eid, kind, for_nic)
+    for w, owner, sticky in cfg.rules:
+        ctx.add_match(make_want(w["dst"], w["proto"], w["dport"], w["src"], w["sport"]), owner, sticky)
+    for m in cfg.bridge:
+        ctx.bridge_add(m)
