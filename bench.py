@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident usnetd match-path throughput on MI355X.
+
+Metric (BASELINE.json): Mpkts/s of device-resident L4 classification of 64 B
+frames, and the achieved HBM GB/s of the classify kernel against the gfx950
+peak.  One step = one usn_classify pass over one batch of the configuration
+the metric is quoted on (BASELINE.json configs[1] = "c2": 1M x 64 B IPv4/UDP
+frames, 16-rule endpoint table), frames already resident in HBM.  Batches
+rotate over --batches distinct buffers (> 256 MiB in total) so the Infinity
+Cache cannot serve them.  Multi-GPU: one process per GPU, each classifying its
+own batches with a replicated rule table ("replicas only", weak scaling; no
+collective on the data path -- gloo carries only the timing barrier/max).
+
+Usage: python bench.py [--gpus N --steps K --warmup W] (torchrun for N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ALGO_BYTES = 64 + 2 + 4 + 2   # header window + length + decision + order index per frame
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--frames", type=int, default=0, help="frames per batch (default: config's)")
+    ap.add_argument("--batches", type=int, default=5, help="distinct rotating batches")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch-probe", type=int, default=100, help="per-launch event pairs")
+    return ap.parse_args()
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from usnetd_amd import lib, traffic
+    L = lib.load()            # the HIP runtime is loaded here, before torch (if any)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        dist_mod.init_process_group("gloo")
+        dist = dist_mod
+
+    defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20}
+    n = args.frames or defaults[args.config]
+    ctx = lib.Ctx(local)
+    batches, results, cfg0 = [], [], None
+    for k in range(args.batches):
+        cfg = traffic.config(args.config, n=n, seed=1000 * rank + 17 * k + 2)
+        if k == 0:
+            cfg0 = cfg
+            traffic.install_ctx(ctx, cfg)
+        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride))
+        results.append(lib.DeviceResult(ctx, n))
+        if k:
+            del cfg
+    stream = ctx.stream()
+    classify = L.usn_classify
+    h = ctx.h
+    bdesc = [C.byref(b.desc) for b in batches]
+    rdesc = [C.byref(r.desc) for r in results]
+    nb = len(batches)
+
+    def step(i):
+        rc = classify(h, bdesc[i % nb], rdesc[i % nb], stream)
+        if rc:
+            lib.check(rc, "usn_classify")
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.sync(stream)
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    ev0, ev1 = ctx.event(), ctx.event()
+    t0 = time.perf_counter()
+    ctx.record(ev0, stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ctx.record(ev1, stream)
+    ctx.sync(stream)
+    ctx.sync()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    wall = t1 - t0
+    ev_ms = ctx.elapsed_ms(ev0, ev1)
+    elapsed = wall
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # every batch of the last rotation: the ordered host stage had nothing to do
+    host_frames, flags = 0, 0
+    for k in range(nb):
+        info = ctx.finalize(batches[k], results[k], stream)
+        host_frames += info.n_host
+        flags |= info.flags
+    cls = list(info.class_count)
+
+    # per-launch kernel duration (HIP events on the launch stream)
+    probe = []
+    evs = [(ctx.event(), ctx.event()) for _ in range(args.launch_probe)]
+    for i, (a, b) in enumerate(evs):
+        ctx.record(a, stream)
+        step(i)
+        ctx.record(b, stream)
+    ctx.sync(stream)
+    for a, b in evs:
+        probe.append(ctx.elapsed_ms(a, b))
+    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, args.steps)
+    achieved = ALGO_BYTES * n / (kern_ms * 1e-3) / 1e9
+
+    total_frames = world * args.steps * n
+    value = total_frames / elapsed / 1e6
+    out = {
+        "metric": "Mpkts/s device-resident L4 classify @64B frames; HBM GB/s vs roofline",
+        "value": round(value, 2),
+        "unit": "Mpkts/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic frames generated on the host (no captures), resident in HBM",
+        "config": {
+            "workload": "%s: %d x 64B IPv4/UDP frames per batch, %d-rule endpoint table, NIC rx"
+                        % (args.config, n, len(cfg0.rules)),
+            "frames_per_batch": n,
+            "rotating_batches": nb,
+            "rotating_bytes": int(nb * (n * cfg0.stride + n * 2)),
+            "parallelism": "replicas%d" % world,
+            "host_stage_frames": int(host_frames),
+            "summary_flags": int(flags),
+            "class_count_last_batch": cls,
+            "event_ms_per_step": round(ev_ms / args.steps, 5),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "classify_rx_kernel",
+            "kernel_us_median": round(kern_ms * 1e3, 3),
+            "algo_bytes_per_frame": ALGO_BYTES,
+        },
+        "cpu_baseline": None,
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                pm = json.load(fh)
+            if int(pm.get("frames_per_batch", -1)) == n:
+                out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+                out["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
+        except Exception:
+            pass
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    for b in batches:
+        b.free()
+    for r in results:
+        r.free()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, seconds):
+    """The sequential C oracle (restatement of the reference matcher, one
+    thread) timed on this host on the same batch, repeated for ~`seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle
+    coracle.build()
+    o = coracle.Oracle()
+    coracle.install_oracle(o, cfg)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(passes * cfg.n / el / 1e6, 3), "unit": "Mpkts/s", "cores": 1,
+            "kind": "port",
+            "sample": "%d passes over one %s batch (%d x 64B frames), sequential C restatement "
+                      "with the 1-entry cache, %.1f s" % (passes, cfg.name, cfg.n, el)}
+
+
+if __name__ == "__main__":
+    main()

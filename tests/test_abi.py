@@ -1,0 +1,51 @@
+"""CPU tests of the drop-in boundary: the library builds for gfx950, loads,
+and exports every entry point include/usn_classify.h declares (no GPU calls)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    src = open(os.path.join(ROOT, "include", "usn_classify.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(usn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_api():
+    names = declared()
+    for must in ("usn_ctx_create", "usn_classify", "usn_finalize", "usn_add_match",
+                 "usn_remove_match", "usn_result_bind", "usn_endpoint_add"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from usnetd_amd import lib
+    L = ctypes.CDLL(lib.LIB_PATH)
+    missing = [n for n in declared() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(declared()) <= set(lib.EXPORTED)
+    assert L.usn_abi_version() == 1
+
+
+def test_device_code_is_gfx950():
+    from usnetd_amd import lib
+    blob = open(lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob      # the embedded offload bundle
+    assert b"amdgcn-amd-amdhsa--gfx942" not in blob
+
+
+def test_result_layout():
+    from usnetd_amd import lib
+    L = lib.load()
+    n = 5000
+    nbytes = L.usn_result_bytes(n)
+    buf = ctypes.create_string_buffer(nbytes + 256)
+    base = (ctypes.addressof(buf) + 255) & ~255
+    r = lib.Result()
+    assert L.usn_result_bind(base, nbytes, n, ctypes.byref(r)) == 0
+    ptrs = [r.decisions, r.order, r.runs, r.tiles, r.summary, r.host_list]
+    assert ptrs == sorted(ptrs) and all(p % 256 == 0 for p in ptrs)
+    assert r.order - r.decisions >= 4 * n
+    assert L.usn_result_bind(base, nbytes - 1, n, ctypes.byref(r)) == -34
