@@ -36,3 +36,14 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean resources asm
+
+# A/B experiment builds (tools/abl.py): build/abl/<variant>/libusn.so,
+# one variant per line of tools/abl_variants.txt: "<name> <extra hipcc flags>"
+abl: build/usn_host.o
+	@while read -r name flags; do \
+	  case "$$name" in ''|'#'*) continue;; esac; \
+	  mkdir -p build/abl/$$name; echo "variant $$name: $$flags"; \
+	  $(HIPCC) $(HIPFLAGS) $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/usn_host.o || exit 1; \
+	done < tools/abl_variants.txt
+.PHONY: abl

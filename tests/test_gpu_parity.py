@@ -168,7 +168,8 @@ def test_offsets_layout(coracle_mod):
     offs = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64)
     buf = np.zeros(int(slot.sum()) + 64, np.uint8)
     for i in range(n):
-        buf[offs[i]:offs[i] + lens[i]] = cfg.frames[i * cfg.stride:i * cfg.stride + lens[i]]
+        o_, l_ = int(offs[i]), int(lens[i])
+        buf[o_:o_ + l_] = cfg.frames[i * cfg.stride:i * cfg.stride + l_]
     o = coracle_mod.Oracle()
     coracle_mod.install_oracle(o, cfg)
     want = o.forward_batch(0, buf, cfg.lens, offsets=offs)

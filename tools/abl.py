@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants in ONE process (cdna guide §5.4
+rule 24).  Each variant is a build of the same C ABI (make abl ->
+build/abl/<name>/libusn.so).  Prints per-variant median kernel time per
+launch (HIP events around each launch) and back-to-back time per step.
+
+usage: python tools/abl.py [--config c2] [--frames N] [--rounds 5] [--launches 100] [variants...]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from usnetd_amd import lib, traffic  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--batches", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=100)
+    ap.add_argument("--json", default="")
+    ap.add_argument("variants", nargs="*")
+    a = ap.parse_args()
+    names = a.variants or sorted(os.listdir(os.path.join(ROOT, "build", "abl")))
+    cfgs = [traffic.config(a.config, n=a.frames, seed=17 * k + 2) for k in range(a.batches)]
+    runs = {}
+    for nm in names:
+        path = os.path.join(ROOT, "build", "abl", nm, "libusn.so")
+        ctx = lib.Ctx(0, libpath=path)
+        traffic.install_ctx(ctx, cfgs[0])
+        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+        rs = [lib.DeviceResult(ctx, a.frames) for _ in cfgs]
+        s = ctx.stream()
+        evs = [(ctx.event(), ctx.event()) for _ in range(a.launches)]
+        e0, e1 = ctx.event(), ctx.event()
+        runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, evs=evs, e0=e0, e1=e1, per=[], b2b=[])
+    for rnd in range(a.rounds):
+        for nm in names:
+            R = runs[nm]
+            ctx, s = R["ctx"], R["s"]
+            L = ctx.L
+            bd = [C.byref(b.desc) for b in R["bs"]]
+            rd = [C.byref(r.desc) for r in R["rs"]]
+            for i in range(10):
+                L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+            for i, (x, y) in enumerate(R["evs"]):
+                ctx.record(x, s)
+                rc = L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+                assert rc == 0, rc
+                ctx.record(y, s)
+            ctx.sync(s)
+            R["per"] += [ctx.elapsed_ms(x, y) * 1e3 for x, y in R["evs"]]
+            ctx.record(R["e0"], s)
+            for i in range(a.launches):
+                L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+            ctx.record(R["e1"], s)
+            ctx.sync(s)
+            R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches)
+    ref = None
+    out = {}
+    for nm in names:
+        R = runs[nm]
+        d = R["rs"][0].decisions()
+        if ref is None:
+            ref = d
+        same = bool(((d ^ ref) & lib.PARITY_MASK).max() == 0) if d.shape == ref.shape else False
+        med = statistics.median(R["per"])
+        b2b = statistics.median(R["b2b"])
+        gbs = 72 * a.frames / (med * 1e-6) / 1e9
+        out[nm] = dict(kernel_us=round(med, 2), kernel_us_min=round(min(R["per"]), 2),
+                       step_us=round(b2b, 2), gbs=round(gbs, 1),
+                       mpps=round(a.frames / b2b, 1), same_as_first=same)
+        print("%-12s kernel %8.2f us (min %8.2f)  step %8.2f us  %7.1f GB/s  %9.1f Mpkt/s  same=%s"
+              % (nm, med, min(R["per"]), b2b, gbs, a.frames / b2b, same), flush=True)
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(dict(config=a.config, frames=a.frames, variants=out), fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Stops at the first fault / abort / timeout (exit >= 124); plain test
+# failures (exit 1) do not stop the later measurement steps.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "fatal rc=$rc in $name: stopping"; exit $rc
+  fi
+  return 0
+}
+for s in ${STEPS:-tests smoke bench prof}; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -rf ;;
+    testsall) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
+    abl) step abl 600 python tools/abl.py --json gpurun_out/abl.json ${ABL_ARGS:-} ;;
+    counters)
+      step listctr 120 rocprofv3 -L
+      i=0
+      for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+                 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+                 "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT" \
+                 "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS"; do
+        i=$((i+1))
+        step pmc$i 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 tools/kbench.py ${KB_ARGS:-c2 1048576 30}
+      done
+      step pmcsum 60 python3 tools/pmc_summary.py gpurun_out/pmc ;;
+    pmc) step pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --launch-probe 0 ;;
+    pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --launch-probe 0 ;;
+  esac
+done
+echo "=== done"

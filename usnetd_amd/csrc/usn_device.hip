@@ -35,10 +35,18 @@ namespace usn {
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
-/* streaming 16-byte load: frame headers are read once per batch */
+#ifndef USN_LOAD_NT
+#define USN_LOAD_NT 0
+#endif
+
+/* 16-byte header load (`nt` streaming hint only when USN_LOAD_NT) */
 __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
+#if USN_LOAD_NT
   const v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
 }
 
 __device__ __forceinline__ uint32_t be16lo(uint32_t v) {  // bytes [0,1] of v as big-endian u16
@@ -178,8 +186,9 @@ struct Lds {
   uint16_t *bstart;   // [nbins]: tile totals, then bin start slots
   uint16_t *order;    // [TILE]
   uint16_t *fbin;     // [TILE]: bin of each tile-local frame
-  uint32_t *scratch;  // [64]
+  uint32_t *scratch;  // [16]
   uint4 *table;       // staged rule table (optional)
+  uint4 *stage;       // dense layout: 4 KiB per wave for the header transpose
 };
 
 __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins) {
@@ -187,11 +196,13 @@ __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins) {
   size_t bst = (size_t)nbins * 2;
   size_t b = cnt + bst;
   b = (b + 15) & ~(size_t)15;
-  b += TILE * 2 + TILE * 2 + 64 * 4;
+  b += TILE * 2 + TILE * 2 + 16 * 4;
   return (b + 15) & ~(size_t)15;
 }
 
-__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins) {
+#define STAGE_BYTES ((NTHREADS / 64) * 4096)
+
+__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, bool dense = false) {
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
   L.bstart = L.cnt + (size_t)NSEG * nbins;
@@ -199,7 +210,8 @@ __device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins) {
   L.order = reinterpret_cast<uint16_t *>(smem + off);
   L.fbin = L.order + TILE;
   L.scratch = reinterpret_cast<uint32_t *>(L.fbin + TILE);
-  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
+  L.stage = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
+  L.table = L.stage + (dense ? (NTHREADS / 64) * 256 : 0);
   return L;
 }
 
@@ -339,39 +351,53 @@ __device__ uint32_t tile_emit(uint32_t tile, uint32_t nt, const Lds &L, uint16_t
 }
 
 /* --------------------------------------------------------------------------- */
-/* Carried-in decision cache for this batch (block 0, thread 0).               */
-__device__ void resolve_carry(const ClassifyArgs &a, uint32_t &state, uint32_t &dst,
-                              uint32_t info[4]) {
-  state = 0; dst = 0; info[0] = info[1] = info[2] = info[3] = 0;
+/* Carried-in decision cache for this batch, resolved by all threads of
+ * workgroup 0: the state after the last cache-touching frame of the previous
+ * batch (its tiles are scanned in parallel), or that batch's own carried-in
+ * state when none of its frames touched the cache.  out[0..5] in LDS. */
+__device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *scratch) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const bool chain = a.carry_mode == CARRY_CHAIN && !(a.prev_summary->flags & USN_S_COUT);
+  uint32_t best = 0;   // 1 + index of the last previous tile with a touching frame
+  if (chain) {
+    for (uint32_t t = tid; t < a.prev_ntiles; t += NTHREADS)
+      if (a.prev_tiles[t].last_state & USN_TS_HAS) best = t + 1;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) best = max(best, (uint32_t)__shfl_xor(best, d, 64));
+    if (tid == 0) scratch[8] = 0;
+    __syncthreads();
+    if (lane == 0 && best) atomicMax(&scratch[8], best);
+    __syncthreads();
+    best = scratch[8];
+  }
+  if (tid != 0) return;
+  uint32_t st = 0, dst = 0, info[4] = {0, 0, 0, 0};
   if (a.carry_mode == CARRY_EXPLICIT) {
-    state = a.cin_state; dst = a.cin_dst;
+    st = a.cin_state; dst = a.cin_dst;
     for (int k = 0; k < 4; ++k) info[k] = a.cin_info[k];
-    return;
-  }
-  if (a.carry_mode != CARRY_CHAIN) return;
-  const usn_summary *ps = a.prev_summary;
-  if (ps->flags & USN_S_COUT) {
-    state = ps->cout_state; dst = ps->cout_dst;
-    for (int k = 0; k < 4; ++k) info[k] = ps->cout_info[k];
-    return;
-  }
-  for (int t = (int)a.prev_ntiles - 1; t >= 0; --t) {
-    const usn_tile_hdr &h = a.prev_tiles[t];
-    if (h.last_state & USN_TS_HAS) {
+  } else if (a.carry_mode == CARRY_CHAIN) {
+    const usn_summary *ps = a.prev_summary;
+    if (!chain) {                                   // finalize wrote the authoritative state
+      st = ps->cout_state; dst = ps->cout_dst;
+      for (int k = 0; k < 4; ++k) info[k] = ps->cout_info[k];
+    } else if (best) {
+      const usn_tile_hdr &h = a.prev_tiles[best - 1];
       if ((h.last_state & USN_TS_RETAINED) && !(h.last_state & USN_TS_UNKNOWN)) {
-        state = USN_CS_VALID; dst = h.last_dst;
+        st = USN_CS_VALID; dst = h.last_dst;
         for (int k = 0; k < 4; ++k) info[k] = h.last_info[k];
       }
-      return;
+    } else {
+      st = ps->cin_state; dst = ps->cin_dst;
+      for (int k = 0; k < 4; ++k) info[k] = ps->cin_info[k];
     }
   }
-  state = ps->cin_state; dst = ps->cin_dst;
-  for (int k = 0; k < 4; ++k) info[k] = ps->cin_info[k];
+  out[0] = st; out[1] = dst;
+  for (int k = 0; k < 4; ++k) out[2 + k] = info[k];
 }
 
 /* Decision for a carried PacketInfo X under the current table (rx). */
 template <bool LDS>
-__device__ uint32_t decide_info_rx(const uint4 *T, uint32_t bmask, const uint32_t info[4],
+__device__ uint32_t decide_info_rx(const uint4 *T, uint32_t bmask, const uint32_t *info,
                                    uint32_t src) {
   Parsed p;
   p.status = 1; p.i0 = info[0]; p.src = info[1]; p.dst = info[2]; p.ports = info[3];
@@ -381,10 +407,17 @@ __device__ uint32_t decide_info_rx(const uint4 *T, uint32_t bmask, const uint32_
 }
 
 /* --------------------------------------------------------------------------- */
-template <bool LDS>
+/* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
+ * XOR with (f >> 2) & 3 makes both the linear writes and the per-frame reads
+ * of ds_*_b128 bank-conflict free. */
+__device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
+  return 4 * f + (j ^ ((f >> 2) & 3u));
+}
+
+template <bool LDS, bool DENSE>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
-  const Lds L = carve(smem, a.nbins);
+  const Lds L = carve(smem, a.nbins, DENSE);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
@@ -399,9 +432,21 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     const uint32_t local = r * NTHREADS + tid;
     const uint64_t i = base + (local < nt ? local : 0);
     fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-    const uint4 *w = reinterpret_cast<const uint4 *>(fp[r]);
+    if (DENSE) {
+      // 64 contiguous 64-byte frames per wave and round: 4 fully coalesced
+      // 1 KiB wave loads; frame lane/4 + 16k arrives in lane (4 lanes each)
+      const uint64_t f0 = base + r * NTHREADS + wave * 64;
+      const uint4 *chunk = reinterpret_cast<const uint4 *>(a.frames + f0 * 64);
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) q[r][k] = ld_stream(w + k);
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t f = f0 + 16 * k + (lane >> 2);
+        q[r][k] = f < a.n ? ld_stream(chunk + 64 * k + lane) : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      const uint4 *w = reinterpret_cast<const uint4 *>(fp[r]);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) q[r][k] = ld_stream(w + k);
+    }
     len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
   }
 
@@ -416,21 +461,19 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   // ---- carried-in cache (block 0): stale check against the current table
   __shared__ uint32_t s_carry[8];
   if (tile == 0) {
+    resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
-      uint32_t st, dst, info[4];
-      resolve_carry(a, st, dst, info);
+      const uint32_t st = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
       if (st & USN_CS_VALID) {
-        const uint32_t now = decide_info_rx<LDS>(T, a.bucket_mask, info, a.src);
+        const uint32_t now = decide_info_rx<LDS>(T, a.bucket_mask, s_carry + 2, a.src);
         if ((now & USN_PARITY_MASK) != (dst & USN_PARITY_MASK)) flags |= USN_S_STALE;
       }
-      s_carry[0] = st; s_carry[1] = dst;
-      for (int k = 0; k < 4; ++k) s_carry[2 + k] = info[k];
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
       usn_summary *S = a.summary;
       S->cin_state = st; S->cin_dst = dst;
-      for (int k = 0; k < 4; ++k) S->cin_info[k] = info[k];
+      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
       S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
     }
     __syncthreads();
@@ -440,6 +483,20 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   uint32_t dec[ROUNDS], bins[ROUNDS], touch[ROUNDS], inf[ROUNDS][4];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
+    if (DENSE) {   // wave-private transpose through LDS: lane <- its own frame
+      uint4 *st = L.stage + wave * 256;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) st[stage_slot(16 * k + (lane >> 2), lane & 3)] = q[r][k];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) q[r][k] = st[stage_slot(lane, k)];
+    }
+#if USN_ABL_LOADONLY
+    const uint32_t x = q[r][0].x ^ q[r][1].y ^ q[r][2].z ^ q[r][3].w ^ len[r];
+    dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, x & 0xFFFF);
+    touch[r] = 0;
+    inf[r][0] = inf[r][1] = inf[r][2] = inf[r][3] = 0;
+    continue;
+#endif
     Parsed p;
     parse(q[r], len[r], fp[r], p);
     dec[r] = decide_rx<LDS>(T, a.bucket_mask, p, a.src);
@@ -534,8 +591,12 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   }
 
   // ---- stable per-endpoint order of the tile
+#if USN_ABL_NOSORT || USN_ABL_LOADONLY
+  const uint32_t n_runs = 0;
+#else
   tile_sort(bins, nt, a.nbins, L);
   const uint32_t n_runs = tile_emit(tile, nt, L, a.order, a.runs);
+#endif
 
   // ---- tile header
   const uint32_t lastp = s_last;
@@ -608,21 +669,28 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
 
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots) {
   return (size_t)table_slots * 16 <= LDS_TABLE_MAX_BYTES &&
-         lds_core_bytes(nbins) + (size_t)table_slots * 16 <= 64u * 1024u;
+         lds_core_bytes(nbins) + STAGE_BYTES + (size_t)table_slots * 16 <= 64u * 1024u;
 }
 
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds) {
-  return lds_core_bytes(nbins) + (table_in_lds ? (size_t)table_slots * 16 : 0);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense) {
+  return lds_core_bytes(nbins) + (dense ? STAGE_BYTES : 0) +
+         (table_in_lds ? (size_t)table_slots * 16 : 0);
 }
+
+#ifndef USN_DENSE
+#define USN_DENSE 1
+#endif
 
 hipError_t launch_classify(const ClassifyArgs &a, hipStream_t stream) {
   if (a.ntiles == 0) return hipSuccess;
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
-  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds);
-  if (in_lds)
-    hipLaunchKernelGGL(classify_rx_kernel<true>, dim3(a.ntiles), dim3(NTHREADS), lds, stream, a);
-  else
-    hipLaunchKernelGGL(classify_rx_kernel<false>, dim3(a.ntiles), dim3(NTHREADS), lds, stream, a);
+  const bool dense = USN_DENSE && a.stride == 64 && a.offsets == nullptr;
+  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, dense);
+  const dim3 g(a.ntiles), b(NTHREADS);
+  if (in_lds && dense) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, a);
+  else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, a);
+  else if (dense) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, a);
+  else hipLaunchKernelGGL((classify_rx_kernel<false, false>), g, b, lds, stream, a);
   return hipGetLastError();
 }
 

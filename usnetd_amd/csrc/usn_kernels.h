@@ -52,7 +52,7 @@ struct ClassifyArgs {
 };
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense);
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
 
 hipError_t launch_classify(const ClassifyArgs &a, hipStream_t stream);

@@ -64,18 +64,19 @@ SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames",
                           ("cout_info", "<u4", (4,))])
 assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 64
 
-_lib = None
+_libs: dict = {}
 
 
-def load():
-    """Load libusn.so (raises if it was not built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(path: str | None = None):
+    """Load libusn.so (raises if it was not built).  `path` selects another
+    build of the same ABI (A/B experiments in tools/)."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise UsnError("%s is missing: run `make` (or __graft_entry__.build()) first; "
-                       "the match path has no CPU fallback" % LIB_PATH)
-    L = C.CDLL(LIB_PATH)
+                       "the match path has no CPU fallback" % path)
+    L = C.CDLL(path)
     P, I, U16, U32, U64, SZ = C.c_void_p, C.c_int, C.c_uint16, C.c_uint32, C.c_uint64, C.c_size_t
     sig = {
         "usn_abi_version": ([], I), "usn_strerror": ([I], C.c_char_p),
@@ -107,7 +108,7 @@ def load():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -124,7 +125,7 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
 
 def check(rc, what=""):
     if rc < 0:
-        L = load()
+        L = load() if LIB_PATH in _libs or not _libs else next(iter(_libs.values()))
         extra = ""
         if rc == -5:
             extra = " (hipError %d)" % L.usn_last_hip_error()
@@ -197,8 +198,8 @@ class DevBuf:
 class Ctx:
     """One usn_ctx bound to one gfx950 device (the daemon's match state)."""
 
-    def __init__(self, device: int = 0):
-        self.L = load()
+    def __init__(self, device: int = 0, libpath: str | None = None):
+        self.L = load(libpath)
         h = C.c_void_p()
         check(self.L.usn_ctx_create(device, C.byref(h)), "usn_ctx_create")
         self.h = h.value
