@@ -3,19 +3,22 @@
  *
  * classify: one workgroup (256 threads, 4 waves) per tile of USN_TILE = 1024
  * frames, one frame per lane per round, four rounds.  Per frame:
- *   1. four 16-byte loads of the 64-byte header window + the 2-byte length
- *      (all 16 loads of a lane issued before any is consumed);
- *   2. extract_pkt_info in registers           /root/reference/src/pkt.rs:158-218
- *   3. get_endpoint: two exact-match probes     /root/reference/src/endpoint.rs:307-338
- *      into the bucketed rule table (LDS copy when it fits, else L2-resident);
- *   4. the per-frame decision of find_forward   /root/reference/src/endpoint.rs:172-296
- *      for a NIC source (incoming): FLOOD / loopback DROP / lookup / DHCP flag;
- *   5. stable per-endpoint order of the tile: wave ballots give each frame its
- *      rank inside its 64-frame segment and per-segment bin counts; a column
- *      scan over the 16 segments and a block scan over bins turn them into
- *      slots; the sorted tile-local indices and the bin runs are written with
+ *   1. the 64-byte header window + the 2-byte length; for the dense layout
+ *      (64-byte stride) four fully coalesced 1 KiB wave loads per round and a
+ *      wave-private transpose through LDS; every load of a lane is issued
+ *      before any is consumed;
+ *   2. extract_pkt_info in registers, branch-free    /root/reference/src/pkt.rs:158-218
+ *   3. get_endpoint: exact-match probes of the bucketed rule table (LDS copy
+ *      when it fits, else L2-resident), only for key shapes the table holds
+ *                                                      /root/reference/src/endpoint.rs:307-338
+ *   4. the decision of find_forward for a NIC source    /root/reference/src/endpoint.rs:172-296
+ *   5. stable per-endpoint order of the tile: bit-sliced wave ballots give
+ *      every frame the mask of lanes holding the same bin (no data-dependent
+ *      loop), hence its rank in its 64-frame segment and per-segment counts;
+ *      a column scan over the 16 segments and one block scan over bins give
+ *      the slots and the bin runs; sorted tile-local indices are written with
  *      coalesced stores.
- * No MFMA: this is byte parsing and hash probing, bounded by HBM reads.
+ * No MFMA: byte parsing and hash probing, bounded by HBM reads.
  *
  * Order-dependent state (fragment map, DHCP next endpoint, a stale carried
  * cache entry) never changes a decision silently: frames that need it carry
@@ -32,6 +35,7 @@ namespace usn {
 #define NTHREADS 256
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
+#define MAX_NBITS 10   /* nbins <= 1024 */
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
@@ -60,123 +64,110 @@ struct Parsed {
 };
 
 /* extract_pkt_info (pkt.rs:158-218) with smoltcp 0.7.0's EthernetFrame /
- * Ipv4Packet::new_checked length rules.  q = 64-byte window, little-endian
- * words; every field offset is a compile-time constant except the L4 ports. */
+ * Ipv4Packet::new_checked length rules, computed for every lane with selects
+ * (no divergent early exits).  q = 64-byte window as little-endian words. */
 __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint8_t *frame,
                                       Parsed &p) {
-  p.status = 0; p.i0 = 0; p.src = 0; p.dst = 0; p.ports = 0;
-  p.sport = 0; p.dport = 0; p.proto = 0; p.has_ports = 0; p.frag_first = 0;
-  if (len < 14) return;                                    // EthernetFrame::new_checked
-  const uint32_t w3 = q[0].w;
-  const uint32_t et = be16lo(w3);                          // bytes 12..13
-  if (et == 0x0806u) { p.status = 2; p.i0 = USN_INFO_ARP; return; }     // pkt.rs:167
-  if (et == 0x888Eu) { p.status = 3; p.i0 = USN_INFO_EAPOL; return; }   // pkt.rs:206-213
-  if (et != 0x0800u) return;                               // IPv6, 802.1Q, ...: None
-  const uint32_t n = len - 14;
-  if (n < 20) return;                                      // Ipv4Packet::check_len
-  const uint32_t ihl = (w3 >> 16) & 0xFu;                  // byte 14
-  const uint32_t hl = ihl * 4;
-  const uint32_t w4 = q[1].x, w5 = q[1].y, w6 = q[1].z, w7 = q[1].w;
+  const uint32_t w3 = q[0].w, w4 = q[1].x, w5 = q[1].y, w6 = q[1].z, w7 = q[1].w;
   const uint32_t w8 = q[2].x, w9 = q[2].y;
-  const uint32_t tl = be16lo(w4);                          // bytes 16..17
-  if (n < hl || hl > tl || n < tl) return;
-  const uint32_t ff = be16lo(w5);                          // bytes 20..21
-  p.proto = w5 >> 24;                                      // byte 23
-  p.src = __builtin_bswap32(__builtin_amdgcn_alignbyte(w7, w6, 2));   // bytes 26..29
-  p.dst = __builtin_bswap32(__builtin_amdgcn_alignbyte(w8, w7, 2));   // bytes 30..33
-  if (ff & 0x1FFFu) { p.status = 4; return; }              // frag_offset() > 0: pkt.rs:172
-  const uint32_t pr = p.proto;
-  const bool port_proto = pr == 6u || pr == 17u || pr == 0x21u || pr == 0x84u || pr == 0x88u;
-  p.has_ports = (port_proto && (tl - hl) > 4u) ? 1u : 0u;  // pkt.rs:128-133, 179
-  if (p.has_ports) {
-    uint32_t a, b;
-    if (ihl == 5u) {
-      a = w8; b = w9;                                      // ports at bytes 34..37
-    } else {                                               // ports at 14+hl: reload (rare)
-      a = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
-      b = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
-    }
-    p.sport = be16lo(a >> 16);
-    p.dport = be16lo(b);
-    p.ports = p.sport | (p.dport << 16);
+  const uint32_t et = be16lo(w3);                                    // bytes 12..13
+  const uint32_t ihl = (w3 >> 16) & 0xFu, hl = ihl * 4;              // byte 14
+  const uint32_t tl = be16lo(w4);                                    // bytes 16..17
+  const uint32_t ff = be16lo(w5);                                    // bytes 20..21
+  const uint32_t pr = w5 >> 24;                                      // byte 23
+  const uint32_t n = len - 14;                                       // valid when len >= 14
+  const bool eth = len >= 14;                                        // EthernetFrame::new_checked
+  const bool ip = eth && et == 0x0800u && len >= 34 &&               // Ipv4Packet::check_len
+                  n >= hl && hl <= tl && n >= tl;
+  const bool later = ip && (ff & 0x1FFFu) != 0;                      // frag_offset() > 0
+  const bool pp = pr == 6u || pr == 17u || pr == 0x21u || pr == 0x84u || pr == 0x88u;
+  const bool has = ip && !later && pp && (tl - hl) > 4u;             // pkt.rs:128-133, 179
+  uint32_t a = w8, b = w9;                                           // ports at bytes 34..37
+  if (has && ihl != 5u) {                                            // ports at 14+hl (rare)
+    a = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
+    b = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
   }
-  p.i0 = USN_INFO_IPV4 | (pr << 8) | (p.has_ports << 16);
-  p.frag_first = (!(ff & 0x4000u) && (ff & 0x2000u)) ? 1u : 0u;   // pkt.rs:198
-  p.status = 1;
+  p.sport = has ? be16lo(a >> 16) : 0u;
+  p.dport = has ? be16lo(b) : 0u;
+  p.ports = p.sport | (p.dport << 16);
+  p.has_ports = has ? 1u : 0u;
+  p.proto = pr;
+  p.src = __builtin_bswap32(__builtin_amdgcn_alignbyte(w7, w6, 2));  // bytes 26..29
+  p.dst = __builtin_bswap32(__builtin_amdgcn_alignbyte(w8, w7, 2));  // bytes 30..33
+  p.frag_first = (!(ff & 0x4000u) && (ff & 0x2000u)) ? 1u : 0u;      // pkt.rs:198
+  const bool arp = eth && et == 0x0806u, eapol = eth && et == 0x888Eu;
+  p.status = arp ? 2u : eapol ? 3u : !ip ? 0u : later ? 4u : 1u;
+  p.i0 = arp ? USN_INFO_ARP : eapol ? USN_INFO_EAPOL
+       : (p.status == 1u ? (USN_INFO_IPV4 | (pr << 8) | (p.has_ports << 16)) : 0u);
 }
 
-/* One exact-match probe.  Returns the slot's meta word (0 = miss). */
-template <bool LDS>
+__device__ __forceinline__ bool slot_is(const uint4 &t, uint32_t x, uint32_t y, uint32_t z,
+                                        uint32_t meta) {
+  return ((t.x ^ x) | (t.y ^ y) | (t.z ^ z) | ((t.w ^ meta) & USN_KEY_META_MASK)) == 0u;
+}
+
+/* One exact-match probe: the home bucket (one 64-byte line) is checked with
+ * selects; the chain is followed only when that bucket is full and holds no
+ * match (rare at load <= 1/2).  Returns the slot's meta word, 0 = miss. */
 __device__ __forceinline__ uint32_t probe(const uint4 *T, uint32_t bmask, uint32_t x, uint32_t y,
                                           uint32_t z, uint32_t meta) {
   uint32_t b = usn_key_hash(x, y, z, meta) & bmask;
-  for (uint32_t it = 0; it <= bmask; ++it) {
-    const uint4 *s = T + b * 4;
-    const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-    if (s0.x == x && s0.y == y && s0.z == z && (s0.w & USN_KEY_META_MASK) == meta) return s0.w;
-    if (s1.x == x && s1.y == y && s1.z == z && (s1.w & USN_KEY_META_MASK) == meta) return s1.w;
-    if (s2.x == x && s2.y == y && s2.z == z && (s2.w & USN_KEY_META_MASK) == meta) return s2.w;
-    if (s3.x == x && s3.y == y && s3.z == z && (s3.w & USN_KEY_META_MASK) == meta) return s3.w;
-    if (!(s3.w & USN_SLOT_VALID)) return 0;                // bucket not full: chain ends
-    b = (b + 1) & bmask;
+  const uint4 *s = T + b * 4;
+  uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+  uint32_t hit = slot_is(s0, x, y, z, meta) ? s0.w : slot_is(s1, x, y, z, meta) ? s1.w
+               : slot_is(s2, x, y, z, meta) ? s2.w : slot_is(s3, x, y, z, meta) ? s3.w : 0u;
+  if (!hit && (s3.w & USN_SLOT_VALID)) {
+    for (uint32_t it = 0; it < bmask; ++it) {
+      b = (b + 1) & bmask;
+      s = T + b * 4;
+      s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
+      hit = slot_is(s0, x, y, z, meta) ? s0.w : slot_is(s1, x, y, z, meta) ? s1.w
+          : slot_is(s2, x, y, z, meta) ? s2.w : slot_is(s3, x, y, z, meta) ? s3.w : 0u;
+      if (hit || !(s3.w & USN_SLOT_VALID)) break;
+    }
   }
-  return 0;
+  return hit;
 }
 
-/* get_endpoint (endpoint.rs:307-338): key1 = to_match_want_with_src(true),
- * key2 = ..(false) only on a key1 miss; a hit on a NIC-owned rule or on the
- * source itself yields None with no retry.  Returns owner, or -1 with *excl. */
-template <bool LDS>
-__device__ __forceinline__ int get_endpoint(const uint4 *T, uint32_t bmask, const Parsed &p,
-                                            uint32_t src, bool &excl) {
-  const uint32_t pres1 = p.has_ports ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT) : USN_WANT_SRC;
-  const uint32_t z1 = p.has_ports ? (p.dport | (p.sport << 16)) : 0u;
-  uint32_t w = probe<LDS>(T, bmask, p.dst, p.src, z1, usn_key_meta(p.proto, pres1));
-  if (!w) {
-    const uint32_t pres2 = p.has_ports ? USN_WANT_DPORT : 0u;
-    const uint32_t z2 = p.has_ports ? p.dport : 0u;
-    w = probe<LDS>(T, bmask, p.dst, 0u, z2, usn_key_meta(p.proto, pres2));
-  }
-  excl = false;
-  if (!w) return -1;
+/* find_forward for a NIC source (incoming == true), cache handled outside:
+ * ARP/EAPOL -> FLOOD, loopback -> DROP, else get_endpoint (endpoint.rs:307-338:
+ * key1 = with src, key2 = without, only on a key1 miss; a hit on a NIC-owned
+ * rule or on the source itself is None with no retry), else DHCP / DROP. */
+__device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs &a,
+                                              const Parsed &p) {
+  const bool has = p.has_ports != 0;
+  uint32_t w1 = 0, w2 = 0;
+  if (a.probe_mask & 1u)
+    w1 = probe(T, a.bucket_mask, p.dst, p.src, has ? (p.dport | (p.sport << 16)) : 0u,
+               usn_key_meta(p.proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT)
+                                         : USN_WANT_SRC));
+  if (a.probe_mask & 2u)
+    w2 = probe(T, a.bucket_mask, p.dst, 0u, has ? p.dport : 0u,
+               usn_key_meta(p.proto, has ? USN_WANT_DPORT : 0u));
+  const uint32_t w = w1 ? w1 : w2;
   const uint32_t owner = w >> 16;
-  if ((w & USN_SLOT_NICOWNER) || owner == src) { excl = true; return -1; }
-  return (int)owner;
-}
-
-/* find_forward for a NIC source (incoming == true), cache handled outside. */
-template <bool LDS>
-__device__ __forceinline__ uint32_t decide_rx(const uint4 *T, uint32_t bmask, const Parsed &p,
-                                              uint32_t src) {
-  switch (p.status) {
-    case 0: return usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
-    case 4: return usn_mkdec(USN_CLS_DROP, USN_R_FRAGMISS, 0xFFFFu) | USN_F_FRAGN | USN_F_HOST;
-    case 2:
-    case 3: return usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);    // endpoint.rs:199-204
-    default: break;
-  }
-  if ((p.dst >> 24) == 127u) return usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
-  bool excl;
-  const int e = get_endpoint<LDS>(T, bmask, p, src, excl);
-  uint32_t d;
-  if (e >= 0) {
-    d = usn_mkdec(USN_CLS_EP, USN_R_NONE, (uint32_t)e);
-  } else if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) {
-    // is_dhcp_answer with no rule: next_dhcp_endpoint.take() is ordered state
-    d = usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) | USN_F_DHCP | USN_F_HOST;
-  } else {
-    d = usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
-  }
-  if (p.frag_first) d |= USN_F_FRAG1 | USN_F_HOST;
+  const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
+  const bool dhcp = p.proto == 17u && has && p.sport == 67u && p.dport == 68u;
+  const uint32_t d_look =
+      (w && !excl) ? usn_mkdec(USN_CLS_EP, USN_R_NONE, owner)
+      : dhcp ? (usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) | USN_F_DHCP | USN_F_HOST)
+             : usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
+  uint32_t d =
+      p.status == 0u ? usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu)
+      : p.status == 4u ? (usn_mkdec(USN_CLS_DROP, USN_R_FRAGMISS, 0xFFFFu) | USN_F_FRAGN | USN_F_HOST)
+      : p.status != 1u ? usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu)            // ARP/EAPOL
+      : (p.dst >> 24) == 127u ? usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu)   // :205-208
+                              : d_look;
+  // a first fragment is remembered by extract_pkt_info before any decision
+  if (p.status == 1u && p.frag_first) d |= USN_F_FRAG1 | USN_F_HOST;
   return d;
 }
 
 __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
   const uint32_t c = USN_DEC_CLASS(d);
-  if (c == USN_CLS_EP) return USN_DEC_EP(d);
-  if (c == USN_CLS_NIC) return USN_BIN_NIC(n_ep);
-  if (c == USN_CLS_FLOOD) return USN_BIN_FLOOD(n_ep);
-  return USN_BIN_DROP(n_ep);
+  return c == USN_CLS_EP ? USN_DEC_EP(d)
+       : c == USN_CLS_NIC ? USN_BIN_NIC(n_ep)
+       : c == USN_CLS_FLOOD ? USN_BIN_FLOOD(n_ep) : USN_BIN_DROP(n_ep);
 }
 
 /* --------------------------------------------------------------------------- */
@@ -185,18 +176,15 @@ struct Lds {
   uint16_t *cnt;      // [NSEG][nbins]: per-segment counts, then segment prefixes
   uint16_t *bstart;   // [nbins]: tile totals, then bin start slots
   uint16_t *order;    // [TILE]
-  uint16_t *fbin;     // [TILE]: bin of each tile-local frame
   uint32_t *scratch;  // [16]
-  uint4 *table;       // staged rule table (optional)
   uint4 *stage;       // dense layout: 4 KiB per wave for the header transpose
+  uint4 *table;       // staged rule table (optional)
 };
 
 __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins) {
-  size_t cnt = (size_t)NSEG * nbins * 2;
-  size_t bst = (size_t)nbins * 2;
-  size_t b = cnt + bst;
+  size_t b = (size_t)NSEG * nbins * 2 + (size_t)nbins * 2;
   b = (b + 15) & ~(size_t)15;
-  b += TILE * 2 + TILE * 2 + 16 * 4;
+  b += TILE * 2 + 16 * 4;
   return (b + 15) & ~(size_t)15;
 }
 
@@ -206,10 +194,9 @@ __device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, bool dense =
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
   L.bstart = L.cnt + (size_t)NSEG * nbins;
-  size_t off = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
+  const size_t off = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
   L.order = reinterpret_cast<uint16_t *>(smem + off);
-  L.fbin = L.order + TILE;
-  L.scratch = reinterpret_cast<uint32_t *>(L.fbin + TILE);
+  L.scratch = reinterpret_cast<uint32_t *>(L.order + TILE);
   L.stage = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
   L.table = L.stage + (dense ? (NTHREADS / 64) * 256 : 0);
   return L;
@@ -249,35 +236,49 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
   return base + inc - v;
 }
 
-/* Stable counting sort of the tile by bin.  bins[r] is the bin of tile-local
- * frame r*256 + tid (valid when < nt).  Leaves L.order sorted, L.fbin filled. */
-__device__ void tile_sort(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbins, const Lds &L) {
+/* Mask of the lanes of this wave whose bin equals this lane's bin: one
+ * ballot per bin bit (bit-sliced match), restricted to `valid`. */
+__device__ __forceinline__ uint64_t match_bin(uint32_t b, uint64_t valid, uint32_t nbits) {
+  uint64_t same = valid;
+#pragma unroll
+  for (uint32_t k = 0; k < MAX_NBITS; ++k) {
+    if (k < nbits) {
+      const bool bit = (b >> k) & 1u;
+      const uint64_t bal = __ballot(bit);
+      same &= bit ? bal : ~bal;
+    }
+  }
+  return same;
+}
+
+/* Stable counting sort of the tile by bin, written out as the tile's order
+ * (tile-local indices) and bin runs.  bins[r] belongs to tile-local frame
+ * r*256 + tid (valid when < nt).  L.cnt must be zero on entry.  Returns the
+ * number of runs; cls[1..3] receive this thread's share of the NIC, FLOOD and
+ * DROP bin totals. */
+__device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbins,
+                               uint32_t nbits, uint32_t n_ep, const Lds &L, uint32_t tile,
+                               uint16_t *order_out, uint32_t *runs_out, uint32_t cls[4]) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (uint32_t i = tid; i < NSEG * nbins; i += NTHREADS) L.cnt[i] = 0;
-  __syncthreads();
   uint32_t rank[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    const bool valid = local < nt;
-    const uint32_t s = r * (NTHREADS / 64) + wave;        // 64-frame segment, index order
-    const uint32_t b = bins[r];
-    uint64_t remaining = __ballot(valid);
-    rank[r] = 0;
-    while (remaining) {                                    // one pass per distinct bin
-      const uint32_t leader = (uint32_t)__builtin_ctzll(remaining);
-      const uint32_t lb = __builtin_amdgcn_readlane(b, leader);
-      const bool mine = valid && b == lb;
-      const uint64_t m = __ballot(mine);
-      if (mine) rank[r] = (uint32_t)__popcll(m & lanemask_lt(lane));
-      if (lane == leader) L.cnt[s * nbins + lb] = (uint16_t)__popcll(m);
-      remaining &= ~m;
-    }
-    if (valid) L.fbin[local] = (uint16_t)b;
+    const uint32_t s = r * (NTHREADS / 64) + wave;         // 64-frame segment, index order
+    const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
+    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+    if (local < nt && rank[r] == 0) L.cnt[s * nbins + bins[r]] = (uint16_t)__popcll(same);
   }
   __syncthreads();
-  // column scan over segments: cnt[s][b] := frames of bin b in segments < s
-  for (uint32_t b = tid; b < nbins; b += NTHREADS) {
+  // each thread owns a contiguous chunk of bins: column scan over the 16
+  // segments (cnt[s][b] := frames of bin b in earlier segments), then one
+  // block scan of (present << 16 | total) gives bin starts and run indices
+  const uint32_t per = (nbins + NTHREADS - 1) / NTHREADS;
+  const uint32_t b0 = tid * per;
+  uint32_t packed = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t b = b0 + k;
+    if (b >= nbins) break;
     uint32_t acc = 0;
 #pragma unroll
     for (uint32_t s = 0; s < NSEG; ++s) {
@@ -286,22 +287,21 @@ __device__ void tile_sort(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbi
       acc += c;
     }
     L.bstart[b] = (uint16_t)acc;
+    packed += acc | (acc ? 0x10000u : 0u);
   }
-  __syncthreads();
-  // exclusive scan of bin totals: each thread owns a contiguous chunk of bins
-  const uint32_t per = (nbins + NTHREADS - 1) / NTHREADS;
-  const uint32_t b0 = tid * per;
-  uint32_t sum = 0;
-  for (uint32_t k = 0; k < per; ++k)
-    if (b0 + k < nbins) sum += L.bstart[b0 + k];
   uint32_t total;
-  uint32_t run = block_excl_scan(sum, L.scratch, &total);
-  for (uint32_t k = 0; k < per; ++k)
-    if (b0 + k < nbins) {
-      const uint32_t c = L.bstart[b0 + k];
-      L.bstart[b0 + k] = (uint16_t)run;
-      run += c;
-    }
+  uint32_t run = block_excl_scan(packed, L.scratch, &total);
+  uint32_t *rdst = runs_out + (size_t)tile * TILE;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t b = b0 + k;
+    if (b >= nbins) break;
+    const uint32_t c = L.bstart[b];
+    const uint32_t start = run & 0xFFFFu;
+    L.bstart[b] = (uint16_t)start;
+    if (c) rdst[run >> 16] = (b << 16) | start;
+    run += c | (c ? 0x10000u : 0u);
+    if (b >= n_ep) cls[b - n_ep + 1] = c;                 // NIC, FLOOD, DROP totals
+  }
   __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -309,45 +309,19 @@ __device__ void tile_sort(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbi
     if (local < nt) {
       const uint32_t s = r * (NTHREADS / 64) + wave;
       const uint32_t b = bins[r];
-      const uint32_t dest = L.bstart[b] + L.cnt[s * nbins + b] + rank[r];
-      L.order[dest] = (uint16_t)local;
+      L.order[L.bstart[b] + L.cnt[s * nbins + b] + rank[r]] = (uint16_t)local;
     }
   }
   __syncthreads();
-}
-
-/* Write the sorted tile (coalesced) and its bin runs; returns n_runs. */
-__device__ uint32_t tile_emit(uint32_t tile, uint32_t nt, const Lds &L, uint16_t *order_out,
-                              uint32_t *runs_out) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t p0 = tid * ROUNDS;
   uint16_t *dst = order_out + (size_t)tile * TILE;
+  const uint32_t p0 = tid * ROUNDS;
   if (p0 + ROUNDS <= nt) {
-    const uint2 v = *reinterpret_cast<const uint2 *>(L.order + p0);
-    *reinterpret_cast<uint2 *>(dst + p0) = v;
+    *reinterpret_cast<uint2 *>(dst + p0) = *reinterpret_cast<const uint2 *>(L.order + p0);
   } else {
     for (uint32_t k = 0; k < ROUNDS; ++k)
       if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
   }
-  uint32_t heads = 0;
-  uint32_t hb[ROUNDS];
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) {
-    const uint32_t p = p0 + k;
-    hb[k] = 0xFFFFFFFFu;
-    if (p < nt) {
-      const uint32_t b = L.fbin[L.order[p]];
-      const bool head = p == 0 || L.fbin[L.order[p - 1]] != b;
-      if (head) { hb[k] = b; ++heads; }
-    }
-  }
-  uint32_t n_runs;
-  uint32_t pos = block_excl_scan(heads, L.scratch, &n_runs);
-  uint32_t *rdst = runs_out + (size_t)tile * TILE;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k)
-    if (hb[k] != 0xFFFFFFFFu) rdst[pos++] = (hb[k] << 16) | (p0 + k);
-  return n_runs;
+  return total >> 16;
 }
 
 /* --------------------------------------------------------------------------- */
@@ -396,17 +370,14 @@ __device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *sc
 }
 
 /* Decision for a carried PacketInfo X under the current table (rx). */
-template <bool LDS>
-__device__ uint32_t decide_info_rx(const uint4 *T, uint32_t bmask, const uint32_t *info,
-                                   uint32_t src) {
+__device__ uint32_t decide_info_rx(const uint4 *T, const ClassifyArgs &a, const uint32_t *info) {
   Parsed p;
   p.status = 1; p.i0 = info[0]; p.src = info[1]; p.dst = info[2]; p.ports = info[3];
   p.proto = (info[0] >> 8) & 0xFFu; p.has_ports = (info[0] >> 16) & 1u;
   p.sport = info[3] & 0xFFFFu; p.dport = info[3] >> 16; p.frag_first = 0;
-  return decide_rx<LDS>(T, bmask, p, src);
+  return decide_rx(T, a, p);
 }
 
-/* --------------------------------------------------------------------------- */
 /* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
  * XOR with (f >> 2) & 3 makes both the linear writes and the per-frame reads
  * of ds_*_b128 bank-conflict free. */
@@ -414,6 +385,7 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
   return 4 * f + (j ^ ((f >> 2) & 3u));
 }
 
+/* --------------------------------------------------------------------------- */
 template <bool LDS, bool DENSE>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -434,7 +406,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
     if (DENSE) {
       // 64 contiguous 64-byte frames per wave and round: 4 fully coalesced
-      // 1 KiB wave loads; frame lane/4 + 16k arrives in lane (4 lanes each)
+      // 1 KiB wave loads; part lane&3 of frame 16k + lane/4 arrives in lane
       const uint64_t f0 = base + r * NTHREADS + wave * 64;
       const uint4 *chunk = reinterpret_cast<const uint4 *>(a.frames + f0 * 64);
 #pragma unroll
@@ -450,25 +422,27 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
   }
 
-  // ---- stage the rule table into LDS
+  // ---- while they fly: zero the segment counters, stage the rule table
+  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   const uint4 *T = a.table;
   if (LDS) {
     for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
     T = L.table;
   }
+  __shared__ uint32_t s_carry[8];
+  __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+  if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
 
   // ---- carried-in cache (block 0): stale check against the current table
-  __shared__ uint32_t s_carry[8];
   if (tile == 0) {
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
       const uint32_t st = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
-      if (st & USN_CS_VALID) {
-        const uint32_t now = decide_info_rx<LDS>(T, a.bucket_mask, s_carry + 2, a.src);
-        if ((now & USN_PARITY_MASK) != (dst & USN_PARITY_MASK)) flags |= USN_S_STALE;
-      }
+      if ((st & USN_CS_VALID) &&
+          ((decide_info_rx(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
+        flags |= USN_S_STALE;
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
       usn_summary *S = a.summary;
@@ -478,11 +452,16 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     }
     __syncthreads();
   }
+  const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
 
   // ---- parse + decide
-  uint32_t dec[ROUNDS], bins[ROUNDS], touch[ROUNDS], inf[ROUNDS][4];
+  uint32_t dec[ROUNDS], bins[ROUNDS];
+  uint32_t differs = 0;          // stale mode: bit r = touching frame whose info != carried
+  uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
+  uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
     if (DENSE) {   // wave-private transpose through LDS: lane <- its own frame
       uint4 *st = L.stage + wave * 256;
 #pragma unroll
@@ -490,50 +469,50 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; ++k) q[r][k] = st[stage_slot(lane, k)];
     }
-#if USN_ABL_LOADONLY
-    const uint32_t x = q[r][0].x ^ q[r][1].y ^ q[r][2].z ^ q[r][3].w ^ len[r];
-    dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, x & 0xFFFF);
-    touch[r] = 0;
-    inf[r][0] = inf[r][1] = inf[r][2] = inf[r][3] = 0;
+#if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
+    dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
+                       (q[r][0].x ^ q[r][1].y ^ q[r][2].z ^ q[r][3].w ^ len[r]) & 0xFFFFu);
     continue;
 #endif
     Parsed p;
     parse(q[r], len[r], fp[r], p);
-    dec[r] = decide_rx<LDS>(T, a.bucket_mask, p, a.src);
+    dec[r] = decide_rx(T, a, p);
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
-    touch[r] = p.status == 0 ? 0u
-             : p.status == 4 ? 3u
-             : (p.status == 1 && (p.dst >> 24) != 127u) ? 1u : 2u;
-    inf[r][0] = p.i0; inf[r][1] = p.src; inf[r][2] = p.dst; inf[r][3] = p.ports;
-    if (r * NTHREADS + tid >= nt) touch[r] = 0;
+    uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
+                   : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
+    if (local >= nt) touch = 0;
+    if (touch) {
+      my_last = local + 1; my_touch = touch; my_dec = dec[r];
+      my_info[0] = p.i0; my_info[1] = p.src; my_info[2] = p.dst; my_info[3] = p.ports;
+    }
+    if (stale && touch && !(touch == 1 && p.i0 == s_carry[2] && p.src == s_carry[3] &&
+                            p.dst == s_carry[4] && p.ports == s_carry[5]))
+      differs |= 1u << r;        // later fragments also stop the device prefix
   }
 
   // ---- stale carried cache: frames before the first break take the cached
   //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
-  if (tile == 0 && (s_carry[6] & USN_S_STALE)) {
+  if (stale) {
     uint32_t fb = TILE;
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (touch[r] == 0) continue;
-      const bool same = touch[r] == 1 && inf[r][0] == s_carry[2] && inf[r][1] == s_carry[3] &&
-                        inf[r][2] == s_carry[4] && inf[r][3] == s_carry[5];
-      if (!same) fb = min(fb, local);   // later fragments also stop the device prefix
-    }
+    for (uint32_t r = 0; r < ROUNDS; ++r)
+      if (differs & (1u << r)) fb = min(fb, r * NTHREADS + tid);
     atomicMin(&s_carry[7], fb);
     __syncthreads();
     const uint32_t first = s_carry[7];
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) {
       const uint32_t local = r * NTHREADS + tid;
-      if (local < first && touch[r] == 1)
-        dec[r] = (s_carry[1] & USN_PARITY_MASK) | USN_F_CACHE | (dec[r] & USN_F_HOST) |
-                 (dec[r] & (USN_F_FRAG1 | USN_F_DHCP));
+      const bool touching_same = local < nt && local < first &&
+                                 USN_DEC_REASON(dec[r]) != USN_R_PARSE;
+      if (touching_same)
+        dec[r] = (s_carry[1] & USN_PARITY_MASK) | USN_F_CACHE |
+                 (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_DHCP));
+      if (local + 1 == my_last && touching_same) my_dec = dec[r];
     }
     if (tid == 0) {
       uint32_t f = s_carry[6];
       if (first >= nt && a.n > TILE) f |= USN_S_STALE_EXTENDS;
-      // a later fragment at the break: the host decides whether the prefix goes on
       a.summary->first_break = first;
       s_carry[6] = f;
     }
@@ -543,88 +522,58 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     if (!(s_carry[6] & USN_S_STALE)) a.summary->first_break = 0xFFFFFFFFu;
   }
 
-  // ---- decisions out (coalesced) + host list
-  uint32_t nhost = 0;
+  // ---- decisions out (coalesced), host list, last touching frame
+  uint32_t *hl = a.host_list + (size_t)tile * TILE;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    if (local < nt) {
-      a.decisions[base + local] = dec[r];
-      nhost += (dec[r] & USN_F_HOST) ? 1u : 0u;
-    }
+    const bool v = local < nt;
+    if (v) a.decisions[base + local] = dec[r];
     bins[r] = dec_bin(dec[r], a.n_ep);
-  }
-
-  // ---- per-tile class counts and host list
-  __shared__ uint32_t s_cls[4];
-  __shared__ uint32_t s_last;
-  if (tid < 4) s_cls[tid] = 0;
-  if (tid == 0) s_last = 0;
-  __syncthreads();
-  uint32_t cc[4] = {0, 0, 0, 0};
-  uint32_t last = 0;   // 1 + tile-local index of the last cache-touching frame
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local < nt) cc[USN_DEC_CLASS(dec[r])]++;
-    if (touch[r]) last = local + 1;
-  }
-#pragma unroll
-  for (uint32_t c = 0; c < 4; ++c) {
-    uint32_t v = cc[c];
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (lane == 0 && v) atomicAdd(&s_cls[c], v);
-  }
-  uint32_t lm = last;
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) lm = max(lm, (uint32_t)__shfl_xor(lm, d, 64));
-  if (lane == 0 && lm) atomicMax(&s_last, lm);
-  uint32_t total_host;
-  uint32_t hpos = block_excl_scan(nhost, L.scratch, &total_host);
-  if (nhost) {
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local < nt && (dec[r] & USN_F_HOST)) a.host_list[(size_t)tile * TILE + hpos++] = (uint32_t)(base + local);
+    const bool host = v && (dec[r] & USN_F_HOST);
+    if (__ballot(host)) {                                // rare: unordered append (host sorts)
+      if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
     }
+  }
+  {
+    uint32_t lm = my_last;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) lm = max(lm, (uint32_t)__shfl_xor(lm, d, 64));
+    if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
   }
 
   // ---- stable per-endpoint order of the tile
-#if USN_ABL_NOSORT || USN_ABL_LOADONLY
+  uint32_t cls[4] = {0, 0, 0, 0};
+#if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
   const uint32_t n_runs = 0;
 #else
-  tile_sort(bins, nt, a.nbins, L);
-  const uint32_t n_runs = tile_emit(tile, nt, L, a.order, a.runs);
+  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
+                                     a.runs, cls);
 #endif
+  if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
+  if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
+  if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
+  __syncthreads();
 
   // ---- tile header
-  const uint32_t lastp = s_last;
-  if (lastp) {
-    const uint32_t li = lastp - 1;
-    if ((li & (NTHREADS - 1)) == tid) {
-      const uint32_t r = li / NTHREADS;
-      usn_tile_hdr *H = a.tiles + tile;
-      uint32_t st = USN_TS_HAS;
-#pragma unroll
-      for (uint32_t rr = 0; rr < ROUNDS; ++rr) {
-        if (rr != r) continue;
-        if (touch[rr] == 1) st |= USN_TS_RETAINED;
-        if (touch[rr] == 3) st |= USN_TS_UNKNOWN;
-        H->last_dst = dec[rr] & USN_PARITY_MASK;
-        for (int k = 0; k < 4; ++k) H->last_info[k] = inf[rr][k];
-      }
-      H->last_state = st;
-      H->last_idx = (uint32_t)(base + li);
-    }
+  usn_tile_hdr *H = a.tiles + tile;
+  const uint32_t lastp = s_misc[0];
+  if (lastp && my_last == lastp) {
+    H->last_state = USN_TS_HAS | (my_touch == 1u ? USN_TS_RETAINED : 0u) |
+                    (my_touch == 3u ? USN_TS_UNKNOWN : 0u);
+    H->last_dst = my_dec & USN_PARITY_MASK;
+    for (int k = 0; k < 4; ++k) H->last_info[k] = my_info[k];
+    H->last_idx = (uint32_t)(base + lastp - 1);
   }
   if (tid == 0) {
-    usn_tile_hdr *H = a.tiles + tile;
     H->n_frames = (uint16_t)nt;
     H->n_runs = (uint16_t)n_runs;
-    H->n_host = (uint16_t)total_host;
+    H->n_host = (uint16_t)s_misc[1];
     H->_reserved = 0;
-    for (int c = 0; c < 4; ++c) H->class_count[c] = (uint16_t)s_cls[c];
+    H->class_count[0] = (uint16_t)s_misc[5];                       // DROP bin
+    H->class_count[2] = (uint16_t)s_misc[3];                       // NIC bin
+    H->class_count[3] = (uint16_t)s_misc[4];                       // FLOOD bin
+    H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
 }
@@ -633,34 +582,33 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
 __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32_t t0) {
   extern __shared__ __align__(16) uint8_t smem[];
   const Lds L = carve(smem, a.nbins);
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t tid = threadIdx.x;
   const uint32_t tile = t0 + blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   __shared__ uint32_t s_cls[4];
   if (tid < 4) s_cls[tid] = 0;
+  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   uint32_t bins[ROUNDS];
-  uint32_t cc[4] = {0, 0, 0, 0};
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    const uint32_t d = local < nt ? a.decisions[base + local] : 0u;
-    bins[r] = dec_bin(d, a.n_ep);
-    if (local < nt) cc[USN_DEC_CLASS(d)]++;
+    bins[r] = dec_bin(local < nt ? a.decisions[base + local] : 0u, a.n_ep);
   }
   __syncthreads();
-#pragma unroll
-  for (uint32_t c = 0; c < 4; ++c) {
-    uint32_t v = cc[c];
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (lane == 0 && v) atomicAdd(&s_cls[c], v);
-  }
-  tile_sort(bins, nt, a.nbins, L);
-  const uint32_t n_runs = tile_emit(tile, nt, L, a.order, a.runs);
+  uint32_t cls[4] = {0, 0, 0, 0};
+  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
+                                     a.runs, cls);
+  for (int c = 1; c < 4; ++c)
+    if (cls[c]) atomicAdd(&s_cls[c], cls[c]);
+  __syncthreads();
   if (tid == 0) {
-    a.tiles[tile].n_runs = (uint16_t)n_runs;
-    for (int c = 0; c < 4; ++c) a.tiles[tile].class_count[c] = (uint16_t)s_cls[c];
+    usn_tile_hdr *H = a.tiles + tile;
+    H->n_runs = (uint16_t)n_runs;
+    H->class_count[0] = (uint16_t)s_cls[3];
+    H->class_count[2] = (uint16_t)s_cls[1];
+    H->class_count[3] = (uint16_t)s_cls[2];
+    H->class_count[1] = (uint16_t)(nt - s_cls[1] - s_cls[2] - s_cls[3]);
   }
 }
 

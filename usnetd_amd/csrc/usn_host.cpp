@@ -157,6 +157,7 @@ struct usn_ctx {
   uint4 *d_table = nullptr;
   size_t d_table_cap = 0;
   uint32_t table_slots = 0, bucket_mask = 0;
+  uint32_t probe_mask = 0;   // key shapes present in the table (ClassifyArgs::probe_mask)
   bool bridge_dirty = true;
   uint64_t *d_bridge = nullptr;
   size_t d_bridge_cap = 0;
@@ -175,8 +176,14 @@ int rebuild_table(usn_ctx *c) {
   uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
   std::vector<uint4> img((size_t)nb * 4);
   std::memset(img.data(), 0, img.size() * sizeof(uint4));
+  uint32_t pmask = 0;
   for (const auto &kv : c->rules) {
     const WantKey &k = kv.first;
+    /* key1 (to_match_want_with_src(true)) always has src and has both ports or
+     * neither; key2 has neither src nor src_port.  Other shapes never match. */
+    if (k.present == USN_WANT_SRC || k.present == (USN_WANT_SRC | USN_WANT_DPORT | USN_WANT_SPORT))
+      pmask |= 1u;
+    if (k.present == 0 || k.present == USN_WANT_DPORT) pmask |= 2u;
     const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
     const uint32_t meta = usn_key_meta(k.proto, k.present);
     uint32_t b = usn_key_hash(k.dst, k.src, z, meta) & (nb - 1);
@@ -206,6 +213,7 @@ int rebuild_table(usn_ctx *c) {
   HIPCHK(hipMemcpy(c->d_table, img.data(), bytes, hipMemcpyHostToDevice));
   c->table_slots = nb * 4;
   c->bucket_mask = nb - 1;
+  c->probe_mask = pmask;
   c->table_dirty = false;
   return USN_OK;
 }
@@ -624,6 +632,9 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   a.for_nic = S.for_nic < 0 ? 0xFFFFu : (uint32_t)S.for_nic;
   a.n_ep = c->n_ep;
   a.nbins = c->n_ep + 3;
+  a.nbits = 1;
+  while ((1u << a.nbits) < a.nbins) ++a.nbits;
+  a.probe_mask = c->probe_mask;
   return USN_OK;
 }
 

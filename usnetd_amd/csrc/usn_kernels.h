@@ -41,7 +41,9 @@ struct ClassifyArgs {
   uint32_t src_is_nic;
   uint32_t for_nic;
   uint32_t nbins;           /* endpoints + 3 */
+  uint32_t nbits;           /* bits to tell bins apart (ceil log2 nbins) */
   uint32_t n_ep;            /* endpoints (bin of NIC) */
+  uint32_t probe_mask;      /* bit0: rules key1 can hit exist; bit1: rules key2 can hit */
   /* carried 1-entry decision cache */
   uint32_t carry_mode;
   uint32_t cin_state, cin_dst;
