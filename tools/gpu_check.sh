@@ -25,10 +25,12 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
     abl) step abl 600 python tools/abl.py --json gpurun_out/abl.json ${ABL_ARGS:-} ;;
+    stamps) step stamps 300 python tools/stamps.py ${STAMP_ARGS:-c2} ;;
+    ablsmall) step ablsmall 600 python tools/abl.py --frames 131072 --batches 1 --json gpurun_out/ablsmall.json ;;
     counters)
       step listctr 120 rocprofv3 -L
       i=0
-      for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+      for set in ${PMC_SETS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"} \
                  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
                  "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT" \
                  "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS"; do

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Phase timeline of the classify kernel from the diagnostic build
+(build/abl/stamps: -DUSN_STAMPS=1).  Wave 0 of each workgroup stamps the
+global 100 MHz clock at 12 phase boundaries; this prints, over workgroups,
+the median / p90 of each phase and the spread of start and end times.
+Only the SHARES are meaningful (the stamps add waits of their own)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from usnetd_amd import lib, traffic  # noqa: E402
+
+NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided",
+         "all rounds decided", "stores+hostlist+lastreduce", "match+cnt barrier",
+         "colscan+blockscan+runs", "order scatter", "order store+cls", "header"]
+
+
+def main():
+    cfgname = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+    path = os.path.join(ROOT, "build", "abl", "stamps", "libusn.so")
+    ctx = lib.Ctx(0, libpath=path)
+    cfgs = [traffic.config(cfgname, n=n, seed=17 * k + 2) for k in range(5)]
+    traffic.install_ctx(ctx, cfgs[0])
+    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+    rs = [lib.DeviceResult(ctx, n) for _ in cfgs]
+    s = ctx.stream()
+    for i in range(40):
+        lib.check(ctx.L.usn_classify(ctx.h, C.byref(bs[i % 5].desc), C.byref(rs[i % 5].desc), s))
+    ctx.sync(s)
+    ntiles = (n + 1023) // 1024
+    buf = np.zeros(16384 * 16, np.uint64)
+    ctx.L.usn_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
+    rc = ctx.L.usn_debug_stamps(buf.ctypes.data, buf.nbytes)
+    assert rc == 0, rc
+    st = buf.reshape(16384, 16)[:ntiles, :12].astype(np.int64)
+    t0 = st[:, 0].min()
+    us = lambda x: x / 100.0   # 100 MHz ticks -> us
+    print("%s n=%d tiles=%d  kernel span %.2f us" % (cfgname, n, ntiles, us(st[:, 11].max() - t0)))
+    print("start offset: median %.2f p90 %.2f max %.2f us" % tuple(
+        us(np.percentile(st[:, 0] - t0, q)) for q in (50, 90, 100)))
+    print("end   offset: median %.2f p90 %.2f max %.2f us" % tuple(
+        us(np.percentile(st[:, 11] - t0, q)) for q in (50, 90, 100)))
+    for k in range(1, 12):
+        d = st[:, k] - st[:, k - 1]
+        print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % (
+            NAMES[k], us(np.median(d)), us(np.percentile(d, 90)), us(d.max())))
+    tot = st[:, 11] - st[:, 0]
+    print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % ("TOTAL per block", us(np.median(tot)),
+                                                        us(np.percentile(tot, 90)), us(tot.max())))
+
+
+if __name__ == "__main__":
+    main()

@@ -39,6 +39,26 @@ namespace usn {
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
+/* Diagnostic build only (-DUSN_STAMPS=1, tools/stamps.py): wave 0 of every
+ * workgroup records the global 100 MHz clock at phase boundaries.  The stamps
+ * go to their own buffer; no output depends on them. */
+#ifndef USN_STAMPS
+#define USN_STAMPS 0
+#endif
+#if USN_STAMPS
+#define USN_NSTAMP 16
+__device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
+#define STAMP(k)                                                                 \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    if (threadIdx.x == 0)                                                        \
+      usn_stamp_buf[(blockIdx.x & 16383) * USN_NSTAMP + (k)] = wall_clock64();   \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+  } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 #ifndef USN_LOAD_NT
 #define USN_LOAD_NT 0
 #endif
@@ -270,6 +290,7 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     if (local < nt && rank[r] == 0) L.cnt[s * nbins + bins[r]] = (uint16_t)__popcll(same);
   }
   __syncthreads();
+  STAMP(7);
   // each thread owns a contiguous chunk of bins: column scan over the 16
   // segments (cnt[s][b] := frames of bin b in earlier segments), then one
   // block scan of (present << 16 | total) gives bin starts and run indices
@@ -303,6 +324,7 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     if (b >= n_ep) cls[b - n_ep + 1] = c;                 // NIC, FLOOD, DROP totals
   }
   __syncthreads();
+  STAMP(8);
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
@@ -313,6 +335,7 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     }
   }
   __syncthreads();
+  STAMP(9);
   uint16_t *dst = order_out + (size_t)tile * TILE;
   const uint32_t p0 = tid * ROUNDS;
   if (p0 + ROUNDS <= nt) {
@@ -394,6 +417,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  STAMP(0);
 
   // ---- issue every header load of this thread first (16 x 16 B + 4 lengths)
   uint4 q[ROUNDS][4];
@@ -422,6 +446,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
   }
 
+  STAMP(1);
   // ---- while they fly: zero the segment counters, stage the rule table
   for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   const uint4 *T = a.table;
@@ -433,6 +458,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
+  STAMP(2);
 
   // ---- carried-in cache (block 0): stale check against the current table
   if (tile == 0) {
@@ -453,6 +479,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     __syncthreads();
   }
   const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
+  STAMP(3);
 
   // ---- parse + decide
   uint32_t dec[ROUNDS], bins[ROUNDS];
@@ -488,7 +515,9 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     if (stale && touch && !(touch == 1 && p.i0 == s_carry[2] && p.src == s_carry[3] &&
                             p.dst == s_carry[4] && p.ports == s_carry[5]))
       differs |= 1u << r;        // later fragments also stop the device prefix
+    if (r == 0) STAMP(4);
   }
+  STAMP(5);
 
   // ---- stale carried cache: frames before the first break take the cached
   //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
@@ -542,6 +571,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
   }
 
+  STAMP(6);
   // ---- stable per-endpoint order of the tile
   uint32_t cls[4] = {0, 0, 0, 0};
 #if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
@@ -554,6 +584,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
   if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
   __syncthreads();
+  STAMP(10);
 
   // ---- tile header
   usn_tile_hdr *H = a.tiles + tile;
@@ -576,6 +607,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
+  STAMP(11);
 }
 
 /* Rebuild order / runs / class counts of tiles from patched decisions. */
@@ -650,3 +682,10 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
 }
 
 }  // namespace usn
+
+#if USN_STAMPS
+extern "C" int usn_debug_stamps(void *host, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(usn::usn_stamp_buf), bytes, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
