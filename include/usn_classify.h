@@ -234,6 +234,8 @@ int usn_event_create(usn_ctx *ctx, void **ev);
 int usn_event_destroy(usn_ctx *ctx, void *ev);
 int usn_event_record(usn_ctx *ctx, void *ev, void *hip_stream);
 int usn_event_elapsed_ms(usn_ctx *ctx, void *ev_start, void *ev_end, float *ms);
+/* Make `hip_stream` wait (on the device) for an event recorded on another stream. */
+int usn_stream_wait_event(usn_ctx *ctx, void *hip_stream, void *ev);
 
 #ifdef __cplusplus
 }

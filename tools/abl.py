@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--json", default="")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="round-robin batches over S streams, one NIC rx queue (source) each")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     names = a.variants or sorted(os.listdir(os.path.join(ROOT, "build", "abl")))
@@ -37,12 +39,16 @@ def main():
         path = os.path.join(ROOT, "build", "abl", nm, "libusn.so")
         ctx = lib.Ctx(0, libpath=path)
         traffic.install_ctx(ctx, cfgs[0])
-        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+        nics = [0] + list(traffic.extra_nics(cfgs[0], a.streams - 1, ctx))
+        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k % a.streams], stride=c.stride)
+              for k, c in enumerate(cfgs)]
         rs = [lib.DeviceResult(ctx, a.frames) for _ in cfgs]
         s = ctx.stream()
+        ss = [s] + [ctx.stream() for _ in range(a.streams - 1)]
         evs = [(ctx.event(), ctx.event()) for _ in range(a.launches)]
         e0, e1 = ctx.event(), ctx.event()
-        runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, evs=evs, e0=e0, e1=e1, per=[], b2b=[])
+        runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, ss=ss, evs=evs, e0=e0, e1=e1, per=[], b2b=[],
+                        ejoin=[ctx.event() for _ in ss])
     for rnd in range(a.rounds):
         for nm in names:
             R = runs[nm]
@@ -59,9 +65,17 @@ def main():
                 ctx.record(y, s)
             ctx.sync(s)
             R["per"] += [ctx.elapsed_ms(x, y) * 1e3 for x, y in R["evs"]]
+            ss = R["ss"]
             ctx.record(R["e0"], s)
+            for x in ss[1:]:
+                ctx.wait_event(x, R["e0"])
             for i in range(a.launches):
-                L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+                # batch k always goes to stream k % S (its rx queue): per-source order kept
+                k = i % len(bd)
+                L.usn_classify(ctx.h, bd[k], rd[k], ss[k % len(ss)])
+            for x, ej in zip(ss[1:], R["ejoin"]):
+                ctx.record(ej, x)
+                ctx.wait_event(s, ej)
             ctx.record(R["e1"], s)
             ctx.sync(s)
             R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches)

@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 from usnetd_amd import lib, traffic  # noqa: E402
 
 NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided",
-         "all rounds decided", "stores+hostlist+lastreduce", "match+cnt barrier",
-         "colscan+blockscan+runs", "order scatter", "order store+cls", "header"]
+         "all rounds decided", "stores+hostlist+lastreduce", "-", "-", "-",
+         "tile_order+cls", "header"]
 
 
 def main():
@@ -45,8 +45,9 @@ def main():
         us(np.percentile(st[:, 0] - t0, q)) for q in (50, 90, 100)))
     print("end   offset: median %.2f p90 %.2f max %.2f us" % tuple(
         us(np.percentile(st[:, 11] - t0, q)) for q in (50, 90, 100)))
-    for k in range(1, 12):
-        d = st[:, k] - st[:, k - 1]
+    for k in [1, 2, 3, 4, 5, 6, 10, 11]:
+        prev = {10: 6}.get(k, k - 1)
+        d = st[:, k] - st[:, prev]
         print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % (
             NAMES[k], us(np.median(d)), us(np.percentile(d, 90)), us(d.max())))
     tot = st[:, 11] - st[:, 0]

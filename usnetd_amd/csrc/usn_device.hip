@@ -36,6 +36,7 @@ namespace usn {
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
 #define MAX_NBITS 10   /* nbins <= 1024 */
+#define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule tables up to 2048 slots live in LDS */
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
@@ -48,15 +49,25 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 #if USN_STAMPS
 #define USN_NSTAMP 16
 __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
+/* stamps live in registers until the end: a global store per stamp would
+ * queue behind the header loads and time the memory queue instead */
 #define STAMP(k)                                                                 \
   do {                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                           \
-    if (threadIdx.x == 0)                                                        \
-      usn_stamp_buf[(blockIdx.x & 16383) * USN_NSTAMP + (k)] = wall_clock64();   \
+    stamp_t[(k)] = wall_clock64();                                               \
     __builtin_amdgcn_sched_barrier(0);                                           \
+  } while (0)
+#define STAMP_DECL unsigned long long stamp_t[12] = {0};
+#define STAMP_FLUSH()                                                            \
+  do {                                                                           \
+    if (threadIdx.x == 0)                                                        \
+      for (int k_ = 0; k_ < 12; ++k_)                                            \
+        usn_stamp_buf[(blockIdx.x & 16383) * USN_NSTAMP + k_] = stamp_t[k_];     \
   } while (0)
 #else
 #define STAMP(k) do { } while (0)
+#define STAMP_DECL
+#define STAMP_FLUSH() do { } while (0)
 #endif
 
 #ifndef USN_LOAD_NT
@@ -193,7 +204,7 @@ __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
 /* --------------------------------------------------------------------------- */
 /* LDS layout of a block                                                        */
 struct Lds {
-  uint16_t *cnt;      // [NSEG][nbins]: per-segment counts, then segment prefixes
+  uint16_t *cnt;      // [nbins][NSEG]: per-segment counts, then segment prefixes
   uint16_t *bstart;   // [nbins]: tile totals, then bin start slots
   uint16_t *order;    // [TILE]
   uint32_t *scratch;  // [16]
@@ -226,13 +237,16 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) {
   return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-/* Inclusive scan of v across the 64 lanes of a wave. */
+/* Inclusive scan of v across the 64 lanes of a wave with DPP row shifts and
+ * row broadcasts (VALU only; no LDS permute traffic). */
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
+  (void)lane;
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1,3
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2,3
   return v;
 }
 
@@ -254,6 +268,15 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
   __syncthreads();
   *total = tot;
   return base + inc - v;
+}
+
+/* Largest r (0..ROUNDS-1) among the lanes with `valid`, via one ballot per round. */
+__device__ __forceinline__ uint32_t __reduce_max_rounds(uint32_t r, bool valid) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < ROUNDS; ++k)
+    if (__ballot(valid && r >= k)) m = k;
+  return m;
 }
 
 /* Mask of the lanes of this wave whose bin equals this lane's bin: one
@@ -287,10 +310,9 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     const uint32_t s = r * (NTHREADS / 64) + wave;         // 64-frame segment, index order
     const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
     rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-    if (local < nt && rank[r] == 0) L.cnt[s * nbins + bins[r]] = (uint16_t)__popcll(same);
+    if (local < nt && rank[r] == 0) L.cnt[bins[r] * NSEG + s] = (uint16_t)__popcll(same);
   }
   __syncthreads();
-  STAMP(7);
   // each thread owns a contiguous chunk of bins: column scan over the 16
   // segments (cnt[s][b] := frames of bin b in earlier segments), then one
   // block scan of (present << 16 | total) gives bin starts and run indices
@@ -300,13 +322,22 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t b = b0 + k;
     if (b >= nbins) break;
+    // the 16 u16 counts of bin b are 32 contiguous bytes: two 16-byte LDS
+    // reads, an exclusive prefix in registers, two 16-byte writes
+    uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
+    uint32_t w[8];
+    const uint4 r0 = row[0], r1 = row[1];
+    w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
+    w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
     uint32_t acc = 0;
 #pragma unroll
-    for (uint32_t s = 0; s < NSEG; ++s) {
-      const uint32_t c = L.cnt[s * nbins + b];
-      L.cnt[s * nbins + b] = (uint16_t)acc;
-      acc += c;
+    for (uint32_t k2 = 0; k2 < 8; ++k2) {
+      const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
+      w[k2] = acc | ((acc + lo) << 16);
+      acc += lo + hi;
     }
+    row[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    row[1] = make_uint4(w[4], w[5], w[6], w[7]);
     L.bstart[b] = (uint16_t)acc;
     packed += acc | (acc ? 0x10000u : 0u);
   }
@@ -321,21 +352,22 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     L.bstart[b] = (uint16_t)start;
     if (c) rdst[run >> 16] = (b << 16) | start;
     run += c | (c ? 0x10000u : 0u);
-    if (b >= n_ep) cls[b - n_ep + 1] = c;                 // NIC, FLOOD, DROP totals
+    // NIC, FLOOD, DROP totals (selects: a runtime index would put cls in scratch)
+    cls[1] = b == n_ep ? c : cls[1];
+    cls[2] = b == n_ep + 1 ? c : cls[2];
+    cls[3] = b == n_ep + 2 ? c : cls[3];
   }
   __syncthreads();
-  STAMP(8);
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     if (local < nt) {
       const uint32_t s = r * (NTHREADS / 64) + wave;
       const uint32_t b = bins[r];
-      L.order[L.bstart[b] + L.cnt[s * nbins + b] + rank[r]] = (uint16_t)local;
+      L.order[L.bstart[b] + L.cnt[b * NSEG + s] + rank[r]] = (uint16_t)local;
     }
   }
   __syncthreads();
-  STAMP(9);
   uint16_t *dst = order_out + (size_t)tile * TILE;
   const uint32_t p0 = tid * ROUNDS;
   if (p0 + ROUNDS <= nt) {
@@ -408,6 +440,29 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
   return 4 * f + (j ^ ((f >> 2) & 3u));
 }
 
+/* Header loads of one round.  DENSE: 64 contiguous 64-byte frames per wave,
+ * 4 fully coalesced 1 KiB wave loads; part lane&3 of frame 16k + lane/4
+ * arrives in lane (transposed through LDS later).  Else one 64-byte window
+ * per lane. */
+template <bool DENSE>
+__device__ __forceinline__ void issue_round(const ClassifyArgs &a, uint64_t base, uint32_t r,
+                                            uint32_t wave, uint32_t lane, const uint8_t *fp,
+                                            uint4 (&q)[4]) {
+  if (DENSE) {
+    const uint64_t f0 = base + r * NTHREADS + wave * 64;
+    const uint4 *chunk = reinterpret_cast<const uint4 *>(a.frames + f0 * 64);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint64_t f = f0 + 16 * k + (lane >> 2);
+      q[k] = f < a.n ? ld_stream(chunk + 64 * k + lane) : make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    const uint4 *w = reinterpret_cast<const uint4 *>(fp);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(w + k);
+  }
+}
+
 /* --------------------------------------------------------------------------- */
 template <bool LDS, bool DENSE>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
@@ -417,41 +472,37 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  STAMP_DECL
   STAMP(0);
 
-  // ---- issue every header load of this thread first (16 x 16 B + 4 lengths)
+  // ---- loads, oldest first: rule table (tiny, L2-resident), lengths, then
+  //      the headers of round 0; round r+1 is issued just before round r is
+  //      decided.  Waves issue in order, so a wave that queued all 16 header
+  //      loads up front would sit behind HBM back-pressure instead of computing
+  //      on data that has already arrived; 16 waves per CU x one 4 KiB round
+  //      in flight keep the CU's share of HBM busy.
   uint4 q[ROUNDS][4];
   uint32_t len[ROUNDS];
   const uint8_t *fp[ROUNDS];
+  uint4 tb0 = make_uint4(0, 0, 0, 0);   // first 256 slots staged through registers
+  if (LDS && tid < a.table_slots) tb0 = a.table[tid];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     const uint64_t i = base + (local < nt ? local : 0);
     fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-    if (DENSE) {
-      // 64 contiguous 64-byte frames per wave and round: 4 fully coalesced
-      // 1 KiB wave loads; part lane&3 of frame 16k + lane/4 arrives in lane
-      const uint64_t f0 = base + r * NTHREADS + wave * 64;
-      const uint4 *chunk = reinterpret_cast<const uint4 *>(a.frames + f0 * 64);
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        const uint64_t f = f0 + 16 * k + (lane >> 2);
-        q[r][k] = f < a.n ? ld_stream(chunk + 64 * k + lane) : make_uint4(0, 0, 0, 0);
-      }
-    } else {
-      const uint4 *w = reinterpret_cast<const uint4 *>(fp[r]);
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) q[r][k] = ld_stream(w + k);
-    }
     len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
   }
+  issue_round<DENSE>(a, base, 0, wave, lane, fp[0], q[0]);
+  __builtin_amdgcn_sched_barrier(0);
 
   STAMP(1);
   // ---- while they fly: zero the segment counters, stage the rule table
   for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   const uint4 *T = a.table;
   if (LDS) {
-    for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    if (tid < a.table_slots) L.table[tid] = tb0;
+    for (uint32_t k = tid + NTHREADS; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
     T = L.table;
   }
   __shared__ uint32_t s_carry[8];
@@ -489,6 +540,11 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
+    if (r + 1 < ROUNDS) {        // one round of headers in flight ahead of the one decided
+      __builtin_amdgcn_sched_barrier(0);
+      issue_round<DENSE>(a, base, r + 1, wave, lane, fp[r + 1], q[r + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (DENSE) {   // wave-private transpose through LDS: lane <- its own frame
       uint4 *st = L.stage + wave * 256;
 #pragma unroll
@@ -516,6 +572,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
                             p.dst == s_carry[4] && p.ports == s_carry[5]))
       differs |= 1u << r;        // later fragments also stop the device prefix
     if (r == 0) STAMP(4);
+
   }
   STAMP(5);
 
@@ -565,10 +622,16 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     }
   }
   {
-    uint32_t lm = my_last;
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) lm = max(lm, (uint32_t)__shfl_xor(lm, d, 64));
-    if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
+    // the wave's last touching frame: highest lane of the latest round with one
+    const uint64_t rounds_with = __ballot(my_last != 0);
+    if (rounds_with) {
+      const uint32_t r_last = (my_last - 1) / NTHREADS;
+      const uint32_t rmax = __builtin_amdgcn_readfirstlane(
+          __reduce_max_rounds(r_last, my_last != 0));
+      const uint64_t in_r = __ballot(my_last != 0 && r_last == rmax);
+      const uint32_t hi = 63 - (uint32_t)__builtin_clzll(in_r);
+      if (lane == 0) atomicMax(&s_misc[0], rmax * NTHREADS + wave * 64 + hi + 1);
+    }
   }
 
   STAMP(6);
@@ -608,6 +671,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
   STAMP(11);
+  STAMP_FLUSH();
 }
 
 /* Rebuild order / runs / class counts of tiles from patched decisions. */
@@ -645,8 +709,6 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
 }
 
 /* --------------------------------------------------------------------------- */
-#define LDS_TABLE_MAX_BYTES (32u * 1024u)
-
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots) {
   return (size_t)table_slots * 16 <= LDS_TABLE_MAX_BYTES &&
          lds_core_bytes(nbins) + STAGE_BYTES + (size_t)table_slots * 16 <= 64u * 1024u;

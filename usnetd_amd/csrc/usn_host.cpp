@@ -941,4 +941,10 @@ int usn_event_elapsed_ms(usn_ctx *c, void *a, void *b, float *ms) {
   return USN_OK;
 }
 
+int usn_stream_wait_event(usn_ctx *c, void *s, void *ev) {
+  if (!c || !ev) return USN_EINVAL;
+  HIPCHK(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)ev, 0));
+  return USN_OK;
+}
+
 }  // extern "C"

@@ -103,6 +103,7 @@ def load(path: str | None = None):
         "usn_event_create": ([P, C.POINTER(P)], I), "usn_event_destroy": ([P, P], I),
         "usn_event_record": ([P, P, P], I),
         "usn_event_elapsed_ms": ([P, P, P, C.POINTER(C.c_float)], I),
+        "usn_stream_wait_event": ([P, P, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -120,7 +121,7 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_host_alloc_pinned", "usn_host_free_pinned", "usn_memcpy_h2d", "usn_memcpy_d2h",
             "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
             "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
-            "usn_event_elapsed_ms"]
+            "usn_event_elapsed_ms", "usn_stream_wait_event"]
 
 
 def check(rc, what=""):
@@ -273,6 +274,9 @@ class Ctx:
 
     def record(self, ev, stream):
         check(self.L.usn_event_record(self.h, ev, stream), "usn_event_record")
+
+    def wait_event(self, stream, ev):
+        check(self.L.usn_stream_wait_event(self.h, stream, ev), "usn_stream_wait_event")
 
     def elapsed_ms(self, a, b) -> float:
         ms = C.c_float()

@@ -234,6 +234,18 @@ def config(name, n=None, seed=None, **kw):
     return f(**kw)
 
 
+def extra_nics(cfg: Config, k: int, ctx=None):
+    """Ids of k more NIC endpoints (further rx queues) after the config's own;
+    registers them in ctx when given.  The rule table is shared: get_endpoint
+    does not check which NIC a rule's owner belongs to (endpoint.rs:307-338)."""
+    first = max(e[0] for e in cfg.endpoints) + 1
+    ids = list(range(first, first + k))
+    if ctx is not None:
+        for i in ids:
+            ctx.endpoint_add(i, EP_NIC, None)
+    return ids
+
+
 def install_ctx(ctx, cfg: Config):
     from .lib import make_want
     for eid, kind, for_nic in cfg.endpoints:
