@@ -205,6 +205,11 @@ int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
  * decision cache is carried on the device from the previous batch's result,
  * which must stay allocated until this call's work has been enqueued. */
 int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream);
+/* Several drained rings of DISTINCT sources (e.g. the rx queues of the NICs
+ * polled in one poll() round, main.rs:1029-1046) in one launch: b[k] -> r[k],
+ * count <= 8.  Same semantics as `count` usn_classify calls. */
+int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
+                       void *hip_stream);
 
 /* Ordered host stage for one classified batch (synchronises the stream).
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in

@@ -183,3 +183,35 @@ def test_offsets_layout(coracle_mod):
     got = r.decisions()
     assert ((got & katrun.PARITY_MASK) == (want & katrun.PARITY_MASK)).all()
     ctx.close()
+
+
+def test_classify_multi_matches_separate(coracle_mod):
+    """One launch over the drained rings of several NICs (usn_classify_multi)
+    gives each source exactly its sequential decisions and carried cache."""
+    import ctypes as C
+    from usnetd_amd import lib, traffic
+    cfgs = [traffic.config("c2", n=n, seed=40 + k) for k, n in enumerate([5000, 1024, 20000])]
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfgs[0])
+    nics = [0] + traffic.extra_nics(cfgs[0], 2, ctx)
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfgs[0])
+    for nid in nics[1:]:
+        o.add_endpoint(nid, 0, -1)
+    s = ctx.stream()
+    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k], stride=c.stride) for k, c in enumerate(cfgs)]
+    for rep in range(2):                      # the second launch uses the device-carried caches
+        rs = [lib.DeviceResult(ctx, c.n) for c in cfgs]
+        ba = (lib.Batch * 3)(*[b.desc for b in bs])
+        ra = (lib.Result * 3)(*[r.desc for r in rs])
+        lib.check(ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 3, s))
+        for k, c in enumerate(cfgs):
+            ctx.finalize(bs[k], rs[k], s)
+            want = o.forward_batch(nics[k], c.frames, c.lens, stride=c.stride)
+            got = rs[k].decisions()
+            assert ((got & katrun.PARITY_MASK) == (want & katrun.PARITY_MASK)).all(), (rep, k)
+    # the same source twice in one launch is refused
+    ba = (lib.Batch * 2)(bs[0].desc, bs[0].desc)
+    ra = (lib.Result * 2)(rs[0].desc, rs[1].desc)
+    assert ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 2, s) == -22
+    ctx.close()

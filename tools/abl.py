@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--streams", type=int, default=1,
                     help="round-robin batches over S streams, one NIC rx queue (source) each")
+    ap.add_argument("--multi", type=int, default=1,
+                    help="classify Q batches of Q distinct rx queues per launch (usn_classify_multi)")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     names = a.variants or sorted(os.listdir(os.path.join(ROOT, "build", "abl")))
@@ -39,16 +41,24 @@ def main():
         path = os.path.join(ROOT, "build", "abl", nm, "libusn.so")
         ctx = lib.Ctx(0, libpath=path)
         traffic.install_ctx(ctx, cfgs[0])
-        nics = [0] + list(traffic.extra_nics(cfgs[0], a.streams - 1, ctx))
-        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k % a.streams], stride=c.stride)
+        nq = max(a.streams, a.multi)
+        nics = [0] + list(traffic.extra_nics(cfgs[0], nq - 1, ctx))
+        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k % nq], stride=c.stride)
               for k, c in enumerate(cfgs)]
         rs = [lib.DeviceResult(ctx, a.frames) for _ in cfgs]
         s = ctx.stream()
         ss = [s] + [ctx.stream() for _ in range(a.streams - 1)]
         evs = [(ctx.event(), ctx.event()) for _ in range(a.launches)]
         e0, e1 = ctx.event(), ctx.event()
+        groups = []
+        if a.multi > 1:
+            assert a.batches % a.multi == 0
+            for g in range(a.batches // a.multi):
+                ba = (lib.Batch * a.multi)(*[bs[g * a.multi + j].desc for j in range(a.multi)])
+                ra = (lib.Result * a.multi)(*[rs[g * a.multi + j].desc for j in range(a.multi)])
+                groups.append((ba, ra))
         runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, ss=ss, evs=evs, e0=e0, e1=e1, per=[], b2b=[],
-                        ejoin=[ctx.event() for _ in ss])
+                        ejoin=[ctx.event() for _ in ss], groups=groups)
     for rnd in range(a.rounds):
         for nm in names:
             R = runs[nm]
@@ -56,11 +66,19 @@ def main():
             L = ctx.L
             bd = [C.byref(b.desc) for b in R["bs"]]
             rd = [C.byref(r.desc) for r in R["rs"]]
+            G = R["groups"]
+
+            def launch(i, stream):
+                if G:
+                    ba, ra = G[i % len(G)]
+                    return L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p),
+                                                a.multi, stream)
+                return L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], stream)
             for i in range(10):
-                L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+                launch(i, s)
             for i, (x, y) in enumerate(R["evs"]):
                 ctx.record(x, s)
-                rc = L.usn_classify(ctx.h, bd[i % len(bd)], rd[i % len(rd)], s)
+                rc = launch(i, s)
                 assert rc == 0, rc
                 ctx.record(y, s)
             ctx.sync(s)
@@ -71,14 +89,17 @@ def main():
                 ctx.wait_event(x, R["e0"])
             for i in range(a.launches):
                 # batch k always goes to stream k % S (its rx queue): per-source order kept
-                k = i % len(bd)
-                L.usn_classify(ctx.h, bd[k], rd[k], ss[k % len(ss)])
+                if G:
+                    launch(i, ss[i % len(ss)])
+                else:
+                    k = i % len(bd)
+                    L.usn_classify(ctx.h, bd[k], rd[k], ss[k % len(ss)])
             for x, ej in zip(ss[1:], R["ejoin"]):
                 ctx.record(ej, x)
                 ctx.wait_event(s, ej)
             ctx.record(R["e1"], s)
             ctx.sync(s)
-            R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches)
+                R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches / max(1, a.multi))
     ref = None
     out = {}
     for nm in names:
@@ -87,7 +108,7 @@ def main():
         if ref is None:
             ref = d
         same = bool(((d ^ ref) & lib.PARITY_MASK).max() == 0) if d.shape == ref.shape else False
-        med = statistics.median(R["per"])
+        med = statistics.median(R["per"]) / max(1, a.multi)   # per batch
         b2b = statistics.median(R["b2b"])
         gbs = 72 * a.frames / (med * 1e-6) / 1e9
         out[nm] = dict(kernel_us=round(med, 2), kernel_us_min=round(min(R["per"]), 2),

@@ -168,6 +168,9 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
                                               const Parsed &p) {
   const bool has = p.has_ports != 0;
   uint32_t w1 = 0, w2 = 0;
+#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
+  w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
+#else
   if (a.probe_mask & 1u)
     w1 = probe(T, a.bucket_mask, p.dst, p.src, has ? (p.dport | (p.sport << 16)) : 0u,
                usn_key_meta(p.proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT)
@@ -175,6 +178,7 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
   if (a.probe_mask & 2u)
     w2 = probe(T, a.bucket_mask, p.dst, 0u, has ? p.dport : 0u,
                usn_key_meta(p.proto, has ? USN_WANT_DPORT : 0u));
+#endif
   const uint32_t w = w1 ? w1 : w2;
   const uint32_t owner = w >> 16;
   const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
@@ -465,11 +469,15 @@ __device__ __forceinline__ void issue_round(const ClassifyArgs &a, uint64_t base
 
 /* --------------------------------------------------------------------------- */
 template <bool LDS, bool DENSE>
-__global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(ClassifyArgs a) {
+__global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   extern __shared__ __align__(16) uint8_t smem[];
+  uint32_t bi = 0;                       // which batch of the launch (uniform)
+  for (uint32_t k = 1; k < m.count; ++k)
+    if (blockIdx.x >= m.tile_base[k]) bi = k;
+  const ClassifyArgs &a = m.b[bi];
   const Lds L = carve(smem, a.nbins, DENSE);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;
+  const uint32_t tile = blockIdx.x - m.tile_base[bi];
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   STAMP_DECL
@@ -719,20 +727,27 @@ size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_ld
          (table_in_lds ? (size_t)table_slots * 16 : 0);
 }
 
+/* The dense-layout transpose (coalesced 1 KiB loads + LDS transpose) is an
+ * experiment: with launches overlapping, per-lane loads (no LDS traffic) were
+ * faster (tools/abl.py, 3 streams: 13.8 vs 15.2 us per 1M frames). */
 #ifndef USN_DENSE
-#define USN_DENSE 1
+#define USN_DENSE 0
 #endif
 
-hipError_t launch_classify(const ClassifyArgs &a, hipStream_t stream) {
-  if (a.ntiles == 0) return hipSuccess;
+hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
+  const uint32_t tiles = m.tile_base[m.count];
+  if (tiles == 0) return hipSuccess;
+  const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
-  const bool dense = USN_DENSE && a.stride == 64 && a.offsets == nullptr;
+  bool dense = USN_DENSE != 0;
+  for (uint32_t k = 0; k < m.count; ++k)
+    dense = dense && m.b[k].stride == 64 && m.b[k].offsets == nullptr;
   const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, dense);
-  const dim3 g(a.ntiles), b(NTHREADS);
-  if (in_lds && dense) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, a);
-  else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, a);
-  else if (dense) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, a);
-  else hipLaunchKernelGGL((classify_rx_kernel<false, false>), g, b, lds, stream, a);
+  const dim3 g(tiles), b(NTHREADS);
+  if (in_lds && dense) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
+  else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);
+  else if (dense) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, m);
+  else hipLaunchKernelGGL((classify_rx_kernel<false, false>), g, b, lds, stream, m);
   return hipGetLastError();
 }
 

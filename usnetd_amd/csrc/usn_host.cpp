@@ -638,38 +638,63 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   return USN_OK;
 }
 
-int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
-  if (!c || !b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
+static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
+  if (!b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
   if ((b->stride == 0) == (b->offsets == nullptr)) return USN_EINVAL;
   if (b->stride && (b->stride % 16 != 0 || b->stride < USN_WINDOW)) return USN_EINVAL;
   if (((uintptr_t)b->frames & 15) != 0) return USN_EINVAL;
   if (b->n > 0xFFFFFFFFull) return USN_ERANGE;
-  std::lock_guard<std::mutex> g(c->mu);
   if (b->src_endpoint >= USN_MAX_ENDPOINTS || !c->eps[b->src_endpoint].used) return USN_EINVAL;
   if (c->eps[b->src_endpoint].kind != USN_EP_NIC) return USN_EINVAL;   // tx: not yet on device
+  return USN_OK;
+}
+
+int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t count,
+                       void *stream) {
+  if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (uint32_t k = 0; k < count; ++k) {
+    int st = check_batch(c, &b[k], &r[k]);
+    if (st) return st;
+    for (uint32_t j = 0; j < k; ++j)
+      if (b[j].src_endpoint == b[k].src_endpoint) return USN_EINVAL;   // one batch per source
+  }
   HIPCHK(hipSetDevice(c->device));
   if (c->table_dirty) { int s = rebuild_table(c); if (s) return s; }
   if (c->bridge_dirty) { int s = rebuild_bridge(c); if (s) return s; }
-  ClassifyArgs a;
-  fill_args(c, b, r, a);
-  Chain &ch = c->chains[b->src_endpoint];
-  if (ch.device_chain) {
-    a.carry_mode = usn::CARRY_CHAIN;
-    a.prev_tiles = ch.tiles;
-    a.prev_ntiles = ch.ntiles;
-    a.prev_summary = ch.summary;
-  } else {
-    a.carry_mode = usn::CARRY_EXPLICIT;
-    a.cin_state = ch.state;
-    a.cin_dst = ch.dst;
-    std::memcpy(a.cin_info, ch.info, sizeof ch.info);
+  usn::MultiArgs m;
+  std::memset(&m, 0, sizeof m);
+  m.count = count;
+  for (uint32_t k = 0; k < count; ++k) {
+    ClassifyArgs &a = m.b[k];
+    fill_args(c, &b[k], &r[k], a);
+    Chain &ch = c->chains[b[k].src_endpoint];
+    if (ch.device_chain) {
+      a.carry_mode = usn::CARRY_CHAIN;
+      a.prev_tiles = ch.tiles;
+      a.prev_ntiles = ch.ntiles;
+      a.prev_summary = ch.summary;
+    } else {
+      a.carry_mode = usn::CARRY_EXPLICIT;
+      a.cin_state = ch.state;
+      a.cin_dst = ch.dst;
+      std::memcpy(a.cin_info, ch.info, sizeof ch.info);
+    }
+    m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
-  HIPCHK(usn::launch_classify(a, (hipStream_t)stream));
-  ch.device_chain = true;
-  ch.tiles = r->tiles;
-  ch.ntiles = a.ntiles;
-  ch.summary = r->summary;
+  HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+  for (uint32_t k = 0; k < count; ++k) {
+    Chain &ch = c->chains[b[k].src_endpoint];
+    ch.device_chain = true;
+    ch.tiles = r[k].tiles;
+    ch.ntiles = m.b[k].ntiles;
+    ch.summary = r[k].summary;
+  }
   return USN_OK;
+}
+
+int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
+  return usn_classify_multi(c, b, r, 1, stream);
 }
 
 /* ---- ordered host stage --------------------------------------------------- */

@@ -53,11 +53,20 @@ struct ClassifyArgs {
   const usn_summary *prev_summary;
 };
 
+/* Several batches (distinct sources) classified by one launch: workgroup w
+ * takes tile w - tile_base[i] of batch i, tile_base[i] <= w < tile_base[i+1]. */
+#define USN_MAX_MULTI 8
+struct MultiArgs {
+  ClassifyArgs b[USN_MAX_MULTI];
+  uint32_t tile_base[USN_MAX_MULTI + 1];
+  uint32_t count;
+};
+
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense);
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
 
-hipError_t launch_classify(const ClassifyArgs &a, hipStream_t stream);
+hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
 /* Rebuild order/runs/counts of tiles [t0, t1) from the (patched) decisions. */
 hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
 

@@ -104,6 +104,7 @@ def load(path: str | None = None):
         "usn_event_record": ([P, P, P], I),
         "usn_event_elapsed_ms": ([P, P, P, C.POINTER(C.c_float)], I),
         "usn_stream_wait_event": ([P, P, P], I),
+        "usn_classify_multi": ([P, P, P, U32, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -121,7 +122,7 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_host_alloc_pinned", "usn_host_free_pinned", "usn_memcpy_h2d", "usn_memcpy_d2h",
             "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
             "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
-            "usn_event_elapsed_ms", "usn_stream_wait_event"]
+            "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi"]
 
 
 def check(rc, what=""):
