@@ -42,6 +42,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--launch-probe", type=int, default=100, help="per-launch event pairs")
+    ap.add_argument("--queues", type=int, default=4,
+                    help="NIC rx queues (sources) drained per poll round; their batches are "
+                         "classified by one usn_classify_multi launch")
     return ap.parse_args()
 
 
@@ -61,48 +64,70 @@ def main():
 
     defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20}
     n = args.frames or defaults[args.config]
+    Q = max(1, min(args.queues, 8))
+    nb = max(args.batches, 2 * Q)
+    nb -= nb % Q
     ctx = lib.Ctx(local)
     batches, results, cfg0 = [], [], None
-    for k in range(args.batches):
+    nics = None
+    for k in range(nb):
         cfg = traffic.config(args.config, n=n, seed=1000 * rank + 17 * k + 2)
         if k == 0:
             cfg0 = cfg
             traffic.install_ctx(ctx, cfg)
-        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride))
+            nics = [cfg.src] + traffic.extra_nics(cfg, Q - 1, ctx)
+        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, nics[k % Q], stride=cfg.stride))
         results.append(lib.DeviceResult(ctx, n))
         if k:
             del cfg
     stream = ctx.stream()
-    classify = L.usn_classify
     h = ctx.h
+    # launch groups: batches [gQ, gQ+Q) of the Q queues, one launch each
+    groups = []
+    for g in range(nb // Q):
+        ba = (lib.Batch * Q)(*[batches[g * Q + j].desc for j in range(Q)])
+        ra = (lib.Result * Q)(*[results[g * Q + j].desc for j in range(Q)])
+        groups.append((C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), ba, ra))
+    multi = L.usn_classify_multi
+    single = L.usn_classify
     bdesc = [C.byref(b.desc) for b in batches]
     rdesc = [C.byref(r.desc) for r in results]
-    nb = len(batches)
 
-    def step(i):
-        rc = classify(h, bdesc[i % nb], rdesc[i % nb], stream)
+    def launch(i, q=Q, count=None):
+        """Launch i of a q-queue run: `count` (default q) batches -> that many steps."""
+        if q == 1:
+            rc = single(h, bdesc[i % nb], rdesc[i % nb], stream)
+        else:
+            g = groups[i % len(groups)]
+            rc = multi(h, g[0], g[1], count or q, stream)
         if rc:
             lib.check(rc, "usn_classify")
 
-    for i in range(args.warmup):
-        step(i)
-    ctx.sync(stream)
-    if dist:
-        dist.barrier()
-    ctx.sync()
+    def timed(steps, q):
+        """Exactly `steps` batches, q per launch (the last launch takes the rest)."""
+        full, rest = divmod(steps, q)
+        ctx.sync(stream)
+        if dist:
+            dist.barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.record(ev0, stream)
+        for i in range(full):
+            launch(i, q)
+        if rest:
+            launch(full, q, rest)
+        ctx.record(ev1, stream)
+        ctx.sync(stream)
+        ctx.sync()
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        return t1 - t0, ctx.elapsed_ms(ev0, ev1), steps
+
     ev0, ev1 = ctx.event(), ctx.event()
-    t0 = time.perf_counter()
-    ctx.record(ev0, stream)
-    for i in range(args.steps):
-        step(args.warmup + i)
-    ctx.record(ev1, stream)
-    ctx.sync(stream)
-    ctx.sync()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    wall = t1 - t0
-    ev_ms = ctx.elapsed_ms(ev0, ev1)
+    for i in range((args.warmup + Q - 1) // Q):
+        launch(i)
+    wall, ev_ms, done = timed(args.steps, Q)
     elapsed = wall
     if dist:
         import torch
@@ -112,51 +137,61 @@ def main():
 
     # every batch of the last rotation: the ordered host stage had nothing to do
     host_frames, flags = 0, 0
+    cls = [0, 0, 0, 0]
     for k in range(nb):
         info = ctx.finalize(batches[k], results[k], stream)
         host_frames += info.n_host
         flags |= info.flags
-    cls = list(info.class_count)
+        cls = [x + y for x, y in zip(cls, info.class_count)]
 
     # per-launch kernel duration (HIP events on the launch stream)
     probe = []
     evs = [(ctx.event(), ctx.event()) for _ in range(args.launch_probe)]
-    for i, (a, b) in enumerate(evs):
-        ctx.record(a, stream)
-        step(i)
-        ctx.record(b, stream)
+    for i, (ea, eb) in enumerate(evs):
+        ctx.record(ea, stream)
+        launch(i)
+        ctx.record(eb, stream)
     ctx.sync(stream)
-    for a, b in evs:
-        probe.append(ctx.elapsed_ms(a, b))
-    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, args.steps)
-    achieved = ALGO_BYTES * n / (kern_ms * 1e-3) / 1e9
+    for ea, eb in evs:
+        probe.append(ctx.elapsed_ms(ea, eb))
+    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, done // Q)
+    achieved = ALGO_BYTES * n * Q / (kern_ms * 1e-3) / 1e9
 
-    total_frames = world * args.steps * n
+    # the same batches one per launch (single rx queue), for reference
+    single_mpps = None
+    if Q > 1 and args.steps >= 4:
+        w1, _, d1 = timed(max(4, args.steps // 2), 1)
+        single_mpps = round(d1 * n / w1 / 1e6, 1)
+
+    total_frames = world * done * n
     value = total_frames / elapsed / 1e6
     out = {
         "metric": "Mpkts/s device-resident L4 classify @64B frames; HBM GB/s vs roofline",
         "value": round(value, 2),
         "unit": "Mpkts/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": done,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "ms_per_step": round(elapsed * 1e3 / done, 5),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic frames generated on the host (no captures), resident in HBM",
         "config": {
-            "workload": "%s: %d x 64B IPv4/UDP frames per batch, %d-rule endpoint table, NIC rx"
-                        % (args.config, n, len(cfg0.rules)),
+            "workload": "%s: %d x 64B IPv4/UDP frames per batch (one drained rx ring), %d-rule "
+                        "endpoint table, NIC rx; %d rx queues per poll round, one launch each"
+                        % (args.config, n, len(cfg0.rules), Q),
             "frames_per_batch": n,
+            "rx_queues_per_launch": Q,
             "rotating_batches": nb,
             "rotating_bytes": int(nb * (n * cfg0.stride + n * 2)),
             "parallelism": "replicas%d" % world,
             "host_stage_frames": int(host_frames),
             "summary_flags": int(flags),
-            "class_count_last_batch": cls,
-            "event_ms_per_step": round(ev_ms / args.steps, 5),
+            "class_count_last_rotation": [int(x) for x in cls],
+            "event_ms_per_step": round(ev_ms / done, 5),
+            "single_queue_mpps": single_mpps,
         },
         "roofline": {
             "bound": "hbm",
@@ -167,6 +202,7 @@ def main():
             "traffic": None,
             "kernel": "classify_rx_kernel",
             "kernel_us_median": round(kern_ms * 1e3, 3),
+            "batches_per_launch": Q,
             "algo_bytes_per_frame": ALGO_BYTES,
         },
         "cpu_baseline": None,
@@ -176,7 +212,7 @@ def main():
         try:
             with open(pmc) as fh:
                 pm = json.load(fh)
-            if int(pm.get("frames_per_batch", -1)) == n:
+            if int(pm.get("frames_per_launch", -1)) == n * Q:
                 out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
                 out["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
         except Exception:

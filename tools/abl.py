@@ -99,7 +99,7 @@ def main():
                 ctx.wait_event(s, ej)
             ctx.record(R["e1"], s)
             ctx.sync(s)
-                R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches / max(1, a.multi))
+            R["b2b"].append(ctx.elapsed_ms(R["e0"], R["e1"]) * 1e3 / a.launches / max(1, a.multi))
     ref = None
     out = {}
     for nm in names:
