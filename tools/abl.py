@@ -90,7 +90,7 @@ def main():
             for i in range(a.launches):
                 # batch k always goes to stream k % S (its rx queue): per-source order kept
                 if G:
-                    launch(i, ss[i % len(ss)])
+                    launch(i, ss[(i % len(G)) % len(ss)])
                 else:
                     k = i % len(bd)
                     L.usn_classify(ctx.h, bd[k], rd[k], ss[k % len(ss)])
