@@ -42,9 +42,11 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--launch-probe", type=int, default=100, help="per-launch event pairs")
-    ap.add_argument("--queues", type=int, default=4,
-                    help="NIC rx queues (sources) drained per poll round; their batches are "
-                         "classified by one usn_classify_multi launch")
+    ap.add_argument("--queues", type=int, default=8,
+                    help="NIC rx queues (sources) drained per poll round")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams; stream s owns queues [s*Q/S, (s+1)*Q/S) and classifies "
+                         "their drained rings with one usn_classify_multi launch per round")
     return ap.parse_args()
 
 
@@ -64,9 +66,12 @@ def main():
 
     defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20}
     n = args.frames or defaults[args.config]
-    Q = max(1, min(args.queues, 8))
-    nb = max(args.batches, 2 * Q)
-    nb -= nb % Q
+    S = max(1, args.streams)
+    Qt = max(S, args.queues - args.queues % S)   # rx queues in total
+    P = min(8, Qt // S)                           # queues (batches) per launch
+    Qt = P * S
+    R = max(2, -(-args.batches // Qt))            # rounds of distinct batches rotated through
+    nb = R * Qt
     ctx = lib.Ctx(local)
     batches, results, cfg0 = [], [], None
     nics = None
@@ -75,47 +80,58 @@ def main():
         if k == 0:
             cfg0 = cfg
             traffic.install_ctx(ctx, cfg)
-            nics = [cfg.src] + traffic.extra_nics(cfg, Q - 1, ctx)
-        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, nics[k % Q], stride=cfg.stride))
+            nics = [cfg.src] + traffic.extra_nics(cfg, Qt - 1, ctx)
+        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, nics[k % Qt], stride=cfg.stride))
         results.append(lib.DeviceResult(ctx, n))
         if k:
             del cfg
-    stream = ctx.stream()
+    streams = [ctx.stream() for _ in range(S)]
+    stream = streams[0]
     h = ctx.h
-    # launch groups: batches [gQ, gQ+Q) of the Q queues, one launch each
-    groups = []
-    for g in range(nb // Q):
-        ba = (lib.Batch * Q)(*[batches[g * Q + j].desc for j in range(Q)])
-        ra = (lib.Result * Q)(*[results[g * Q + j].desc for j in range(Q)])
-        groups.append((C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), ba, ra))
+    # launch (round r, stream s): the batches of queues [sP, sP+P) of round r
+    groups = {}
+    for r in range(R):
+        for si in range(S):
+            ks = [r * Qt + si * P + j for j in range(P)]
+            ba = (lib.Batch * P)(*[batches[k].desc for k in ks])
+            ra = (lib.Result * P)(*[results[k].desc for k in ks])
+            groups[(r, si)] = (C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), ba, ra)
     multi = L.usn_classify_multi
     single = L.usn_classify
     bdesc = [C.byref(b.desc) for b in batches]
     rdesc = [C.byref(r.desc) for r in results]
+    joins = [ctx.event() for _ in streams]
 
-    def launch(i, q=Q, count=None):
-        """Launch i of a q-queue run: `count` (default q) batches -> that many steps."""
-        if q == 1:
+    def launch(i, per=P, count=None):
+        """Launch i: `count` (default per) batches of one stream's queues."""
+        if per == 1:
             rc = single(h, bdesc[i % nb], rdesc[i % nb], stream)
         else:
-            g = groups[i % len(groups)]
-            rc = multi(h, g[0], g[1], count or q, stream)
+            si = i % S
+            g = groups[((i // S) % R, si)]
+            rc = multi(h, g[0], g[1], count or per, streams[si])
         if rc:
             lib.check(rc, "usn_classify")
 
-    def timed(steps, q):
-        """Exactly `steps` batches, q per launch (the last launch takes the rest)."""
-        full, rest = divmod(steps, q)
-        ctx.sync(stream)
+    def timed(steps, per):
+        """Exactly `steps` batches, `per` per launch (the last launch takes the rest)."""
+        full, rest = divmod(steps, per)
+        for x in streams:
+            ctx.sync(x)
         if dist:
             dist.barrier()
         ctx.sync()
         t0 = time.perf_counter()
         ctx.record(ev0, stream)
+        for x in streams[1:]:
+            ctx.wait_event(x, ev0)
         for i in range(full):
-            launch(i, q)
+            launch(i, per)
         if rest:
-            launch(full, q, rest)
+            launch(full, per, rest)
+        for x, ej in zip(streams[1:], joins[1:]):
+            ctx.record(ej, x)
+            ctx.wait_event(stream, ej)
         ctx.record(ev1, stream)
         ctx.sync(stream)
         ctx.sync()
@@ -125,9 +141,9 @@ def main():
         return t1 - t0, ctx.elapsed_ms(ev0, ev1), steps
 
     ev0, ev1 = ctx.event(), ctx.event()
-    for i in range((args.warmup + Q - 1) // Q):
+    for i in range(-(-args.warmup // P)):
         launch(i)
-    wall, ev_ms, done = timed(args.steps, Q)
+    wall, ev_ms, done = timed(args.steps, P)
     elapsed = wall
     if dist:
         import torch
@@ -138,28 +154,32 @@ def main():
     # every batch of the last rotation: the ordered host stage had nothing to do
     host_frames, flags = 0, 0
     cls = [0, 0, 0, 0]
+    for x in streams:
+        ctx.sync(x)
     for k in range(nb):
-        info = ctx.finalize(batches[k], results[k], stream)
+        info = ctx.finalize(batches[k], results[k], streams[(k % Qt) // P])
         host_frames += info.n_host
         flags |= info.flags
         cls = [x + y for x, y in zip(cls, info.class_count)]
 
     # per-launch kernel duration (HIP events on the launch stream)
+    # (one stream at a time: a launch's duration is not shared with another's)
     probe = []
     evs = [(ctx.event(), ctx.event()) for _ in range(args.launch_probe)]
     for i, (ea, eb) in enumerate(evs):
-        ctx.record(ea, stream)
+        si = i % S
+        ctx.record(ea, streams[si])
         launch(i)
-        ctx.record(eb, stream)
-    ctx.sync(stream)
+        ctx.record(eb, streams[si])
+        ctx.sync(streams[si])
     for ea, eb in evs:
         probe.append(ctx.elapsed_ms(ea, eb))
-    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, done // Q)
-    achieved = ALGO_BYTES * n * Q / (kern_ms * 1e-3) / 1e9
+    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, done // P)
+    achieved = ALGO_BYTES * n * P / (kern_ms * 1e-3) / 1e9
 
     # the same batches one per launch (single rx queue), for reference
     single_mpps = None
-    if Q > 1 and args.steps >= 4:
+    if P > 1 and args.steps >= 4:
         w1, _, d1 = timed(max(4, args.steps // 2), 1)
         single_mpps = round(d1 * n / w1 / 1e6, 1)
 
@@ -180,10 +200,12 @@ def main():
         "data": "synthetic frames generated on the host (no captures), resident in HBM",
         "config": {
             "workload": "%s: %d x 64B IPv4/UDP frames per batch (one drained rx ring), %d-rule "
-                        "endpoint table, NIC rx; %d rx queues per poll round, one launch each"
-                        % (args.config, n, len(cfg0.rules), Q),
+                        "endpoint table, NIC rx; %d rx queues on %d streams, %d rings per launch"
+                        % (args.config, n, len(cfg0.rules), Qt, S, P),
             "frames_per_batch": n,
-            "rx_queues_per_launch": Q,
+            "rx_queues": Qt,
+            "streams": S,
+            "batches_per_launch": P,
             "rotating_batches": nb,
             "rotating_bytes": int(nb * (n * cfg0.stride + n * 2)),
             "parallelism": "replicas%d" % world,
@@ -202,7 +224,7 @@ def main():
             "traffic": None,
             "kernel": "classify_rx_kernel",
             "kernel_us_median": round(kern_ms * 1e3, 3),
-            "batches_per_launch": Q,
+            "batches_per_launch": P,
             "algo_bytes_per_frame": ALGO_BYTES,
         },
         "cpu_baseline": None,
@@ -212,7 +234,7 @@ def main():
         try:
             with open(pmc) as fh:
                 pm = json.load(fh)
-            if int(pm.get("frames_per_launch", -1)) == n * Q:
+            if int(pm.get("frames_per_launch", -1)) == n * P:
                 out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
                 out["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
         except Exception:

@@ -23,7 +23,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     testsall) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
+    prof) rm -rf gpurun_out/prof; step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline ;;
     abl) step abl 600 python tools/abl.py --json gpurun_out/abl.json ${ABL_ARGS:-} ;;
     stamps) step stamps 300 python tools/stamps.py ${STAMP_ARGS:-c2} ;;
     ablms) step ablms 600 python tools/abl.py --streams ${NSTREAMS:-2} --batches 6 --json gpurun_out/ablms.json ${ABL_VARIANTS:-base loadonly} ;;
@@ -40,8 +40,11 @@ for s in ${STEPS:-tests smoke bench prof}; do
         step pmc$i 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 tools/kbench.py ${KB_ARGS:-c2 1048576 30}
       done
       step pmcsum 60 python3 tools/pmc_summary.py gpurun_out/pmc ;;
-    pmc) step pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --launch-probe 0 ;;
-    pmcw) step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --launch-probe 0 ;;
+    traffic)
+      rm -rf gpurun_out/pmcf gpurun_out/pmcw
+      step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf -o run -- python3 bench.py --steps 64 --warmup 8 --no-cpu-baseline --launch-probe 0
+      step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --steps 64 --warmup 8 --no-cpu-baseline --launch-probe 0
+      step pmctraffic 60 python3 tools/pmc_traffic.py gpurun_out/pmcf gpurun_out/pmcw ${PMC_FRAMES:-4194304} gpurun_out/pmc_c2.json ;;
   esac
 done
 echo "=== done"
