@@ -15,18 +15,21 @@ import statistics
 import sys
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, frames):
+    """Counter values of the classify dispatches covering `frames` frames
+    (grid = frames / 4 threads: 256-thread workgroups of 1024 frames)."""
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "classify_rx_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter:
+            if ("classify_rx_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter
+                    and int(r["Grid_Size"]) == frames // 4):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
 
 fd, wd, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-fetch = per_dispatch(fd, "FETCH_SIZE")
-write = per_dispatch(wd, "WRITE_SIZE")
+fetch = per_dispatch(fd, "FETCH_SIZE", frames)
+write = per_dispatch(wd, "WRITE_SIZE", frames)
 f_kb = statistics.median(fetch)
 w_kb = statistics.median(write)
 read_algo = frames * (64 + 2)
