@@ -55,7 +55,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    from usnetd_amd import lib, traffic
+    from usnetd_amd import lib, shard, traffic
     L = lib.load()            # the HIP runtime is loaded here, before torch (if any)
     dist = None
     if world > 1:
@@ -76,7 +76,7 @@ def main():
     batches, results, cfg0 = [], [], None
     nics = None
     for k in range(nb):
-        cfg = traffic.config(args.config, n=n, seed=1000 * rank + 17 * k + 2)
+        cfg = traffic.config(args.config, n=n, seed=shard.batch_seed(rank, k))
         if k == 0:
             cfg0 = cfg
             traffic.install_ctx(ctx, cfg)
@@ -144,12 +144,7 @@ def main():
     for i in range(-(-args.warmup // P)):
         launch(i)
     wall, ev_ms, done = timed(args.steps, P)
-    elapsed = wall
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(wall, dist)
 
     # every batch of the last rotation: the ordered host stage had nothing to do
     host_frames, flags = 0, 0

@@ -1,0 +1,89 @@
+"""world_size-2 gloo tests of the multi-GPU path (CPU only, no GPU needed).
+
+Replicas only: each rank owns disjoint rx queues (sources) and a replica of
+the rule table.  The per-rank classifier here is the C oracle standing in for
+the device (the GPU path is covered by tests/test_gpu_parity.py); what is
+tested is the partitioning: every queue is classified exactly once, the
+union of the ranks' per-queue decision streams equals a single process
+classifying every queue, and the timing reduction is a max over ranks."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from usnetd_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _classify_queues(queues, n):
+    import coracle
+    from usnetd_amd import traffic
+    out = {}
+    o = coracle.Oracle()
+    base = traffic.config("c2", n=n, seed=shard.batch_seed(0, 0))
+    coracle.install_oracle(o, base)
+    first = max(e[0] for e in base.endpoints) + 1
+    for q in range(8):
+        if q:
+            o.add_endpoint(first + q - 1, 0, -1)
+    for q in queues:
+        src = 0 if q == 0 else first + q - 1
+        cfg = traffic.config("c2", n=n, seed=shard.batch_seed(0, 1 + q))
+        d = o.forward_batch(src, cfg.frames, cfg.lens, stride=cfg.stride)
+        out[q] = d.tolist()
+    return out
+
+
+def _worker(rank, world, port, n, ret):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = shard.rank_queues(8, world, rank)
+    res = _classify_queues(mine, n)
+    elapsed = shard.max_over_ranks(1.0 + rank, dist)
+    allres = shard.gather_objects(res, dist)
+    if rank == 0:
+        merged = {}
+        for r in allres:
+            assert not set(r) & set(merged), "a queue was classified twice"
+            merged.update(r)
+        ret["merged"] = merged
+        ret["elapsed"] = elapsed
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_queues_partition():
+    for world in (1, 2, 3, 4, 8):
+        got = [q for r in range(world) for q in shard.rank_queues(8, world, r)]
+        assert got == list(range(8))
+    with pytest.raises(ValueError):
+        shard.rank_queues(2, 4, 0)
+    assert shard.batch_seed(0, 3) != shard.batch_seed(1, 3)
+
+
+def test_two_rank_replicas_match_single_process():
+    import coracle
+    coracle.build()
+    n = 3000
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), n, ret), nprocs=2, join=True)
+    single = _classify_queues(list(range(8)), n)
+    merged = dict(ret["merged"])
+    assert sorted(merged) == list(range(8))
+    for q in range(8):
+        assert np.array_equal(np.array(merged[q]) & 0xFFFFFF, np.array(single[q]) & 0xFFFFFF), q
+    assert ret["elapsed"] == 2.0      # max over ranks (rank 1 reported 2.0)
