@@ -48,6 +48,7 @@ extern "C" {
 #define USN_EHIP (-5)        /* HIP runtime error; usn_last_hip_error() */
 #define USN_ENODEV (-19)     /* no gfx950 device */
 #define USN_ERANGE (-34)
+#define USN_EBUSY (-16)      /* a tx batch awaits usn_finalize (shared state not final yet) */
 
 /* ---- decision word (u32), one per frame --------------------------------
  *   [15:0]  endpoint id (0xFFFF = none)            Target::Endpoint/EndpointRef
@@ -203,11 +204,15 @@ int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
  * Asynchronous: writes decisions, per-tile order/runs and the summary.
  * Consecutive batches of one source may be enqueued back to back; the 1-entry
  * decision cache is carried on the device from the previous batch's result,
- * which must stay allocated until this call's work has been enqueued. */
+ * which must stay allocated until this call's work has been enqueued.
+ * A batch sent by a non-NIC endpoint (tx: find_forward with incoming ==
+ * false) learns bridge MACs and answer rules; until its usn_finalize every
+ * other call that reads or changes the registry returns USN_EBUSY. */
 int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream);
 /* Several drained rings of DISTINCT sources (e.g. the rx queues of the NICs
  * polled in one poll() round, main.rs:1029-1046) in one launch: b[k] -> r[k],
- * count <= 8.  Same semantics as `count` usn_classify calls. */
+ * count <= 8.  Same semantics as `count` usn_classify calls.  A tx batch
+ * must be classified alone (count == 1). */
 int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
                        void *hip_stream);
 

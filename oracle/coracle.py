@@ -69,6 +69,7 @@ def lib():
         L.uso_remove_match.argtypes = [P, C.POINTER(Want), C.c_int]
         L.uso_lookup.argtypes = [P, C.POINTER(Want)]
         L.uso_rule_count.argtypes = [P]
+        L.uso_rules.argtypes = [P, P, P, P, C.c_int]
         L.uso_bridge_add.argtypes = [P, C.c_char_p]
         L.uso_bridge_count.argtypes = [P]
         L.uso_frag_clear.argtypes = [P]
@@ -114,6 +115,24 @@ class Oracle:
 
     def lookup(self, want: Want) -> int:
         return self.L.uso_lookup(self.h, C.byref(want))
+
+    def rule_count(self) -> int:
+        return self.L.uso_rule_count(self.h)
+
+    def rules(self):
+        """[(dst, src, dport, sport, proto, mask, owner)] with absent fields zeroed."""
+        n = self.rule_count()
+        ws = (Want * max(n, 1))()
+        owners = np.zeros(max(n, 1), np.int32)
+        sticky = np.zeros(max(n, 1), np.uint8)
+        got = self.L.uso_rules(self.h, C.cast(ws, C.c_void_p), owners.ctypes.data,
+                               sticky.ctypes.data, n)
+        return [(w.dst_addr, w.src_addr if w.mask & 2 else 0, w.dst_port if w.mask & 1 else 0,
+                 w.src_port if w.mask & 4 else 0, w.protocol, w.mask, int(owners[i]))
+                for i, w in enumerate(ws[:got])]
+
+    def bridge_count(self) -> int:
+        return self.L.uso_bridge_count(self.h)
 
     def bridge_add(self, mac: bytes):
         self.L.uso_bridge_add(self.h, bytes(mac))

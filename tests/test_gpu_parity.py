@@ -34,15 +34,15 @@ def test_library_is_native_and_gfx950():
 
 
 @pytest.mark.parametrize("kat", katrun.load_kats(), ids=lambda k: k["name"])
-@pytest.mark.xfail(reason="tx direction not yet on the device", strict=False)
 def test_kat_gpu(kat, coracle_mod):
     bad = katrun.run_kat(kat, _gpu())
     assert not bad, "\n".join("step %d: got %#x want %#x (%s)" % b for b in bad)
 
 
+@pytest.mark.parametrize("tx_frac", [0.0, 0.5])
 @pytest.mark.parametrize("seed", range(8))
-def test_random_streams_gpu(seed, coracle_mod):
-    stream = randtraffic.make_stream(100 + seed, n_events=700, tx_frac=0.0)
+def test_random_streams_gpu(seed, tx_frac, coracle_mod):
+    stream = randtraffic.make_stream(100 + seed, n_events=700, tx_frac=tx_frac)
     want = randtraffic.run_stream(stream, katrun.COracleBackend())
     got = randtraffic.run_stream(stream, _gpu())
     assert len(want) == len(got)

@@ -21,6 +21,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -rf ;;
     testsall) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    txtests) step pytest_tx 900 python -m pytest tests/test_gpu_tx.py tests/test_gpu_parity.py -m gpu -q -rf -k "${TX_K:-tx or kat or random}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof) rm -rf gpurun_out/prof; step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline ;;

@@ -185,7 +185,10 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
   const bool dhcp = p.proto == 17u && has && p.sport == 67u && p.dport == 68u;
   const uint32_t d_look =
       (w && !excl) ? usn_mkdec(USN_CLS_EP, USN_R_NONE, owner)
-      : dhcp ? (usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) | USN_F_DHCP | USN_F_HOST)
+      // is_dhcp_answer: next_dhcp_endpoint.take() (endpoint.rs:262-273) is ordered
+      // state, so the host decides -- unless it is None, when it is a plain drop
+      : dhcp ? (usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) |
+                (a.next_dhcp_set ? (USN_F_DHCP | USN_F_HOST) : 0u))
              : usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
   uint32_t d =
       p.status == 0u ? usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu)
@@ -714,6 +717,543 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
     H->class_count[3] = (uint16_t)s_cls[2];
     H->class_count[1] = (uint16_t)(nt - s_cls[1] - s_cls[2] - s_cls[3]);
   }
+}
+
+/* ===========================================================================
+ * tx direction: frames sent by a non-NIC endpoint S (incoming == false).
+ * find_forward then also learns: unicast source MACs join the inner L2
+ * bridge (endpoint.rs:195-197) and answer keys become rules owned by S
+ * (:210-253), while the 1-entry cache ignores MACs (:186-191).  Every
+ * decision depends on what earlier frames of the batch learned, so the batch
+ * is classified exactly, in four launches:
+ *   tx_scan   parse, snapshot membership (bridge, table, S.listening) -> records
+ *   tx_hits   each frame's previous cache-touching frame -> cache hits; the
+ *             frames that really learn insert (key, first index) into
+ *             epoch-tagged hash sets (first occurrence = atomic max of ~index)
+ *   tx_decide decisions of non-hit frames against snapshot + "learned by a
+ *             frame <= me"; the first learner of each item is listed
+ *   tx_fill   a hit copies its run head's decision; tile order + headers
+ * Frames whose decision needs ordered host state (later fragments, a DHCP
+ * request's cross-endpoint side effect, steered DHCP answers) are flagged;
+ * usn_finalize resolves them sequentially from the first one.
+ * =========================================================================== */
+
+__device__ __forceinline__ uint32_t tx_touch(const uint4 &r0) { return (r0.x >> TXR_TOUCH_SHIFT) & 3u; }
+__device__ __forceinline__ uint64_t rec_smac(const uint4 &r1) {
+  return (uint64_t)r1.x | ((uint64_t)(r1.y & 0xFFFFu) << 32);
+}
+__device__ __forceinline__ uint64_t rec_dmac(const uint4 &r1) {
+  return (uint64_t)(r1.y >> 16) | ((uint64_t)r1.z << 16);
+}
+
+__device__ __forceinline__ bool bridge_has(const unsigned long long *set, uint32_t mask, uint64_t mac) {
+  uint32_t h = usn_mac_hash(mac) & mask;
+  for (uint32_t it = 0; it <= mask; ++it) {
+    const unsigned long long v = set[h];
+    if (!(v >> 63)) return false;
+    if ((v & 0xFFFFFFFFFFFFull) == mac) return true;
+    h = (h + 1) & mask;
+  }
+  return false;
+}
+
+/* atomic max of (epoch << 32 | ~idx): the newest epoch wins, then the smallest index */
+__device__ __forceinline__ void first_index_update(unsigned long long *w, uint32_t epoch, uint32_t idx) {
+  atomicMax(w, ((unsigned long long)epoch << 32) | (unsigned long long)(~idx));
+}
+
+/* Insert a 48-bit key into an epoch-tagged set (slot stride in u64 words). */
+__device__ __forceinline__ unsigned long long *set_claim(unsigned long long *set, uint32_t mask,
+                                                         uint32_t stride, uint32_t epoch,
+                                                         uint64_t key48, uint32_t home,
+                                                         uint32_t *overflow) {
+  const unsigned long long key = ((unsigned long long)epoch << 48) | key48;
+  uint32_t h = home & mask;
+  for (uint32_t it = 0; it <= mask; ++it) {
+    unsigned long long *slot = set + (size_t)h * stride;
+    unsigned long long cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur >> 48) != epoch) {                      // free in this epoch: try to claim
+      const unsigned long long prev = atomicCAS(slot, cur, key);
+      if (prev == cur) return slot;
+      cur = prev;
+    }
+    if (cur == key) return slot;
+    h = (h + 1) & mask;
+  }
+  atomicOr(overflow, 1u);
+  return nullptr;
+}
+
+/* Look up a 48-bit key; returns the slot or nullptr. */
+__device__ __forceinline__ const unsigned long long *set_find(const unsigned long long *set,
+                                                              uint32_t mask, uint32_t stride,
+                                                              uint32_t epoch, uint64_t key48,
+                                                              uint32_t home) {
+  const unsigned long long key = ((unsigned long long)epoch << 48) | key48;
+  uint32_t h = home & mask;
+  for (uint32_t it = 0; it <= mask; ++it) {
+    const unsigned long long *slot = set + (size_t)h * stride;
+    const unsigned long long cur = slot[0];
+    if ((cur >> 48) != epoch) return nullptr;
+    if (cur == key) return slot;
+    h = (h + 1) & mask;
+  }
+  return nullptr;
+}
+
+/* first index recorded in a set slot, or ~0 */
+__device__ __forceinline__ uint32_t slot_first(const unsigned long long *slot, uint32_t epoch) {
+  if (!slot) return 0xFFFFFFFFu;
+  const unsigned long long v = slot[1];
+  return (uint32_t)(v >> 32) == epoch ? ~(uint32_t)v : 0xFFFFFFFFu;
+}
+
+/* answer key to_want (pkt.rs:78-95) of an IPv4 PacketInfo, packed as a table key */
+__device__ __forceinline__ void want_key(const uint4 &r0, uint32_t &x, uint32_t &y, uint32_t &z,
+                                         uint32_t &meta) {
+  const uint32_t proto = (r0.x >> 8) & 0xFFu, has = (r0.x >> 16) & 1u;
+  x = r0.y;                       // dst_addr := src
+  y = r0.z;                       // src_addr := Some(dst)
+  z = has ? ((r0.w & 0xFFFFu) | ((r0.w >> 16) << 16)) : 0u;   // dport := sport, sport := dport
+  meta = usn_key_meta(proto, USN_WANT_SRC | (has ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0u));
+}
+
+/* key1 = to_match_want_with_src(true) */
+__device__ __forceinline__ void key1_of(const uint4 &r0, uint32_t &x, uint32_t &y, uint32_t &z,
+                                        uint32_t &meta) {
+  const uint32_t proto = (r0.x >> 8) & 0xFFu, has = (r0.x >> 16) & 1u;
+  x = r0.z;
+  y = r0.y;
+  z = has ? ((r0.w >> 16) | ((r0.w & 0xFFFFu) << 16)) : 0u;
+  meta = usn_key_meta(proto, USN_WANT_SRC | (has ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0u));
+}
+
+/* Exclusive prefix max, in tile-local frame order, of v[r] (frame r*256+tid).
+ * Values are <= TILE.  Uses L.order as a u16 scratch row and L.scratch. */
+__device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t out[ROUNDS]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) L.order[r * NTHREADS + tid] = (uint16_t)v[r];
+  __syncthreads();
+  const uint32_t p0 = tid * ROUNDS;                        // contiguous chunk of 4 frames
+  uint32_t e[ROUNDS], m = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < ROUNDS; ++k) { e[k] = L.order[p0 + k]; m = max(m, e[k]); }
+  uint32_t inc = m;                                        // wave inclusive max scan (DPP)
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xF, 0xF, true));
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xF, 0xF, true));
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xF, 0xF, true));
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xF, 0xF, true));
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xA, 0xF, false));
+  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xC, 0xF, false));
+  uint32_t exc = __shfl_up(inc, 1, 64);
+  if (lane == 0) exc = 0;
+  if (lane == 63) L.scratch[wave] = inc;
+  __syncthreads();
+  for (uint32_t w = 0; w < wave; ++w) exc = max(exc, L.scratch[w]);
+  uint32_t run = exc;
+#pragma unroll
+  for (uint32_t k = 0; k < ROUNDS; ++k) {
+    const uint32_t x = e[k];
+    L.order[p0 + k] = (uint16_t)run;
+    run = max(run, x);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) out[r] = L.order[r * NTHREADS + tid];
+  __syncthreads();
+}
+
+/* 1 + the batch-global index of the last frame before tile `tile` with aux
+ * word `w` set (walks the earlier tiles' aux rows), or 0. */
+__device__ uint32_t prev_tiles_last(const uint32_t *aux, uint32_t tile, uint32_t w) {
+  for (int t = (int)tile - 1; t >= 0; --t) {
+    const uint32_t v = aux[t * 4 + w];
+    if (v) return (uint32_t)t * TILE + v;
+  }
+  return 0;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const ClassifyArgs &a = t.a;
+  const Lds L = carve(smem, a.nbins);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  const uint4 *T = a.table;
+  if (LDS) {
+    for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    T = L.table;
+  }
+  __shared__ uint32_t s_carry[8];
+  __shared__ uint32_t s_last;
+  if (tid == 0) s_last = 0;
+  __syncthreads();
+  if (tile == 0) {   // carried-in cache of this source, for tx_hits / tx_fill
+    resolve_carry(a, s_carry, L.scratch);
+    if (tid == 0) {
+      usn_summary *S = a.summary;
+      S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
+      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
+      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      S->flags = 0; S->first_break = 0xFFFFFFFFu;
+    }
+  }
+  uint32_t last = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint64_t i = base + local;
+    const uint8_t *fp = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
+    uint4 q[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(reinterpret_cast<const uint4 *>(fp) + k);
+    const uint32_t len = a.lens[i];
+    Parsed p;
+    parse(q, len, fp, p);
+    const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
+    const uint64_t smac = (uint64_t)(q[0].y >> 16) | ((uint64_t)q[0].z << 16);
+    const bool loop = p.status == 1u && (p.dst >> 24) == 127u;
+    const uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
+                         : (p.status == 1u && !loop) ? 1u : 2u;
+    uint32_t f = (touch << TXR_TOUCH_SHIFT);
+    if (touch == 1u || touch == 2u) {
+      const bool s_in = bridge_has(t.bridge_set, t.bridge_mask, smac);
+      const bool d_in = bridge_has(t.bridge_set, t.bridge_mask, dmac);
+      if (s_in) f |= TXR_SMAC_IN;
+      if (d_in) f |= TXR_DMAC_IN;
+      if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
+    }
+    if (touch == 3u) f |= TXR_HOST;                           // later fragment: map lookup
+    if (touch == 1u) {
+      // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
+      bool listening = false;
+      for (uint32_t k = 0; k < t.n_listen; ++k) {
+        const uint32_t ld = t.listen[2 * k], lw = t.listen[2 * k + 1];
+        const uint32_t lhas = (lw >> 8) & 1u;
+        listening |= ld == p.src && (lw & 0xFFu) == p.proto && lhas == p.has_ports &&
+                     (!lhas || (lw >> 16) == p.sport);
+      }
+      const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
+                            p.dport == 67u && (p.dst & 0xFFu) == 255u;
+      if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
+      if (!listening && !dhcp_req) {
+        uint4 r0 = make_uint4(p.i0, p.src, p.dst, p.ports);
+        uint32_t x, y, z, meta;
+        want_key(r0, x, y, z, meta);
+        if (!probe(T, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
+      }
+      if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
+    }
+    uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
+    if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
+    r0.x = (r0.x & TXR_I0_MASK) | f;
+    uint4 r1 = make_uint4((uint32_t)smac, (uint32_t)(smac >> 32) | ((uint32_t)dmac << 16),
+                          (uint32_t)(dmac >> 16), p.status == 1u ? p.frag_first : 0u);
+    t.rec[2 * i] = r0;
+    t.rec[2 * i + 1] = r1;
+    if (touch) last = local + 1;
+  }
+  if (last) atomicMax(&s_last, last);
+  __syncthreads();
+  if (tid == 0) t.aux[tile * 4 + 0] = s_last;
+}
+
+__global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const ClassifyArgs &a = t.a;
+  const Lds L = carve(smem, a.nbins);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  __shared__ uint32_t s_last_nh;
+  if (tid == 0) s_last_nh = 0;
+  uint4 r0[ROUNDS];
+  uint32_t v[ROUNDS], prev[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    r0[r] = local < nt ? t.rec[2 * (base + local)] : make_uint4(0, 0, 0, 0);
+    v[r] = (local < nt && tx_touch(r0[r])) ? local + 1 : 0u;
+  }
+  tile_prefix_max(v, L, prev);
+  const usn_summary *S = a.summary;
+  const uint32_t before = prev_tiles_last(t.aux, tile, 0);   // last touching frame of earlier tiles
+  uint32_t last_nh = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint64_t i = base + local;
+    uint32_t fl = r0[r].x;
+    const uint32_t touch = tx_touch(r0[r]);
+    if (!touch) continue;
+    bool hit = false;
+    if (touch == 1u) {
+      const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
+      const uint32_t info0 = fl & TXR_I0_MASK;
+      if (k1) {
+        const uint4 pr = t.rec[2 * (size_t)(k1 - 1)];
+        const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == r0[r].y &&
+                          pr.z == r0[r].z && pr.w == r0[r].w;
+        if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
+        else hit = same;
+      } else {
+        hit = (S->cin_state & USN_CS_VALID) && S->cin_info[0] == info0 && S->cin_info[1] == r0[r].y &&
+              S->cin_info[2] == r0[r].z && S->cin_info[3] == r0[r].w;
+      }
+    }
+    if (hit) fl |= TXR_HIT;
+    if (fl != r0[r].x) t.rec[2 * i].x = fl;
+    if (!hit) last_nh = local + 1;
+    if (hit || (fl & TXR_HOST)) continue;
+    // this frame really learns: first occurrence per item
+    if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
+      const uint4 r1 = t.rec[2 * i + 1];
+      if (fl & TXR_LEARNMAC) {
+        const uint64_t m = rec_smac(r1);
+        unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
+                                             usn_mac_hash(m), t.counters + 1);
+        if (slot) first_index_update(slot + 1, t.epoch, (uint32_t)i);
+      }
+      if (fl & TXR_LEARNRULE) {
+        uint32_t x, y, z, meta;
+        want_key(r0[r], x, y, z, meta);
+        const uint64_t fp = usn_key_fp48(x, y, z, meta);
+        unsigned long long *slot = set_claim(t.ruleset, t.ruleset_mask, 4, t.epoch, fp,
+                                             usn_key_hash(x, y, z, meta), t.counters + 1);
+        if (slot) {
+          slot[2] = ((unsigned long long)y << 32) | x;   // full key: collision check in tx_decide
+          slot[3] = ((unsigned long long)meta << 32) | z;
+          first_index_update(slot + 1, t.epoch, (uint32_t)i);
+        }
+      }
+    }
+  }
+  if (last_nh) atomicMax(&s_last_nh, last_nh);
+  __syncthreads();
+  if (tid == 0) t.aux[tile * 4 + 1] = s_last_nh;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const ClassifyArgs &a = t.a;
+  const Lds L = carve(smem, a.nbins);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  const uint4 *T = a.table;
+  if (LDS) {
+    for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    T = L.table;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint64_t i = base + local;
+    const uint4 r0 = t.rec[2 * i], r1 = t.rec[2 * i + 1];
+    const uint32_t fl = r0.x, touch = tx_touch(r0), kind = fl & 0xFFu;
+    uint32_t d;
+    if (touch == 0u) {
+      d = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
+    } else if (fl & TXR_HOST) {
+      d = usn_mkdec(USN_CLS_DROP, touch == 3u ? USN_R_FRAGMISS : USN_R_NOMATCH, 0xFFFFu) | USN_F_HOST;
+    } else if (fl & TXR_HIT) {
+      d = USN_F_CACHE;                                     // filled by tx_fill
+    } else if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) {
+      d = usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
+    } else if (touch == 2u) {
+      d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
+    } else {
+      const uint64_t dmac = rec_dmac(r1);
+      bool d_in = (fl & TXR_DMAC_IN) != 0;
+      if (!d_in)                                           // learned by a frame <= i ?
+        d_in = slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, dmac, usn_mac_hash(dmac)),
+                          t.epoch) <= (uint32_t)i;
+      if (!d_in) {
+        d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);  // endpoint.rs:254-255
+      } else {
+        uint32_t x, y, z, meta;
+        key1_of(r0, x, y, z, meta);
+        uint32_t w = (a.probe_mask & 1u) ? probe(T, a.bucket_mask, x, y, z, meta) : 0u;
+        if (!w) {   // a rule learned by a frame <= i is owned by S (so excluded)
+          const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
+                                                    usn_key_fp48(x, y, z, meta),
+                                                    usn_key_hash(x, y, z, meta));
+          if (slot_first(slot, t.epoch) <= (uint32_t)i) {
+            if (slot[2] != (((unsigned long long)y << 32) | x) ||
+                slot[3] != (((unsigned long long)meta << 32) | z))
+              atomicOr(t.counters + 1, 2u);                // fingerprint collision: host redoes
+            w = USN_SLOT_VALID | (a.src << 16);
+          }
+        }
+        const bool has = (r0.x >> 16) & 1u;
+        if (!w && (a.probe_mask & 2u))
+          w = probe(T, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
+                    usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u));
+        const uint32_t owner = w >> 16;
+        const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
+        if (w && !excl) d = usn_mkdec(USN_CLS_EP, USN_R_NONE, owner);
+        else if (fl & TXR_DHCPANS)
+          d = usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) |
+              (a.next_dhcp_set ? (USN_F_DHCP | USN_F_HOST) : 0u);
+        else d = usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
+      }
+    }
+    if (r1.w) d |= USN_F_FRAG1;                            // first fragment: remembered (host map)
+    // the first frame that learns an item lists it for the host registry / bridge
+    if (touch && !(fl & (TXR_HIT | TXR_HOST)) && (fl & (TXR_LEARNMAC | TXR_LEARNRULE))) {
+      bool learned = false;
+      if (fl & TXR_LEARNMAC) {
+        const uint64_t m = rec_smac(r1);
+        if (slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, m, usn_mac_hash(m)), t.epoch) ==
+            (uint32_t)i) {
+          const uint32_t pos = atomicAdd(t.counters, 1u);
+          if (pos < t.learned_cap) {
+            t.learned[2 * pos] = make_uint4((uint32_t)i, 0u, 0u, 0u);
+            t.learned[2 * pos + 1] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, 0u);
+          }
+          else atomicOr(t.counters + 1, 4u);
+          learned = true;
+        }
+      }
+      if (fl & TXR_LEARNRULE) {
+        uint32_t x, y, z, meta;
+        want_key(r0, x, y, z, meta);
+        const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
+                                                  usn_key_fp48(x, y, z, meta),
+                                                  usn_key_hash(x, y, z, meta));
+        if (slot_first(slot, t.epoch) == (uint32_t)i) {
+          if (slot[2] != (((unsigned long long)y << 32) | x) ||
+              slot[3] != (((unsigned long long)meta << 32) | z))
+            atomicOr(t.counters + 1, 2u);
+          const uint32_t pos = atomicAdd(t.counters, 1u);
+          if (pos < t.learned_cap) {
+            t.learned[2 * pos] = make_uint4((uint32_t)i, 1u, 0u, 0u);
+            t.learned[2 * pos + 1] = make_uint4(x, y, z, meta);
+          }
+          else atomicOr(t.counters + 1, 4u);
+          learned = true;
+        }
+      }
+      if (learned) d |= USN_F_LEARN;
+    }
+    a.decisions[i] = d;
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void tx_fill_kernel(TxArgs t) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const ClassifyArgs &a = t.a;
+  const Lds L = carve(smem, a.nbins);
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+  if (tid < 8) s_misc[tid] = 0;
+  for (uint32_t k = tid; k < NSEG * a.nbins; k += NTHREADS) L.cnt[k] = 0;
+  uint4 r0[ROUNDS];
+  uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    r0[r] = local < nt ? t.rec[2 * (base + local)] : make_uint4(0, 0, 0, 0);
+    dec[r] = local < nt ? a.decisions[base + local] : 0u;
+    v[r] = (local < nt && tx_touch(r0[r]) && !(r0[r].x & TXR_HIT)) ? local + 1 : 0u;
+  }
+  tile_prefix_max(v, L, head);
+  const uint32_t before = prev_tiles_last(t.aux, tile, 1);
+  const usn_summary *S = a.summary;
+  uint32_t my_last = 0, my_touch = 0, my_dec = 0, my_host = 0;
+  uint4 my_info = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    if (r0[r].x & TXR_HIT) {   // the run head: the last non-hit touching frame before
+      const uint32_t h = head[r] ? (uint32_t)(base + head[r]) : before;
+      const uint32_t hd = h ? a.decisions[h - 1] : S->cin_dst;
+      dec[r] = (hd & USN_PARITY_MASK) | USN_F_CACHE | (dec[r] & USN_F_FRAG1);
+      a.decisions[base + local] = dec[r];
+    }
+    const uint32_t touch = tx_touch(r0[r]);
+    if (touch) {
+      my_last = local + 1; my_touch = touch; my_dec = dec[r];
+      my_host = (r0[r].x & TXR_HOST) != 0;
+      my_info = make_uint4(r0[r].x & TXR_I0_MASK, r0[r].y, r0[r].z, r0[r].w);
+    }
+  }
+  uint32_t bins[ROUNDS];
+  uint32_t *hl = a.host_list + (size_t)tile * TILE;
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    bins[r] = dec_bin(dec[r], a.n_ep);
+    const bool host = local < nt && (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_LEARN));
+    if (__ballot(host))
+      if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
+  }
+  {
+    uint32_t lm = my_last;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) lm = max(lm, (uint32_t)__shfl_xor(lm, d, 64));
+    if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
+  }
+  __syncthreads();
+  uint32_t cls[4] = {0, 0, 0, 0};
+  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
+                                     a.runs, cls);
+  if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
+  if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
+  if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
+  __syncthreads();
+  usn_tile_hdr *H = a.tiles + tile;
+  const uint32_t lastp = s_misc[0];
+  if (lastp && my_last == lastp) {
+    H->last_state = USN_TS_HAS | (my_touch == 1u && !my_host ? USN_TS_RETAINED : 0u) |
+                    ((my_touch == 3u || my_host) ? USN_TS_UNKNOWN : 0u);
+    H->last_dst = my_dec & USN_PARITY_MASK;
+    H->last_info[0] = my_info.x; H->last_info[1] = my_info.y;
+    H->last_info[2] = my_info.z; H->last_info[3] = my_info.w;
+    H->last_idx = (uint32_t)(base + lastp - 1);
+  }
+  if (tid == 0) {
+    H->n_frames = (uint16_t)nt;
+    H->n_runs = (uint16_t)n_runs;
+    H->n_host = (uint16_t)s_misc[1];
+    H->_reserved = 0;
+    H->class_count[0] = (uint16_t)s_misc[5];
+    H->class_count[2] = (uint16_t)s_misc[3];
+    H->class_count[3] = (uint16_t)s_misc[4];
+    H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
+    if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
+  }
+}
+
+hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
+  const ClassifyArgs &a = t.a;
+  if (a.ntiles == 0) return hipSuccess;
+  const dim3 g(a.ntiles), b(NTHREADS);
+  const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
+  const size_t core = lds_core_bytes(a.nbins);
+  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds, false);
+  if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, with_table, stream, t);
+  else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, with_table, stream, t);
+  hipLaunchKernelGGL(tx_hits_kernel, g, b, core, stream, t);
+  if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, with_table, stream, t);
+  else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, with_table, stream, t);
+  hipLaunchKernelGGL(tx_fill_kernel, g, b, core, stream, t);
+  return hipGetLastError();
 }
 
 /* --------------------------------------------------------------------------- */

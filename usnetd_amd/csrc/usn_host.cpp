@@ -161,6 +161,27 @@ struct usn_ctx {
   bool bridge_dirty = true;
   uint64_t *d_bridge = nullptr;
   size_t d_bridge_cap = 0;
+  unsigned long long *d_bridge_set = nullptr;   // open addressing, bit 63 = used
+  size_t d_bridge_set_cap = 0;
+  uint32_t bridge_mask = 0;
+  /* tx scratch (one tx batch in flight per context) */
+  struct Tx {
+    uint4 *rec = nullptr;
+    uint64_t rec_frames = 0;
+    uint32_t *aux = nullptr;
+    uint32_t aux_tiles = 0;
+    unsigned long long *macset = nullptr, *ruleset = nullptr;
+    uint32_t set_slots = 0;
+    uint4 *learned = nullptr;
+    uint32_t learned_cap = 0;
+    uint32_t *counters = nullptr;
+    uint32_t *listen = nullptr;
+    size_t listen_cap = 0;
+    uint32_t epoch = 0;
+    bool pending = false;   // classified, not finalized: registry not final
+    int src = -1;
+    const uint32_t *decisions = nullptr;
+  } tx;
 };
 
 namespace {
@@ -229,6 +250,22 @@ int rebuild_bridge(usn_ctx *c) {
   }
   if (!c->bridge.empty())
     HIPCHK(hipMemcpy(c->d_bridge, c->bridge.data(), c->bridge.size() * 8, hipMemcpyHostToDevice));
+  /* membership set for tx_scan (innerl2bridge.contains, endpoint.rs:195, 254) */
+  const uint32_t slots = next_pow2(std::max<uint32_t>(16, 2 * (uint32_t)c->bridge.size()));
+  std::vector<unsigned long long> set(slots, 0ull);
+  for (uint64_t m : c->bridge) {
+    uint32_t h = usn_mac_hash(m) & (slots - 1);
+    while ((set[h] >> 63) && (set[h] & 0xFFFFFFFFFFFFull) != m) h = (h + 1) & (slots - 1);
+    set[h] = (1ull << 63) | m;
+  }
+  if (slots * 8ull > c->d_bridge_set_cap) {
+    if (c->d_bridge_set) HIPCHK(hipFree(c->d_bridge_set));
+    c->d_bridge_set = nullptr;
+    HIPCHK(hipMalloc(&c->d_bridge_set, slots * 8ull));
+    c->d_bridge_set_cap = slots * 8ull;
+  }
+  HIPCHK(hipMemcpy(c->d_bridge_set, set.data(), slots * 8ull, hipMemcpyHostToDevice));
+  c->bridge_mask = slots - 1;
   c->bridge_dirty = false;
   return USN_OK;
 }
@@ -415,6 +452,7 @@ const char *usn_strerror(int s) {
     case USN_EHIP: return "HIP runtime error";
     case USN_ENODEV: return "no gfx950 device";
     case USN_ERANGE: return "out of range";
+    case USN_EBUSY: return "a tx batch awaits usn_finalize";
     default: return "unknown";
   }
 }
@@ -443,12 +481,18 @@ void usn_ctx_destroy(usn_ctx *c) {
   (void)hipDeviceSynchronize();
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_bridge) (void)hipFree(c->d_bridge);
+  if (c->d_bridge_set) (void)hipFree(c->d_bridge_set);
+  for (void *p : {(void *)c->tx.rec, (void *)c->tx.aux, (void *)c->tx.macset,
+                  (void *)c->tx.ruleset, (void *)c->tx.learned, (void *)c->tx.counters,
+                  (void *)c->tx.listen})
+    if (p) (void)hipFree(p);
   delete c;
 }
 
 int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
   if (!c || id >= USN_MAX_ENDPOINTS || kind < USN_EP_NIC || kind > USN_EP_UDS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   if (c->eps[id].used) return USN_EEXIST;
   if ((kind == USN_EP_NIC) != (for_nic < 0)) return USN_EINVAL;   // main.rs:157-159
   if (for_nic >= 0 && (for_nic >= USN_MAX_ENDPOINTS || !c->eps[for_nic].used ||
@@ -467,6 +511,7 @@ int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
 int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
   if (!c || id >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   if (!c->eps[id].used) return USN_ENOENT;
   for (auto it = c->rules.begin(); it != c->rules.end();) {   // match_register.retain
     if (it->second.owner == id) { it = c->rules.erase(it); c->table_dirty = true; }
@@ -480,6 +525,7 @@ int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
 int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
   if (!c || !w || owner >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   Ep &e = c->eps[owner];
   if (!e.used) return USN_ENOENT;
   const WantKey k = canon(*w);
@@ -496,6 +542,7 @@ int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
 int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
   if (!c || !w) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   const WantKey k = canon(*w);
   auto it = c->rules.find(k);
   if (it == c->rules.end()) return 0;
@@ -508,12 +555,14 @@ int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
 int usn_rule_count(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   return (int)c->rules.size();
 }
 
 int usn_rules_get(usn_ctx *c, usn_want *w, uint16_t *owner, uint8_t *sticky, uint32_t cap) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   uint32_t n = 0;
   for (const auto &kv : c->rules) {
     if (n >= cap) break;
@@ -537,6 +586,7 @@ int usn_rules_get(usn_ctx *c, usn_want *w, uint16_t *owner, uint8_t *sticky, uin
 int usn_lookup(usn_ctx *c, const usn_want *w) {
   if (!c || !w) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   const int e = registry_get(c, canon(*w));
   return e < 0 ? USN_ENOENT : e;
 }
@@ -544,6 +594,7 @@ int usn_lookup(usn_ctx *c, const usn_want *w) {
 int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
   if (!c || !mac) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   c->bridge.push_back(mac48(mac));
   c->bridge_dirty = true;
   return USN_OK;
@@ -552,12 +603,14 @@ int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
 int usn_bridge_count(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   return (int)c->bridge.size();
 }
 
 int usn_frag_clear(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   c->frags.clear();
   return USN_OK;
 }
@@ -565,6 +618,7 @@ int usn_frag_clear(usn_ctx *c) {
 int usn_cache_clear(usn_ctx *c, uint16_t ep) {
   if (!c || ep >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
   cache_clear(c, ep);
   return USN_OK;
 }
@@ -630,6 +684,7 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   a.src = b->src_endpoint;
   a.src_is_nic = S.kind == USN_EP_NIC;
   a.for_nic = S.for_nic < 0 ? 0xFFFFu : (uint32_t)S.for_nic;
+  a.next_dhcp_set = S.next_dhcp >= 0 ? 1u : 0u;
   a.n_ep = c->n_ep;
   a.nbins = c->n_ep + 3;
   a.nbits = 1;
@@ -645,7 +700,65 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
   if (((uintptr_t)b->frames & 15) != 0) return USN_EINVAL;
   if (b->n > 0xFFFFFFFFull) return USN_ERANGE;
   if (b->src_endpoint >= USN_MAX_ENDPOINTS || !c->eps[b->src_endpoint].used) return USN_EINVAL;
-  if (c->eps[b->src_endpoint].kind != USN_EP_NIC) return USN_EINVAL;   // tx: not yet on device
+  return USN_OK;
+}
+
+/* device scratch of a tx batch of n frames; the epoch-tagged sets are
+ * cleared only when (re)allocated or when the 16-bit epoch wraps */
+static int tx_prepare(usn_ctx *c, uint64_t n, uint32_t ntiles) {
+  usn_ctx::Tx &T = c->tx;
+  if (n > T.rec_frames) {
+    if (T.rec) HIPCHK(hipFree(T.rec));
+    if (T.learned) HIPCHK(hipFree(T.learned));
+    T.rec = nullptr; T.learned = nullptr;
+    HIPCHK(hipMalloc(&T.rec, n * 2 * sizeof(uint4)));
+    HIPCHK(hipMalloc(&T.learned, n * 4 * sizeof(uint4)));   // <= 2 items of 2 x uint4 per frame
+    T.rec_frames = n;
+    T.learned_cap = (uint32_t)(2 * n);
+  }
+  if (ntiles > T.aux_tiles) {
+    if (T.aux) HIPCHK(hipFree(T.aux));
+    T.aux = nullptr;
+    HIPCHK(hipMalloc(&T.aux, (size_t)ntiles * 4 * sizeof(uint32_t)));
+    T.aux_tiles = ntiles;
+  }
+  if (!T.counters) HIPCHK(hipMalloc(&T.counters, 4 * sizeof(uint32_t)));
+  const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
+  bool clear = false;
+  if (slots > T.set_slots) {
+    if (T.macset) HIPCHK(hipFree(T.macset));
+    if (T.ruleset) HIPCHK(hipFree(T.ruleset));
+    T.macset = nullptr; T.ruleset = nullptr;
+    HIPCHK(hipMalloc(&T.macset, (size_t)slots * 2 * 8));
+    HIPCHK(hipMalloc(&T.ruleset, (size_t)slots * 4 * 8));
+    T.set_slots = slots;
+    clear = true;
+  }
+  if (++T.epoch > 0xFFFFu) clear = true;
+  if (clear) {
+    HIPCHK(hipMemset(T.macset, 0, (size_t)T.set_slots * 2 * 8));
+    HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
+    T.epoch = 1;
+  }
+  return USN_OK;
+}
+
+/* S.listening as {dst, proto | has_port << 8 | port << 16} words on the device */
+static int tx_listen(usn_ctx *c, const Ep &S, uint32_t &n_listen) {
+  std::vector<uint32_t> v;
+  for (const Listen &l : S.listening) {
+    v.push_back(l.dst);
+    v.push_back((uint32_t)l.proto | ((uint32_t)l.has_port << 8) | ((uint32_t)l.port << 16));
+  }
+  n_listen = (uint32_t)S.listening.size();
+  if (v.empty()) return USN_OK;
+  if (v.size() * 4 > c->tx.listen_cap) {
+    if (c->tx.listen) HIPCHK(hipFree(c->tx.listen));
+    c->tx.listen = nullptr;
+    HIPCHK(hipMalloc(&c->tx.listen, v.size() * 4));
+    c->tx.listen_cap = v.size() * 4;
+  }
+  HIPCHK(hipMemcpy(c->tx.listen, v.data(), v.size() * 4, hipMemcpyHostToDevice));
   return USN_OK;
 }
 
@@ -653,12 +766,16 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
                        void *stream) {
   if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
+  bool tx = false;
   for (uint32_t k = 0; k < count; ++k) {
     int st = check_batch(c, &b[k], &r[k]);
     if (st) return st;
+    tx |= c->eps[b[k].src_endpoint].kind != USN_EP_NIC;
     for (uint32_t j = 0; j < k; ++j)
       if (b[j].src_endpoint == b[k].src_endpoint) return USN_EINVAL;   // one batch per source
   }
+  if (tx && count != 1) return USN_EINVAL;   // a tx batch changes shared state: alone
   HIPCHK(hipSetDevice(c->device));
   if (c->table_dirty) { int s = rebuild_table(c); if (s) return s; }
   if (c->bridge_dirty) { int s = rebuild_bridge(c); if (s) return s; }
@@ -682,7 +799,36 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     }
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
-  HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+  if (tx) {
+    const usn_batch &tb = b[0];
+    int st = tx_prepare(c, tb.n, m.b[0].ntiles);
+    if (st) return st;
+    usn::TxArgs t;
+    std::memset(&t, 0, sizeof t);
+    t.a = m.b[0];
+    st = tx_listen(c, c->eps[tb.src_endpoint], t.n_listen);
+    if (st) return st;
+    t.rec = c->tx.rec;
+    t.aux = c->tx.aux;
+    t.macset = c->tx.macset;
+    t.ruleset = c->tx.ruleset;
+    t.macset_mask = t.ruleset_mask = c->tx.set_slots - 1;
+    t.epoch = c->tx.epoch;
+    t.learned = c->tx.learned;
+    t.counters = c->tx.counters;
+    t.learned_cap = c->tx.learned_cap;
+    t.bridge_set = c->d_bridge_set;
+    t.bridge_mask = c->bridge_mask;
+    t.listen = c->tx.listen;
+    t.next_dhcp_set = t.a.next_dhcp_set;
+    HIPCHK(hipMemsetAsync(c->tx.counters, 0, 4 * sizeof(uint32_t), (hipStream_t)stream));
+    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));
+    c->tx.pending = true;
+    c->tx.src = tb.src_endpoint;
+    c->tx.decisions = r[0].decisions;
+  } else {
+    HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+  }
   for (uint32_t k = 0; k < count; ++k) {
     Chain &ch = c->chains[b[k].src_endpoint];
     ch.device_chain = true;
@@ -748,6 +894,153 @@ bool retains(uint32_t d) {
 
 }  // namespace
 
+/* Ordered host stage of a tx batch.  Frames before the first F_HOST frame h
+ * are final on the device: apply what they learned in frame order (bridge
+ * MACs, answer rules with the NIC cache reset, first fragments into the map).
+ * From h on, find_forward runs sequentially on the host (endpoint.rs:172-296)
+ * from the cache state just before h.  An overflow of the device sets
+ * (counters[1]) makes h = 0. */
+static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_t s,
+                       usn_finalize_info *info) {
+  const uint64_t n = b->n;
+  const uint32_t ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
+  const int src = b->src_endpoint;
+  Ep &S = c->eps[src];
+  usn_summary sum;
+  HIPCHK(hipMemcpy(&sum, r->summary, sizeof sum, hipMemcpyDeviceToHost));
+  std::vector<usn_tile_hdr> th(ntiles);
+  HIPCHK(hipMemcpy(th.data(), r->tiles, ntiles * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+  uint32_t cnt[4];
+  HIPCHK(hipMemcpy(cnt, c->tx.counters, sizeof cnt, hipMemcpyDeviceToHost));
+  usn_finalize_info fi;
+  std::memset(&fi, 0, sizeof fi);
+  fi.flags = sum.flags;
+  std::vector<uint32_t> hosts;
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
+    if (th[t].n_host) {
+      const size_t at = hosts.size();
+      hosts.resize(at + th[t].n_host);
+      HIPCHK(hipMemcpy(hosts.data() + at, r->host_list + (size_t)t * USN_TILE,
+                       th[t].n_host * 4, hipMemcpyDeviceToHost));
+    }
+  }
+  std::sort(hosts.begin(), hosts.end());
+  HostView hv{c, b, r, s, {}, {}, false, false};
+  int st = hv.fetch_dec();
+  if (st) return st;
+  uint64_t h = n;
+  if (cnt[1]) h = 0;
+  else
+    for (uint32_t j : hosts)
+      if (hv.dec[j] & USN_F_HOST) { h = j; break; }
+  /* learned items and first fragments before h, in frame order */
+  const uint32_t nl = std::min(cnt[0], c->tx.learned_cap);
+  std::vector<uint4> items((size_t)nl * 2);
+  if (nl) HIPCHK(hipMemcpy(items.data(), c->tx.learned, items.size() * sizeof(uint4),
+                           hipMemcpyDeviceToHost));
+  struct Ev { uint64_t idx; uint32_t kind; uint4 key; };   // kind 0 mac, 1 rule, 2 frag1
+  std::vector<Ev> evs;
+  for (uint32_t k = 0; k < nl; ++k)
+    if (items[2 * k].x < h) evs.push_back(Ev{items[2 * k].x, items[2 * k].y, items[2 * k + 1]});
+  for (uint32_t j : hosts)
+    if (j < h && (hv.dec[j] & USN_F_FRAG1)) evs.push_back(Ev{j, 2, make_uint4(0, 0, 0, 0)});
+  std::sort(evs.begin(), evs.end(), [](const Ev &x, const Ev &y) {
+    return x.idx != y.idx ? x.idx < y.idx : x.kind > y.kind;   // the fragment map first
+  });
+  std::vector<uint8_t> buf;
+  uint32_t len = 0;
+  for (const Ev &e : evs) {
+    if (e.kind == 2) {                                   // extract_pkt_info side effect
+      st = hv.frame(e.idx, buf, len);
+      if (st) return st;
+      (void)host_parse(c, buf.data(), len);
+    } else if (e.kind == 0) {                            // endpoint.rs:195-197
+      const uint64_t m = (uint64_t)e.key.x | ((uint64_t)e.key.y << 32);
+      if (!bridge_has(c, m)) { c->bridge.push_back(m); c->bridge_dirty = true; fi.n_learned++; }
+    } else {                                             // endpoint.rs:233-252
+      WantKey w;
+      w.dst = e.key.x;
+      w.src = e.key.y;
+      w.dport = (uint16_t)(e.key.z & 0xFFFFu);
+      w.sport = (uint16_t)(e.key.z >> 16);
+      w.proto = (uint8_t)(e.key.w & 0xFFu);
+      w.present = (uint8_t)((e.key.w >> 8) & 7u);
+      if (!c->rules.count(w)) {
+        if (S.for_nic >= 0) cache_clear(c, S.for_nic);
+        c->rules[w] = Rule{(uint16_t)src, 0};
+        c->table_dirty = true;
+        fi.n_learned++;
+      }
+    }
+  }
+  if (h < n) {
+    /* cache state just before h: carried in, then the last touching frame */
+    CacheState cs;
+    cs.valid = sum.cin_state & USN_CS_VALID;
+    cs.dst = sum.cin_dst;
+    std::memcpy(cs.info.w, sum.cin_info, 16);
+    for (uint64_t k = h; k > 0; --k) {
+      const uint32_t d = hv.dec[k - 1];
+      if (!touches(d)) continue;
+      if (!retains(d)) { cs.valid = false; break; }
+      st = hv.frame(k - 1, buf, len);
+      if (st) return st;
+      ParsedH p = host_parse(c, buf.data(), len);
+      cs.valid = true;
+      cs.info = p.info;
+      cs.dst = d & USN_PARITY_MASK;
+      break;
+    }
+    /* frames [h, n): one strided gather of their header windows */
+    const uint32_t W = 80;
+    std::vector<uint8_t> win;
+    const bool strided = b->stride != 0;
+    const uint32_t width = strided ? (uint32_t)std::min<uint64_t>(b->stride, W) : 0;
+    st = hv.fetch_lens();
+    if (st) return st;
+    if (strided) {
+      win.assign((size_t)(n - h) * W, 0);
+      HIPCHK(hipMemcpy2D(win.data(), W, b->frames + h * b->stride, b->stride, width, n - h,
+                         hipMemcpyDeviceToHost));
+    }
+    std::vector<uint32_t> out(n - h);
+    for (uint64_t j = h; j < n; ++j) {
+      const uint8_t *fp;
+      if (strided && (hv.lens[j] <= width || width == W)) {
+        fp = win.data() + (size_t)(j - h) * W;
+        len = hv.lens[j];
+      } else {
+        st = hv.frame(j, buf, len);
+        if (st) return st;
+        fp = buf.data();
+      }
+      bool learned = false;
+      uint32_t d = host_step(c, src, fp, len, cs, learned) | USN_F_HOST;
+      if (learned) { d |= USN_F_LEARN; fi.n_learned++; }
+      const uint32_t old = hv.dec[j];
+      if ((old & USN_PARITY_MASK) != (d & USN_PARITY_MASK)) fi.n_patched++;
+      fi.class_count[USN_DEC_CLASS(old)]--;
+      fi.class_count[USN_DEC_CLASS(d)]++;
+      out[j - h] = d;
+    }
+    fi.n_host = (uint32_t)(n - h);
+    HIPCHK(hipMemcpy(r->decisions + h, out.data(), out.size() * 4, hipMemcpyHostToDevice));
+    ClassifyArgs a;
+    fill_args(c, b, r, a);
+    HIPCHK(usn::launch_resort(a, (uint32_t)(h / USN_TILE), ntiles, s));
+    usn_summary o = sum;
+    o.flags |= USN_S_COUT;
+    o.cout_state = cs.valid ? USN_CS_VALID : 0u;
+    o.cout_dst = cs.dst;
+    std::memcpy(o.cout_info, cs.info.w, 16);
+    HIPCHK(hipMemcpy(r->summary, &o, sizeof o, hipMemcpyHostToDevice));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  if (info) *info = fi;
+  return USN_OK;
+}
+
 int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
                  usn_finalize_info *info) {
   if (!c || !b || !r || b->n == 0) return USN_EINVAL;
@@ -755,6 +1048,24 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
+  if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
+    if (c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions) {
+      const int st = finalize_tx(c, b, r, s, info);
+      c->tx.pending = false;
+      return st;
+    }
+    if (c->tx.pending) return USN_EBUSY;
+    /* an already finalized tx batch: its results are final */
+    const uint32_t nt = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
+    std::vector<usn_tile_hdr> th(nt);
+    HIPCHK(hipMemcpy(th.data(), r->tiles, nt * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+    usn_finalize_info fi;
+    std::memset(&fi, 0, sizeof fi);
+    for (uint32_t t = 0; t < nt; ++t)
+      for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
+    if (info) *info = fi;
+    return USN_OK;
+  }
   const uint32_t ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
   usn_summary sum;
   HIPCHK(hipMemcpy(&sum, r->summary, sizeof sum, hipMemcpyDeviceToHost));

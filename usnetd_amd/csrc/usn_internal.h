@@ -67,6 +67,23 @@ USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) 
   return h;
 }
 
+/* MAC (48 bits) set hash, shared by the host bridge-set build and the device probe */
+USN_HD uint32_t usn_mac_hash(uint64_t m) {
+  m ^= m >> 29;
+  m *= 0xBF58476D1CE4E5B9ull;
+  m ^= m >> 32;
+  return (uint32_t)m;
+}
+
+/* 48-bit fingerprint of a packed Want key (tx learned-rule set) */
+USN_HD uint64_t usn_key_fp48(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
+  uint64_t h = ((uint64_t)x << 32 | y) * 0x9E3779B97F4A7C15ull;
+  h ^= (((uint64_t)z << 32) | meta) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+  h *= 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 31;
+  return h & 0xFFFFFFFFFFFFull;
+}
+
 USN_HD uint32_t usn_key_meta(uint32_t proto, uint32_t present) {
   return (proto & 0xFFu) | ((present & 7u) << 8) | USN_SLOT_VALID;
 }

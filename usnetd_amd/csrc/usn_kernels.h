@@ -44,6 +44,7 @@ struct ClassifyArgs {
   uint32_t nbits;           /* bits to tell bins apart (ceil log2 nbins) */
   uint32_t n_ep;            /* endpoints (bin of NIC) */
   uint32_t probe_mask;      /* bit0: rules key1 can hit exist; bit1: rules key2 can hit */
+  uint32_t next_dhcp_set;   /* the source's next_dhcp_endpoint is Some: DHCP answers need the host */
   /* carried 1-entry decision cache */
   uint32_t carry_mode;
   uint32_t cin_state, cin_dst;
@@ -61,6 +62,41 @@ struct MultiArgs {
   uint32_t tile_base[USN_MAX_MULTI + 1];
   uint32_t count;
 };
+
+/* ---- tx direction (a non-NIC source sends): four launches ---------------- */
+/* per-frame record (2 x uint4), written by tx_scan:
+ *   r0 = {i0 | TXR_* flags, src, dst, ports}
+ *   r1 = {smac[0..3], smac[4..5] | dmac[0..1] << 16, dmac[2..5], 0}          */
+#define TXR_TOUCH_SHIFT 20u    /* 2 bits: 0 none, 1 retains, 2 leaves None, 3 unknown */
+#define TXR_LEARNMAC (1u << 22)  /* unicast smac not in the bridge snapshot */
+#define TXR_LEARNRULE (1u << 23) /* answer key not listened, not in the table snapshot */
+#define TXR_HOST (1u << 24)      /* ordered host stage decides this frame */
+#define TXR_SMAC_IN (1u << 25)
+#define TXR_DMAC_IN (1u << 26)
+#define TXR_HIT (1u << 27)       /* 1-entry cache hit (set by tx_hits) */
+#define TXR_DHCPANS (1u << 28)
+#define TXR_I0_MASK 0x1FFFFu
+
+struct TxArgs {
+  ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
+  uint4 *rec;                 /* n x 2 */
+  uint32_t *aux;              /* per tile x 4: [0] 1+last touching, [1] 1+last non-hit touching */
+  unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
+  unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
+  uint32_t macset_mask, ruleset_mask;
+  uint32_t epoch;             /* 1..65535 */
+  uint4 *learned;             /* items appended by tx_decide: {frame, kind 0 mac | 1 rule},
+                                 {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
+  uint32_t *counters;         /* [0] learned pairs, [1] overflow flag */
+  uint32_t learned_cap;
+  const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
+  uint32_t bridge_mask;
+  const uint32_t *listen;     /* n_listen x {dst, proto | has_port << 8 | port << 16} */
+  uint32_t n_listen;
+  uint32_t next_dhcp_set;     /* the source's next_dhcp_endpoint is Some */
+};
+
+hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense);

@@ -24,7 +24,8 @@ F_CACHE, F_FRAG1, F_FRAGN, F_DHCP, F_HOST, F_LEARN = (1 << 24, 1 << 25, 1 << 26,
                                                       1 << 28, 1 << 29)
 S_STALE, S_STALE_EXTENDS, S_COUT = 1, 2, 8
 STATUS = {0: "ok", -22: "EINVAL", -12: "ENOMEM", -17: "EEXIST", -2: "ENOENT", -1: "EPERM",
-          -5: "EHIP", -19: "ENODEV", -34: "ERANGE"}
+          -5: "EHIP", -19: "ENODEV", -34: "ERANGE", -16: "EBUSY"}
+USN_EBUSY = -16
 
 
 class UsnError(RuntimeError):
@@ -246,6 +247,9 @@ class Ctx:
 
     def bridge_add(self, mac: bytes):
         check(self.L.usn_bridge_add(self.h, bytes(mac)), "usn_bridge_add")
+
+    def bridge_count(self) -> int:
+        return check(self.L.usn_bridge_count(self.h), "usn_bridge_count")
 
     def frag_clear(self):
         check(self.L.usn_frag_clear(self.h), "usn_frag_clear")

@@ -222,7 +222,62 @@ def c5(n=1 << 23, seed=5):
     return Config("c5", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(1000), rules)
 
 
-CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5}
+def c4tx(n=1 << 18, seed=6, host_at=None):
+    """c4's mix SENT by the host endpoint (tx: find_forward with incoming ==
+    false, endpoint.rs:194-256), the "ADD_MACS learned-MAC path" of
+    BASELINE.json configs[3]: the bridge is prefilled with 64 endpoint MACs
+    (main.rs:450-462); a quarter of the unicast source MACs are not yet in it
+    (learned), some are multicast (never learned); half of the frames go to a
+    bridged MAC (rule lookup), half to the gateway (Target::Nic); every new flow
+    learns its answer rule (to_want); 30 % of frames repeat the previous one
+    (decision cache).  host_at: frame indices replaced by a DHCP request (its
+    effect on the NIC is ordered host work)."""
+    cfg = c4(n, seed)
+    rng = np.random.default_rng(seed + 100)
+    stride = cfg.stride
+    V = cfg.frames[:n * stride].reshape(n, stride)
+    to_bridge = rng.random(n) < 0.5
+    # to the gateway: the local side sends (swap addresses and ports); to a
+    # bridged MAC: endpoint-to-endpoint traffic addressed to the rules' side
+    ip = (V[:, 12] == 0x08) & (V[:, 13] == 0x00) & ~to_bridge
+    a, b = V[ip, 26:30].copy(), V[ip, 30:34].copy()
+    V[ip, 26:30], V[ip, 30:34] = b, a
+    a, b = V[ip, 34:36].copy(), V[ip, 36:38].copy()
+    V[ip, 34:36], V[ip, 36:38] = b, a
+    bridged = np.zeros((64, 6), np.uint8)
+    bridged[:, 0] = 0x02
+    bridged[:, 5] = np.arange(64)
+    bridged[:, 4] = 0xB0
+    pool = np.zeros((256, 6), np.uint8)
+    pool[:, 0] = 0x02
+    pool[:, 4] = 0xC0
+    pool[:, 5] = np.arange(256)
+    pool[:192] = np.concatenate([bridged, bridged, bridged])[:192]   # in the bridge
+    pool[250:, 0] = 0x03                                             # multicast: never learned
+    arp = (V[:, 12] == 0x08) & (V[:, 13] == 0x06)
+    dmac = np.where(to_bridge[:, None], bridged[rng.integers(0, 64, n)],
+                    np.frombuffer(REMMAC, np.uint8)[None, :])
+    dmac[arp] = 0xFF
+    V[:, 0:6] = dmac
+    V[:, 6:12] = pool[rng.integers(0, 256, n)]
+    rep = rng.random(n) < 0.3
+    rep[0] = False
+    idx = np.arange(n)
+    idx[rep] = 0
+    idx = np.maximum.accumulate(np.where(rep, 0, idx))
+    V[:] = V[idx]
+    lens = cfg.lens[idx].copy()
+    if host_at:
+        req = build_ipv4(1, 0xFFFFFFFF, 0, UDP, 68, 67, np.array([64], np.uint16),
+                         dmac=b"\xff" * 6, smac=bytes(pool[3]))
+        for i in host_at:
+            V[i, :64] = req[0]
+            lens[i] = 64
+    return Config("c4tx", n, cfg.frames, lens, stride, 1, cfg.endpoints, cfg.rules,
+                  bridge=[bytes(m) for m in bridged])
+
+
+CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4tx": c4tx}
 
 
 def config(name, n=None, seed=None, **kw):
