@@ -190,9 +190,26 @@ int usn_rules_get(usn_ctx *ctx, usn_want *w, uint16_t *owner, uint8_t *sticky, u
 /* Owner of an exact key, or USN_ENOENT. */
 int usn_lookup(usn_ctx *ctx, const usn_want *w);
 
+/* Bulk registry load (SURVEY §8b usn_table_build): replaces match_register
+ * (main.rs:867) with `n` rules in one call -- e.g. a daemon restoring its
+ * table.  Later duplicates of a key are ignored (HashMap::entry().or_insert).
+ * Listening triples are not touched (only AddMatch records them); every NIC
+ * decision cache is cleared.  Returns the number of rules in the registry. */
+typedef struct {
+  uint32_t dst_addr, src_addr;
+  uint16_t dst_port, src_port;
+  uint8_t protocol;
+  uint8_t present;     /* USN_WANT_* bits | USN_RULE_STICKY */
+  uint16_t endpoint;   /* owner */
+} usn_rule;
+#define USN_RULE_STICKY 0x80u
+int usn_table_build(usn_ctx *ctx, const usn_rule *rules, uint32_t n);
+
 /* ADD_MACS prefill (main.rs:450-462): appends to the inner L2 bridge. */
 int usn_bridge_add(usn_ctx *ctx, const uint8_t mac[6]);
 int usn_bridge_count(usn_ctx *ctx);
+/* Replace the whole bridge with `n` MACs (SURVEY §8b usn_bridge_set). */
+int usn_bridge_set(usn_ctx *ctx, const uint8_t (*macs)[6], uint32_t n);
 /* 90 s cleanup: fragmentation_map.clear() (main.rs Cleanup handler). */
 int usn_frag_clear(usn_ctx *ctx);
 

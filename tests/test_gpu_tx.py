@@ -85,3 +85,28 @@ def test_tx_busy_until_finalize(coracle_mod):
     assert ctx.rule_count() > len(cfg.rules)
     info = ctx.finalize(b, r)   # again: already final
     assert info.n_host == 0
+
+
+def test_bulk_table_build_and_bridge_set(coracle_mod):
+    """usn_table_build / usn_bridge_set give the same decisions as rule-by-rule
+    AddMatch + ADD_MACS (the listening triples aside, which only AddMatch records)."""
+    from usnetd_amd import lib, traffic
+    cfg = traffic.config("c4", n=1 << 14)
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfg)
+    want = o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
+    ctx = lib.Ctx(0)
+    for eid, kind, for_nic in cfg.endpoints:
+        ctx.endpoint_add(eid, kind, for_nic)
+    rules = [(lib.make_want(w["dst"], w["proto"], w["dport"], w["src"], w["sport"]), owner, sticky)
+             for w, owner, sticky in cfg.rules]
+    assert ctx.table_build(rules + rules[:5]) == len(cfg.rules)
+    ctx.bridge_set([bytes.fromhex("02000000b001"), bytes.fromhex("02000000b002")])
+    assert ctx.bridge_count() == 2
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+    r = lib.DeviceResult(ctx, cfg.n)
+    ctx.classify(b, r)
+    ctx.finalize(b, r)
+    got = r.decisions()
+    assert ((got & katrun.PARITY_MASK) == (want & katrun.PARITY_MASK)).all()
+    assert _registry_gpu(ctx) == sorted(o.rules())

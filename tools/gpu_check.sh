@@ -30,6 +30,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     ablms) step ablms 600 python tools/abl.py --streams ${NSTREAMS:-2} --batches 6 --json gpurun_out/ablms.json ${ABL_VARIANTS:-base loadonly} ;;
     ablmulti) step ablmulti_${NMULTI:-4}_${NSTREAMS:-1} 600 python tools/abl.py --multi ${NMULTI:-4} --streams ${NSTREAMS:-1} --batches ${NBATCH:-8} --json gpurun_out/ablmulti.json ${ABL_VARIANTS:-base loadonly} ;;
     hostio) step hostio 300 python tools/hostio.py ${HOSTIO_ARGS:-} ;;
+    txbench) step txbench 600 python tools/txbench.py ${TXB_ARGS:-} ;;
+    txprof) rm -rf gpurun_out/txprof; step txprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txprof -o run -- python3 tools/txbench.py ${TXB_ARGS:-} ;;
     ablsmall) step ablsmall 600 python tools/abl.py --frames 131072 --batches 1 --json gpurun_out/ablsmall.json ;;
     counters)
       step listctr 120 rocprofv3 -L

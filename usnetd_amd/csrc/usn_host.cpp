@@ -154,6 +154,11 @@ struct usn_ctx {
   std::vector<Chain> chains = std::vector<Chain>(USN_MAX_ENDPOINTS);
   /* device table snapshot */
   bool table_dirty = true;
+  /* host image of the device table; inserts go straight into it while the
+   * load stays <= 1/2 (tx learning adds rules in bulk), removals rebuild */
+  std::vector<uint4> img;
+  bool img_valid = false;
+  uint32_t img_pmask = 0;
   uint4 *d_table = nullptr;
   size_t d_table_cap = 0;
   uint32_t table_slots = 0, bucket_mask = 0;
@@ -192,38 +197,54 @@ uint32_t next_pow2(uint32_t v) {
   return p;
 }
 
-int rebuild_table(usn_ctx *c) {
-  const uint32_t n = (uint32_t)c->rules.size();
-  uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
-  std::vector<uint4> img((size_t)nb * 4);
-  std::memset(img.data(), 0, img.size() * sizeof(uint4));
-  uint32_t pmask = 0;
-  for (const auto &kv : c->rules) {
-    const WantKey &k = kv.first;
-    /* key1 (to_match_want_with_src(true)) always has src and has both ports or
-     * neither; key2 has neither src nor src_port.  Other shapes never match. */
-    if (k.present == USN_WANT_SRC || k.present == (USN_WANT_SRC | USN_WANT_DPORT | USN_WANT_SPORT))
-      pmask |= 1u;
-    if (k.present == 0 || k.present == USN_WANT_DPORT) pmask |= 2u;
-    const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
-    const uint32_t meta = usn_key_meta(k.proto, k.present);
-    uint32_t b = usn_key_hash(k.dst, k.src, z, meta) & (nb - 1);
-    for (;;) {
-      uint4 *s = &img[(size_t)b * 4];
-      int free_slot = -1;
-      for (int j = 0; j < 4; ++j)
-        if (!(s[j].w & USN_SLOT_VALID)) { free_slot = j; break; }
-      if (free_slot >= 0) {
-        const uint16_t owner = kv.second.owner;
-        const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
-        s[free_slot] = make_uint4(k.dst, k.src, z,
-                                  meta | (nic ? USN_SLOT_NICOWNER : 0u) | ((uint32_t)owner << 16));
-        break;
+/* key shapes key1/key2 can take (ClassifyArgs::probe_mask): key1
+ * (to_match_want_with_src(true)) always has src and both ports or neither;
+ * key2 has neither src nor src_port.  Other shapes never match. */
+uint32_t shape_bits(const WantKey &k) {
+  uint32_t m = 0;
+  if (k.present == USN_WANT_SRC || k.present == (USN_WANT_SRC | USN_WANT_DPORT | USN_WANT_SPORT))
+    m |= 1u;
+  if (k.present == 0 || k.present == USN_WANT_DPORT) m |= 2u;
+  return m;
+}
+
+void img_put(usn_ctx *c, const WantKey &k, uint16_t owner) {
+  const uint32_t nb = (uint32_t)(c->img.size() / 4);
+  const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
+  const uint32_t meta = usn_key_meta(k.proto, k.present);
+  const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
+  uint32_t b = usn_key_hash(k.dst, k.src, z, meta) & (nb - 1);
+  for (;;) {
+    uint4 *s = &c->img[(size_t)b * 4];
+    for (int j = 0; j < 4; ++j)
+      if (!(s[j].w & USN_SLOT_VALID)) {
+        s[j] = make_uint4(k.dst, k.src, z,
+                          meta | (nic ? USN_SLOT_NICOWNER : 0u) | ((uint32_t)owner << 16));
+        c->img_pmask |= shape_bits(k);
+        return;
       }
-      b = (b + 1) & (nb - 1);
-    }
+    b = (b + 1) & (nb - 1);
   }
-  const size_t bytes = img.size() * sizeof(uint4);
+}
+
+/* registry insert; keeps the host image current when it can */
+void rule_insert(usn_ctx *c, const WantKey &k, Rule r) {
+  c->rules[k] = r;
+  c->table_dirty = true;
+  if (c->img_valid && 2 * c->rules.size() <= c->img.size()) img_put(c, k, r.owner);
+  else c->img_valid = false;
+}
+
+int rebuild_table(usn_ctx *c) {
+  if (!c->img_valid) {
+    const uint32_t n = (uint32_t)c->rules.size();
+    const uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
+    c->img.assign((size_t)nb * 4, make_uint4(0, 0, 0, 0));
+    c->img_pmask = 0;
+    for (const auto &kv : c->rules) img_put(c, kv.first, kv.second.owner);
+    c->img_valid = true;
+  }
+  const size_t bytes = c->img.size() * sizeof(uint4);
   HIPCHK(hipDeviceSynchronize());   // no in-flight batch may read the old snapshot
   if (bytes > c->d_table_cap) {
     if (c->d_table) HIPCHK(hipFree(c->d_table));
@@ -231,10 +252,10 @@ int rebuild_table(usn_ctx *c) {
     HIPCHK(hipMalloc(&c->d_table, bytes));
     c->d_table_cap = bytes;
   }
-  HIPCHK(hipMemcpy(c->d_table, img.data(), bytes, hipMemcpyHostToDevice));
-  c->table_slots = nb * 4;
-  c->bucket_mask = nb - 1;
-  c->probe_mask = pmask;
+  HIPCHK(hipMemcpy(c->d_table, c->img.data(), bytes, hipMemcpyHostToDevice));
+  c->table_slots = (uint32_t)c->img.size();
+  c->bucket_mask = (uint32_t)(c->img.size() / 4) - 1;
+  c->probe_mask = c->img_pmask;
   c->table_dirty = false;
   return USN_OK;
 }
@@ -388,8 +409,7 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
         }
       } else if (!c->rules.count(w)) {
         if (S.for_nic >= 0) cache_clear(c, S.for_nic);
-        c->rules[w] = Rule{(uint16_t)src, 0};
-        c->table_dirty = true;
+        rule_insert(c, w, Rule{(uint16_t)src, 0});
         learned = true;
       }
     }
@@ -514,8 +534,13 @@ int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
   if (c->tx.pending) return USN_EBUSY;
   if (!c->eps[id].used) return USN_ENOENT;
   for (auto it = c->rules.begin(); it != c->rules.end();) {   // match_register.retain
-    if (it->second.owner == id) { it = c->rules.erase(it); c->table_dirty = true; }
-    else ++it;
+    if (it->second.owner == id) {
+      it = c->rules.erase(it);
+      c->table_dirty = true;
+      c->img_valid = false;
+    } else {
+      ++it;
+    }
   }
   c->eps[id] = Ep();
   c->chains[id] = Chain();
@@ -534,8 +559,7 @@ int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
                                k.dport});                            // main.rs:276-279
   if (e.for_nic < 0) return USN_EPERM;                                // main.rs:287-289 panics
   cache_clear(c, e.for_nic);                                          // main.rs:280-286
-  c->rules[k] = Rule{owner, (uint8_t)(sticky ? 1 : 0)};
-  c->table_dirty = true;
+  rule_insert(c, k, Rule{owner, (uint8_t)(sticky ? 1 : 0)});
   return 1;
 }
 
@@ -549,6 +573,7 @@ int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
   if (it->second.owner != requester) return USN_EPERM;               // main.rs:612-616
   c->rules.erase(it);
   c->table_dirty = true;
+  c->img_valid = false;
   return 1;
 }
 
@@ -598,6 +623,44 @@ int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
   c->bridge.push_back(mac48(mac));
   c->bridge_dirty = true;
   return USN_OK;
+}
+
+int usn_bridge_set(usn_ctx *c, const uint8_t (*macs)[6], uint32_t n) {
+  if (!c || (n && !macs)) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
+  c->bridge.clear();
+  for (uint32_t i = 0; i < n; ++i) c->bridge.push_back(mac48(macs[i]));
+  c->bridge_dirty = true;
+  return USN_OK;
+}
+
+int usn_table_build(usn_ctx *c, const usn_rule *rules, uint32_t n) {
+  if (!c || (n && !rules)) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->tx.pending) return USN_EBUSY;
+  for (uint32_t i = 0; i < n; ++i)
+    if (rules[i].endpoint >= USN_MAX_ENDPOINTS || !c->eps[rules[i].endpoint].used)
+      return USN_ENOENT;
+  c->rules.clear();
+  c->rules.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    usn_want w;
+    std::memset(&w, 0, sizeof w);
+    w.dst_addr = rules[i].dst_addr;
+    w.src_addr = rules[i].src_addr;
+    w.dst_port = rules[i].dst_port;
+    w.src_port = rules[i].src_port;
+    w.protocol = rules[i].protocol;
+    w.present = rules[i].present & 7u;
+    c->rules.emplace(canon(w), Rule{rules[i].endpoint,
+                                    (uint8_t)((rules[i].present & USN_RULE_STICKY) ? 1 : 0)});
+  }
+  for (int e = 0; e < USN_MAX_ENDPOINTS; ++e)
+    if (c->eps[e].used && c->eps[e].kind == USN_EP_NIC) cache_clear(c, e);
+  c->table_dirty = true;
+  c->img_valid = false;
+  return (int)c->rules.size();
 }
 
 int usn_bridge_count(usn_ctx *c) {
@@ -892,6 +955,38 @@ bool retains(uint32_t d) {
   return USN_DEC_CLASS(d) != USN_CLS_FLOOD && USN_DEC_REASON(d) != USN_R_LOOPBACK;
 }
 
+/* the per-tile host lists of a result, merged in frame order: one copy per
+ * listed tile, or one bulk copy of the whole area when many tiles list frames */
+int fetch_host_lists(const usn_result *r, const std::vector<usn_tile_hdr> &th,
+                     std::vector<uint32_t> &hosts) {
+  const uint32_t ntiles = (uint32_t)th.size();
+  uint32_t listed = 0;
+  size_t total = 0;
+  for (const usn_tile_hdr &h : th) {
+    listed += h.n_host ? 1u : 0u;
+    total += h.n_host;
+  }
+  hosts.clear();
+  hosts.reserve(total);
+  if (listed > 32) {
+    std::vector<uint32_t> all((size_t)ntiles * USN_TILE);
+    HIPCHK(hipMemcpy(all.data(), r->host_list, all.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t t = 0; t < ntiles; ++t)
+      hosts.insert(hosts.end(), all.begin() + (size_t)t * USN_TILE,
+                   all.begin() + (size_t)t * USN_TILE + th[t].n_host);
+  } else {
+    for (uint32_t t = 0; t < ntiles; ++t) {
+      if (!th[t].n_host) continue;
+      const size_t at = hosts.size();
+      hosts.resize(at + th[t].n_host);
+      HIPCHK(hipMemcpy(hosts.data() + at, r->host_list + (size_t)t * USN_TILE,
+                       th[t].n_host * 4, hipMemcpyDeviceToHost));
+    }
+  }
+  std::sort(hosts.begin(), hosts.end());
+  return USN_OK;
+}
+
 }  // namespace
 
 /* Ordered host stage of a tx batch.  Frames before the first F_HOST frame h
@@ -915,19 +1010,17 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
   fi.flags = sum.flags;
-  std::vector<uint32_t> hosts;
-  for (uint32_t t = 0; t < ntiles; ++t) {
+  for (uint32_t t = 0; t < ntiles; ++t)
     for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
-    if (th[t].n_host) {
-      const size_t at = hosts.size();
-      hosts.resize(at + th[t].n_host);
-      HIPCHK(hipMemcpy(hosts.data() + at, r->host_list + (size_t)t * USN_TILE,
-                       th[t].n_host * 4, hipMemcpyDeviceToHost));
-    }
+  std::vector<uint32_t> hosts;
+  int st = fetch_host_lists(r, th, hosts);
+  if (st) return st;
+  if (hosts.empty() && cnt[0] == 0 && cnt[1] == 0) {   // nothing learned, nothing ordered
+    if (info) *info = fi;
+    return USN_OK;
   }
-  std::sort(hosts.begin(), hosts.end());
   HostView hv{c, b, r, s, {}, {}, false, false};
-  int st = hv.fetch_dec();
+  st = hv.fetch_dec();
   if (st) return st;
   uint64_t h = n;
   if (cnt[1]) h = 0;
@@ -941,6 +1034,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
                            hipMemcpyDeviceToHost));
   struct Ev { uint64_t idx; uint32_t kind; uint4 key; };   // kind 0 mac, 1 rule, 2 frag1
   std::vector<Ev> evs;
+  c->rules.reserve(c->rules.size() + nl);
   for (uint32_t k = 0; k < nl; ++k)
     if (items[2 * k].x < h) evs.push_back(Ev{items[2 * k].x, items[2 * k].y, items[2 * k + 1]});
   for (uint32_t j : hosts)
@@ -968,8 +1062,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       w.present = (uint8_t)((e.key.w >> 8) & 7u);
       if (!c->rules.count(w)) {
         if (S.for_nic >= 0) cache_clear(c, S.for_nic);
-        c->rules[w] = Rule{(uint16_t)src, 0};
-        c->table_dirty = true;
+        rule_insert(c, w, Rule{(uint16_t)src, 0});
         fi.n_learned++;
       }
     }
@@ -1074,15 +1167,12 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
   fi.flags = sum.flags;
-  std::vector<uint32_t> hosts;
-  for (uint32_t t = 0; t < ntiles; ++t) {
+  for (uint32_t t = 0; t < ntiles; ++t)
     for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
-    if (th[t].n_host) {
-      const size_t at = hosts.size();
-      hosts.resize(at + th[t].n_host);
-      HIPCHK(hipMemcpy(hosts.data() + at, r->host_list + (size_t)t * USN_TILE,
-                       th[t].n_host * 4, hipMemcpyDeviceToHost));
-    }
+  std::vector<uint32_t> hosts;
+  {
+    const int e = fetch_host_lists(r, th, hosts);
+    if (e) return e;
   }
   const bool stale_walk = (sum.flags & USN_S_STALE) && sum.first_break < b->n;
   if (hosts.empty() && !stale_walk && !(sum.flags & USN_S_STALE_EXTENDS)) {
@@ -1143,7 +1233,6 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     return USN_OK;
   };
 
-  std::sort(hosts.begin(), hosts.end());
   size_t hi = 0;
   /* stale prefix that the device could not close inside tile 0 */
   if (stale_walk || (sum.flags & USN_S_STALE_EXTENDS)) {

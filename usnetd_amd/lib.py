@@ -63,7 +63,10 @@ SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames",
                           ("n_tiles", "<u4"), ("cin_state", "<u4"), ("cin_dst", "<u4"),
                           ("cin_info", "<u4", (4,)), ("cout_state", "<u4"), ("cout_dst", "<u4"),
                           ("cout_info", "<u4", (4,))])
-assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 64
+RULE_DTYPE = np.dtype([("dst_addr", "<u4"), ("src_addr", "<u4"), ("dst_port", "<u2"),
+                       ("src_port", "<u2"), ("protocol", "u1"), ("present", "u1"),
+                       ("endpoint", "<u2")])
+assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 64 and RULE_DTYPE.itemsize == 16
 
 _libs: dict = {}
 
@@ -90,6 +93,7 @@ def load(path: str | None = None):
         "usn_rules_get": ([P, P, P, P, U32], I),
         "usn_lookup": ([P, C.POINTER(Want)], I),
         "usn_bridge_add": ([P, C.c_char_p], I), "usn_bridge_count": ([P], I),
+        "usn_bridge_set": ([P, P, U32], I), "usn_table_build": ([P, P, U32], I),
         "usn_frag_clear": ([P], I), "usn_cache_clear": ([P, U16], I),
         "usn_result_bytes": ([U64], SZ),
         "usn_result_bind": ([P, SZ, U64, C.POINTER(Result)], I),
@@ -123,7 +127,8 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_host_alloc_pinned", "usn_host_free_pinned", "usn_memcpy_h2d", "usn_memcpy_d2h",
             "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
             "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
-            "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi"]
+            "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi",
+            "usn_bridge_set", "usn_table_build"]
 
 
 def check(rc, what=""):
@@ -247,6 +252,19 @@ class Ctx:
 
     def bridge_add(self, mac: bytes):
         check(self.L.usn_bridge_add(self.h, bytes(mac)), "usn_bridge_add")
+
+    def table_build(self, rules) -> int:
+        """rules: [(Want, owner, sticky)] -> usn_table_build (bulk replace)."""
+        arr = np.zeros(len(rules), RULE_DTYPE)
+        for i, (w, owner, sticky) in enumerate(rules):
+            arr[i] = (w.dst_addr, w.src_addr, w.dst_port, w.src_port, w.protocol,
+                      (w.present & 7) | (0x80 if sticky else 0), owner)
+        return check(self.L.usn_table_build(self.h, arr.ctypes.data, len(rules)),
+                     "usn_table_build")
+
+    def bridge_set(self, macs) -> None:
+        arr = np.frombuffer(b"".join(bytes(m) for m in macs), np.uint8) if macs else np.zeros(6, np.uint8)
+        check(self.L.usn_bridge_set(self.h, arr.ctypes.data, len(macs)), "usn_bridge_set")
 
     def bridge_count(self) -> int:
         return check(self.L.usn_bridge_count(self.h), "usn_bridge_count")
