@@ -7,7 +7,15 @@ CSRC := usnetd_amd/csrc
 LIB := usnetd_amd/libusn.so
 OBJS := build/usn_device.o build/usn_host.o
 
-all: $(LIB) oracle
+DAEMON := usnetd_amd/bin/usnetd
+
+all: $(LIB) $(DAEMON) oracle
+
+# the daemon: plain C++ over the C ABI (links libusn.so; no HIP code of its own)
+$(DAEMON): usnetd_amd/daemon/usnetd.cpp usnetd_amd/daemon/messages.hpp usnetd_amd/daemon/json.hpp include/usn_classify.h $(LIB)
+	@mkdir -p usnetd_amd/bin
+	g++ -O2 -std=c++17 -Wall -Wextra -o $@ $< -Lusnetd_amd -lusn -Wl,-rpath,'$$ORIGIN/..' \
+	    -Wl,-rpath-link,/opt/rocm/lib -lpthread
 
 build/usn_device.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
 	@mkdir -p build
@@ -32,7 +40,7 @@ asm: $(CSRC)/usn_device.hip
 	$(HIPCC) $(HIPFLAGS) -S --offload-device-only -o build/usn_device.s $<
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(DAEMON)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean resources asm

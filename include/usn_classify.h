@@ -167,7 +167,10 @@ int usn_last_hip_error(void);
 
 /* Binds to HIP device `hip_device` (must be gfx950).  Replaces the daemon
  * state set up in main() (main.rs:447-449: fragmentation_map, match_register,
- * innerl2bridge). */
+ * innerl2bridge).  USN_HOST_ONLY gives a registry-only context for a control
+ * plane without a GPU: every device entry point (classify, finalize,
+ * plumbing) then returns USN_ENODEV -- there is no CPU classify path. */
+#define USN_HOST_ONLY (-1)
 int usn_ctx_create(int hip_device, usn_ctx **out);
 void usn_ctx_destroy(usn_ctx *ctx);
 

@@ -480,6 +480,13 @@ const char *usn_strerror(int s) {
 int usn_ctx_create(int hip_device, usn_ctx **out) {
   if (!out) return USN_EINVAL;
   *out = nullptr;
+  if (hip_device == USN_HOST_ONLY) {   // registry only: the control plane without a GPU
+    usn_ctx *c = new (std::nothrow) usn_ctx();
+    if (!c) return USN_ENOMEM;
+    c->device = -1;
+    *out = c;
+    return USN_OK;
+  }
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (hip_device < 0 || hip_device >= ndev) return USN_ENODEV;
@@ -497,6 +504,7 @@ int usn_ctx_create(int hip_device, usn_ctx **out) {
 
 void usn_ctx_destroy(usn_ctx *c) {
   if (!c) return;
+  if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->d_table) (void)hipFree(c->d_table);
@@ -828,6 +836,7 @@ static int tx_listen(usn_ctx *c, const Ep &S, uint32_t &n_listen) {
 int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t count,
                        void *stream) {
   if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
   if (c->tx.pending) return USN_EBUSY;
   bool tx = false;
@@ -1137,6 +1146,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
 int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
                  usn_finalize_info *info) {
   if (!c || !b || !r || b->n == 0) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
@@ -1284,42 +1294,50 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
 /* ---- device plumbing ------------------------------------------------------- */
 int usn_dev_alloc(usn_ctx *c, size_t bytes, void **p) {
   if (!c || !p) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMalloc(p, bytes));
   return USN_OK;
 }
 int usn_dev_free(usn_ctx *c, void *p) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipFree(p));
   return USN_OK;
 }
 int usn_host_alloc_pinned(usn_ctx *c, size_t bytes, void **p) {
   if (!c || !p) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipHostMalloc(p, bytes, hipHostMallocDefault));
   return USN_OK;
 }
 int usn_host_free_pinned(usn_ctx *c, void *p) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipHostFree(p));
   return USN_OK;
 }
 int usn_memcpy_h2d(usn_ctx *c, void *d, const void *h, size_t n, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, (hipStream_t)s));
   return USN_OK;
 }
 int usn_memcpy_d2h(usn_ctx *c, void *h, const void *d, size_t n, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, (hipStream_t)s));
   return USN_OK;
 }
 int usn_memset_d(usn_ctx *c, void *d, int v, size_t n, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipMemsetAsync(d, v, n, (hipStream_t)s));
   return USN_OK;
 }
 int usn_stream_create(usn_ctx *c, void **s) {
   if (!c || !s) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipSetDevice(c->device));
   hipStream_t st;
   HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -1328,22 +1346,26 @@ int usn_stream_create(usn_ctx *c, void **s) {
 }
 int usn_stream_destroy(usn_ctx *c, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipStreamDestroy((hipStream_t)s));
   return USN_OK;
 }
 int usn_stream_sync(usn_ctx *c, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipStreamSynchronize((hipStream_t)s));
   return USN_OK;
 }
 int usn_device_sync(usn_ctx *c) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());
   return USN_OK;
 }
 int usn_event_create(usn_ctx *c, void **ev) {
   if (!c || !ev) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   hipEvent_t e;
   HIPCHK(hipEventCreate(&e));
   *ev = e;
@@ -1351,16 +1373,19 @@ int usn_event_create(usn_ctx *c, void **ev) {
 }
 int usn_event_destroy(usn_ctx *c, void *ev) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipEventDestroy((hipEvent_t)ev));
   return USN_OK;
 }
 int usn_event_record(usn_ctx *c, void *ev, void *s) {
   if (!c) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipEventRecord((hipEvent_t)ev, (hipStream_t)s));
   return USN_OK;
 }
 int usn_event_elapsed_ms(usn_ctx *c, void *a, void *b, float *ms) {
   if (!c || !ms) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipEventSynchronize((hipEvent_t)b));
   HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
   return USN_OK;
@@ -1368,6 +1393,7 @@ int usn_event_elapsed_ms(usn_ctx *c, void *a, void *b, float *ms) {
 
 int usn_stream_wait_event(usn_ctx *c, void *s, void *ev) {
   if (!c || !ev) return USN_EINVAL;
+  if (c->device < 0) return USN_ENODEV;
   HIPCHK(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)ev, 0));
   return USN_OK;
 }
