@@ -42,7 +42,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--launch-probe", type=int, default=100, help="per-launch event pairs")
-    ap.add_argument("--queues", type=int, default=8,
+    ap.add_argument("--queues", type=int, default=16,
                     help="NIC rx queues (sources) drained per poll round")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams; stream s owns queues [s*Q/S, (s+1)*Q/S) and classifies "

@@ -45,7 +45,8 @@ def sock_has_more(sock):
 def test_daemon_forwards_like_the_oracle():
     import coracle
     coracle.build()
-    d = Daemon({"INTERFACES": "eth0", "ADD_MACS": ",".join(MACS), "USNETD_MAX_BATCH": "64"},
+    d = Daemon({"INTERFACES": "eth0", "ADD_MACS": ",".join(MACS), "USNETD_MAX_BATCH": "64",
+                "USNETD_WRITE_WAIT_MS": "5000"},
                control_only=False)
     try:
         assert d.p.poll() is None, d.log_text()
@@ -85,16 +86,28 @@ def test_daemon_forwards_like_the_oracle():
                     if t in expect:
                         expect[t].append(f)
                 s, path = inj[src]
-                if path:
-                    s.sendto(f, path)
-                else:
-                    s.send(f)
+                t_end = time.time() + 10
+                while True:   # AF_UNIX datagram queues are short: keep the sinks drained
+                    try:
+                        if path:
+                            s.sendto(f, path)
+                        else:
+                            s.send(f)
+                        break
+                    except BlockingIOError:
+                        assert time.time() < t_end, "daemon stopped reading"
+                        for k2, s2 in out.items():
+                            _drain(s2, got[k2], time.time() + 0.01)
             deadline = time.time() + 5
             for k, s in out.items():
                 _drain(s, got[k], deadline)
-        time.sleep(0.3)
+        end = time.time() + 15
+        while time.time() < end and any(len(got[k]) < len(expect[k]) for k in out):
+            for k, s in out.items():
+                _drain(s, got[k], time.time() + 0.5)
+        time.sleep(0.2)
         for k, s in out.items():
-            _drain(s, got[k], time.time() + 1)
+            _drain(s, got[k], time.time() + 0.2)
         for k in out:
             assert len(got[k]) == len(expect[k]), (k, len(got[k]), len(expect[k]), d.log_text()[-2000:])
             assert got[k] == expect[k], k

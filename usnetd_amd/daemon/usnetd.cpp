@@ -138,6 +138,7 @@ struct Dev {
   int fd = -1;
   sockaddr_un peer{};         // NIC / host ring: where frames are sent
   socklen_t peer_len = 0;
+  int txfd = -1;              // NIC / host ring: socket connected to `peer` (lazily)
   /* two result buffers per source: the carried cache reads the previous one */
   void *res[2] = {nullptr, nullptr};
   int cur = 0;
@@ -190,6 +191,7 @@ class Daemon {
   uint64_t class_count_[4] = {0, 0, 0, 0};
   bool end_ = false;
   unsigned cleanup_secs_ = 90;
+  int write_wait_ms_ = 5;     // USNETD_WRITE_WAIT_MS: back-pressure before a frame is dropped
 
   /* data path buffers */
   static const uint32_t HDR = 128;        // header window stride on the device
@@ -679,6 +681,7 @@ void Daemon::remove_dev(const DevP &d) {
                       pipe_monitor_.end());
   for (void *r : d->res) if (r) usn_dev_free(ctx_, r);
   if (d->fd >= 0) close(d->fd);
+  if (d->txfd >= 0) close(d->txfd);
   used_ids_[d->id] = 0;
   devices_.erase(it);
   LOGI("cleared endpoint %u", d->id);
@@ -710,16 +713,41 @@ bool Daemon::data_path_init() {
   return true;
 }
 
+/* Endpoint write (EndpointDevice::write).  A full peer queue waits up to
+ * USNETD_WRITE_WAIT_MS for room, then the frame is dropped with a debug log
+ * (a full tx ring); a vanished client is Unaddressable (endpoint.rs:90-105)
+ * and is removed after the round. */
 int Daemon::write_frame(const DevP &t, const uint8_t *p, uint32_t len) {
-  ssize_t r;
-  if (t->kind == USN_EP_UDS) r = send(t->fd, p, len, MSG_DONTWAIT | MSG_NOSIGNAL);
-  else r = sendto(t->fd, p, len, MSG_DONTWAIT | MSG_NOSIGNAL, (sockaddr *)&t->peer, t->peer_len);
-  if (r == (ssize_t)len) { t->frames_out++; return 0; }
-  const int e = errno;
-  LOGD("Write error %s for endpoint %u", std::strerror(e), t->id);
-  // a vanished client is Unaddressable (endpoint.rs:90-105): remove it after the round
-  if (t->kind == USN_EP_UDS && (e == ECONNREFUSED || e == EPIPE || e == ENOTCONN || e == ECONNRESET))
-    return 1;
+  int fd = t->fd;
+  if (t->kind != USN_EP_UDS) {   // the wire / kernel side, connected for flow control
+    if (t->txfd < 0) {
+      t->txfd = socket(AF_UNIX, SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      if (t->txfd >= 0 && connect(t->txfd, (sockaddr *)&t->peer, t->peer_len) != 0) {
+        close(t->txfd);
+        t->txfd = -1;
+      }
+      if (t->txfd < 0) { LOGD("no peer for endpoint %u", t->id); return 0; }
+    }
+    fd = t->txfd;
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const ssize_t r = send(fd, p, len, MSG_DONTWAIT | MSG_NOSIGNAL);
+    if (r == (ssize_t)len) { t->frames_out++; return 0; }
+    const int e = errno;
+    if (e == EAGAIN && attempt == 0 && write_wait_ms_ > 0) {
+      pollfd pf{fd, POLLOUT, 0};
+      poll(&pf, 1, write_wait_ms_);
+      continue;
+    }
+    LOGD("Write error %s for endpoint %u", std::strerror(e), t->id);
+    if (t->kind == USN_EP_UDS && (e == ECONNREFUSED || e == EPIPE || e == ENOTCONN || e == ECONNRESET))
+      return 1;
+    if (t->kind != USN_EP_UDS && (e == ECONNREFUSED || e == ENOTCONN)) {   // peer went away
+      close(t->txfd);
+      t->txfd = -1;
+    }
+    return 0;
+  }
   return 0;
 }
 
@@ -847,6 +875,8 @@ int Daemon::run(int argc, char **argv) {
   test_dump_ = env("USNETD_TEST_DUMP") == "1";
   if (has_env("USNETD_CLEANUP_SECS"))
     cleanup_secs_ = (unsigned)std::max(1L, std::strtol(env("USNETD_CLEANUP_SECS").c_str(), nullptr, 10));
+  if (has_env("USNETD_WRITE_WAIT_MS"))
+    write_wait_ms_ = std::max(0, std::atoi(env("USNETD_WRITE_WAIT_MS").c_str()));
   if (has_env("USNETD_MAX_BATCH"))
     max_batch_ = (uint32_t)std::max(1L, std::strtol(env("USNETD_MAX_BATCH").c_str(), nullptr, 10));
   const int dev = data_path_ ? std::atoi(env("USNETD_HIP_DEVICE", "0").c_str()) : USN_HOST_ONLY;
