@@ -236,6 +236,7 @@ def main():
             pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
+        out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     for b in batches:
@@ -266,6 +267,44 @@ def cpu_baseline(cfg, seconds):
             "kind": "port",
             "sample": "%d passes over one %s batch (%d x 64B frames), sequential C restatement "
                       "with the 1-entry cache, %.1f s" % (passes, cfg.name, cfg.n, el)}
+
+
+def _cpu_worker(arg):
+    """One core: its own oracle, its own rx queue (batch), passes for ~seconds."""
+    name, n, seed, seconds = arg
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle
+    from usnetd_amd import traffic
+    cfg = traffic.config(name, n=n, seed=seed)
+    o = coracle.Oracle()
+    coracle.install_oracle(o, cfg)
+    passes, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
+        passes += 1
+    return passes * cfg.n, time.perf_counter() - t0
+
+
+def cpu_baseline_ncores(name, n, seconds):
+    """SURVEY §8d's N-core variant: the sequential oracle sharded by rx queue,
+    one process per core, N = the host CPUs this job may use (at most 16 on
+    the GPU box).  Aggregate frames / slowest worker's time."""
+    import multiprocessing as mp
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    ncores = max(1, min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)), 16))
+    nshard = min(n, 1 << 18)   # each core's queue: a quarter-size batch keeps memory small
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(ncores) as pool:
+        res = pool.map(_cpu_worker, [(name, nshard, 1000 + k, seconds) for k in range(ncores)])
+    frames = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": round(frames / el / 1e6, 3), "unit": "Mpkts/s", "cores": ncores,
+            "kind": "port",
+            "sample": "%d processes, each the sequential C restatement over its own %s rx queue "
+                      "(%d x 64B frames) for %.1f s" % (ncores, name, nshard, el)}
 
 
 if __name__ == "__main__":

@@ -110,3 +110,82 @@ def test_bulk_table_build_and_bridge_set(coracle_mod):
     got = r.decisions()
     assert ((got & katrun.PARITY_MASK) == (want & katrun.PARITY_MASK)).all()
     assert _registry_gpu(ctx) == sorted(o.rules())
+
+
+def _check(cfg, coracle_mod, offsets=None, frames=None, lens=None, src=None):
+    from usnetd_amd import lib, traffic
+    frames = cfg.frames if frames is None else frames
+    lens = cfg.lens if lens is None else lens
+    src = cfg.src if src is None else src
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfg)
+    if offsets is None:
+        want = o.forward_batch(src, frames, lens, stride=cfg.stride)
+    else:
+        want = o.forward_batch(src, frames, lens, offsets=offsets)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    if offsets is None:
+        b = lib.DeviceBatch(ctx, frames, lens, src, stride=cfg.stride)
+    else:
+        b = lib.DeviceBatch(ctx, frames, lens, src, offsets=offsets)
+    r = lib.DeviceResult(ctx, len(lens))
+    ctx.classify(b, r)
+    info = ctx.finalize(b, r)
+    got = r.decisions()
+    bad = np.nonzero((got & katrun.PARITY_MASK) != (want & katrun.PARITY_MASK))[0]
+    assert bad.size == 0, "%d mismatches, first %d: got %#x want %#x" % (
+        bad.size, bad[0], got[bad[0]], want[bad[0]])
+    check_order(r, got)
+    assert sorted(o.rules()) == _registry_gpu(ctx)
+    assert o.bridge_count() == ctx.bridge_count()
+    return info
+
+
+def test_tx_ragged_offsets(coracle_mod):
+    """Ragged frame lengths packed through an offsets array, sent by an endpoint."""
+    from usnetd_amd import traffic
+    cfg = traffic.c4tx(n=20000, seed=11)
+    rng = np.random.default_rng(3)
+    n = cfg.n
+    lens = rng.integers(0, 129, n).astype(np.uint16)
+    lens[rng.random(n) < 0.7] = 64
+    slot = ((lens.astype(np.int64) + 15) // 16) * 16
+    offs = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(slot.sum()) + 128, np.uint8)
+    for i in range(n):
+        o_, l_ = int(offs[i]), int(lens[i])
+        buf[o_:o_ + l_] = cfg.frames[i * cfg.stride:i * cfg.stride + min(l_, 64)][:l_]
+    _check(cfg, coracle_mod, offsets=offs, frames=buf, lens=lens)
+
+
+def test_tx_fragments(coracle_mod):
+    """First fragments sent by an endpoint are remembered in order; the first
+    later fragment starts the ordered host tail."""
+    from usnetd_amd import traffic
+    cfg = traffic.c4tx(n=8192, seed=12)
+    V = cfg.frames[:cfg.n * cfg.stride].reshape(cfg.n, cfg.stride)
+    ip = np.nonzero((V[:, 12] == 8) & (V[:, 13] == 0))[0]
+    first, later = ip[100:160], ip[3000:3010]
+    V[first, 20], V[first, 21] = 0x20, 0x00            # MF, offset 0
+    V[later, 20], V[later, 21] = 0x00, 0xB9            # offset 185
+    V[later, 18:20] = V[first[:10], 18:20]             # same ident ...
+    V[later, 26:34] = V[first[:10], 26:34]             # ... addresses
+    V[later, 0:12] = V[first[:10], 0:12]               # ... and MACs: map hits
+    V[later, 23] = V[first[:10], 23]
+    info = _check(cfg, coracle_mod)
+    assert info.n_host == cfg.n - int(later[0])
+
+
+def test_tx_imix_stride_2048_from_pipe(coracle_mod):
+    from usnetd_amd import traffic
+    cfg = traffic.config("c3", n=1 << 15)
+    info = _check(cfg, coracle_mod, src=2)          # endpoint 2 (a pipe) sends c3's frames
+    assert info.n_learned > 0
+
+
+@pytest.mark.parametrize("n", [1, 2, 1023, 1025])
+def test_tx_tiny_and_tile_edges(n, coracle_mod):
+    from usnetd_amd import traffic
+    cfg = traffic.c4tx(n=n, seed=13)
+    _check(cfg, coracle_mod)

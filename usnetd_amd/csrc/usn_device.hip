@@ -874,6 +874,8 @@ __device__ uint32_t prev_tiles_last(const uint32_t *aux, uint32_t tile, uint32_t
   return 0;
 }
 
+#define TX_BRIDGE_LDS_SLOTS 2048u   /* bridge sets up to 16 KiB are staged in LDS */
+
 template <bool LDS>
 __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -902,17 +904,36 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       S->flags = 0; S->first_break = 0xFFFFFFFFu;
     }
   }
+  /* all header loads of the tile first (64 B x 4 frames per lane in flight) */
+  uint4 qq[ROUNDS][4];
+  uint32_t ll[ROUNDS];
+  const uint8_t *fps[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    const uint64_t i = base + (local < nt ? local : 0);
+    fps[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
+    ll[r] = a.lens[i];
+  }
+  /* the bridge snapshot set in LDS when small */
+  const unsigned long long *BS = t.bridge_set;
+  if (t.bridge_mask < TX_BRIDGE_LDS_SLOTS) {
+    unsigned long long *bs = reinterpret_cast<unsigned long long *>(L.table + (LDS ? a.table_slots : 0));
+    for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
+    BS = bs;
+  }
+  __syncthreads();
   uint32_t last = 0;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     if (local >= nt) continue;
     const uint64_t i = base + local;
-    const uint8_t *fp = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-    uint4 q[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(reinterpret_cast<const uint4 *>(fp) + k);
-    const uint32_t len = a.lens[i];
+    const uint8_t *fp = fps[r];
+    const uint4 *q = qq[r];
+    const uint32_t len = ll[r];
     Parsed p;
     parse(q, len, fp, p);
     const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
@@ -922,8 +943,8 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
                          : (p.status == 1u && !loop) ? 1u : 2u;
     uint32_t f = (touch << TXR_TOUCH_SHIFT);
     if (touch == 1u || touch == 2u) {
-      const bool s_in = bridge_has(t.bridge_set, t.bridge_mask, smac);
-      const bool d_in = bridge_has(t.bridge_set, t.bridge_mask, dmac);
+      const bool s_in = bridge_has(BS, t.bridge_mask, smac);
+      const bool d_in = bridge_has(BS, t.bridge_mask, dmac);
       if (s_in) f |= TXR_SMAC_IN;
       if (d_in) f |= TXR_DMAC_IN;
       if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
@@ -1247,8 +1268,10 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
   const size_t core = lds_core_bytes(a.nbins);
   const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds, false);
-  if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, with_table, stream, t);
-  else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, with_table, stream, t);
+  const size_t scan_lds =
+      with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
+  if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
+  else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, scan_lds, stream, t);
   hipLaunchKernelGGL(tx_hits_kernel, g, b, core, stream, t);
   if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, with_table, stream, t);
   else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, with_table, stream, t);
