@@ -155,7 +155,8 @@ def test_tx_ragged_offsets(coracle_mod):
     buf = np.zeros(int(slot.sum()) + 128, np.uint8)
     for i in range(n):
         o_, l_ = int(offs[i]), int(lens[i])
-        buf[o_:o_ + l_] = cfg.frames[i * cfg.stride:i * cfg.stride + min(l_, 64)][:l_]
+        c_ = min(l_, 64)
+        buf[o_:o_ + c_] = cfg.frames[i * cfg.stride:i * cfg.stride + c_]
     _check(cfg, coracle_mod, offsets=offs, frames=buf, lens=lens)
 
 

@@ -32,7 +32,10 @@
 namespace usn {
 
 #define TILE USN_TILE
-#define NTHREADS 256
+#ifndef USN_NTHREADS
+#define USN_NTHREADS 256
+#endif
+#define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
 #define MAX_NBITS 10   /* nbins <= 1024 */
@@ -378,7 +381,12 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
   uint16_t *dst = order_out + (size_t)tile * TILE;
   const uint32_t p0 = tid * ROUNDS;
   if (p0 + ROUNDS <= nt) {
-    *reinterpret_cast<uint2 *>(dst + p0) = *reinterpret_cast<const uint2 *>(L.order + p0);
+    if (ROUNDS == 4)
+      *reinterpret_cast<uint2 *>(dst + p0) = *reinterpret_cast<const uint2 *>(L.order + p0);
+    else if (ROUNDS == 2)
+      *reinterpret_cast<uint32_t *>(dst + p0) = *reinterpret_cast<const uint32_t *>(L.order + p0);
+    else
+      dst[p0] = L.order[p0];
   } else {
     for (uint32_t k = 0; k < ROUNDS; ++k)
       if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
@@ -1061,95 +1069,132 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
   if (tid == 0) t.aux[tile * 4 + 1] = s_last_nh;
 }
 
+/* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
+ * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
+ * by a frame <= i. */
+__device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
+                                   const uint4 &r1, uint32_t i) {
+  const ClassifyArgs &a = t.a;
+  const uint32_t fl = r0.x;
+  const uint64_t dmac = rec_dmac(r1);
+  bool d_in = (fl & TXR_DMAC_IN) != 0;
+  if (!d_in)                                           // learned by a frame <= i ?
+    d_in = slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, dmac, usn_mac_hash(dmac)),
+                      t.epoch) <= i;
+  if (!d_in) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
+  uint32_t x, y, z, meta;
+  key1_of(r0, x, y, z, meta);
+  uint32_t w = (a.probe_mask & 1u) ? probe(T, a.bucket_mask, x, y, z, meta) : 0u;
+  if (!w) {   // a rule learned by a frame <= i is owned by S (so excluded)
+    const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
+                                              usn_key_fp48(x, y, z, meta),
+                                              usn_key_hash(x, y, z, meta));
+    if (slot_first(slot, t.epoch) <= i) {
+      if (slot[2] != (((unsigned long long)y << 32) | x) ||
+          slot[3] != (((unsigned long long)meta << 32) | z))
+        atomicOr(t.counters + 1, 2u);                // fingerprint collision: host redoes
+      w = USN_SLOT_VALID | (a.src << 16);
+    }
+  }
+  const bool has = (r0.x >> 16) & 1u;
+  if (!w && (a.probe_mask & 2u))
+    w = probe(T, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
+              usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u));
+  const uint32_t owner = w >> 16;
+  const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
+  if (w && !excl) return usn_mkdec(USN_CLS_EP, USN_R_NONE, owner);
+  if (fl & TXR_DHCPANS)
+    return usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) |
+           (a.next_dhcp_set ? (USN_F_DHCP | USN_F_HOST) : 0u);
+  return usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
+}
+
+/* tx_decide + tx_fill in one launch: non-hit decisions into LDS, then every
+ * hit takes its run head's decision -- from LDS when the head is in the tile,
+ * else from the one head before the tile (recomputed here from its record) or
+ * the carried-in cache -- then the tile order and header. */
 template <bool LDS>
 __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
   extern __shared__ __align__(16) uint8_t smem[];
   const ClassifyArgs &a = t.a;
   const Lds L = carve(smem, a.nbins);
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  uint32_t *sdec = reinterpret_cast<uint32_t *>(L.table + (LDS ? a.table_slots : 0));
+  __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+  __shared__ uint32_t s_head;      // decision of the last non-hit touching frame before the tile
   const uint4 *T = a.table;
   if (LDS) {
     for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
     T = L.table;
   }
-  __syncthreads();
+  if (tid < 8) s_misc[tid] = 0;
+  for (uint32_t k = tid; k < NSEG * a.nbins; k += NTHREADS) L.cnt[k] = 0;
+  uint4 r0[ROUNDS], r1[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
+    const uint64_t i = base + (local < nt ? local : 0);
+    r0[r] = local < nt ? t.rec[2 * i] : make_uint4(0, 0, 0, 0);
+    r1[r] = local < nt ? t.rec[2 * i + 1] : make_uint4(0, 0, 0, 0);
+  }
+  const uint32_t before = prev_tiles_last(t.aux, tile, 1);   // 1 + index, 0 = none
+  __syncthreads();
+  if (tid == 0) {
+    const usn_summary *S = a.summary;
+    uint32_t hd = S->cin_dst;
+    if (before) {
+      const uint4 h0 = t.rec[2 * (size_t)(before - 1)], h1 = t.rec[2 * (size_t)(before - 1) + 1];
+      hd = decide_tx_ipv4(t, T, h0, h1, before - 1);
+    }
+    s_head = hd;
+  }
+  uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    v[r] = 0;
+    dec[r] = 0;
     if (local >= nt) continue;
     const uint64_t i = base + local;
-    const uint4 r0 = t.rec[2 * i], r1 = t.rec[2 * i + 1];
-    const uint32_t fl = r0.x, touch = tx_touch(r0), kind = fl & 0xFFu;
+    const uint32_t fl = r0[r].x, touch = tx_touch(r0[r]), kind = fl & 0xFFu;
     uint32_t d;
     if (touch == 0u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
     } else if (fl & TXR_HOST) {
       d = usn_mkdec(USN_CLS_DROP, touch == 3u ? USN_R_FRAGMISS : USN_R_NOMATCH, 0xFFFFu) | USN_F_HOST;
     } else if (fl & TXR_HIT) {
-      d = USN_F_CACHE;                                     // filled by tx_fill
+      d = USN_F_CACHE;                                     // the run head's, below
     } else if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) {
       d = usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
     } else {
-      const uint64_t dmac = rec_dmac(r1);
-      bool d_in = (fl & TXR_DMAC_IN) != 0;
-      if (!d_in)                                           // learned by a frame <= i ?
-        d_in = slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, dmac, usn_mac_hash(dmac)),
-                          t.epoch) <= (uint32_t)i;
-      if (!d_in) {
-        d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);  // endpoint.rs:254-255
-      } else {
-        uint32_t x, y, z, meta;
-        key1_of(r0, x, y, z, meta);
-        uint32_t w = (a.probe_mask & 1u) ? probe(T, a.bucket_mask, x, y, z, meta) : 0u;
-        if (!w) {   // a rule learned by a frame <= i is owned by S (so excluded)
-          const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
-                                                    usn_key_fp48(x, y, z, meta),
-                                                    usn_key_hash(x, y, z, meta));
-          if (slot_first(slot, t.epoch) <= (uint32_t)i) {
-            if (slot[2] != (((unsigned long long)y << 32) | x) ||
-                slot[3] != (((unsigned long long)meta << 32) | z))
-              atomicOr(t.counters + 1, 2u);                // fingerprint collision: host redoes
-            w = USN_SLOT_VALID | (a.src << 16);
-          }
-        }
-        const bool has = (r0.x >> 16) & 1u;
-        if (!w && (a.probe_mask & 2u))
-          w = probe(T, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
-                    usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u));
-        const uint32_t owner = w >> 16;
-        const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
-        if (w && !excl) d = usn_mkdec(USN_CLS_EP, USN_R_NONE, owner);
-        else if (fl & TXR_DHCPANS)
-          d = usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) |
-              (a.next_dhcp_set ? (USN_F_DHCP | USN_F_HOST) : 0u);
-        else d = usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
-      }
+      d = decide_tx_ipv4(t, T, r0[r], r1[r], (uint32_t)i);
     }
-    if (r1.w) d |= USN_F_FRAG1;                            // first fragment: remembered (host map)
+    if (r1[r].w) d |= USN_F_FRAG1;                         // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge
     if (touch && !(fl & (TXR_HIT | TXR_HOST)) && (fl & (TXR_LEARNMAC | TXR_LEARNRULE))) {
       bool learned = false;
       if (fl & TXR_LEARNMAC) {
-        const uint64_t m = rec_smac(r1);
+        const uint64_t m = rec_smac(r1[r]);
         if (slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, m, usn_mac_hash(m)), t.epoch) ==
             (uint32_t)i) {
           const uint32_t pos = atomicAdd(t.counters, 1u);
           if (pos < t.learned_cap) {
             t.learned[2 * pos] = make_uint4((uint32_t)i, 0u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, 0u);
+          } else {
+            atomicOr(t.counters + 1, 4u);
           }
-          else atomicOr(t.counters + 1, 4u);
           learned = true;
         }
       }
       if (fl & TXR_LEARNRULE) {
         uint32_t x, y, z, meta;
-        want_key(r0, x, y, z, meta);
+        want_key(r0[r], x, y, z, meta);
         const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                                   usn_key_fp48(x, y, z, meta),
                                                   usn_key_hash(x, y, z, meta));
@@ -1161,66 +1206,40 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
           if (pos < t.learned_cap) {
             t.learned[2 * pos] = make_uint4((uint32_t)i, 1u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4(x, y, z, meta);
+          } else {
+            atomicOr(t.counters + 1, 4u);
           }
-          else atomicOr(t.counters + 1, 4u);
           learned = true;
         }
       }
       if (learned) d |= USN_F_LEARN;
     }
-    a.decisions[i] = d;
+    dec[r] = d;
+    sdec[local] = d;
+    v[r] = (touch && !(fl & TXR_HIT)) ? local + 1 : 0u;
   }
-}
-
-__global__ __launch_bounds__(NTHREADS) void tx_fill_kernel(TxArgs t) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  const ClassifyArgs &a = t.a;
-  const Lds L = carve(smem, a.nbins);
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
-  if (tid < 8) s_misc[tid] = 0;
-  for (uint32_t k = tid; k < NSEG * a.nbins; k += NTHREADS) L.cnt[k] = 0;
-  uint4 r0[ROUNDS];
-  uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    r0[r] = local < nt ? t.rec[2 * (base + local)] : make_uint4(0, 0, 0, 0);
-    dec[r] = local < nt ? a.decisions[base + local] : 0u;
-    v[r] = (local < nt && tx_touch(r0[r]) && !(r0[r].x & TXR_HIT)) ? local + 1 : 0u;
-  }
-  tile_prefix_max(v, L, head);
-  const uint32_t before = prev_tiles_last(t.aux, tile, 1);
-  const usn_summary *S = a.summary;
+  tile_prefix_max(v, L, head);   // its barriers also publish sdec and s_head
   uint32_t my_last = 0, my_touch = 0, my_dec = 0, my_host = 0;
   uint4 my_info = make_uint4(0, 0, 0, 0);
+  uint32_t *hl = a.host_list + (size_t)tile * TILE;
+  uint32_t bins[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) continue;
-    if (r0[r].x & TXR_HIT) {   // the run head: the last non-hit touching frame before
-      const uint32_t h = head[r] ? (uint32_t)(base + head[r]) : before;
-      const uint32_t hd = h ? a.decisions[h - 1] : S->cin_dst;
+    const bool valid = local < nt;
+    if (valid && (r0[r].x & TXR_HIT)) {
+      const uint32_t hd = head[r] ? sdec[head[r] - 1] : s_head;
       dec[r] = (hd & USN_PARITY_MASK) | USN_F_CACHE | (dec[r] & USN_F_FRAG1);
-      a.decisions[base + local] = dec[r];
     }
-    const uint32_t touch = tx_touch(r0[r]);
+    if (valid) a.decisions[base + local] = dec[r];
+    const uint32_t touch = valid ? tx_touch(r0[r]) : 0u;
     if (touch) {
       my_last = local + 1; my_touch = touch; my_dec = dec[r];
       my_host = (r0[r].x & TXR_HOST) != 0;
       my_info = make_uint4(r0[r].x & TXR_I0_MASK, r0[r].y, r0[r].z, r0[r].w);
     }
-  }
-  uint32_t bins[ROUNDS];
-  uint32_t *hl = a.host_list + (size_t)tile * TILE;
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
     bins[r] = dec_bin(dec[r], a.n_ep);
-    const bool host = local < nt && (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_LEARN));
+    const bool host = valid && (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_LEARN));
     if (__ballot(host))
       if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
   }
@@ -1273,9 +1292,9 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
   else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, scan_lds, stream, t);
   hipLaunchKernelGGL(tx_hits_kernel, g, b, core, stream, t);
-  if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, with_table, stream, t);
-  else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, with_table, stream, t);
-  hipLaunchKernelGGL(tx_fill_kernel, g, b, core, stream, t);
+  const size_t decide_lds = with_table + TILE * 4;   // + the tile's decisions
+  if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, decide_lds, stream, t);
+  else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, decide_lds, stream, t);
   return hipGetLastError();
 }
 
