@@ -25,8 +25,9 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     distinct = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    libpath = sys.argv[4] if len(sys.argv) > 4 else None   # an A/B build (build/abl/<v>/libusn.so)
     cfgs = [traffic.c4tx(n=n, seed=6 + k) for k in range(distinct)]
-    ctx = lib.Ctx(0)
+    ctx = lib.Ctx(0, libpath) if libpath else lib.Ctx(0)
     traffic.install_ctx(ctx, cfgs[0])
     s = ctx.stream()
     batches = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]

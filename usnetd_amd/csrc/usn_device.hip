@@ -1002,15 +1002,17 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   __shared__ uint32_t s_last_nh;
   if (tid == 0) s_last_nh = 0;
+  uint4 *srec = L.table;   // the tile's first record words, for the previous-frame compares
   uint4 r0[ROUNDS];
   uint32_t v[ROUNDS], prev[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     r0[r] = local < nt ? t.rec[2 * (base + local)] : make_uint4(0, 0, 0, 0);
+    srec[local] = r0[r];
     v[r] = (local < nt && tx_touch(r0[r])) ? local + 1 : 0u;
   }
-  tile_prefix_max(v, L, prev);
+  tile_prefix_max(v, L, prev);   // its barriers also publish srec
   const usn_summary *S = a.summary;
   const uint32_t before = prev_tiles_last(t.aux, tile, 0);   // last touching frame of earlier tiles
   uint32_t last_nh = 0;
@@ -1027,7 +1029,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
       const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
       const uint32_t info0 = fl & TXR_I0_MASK;
       if (k1) {
-        const uint4 pr = t.rec[2 * (size_t)(k1 - 1)];
+        const uint4 pr = prev[r] ? srec[prev[r] - 1] : t.rec[2 * (size_t)(k1 - 1)];
         const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == r0[r].y &&
                           pr.z == r0[r].z && pr.w == r0[r].w;
         if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
@@ -1291,7 +1293,7 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
       with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
   if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
   else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, scan_lds, stream, t);
-  hipLaunchKernelGGL(tx_hits_kernel, g, b, core, stream, t);
+  hipLaunchKernelGGL(tx_hits_kernel, g, b, core + TILE * 16, stream, t);
   const size_t decide_lds = with_table + TILE * 4;   // + the tile's decisions
   if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, decide_lds, stream, t);
   else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, decide_lds, stream, t);
