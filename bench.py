@@ -72,7 +72,13 @@ def main():
     Qt = P * S
     R = max(2, -(-args.batches // Qt))            # rounds of distinct batches rotated through
     nb = R * Qt
-    ctx = lib.Ctx(local)
+    device = local
+    if world > 1:   # one rank per GPU; more ranks than GPUs (a rehearsal) share them round-robin
+        import torch
+        ndev = torch.cuda.device_count()   # counts without initialising the GPU
+        if ndev > 0:
+            device = local % ndev
+    ctx = lib.Ctx(device)
     batches, results, cfg0 = [], [], None
     nics = None
     for k in range(nb):
@@ -219,6 +225,10 @@ def main():
             "traffic": None,
             "kernel": "classify_rx_kernel",
             "kernel_us_median": round(kern_ms * 1e3, 3),
+            "achieved_basis": "isolated launches (HIP events on the launch stream, one at a time)",
+            # the timed region's launches overlap on two streams: per GPU, algorithmic
+            # bytes of all its frames / the timed region's wall time
+            "achieved_steady_state": round(ALGO_BYTES * done * n / elapsed / 1e9, 1),
             "batches_per_launch": P,
             "algo_bytes_per_frame": ALGO_BYTES,
         },
