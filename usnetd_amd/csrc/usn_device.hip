@@ -36,6 +36,12 @@ namespace usn {
 #define USN_NTHREADS 256
 #endif
 #define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
+/* tiles per workgroup: workgroup g takes tiles g, g + grid, ... (grid =
+ * ceil(tiles / USN_TPW)); each next tile's round 0 is loaded during the
+ * previous tile's ordering phase */
+#ifndef USN_TPW
+#define USN_TPW 1
+#endif
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
 #define MAX_NBITS 10   /* nbins <= 1024 */
@@ -479,18 +485,42 @@ __device__ __forceinline__ void issue_round(const ClassifyArgs &a, uint64_t base
 }
 
 /* --------------------------------------------------------------------------- */
+/* Addresses and lengths of rounds [r0, r1) of tile w of a launch; round-0
+ * header loads too when r0 == 0. */
+template <bool DENSE>
+__device__ __forceinline__ void prefetch_tile(const MultiArgs &m, uint32_t w, uint32_t r0,
+                                              uint32_t r1, uint32_t tid, uint32_t wave,
+                                              uint32_t lane, uint4 (&q)[ROUNDS][4],
+                                              uint32_t (&len)[ROUNDS],
+                                              const uint8_t *(&fp)[ROUNDS]) {
+  uint32_t bi = 0;
+  for (uint32_t k = 1; k < m.count; ++k)
+    if (w >= m.tile_base[k]) bi = k;
+  const ClassifyArgs &a = m.b[bi];
+  const uint64_t base = (uint64_t)(w - m.tile_base[bi]) * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    if (r < r0 || r >= r1) continue;
+    const uint32_t local = r * NTHREADS + tid;
+    const uint64_t i = base + (local < nt ? local : 0);
+    fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
+    len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
+  }
+  if (r0 == 0) issue_round<DENSE>(a, base, 0, wave, lane, fp[0], q[0]);
+}
+
+/* USN_TPW 1024-frame tiles per workgroup: w = blockIdx.x, + gridDim.x, ...;
+ * the next tile's lengths and round-0 headers are issued before this tile's
+ * ordering phase, so a workgroup never waits on HBM with nothing in flight.
+ * (A loop with a run-time trip count doubled the VGPRs; the unrolled form
+ * does not.) */
 template <bool LDS, bool DENSE>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   extern __shared__ __align__(16) uint8_t smem[];
-  uint32_t bi = 0;                       // which batch of the launch (uniform)
-  for (uint32_t k = 1; k < m.count; ++k)
-    if (blockIdx.x >= m.tile_base[k]) bi = k;
-  const ClassifyArgs &a = m.b[bi];
-  const Lds L = carve(smem, a.nbins, DENSE);
+  const uint32_t total = m.tile_base[m.count];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x - m.tile_base[bi];
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  const Lds L = carve(smem, m.b[0].nbins, DENSE);   // bins and table are shared by the batches
   STAMP_DECL
   STAMP(0);
 
@@ -504,28 +534,37 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   uint32_t len[ROUNDS];
   const uint8_t *fp[ROUNDS];
   uint4 tb0 = make_uint4(0, 0, 0, 0);   // first 256 slots staged through registers
-  if (LDS && tid < a.table_slots) tb0 = a.table[tid];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const uint64_t i = base + (local < nt ? local : 0);
-    fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-    len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
-  }
-  issue_round<DENSE>(a, base, 0, wave, lane, fp[0], q[0]);
+  if (LDS && tid < m.b[0].table_slots) tb0 = m.b[0].table[tid];
+  uint32_t w = blockIdx.x;
+  prefetch_tile<DENSE>(m, w, 0, ROUNDS, tid, wave, lane, q, len, fp);
   __builtin_amdgcn_sched_barrier(0);
-
-  STAMP(1);
-  // ---- while they fly: zero the segment counters, stage the rule table
-  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
-  const uint4 *T = a.table;
+  bool first = true;
+  const uint4 *T = m.b[0].table;
   if (LDS) {
-    if (tid < a.table_slots) L.table[tid] = tb0;
-    for (uint32_t k = tid + NTHREADS; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    if (tid < m.b[0].table_slots) L.table[tid] = tb0;
+    for (uint32_t k = tid + NTHREADS; k < m.b[0].table_slots; k += NTHREADS)
+      L.table[k] = m.b[0].table[k];
     T = L.table;
   }
   __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+
+#pragma unroll
+  for (uint32_t it = 0; it < USN_TPW; ++it) {
+  uint32_t bi = 0;                       // which batch of the launch (uniform)
+  for (uint32_t k = 1; k < m.count; ++k)
+    if (w >= m.tile_base[k]) bi = k;
+  const ClassifyArgs &a = m.b[bi];
+  const uint32_t tile = w - m.tile_base[bi];
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+
+  // later tiles: round 0 was prefetched during the previous ordering phase
+  if (!first) prefetch_tile<DENSE>(m, w, 1, ROUNDS, tid, wave, lane, q, len, fp);
+  first = false;
+  STAMP(1);
+  // ---- while they fly: zero the segment counters
+  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
   STAMP(2);
@@ -653,6 +692,14 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     }
   }
 
+  // ---- the next tile's lengths and round-0 headers fly during the ordering
+  const uint32_t wn = w + gridDim.x;
+  if (it + 1 < USN_TPW && wn < total) {
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch_tile<DENSE>(m, wn, 0, 1, tid, wave, lane, q, len, fp);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
   STAMP(6);
   // ---- stable per-endpoint order of the tile
   uint32_t cls[4] = {0, 0, 0, 0};
@@ -690,8 +737,13 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
   STAMP(11);
+  if (wn >= total) break;
+  w = wn;
+  __syncthreads();   // s_misc / counters are reused by the next tile
+  }
   STAMP_FLUSH();
 }
+
 
 /* Rebuild order / runs / class counts of tiles from patched decisions. */
 __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32_t t0) {
@@ -1327,7 +1379,9 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   for (uint32_t k = 0; k < m.count; ++k)
     dense = dense && m.b[k].stride == 64 && m.b[k].offsets == nullptr;
   const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, dense);
-  const dim3 g(tiles), b(NTHREADS);
+  uint32_t grid = tiles;
+  grid = (tiles + USN_TPW - 1) / USN_TPW;
+  const dim3 g(grid), b(NTHREADS);
   if (in_lds && dense) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
   else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);
   else if (dense) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, m);
