@@ -1052,8 +1052,9 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  __shared__ uint32_t s_last_nh;
-  if (tid == 0) s_last_nh = 0;
+  __shared__ uint32_t s_last_nh, s_ins;
+  if (tid == 0) { s_last_nh = 0; s_ins = 0; }
+  uint32_t ins = 0;        // bit 0: a MAC was inserted, bit 1: a rule
   uint4 *srec = L.table;   // the tile's first record words, for the previous-frame compares
   uint4 r0[ROUNDS];
   uint32_t v[ROUNDS], prev[ROUNDS];
@@ -1103,6 +1104,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
         unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
                                              usn_mac_hash(m), t.counters + 1);
         if (slot) first_index_update(slot + 1, t.epoch, (uint32_t)i);
+        ins |= 1u;
       }
       if (fl & TXR_LEARNRULE) {
         uint32_t x, y, z, meta;
@@ -1115,31 +1117,36 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
           slot[3] = ((unsigned long long)meta << 32) | z;
           first_index_update(slot + 1, t.epoch, (uint32_t)i);
         }
+        ins |= 2u;
       }
     }
   }
   if (last_nh) atomicMax(&s_last_nh, last_nh);
+  if (ins) atomicOr(&s_ins, ins);
   __syncthreads();
-  if (tid == 0) t.aux[tile * 4 + 1] = s_last_nh;
+  if (tid == 0) {
+    t.aux[tile * 4 + 1] = s_last_nh;
+    if (s_ins) atomicOr(t.counters + 2, s_ins);   // which sets tx_decide must look in
+  }
 }
 
 /* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
  * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
  * by a frame <= i. */
 __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
-                                   const uint4 &r1, uint32_t i) {
+                                   const uint4 &r1, uint32_t i, uint32_t ins) {
   const ClassifyArgs &a = t.a;
   const uint32_t fl = r0.x;
   const uint64_t dmac = rec_dmac(r1);
   bool d_in = (fl & TXR_DMAC_IN) != 0;
-  if (!d_in)                                           // learned by a frame <= i ?
+  if (!d_in && (ins & 1u))                             // learned by a frame <= i ?
     d_in = slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, dmac, usn_mac_hash(dmac)),
                       t.epoch) <= i;
   if (!d_in) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
   uint32_t x, y, z, meta;
   key1_of(r0, x, y, z, meta);
   uint32_t w = (a.probe_mask & 1u) ? probe(T, a.bucket_mask, x, y, z, meta) : 0u;
-  if (!w) {   // a rule learned by a frame <= i is owned by S (so excluded)
+  if (!w && (ins & 2u)) {   // a rule learned by a frame <= i is owned by S (so excluded)
     const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                               usn_key_fp48(x, y, z, meta),
                                               usn_key_hash(x, y, z, meta));
@@ -1195,13 +1202,14 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     r1[r] = local < nt ? t.rec[2 * i + 1] : make_uint4(0, 0, 0, 0);
   }
   const uint32_t before = prev_tiles_last(t.aux, tile, 1);   // 1 + index, 0 = none
+  const uint32_t ins = __builtin_amdgcn_readfirstlane(t.counters[2]);   // sets with items
   __syncthreads();
   if (tid == 0) {
     const usn_summary *S = a.summary;
     uint32_t hd = S->cin_dst;
     if (before) {
       const uint4 h0 = t.rec[2 * (size_t)(before - 1)], h1 = t.rec[2 * (size_t)(before - 1) + 1];
-      hd = decide_tx_ipv4(t, T, h0, h1, before - 1);
+      hd = decide_tx_ipv4(t, T, h0, h1, before - 1, ins);
     }
     s_head = hd;
   }
@@ -1226,7 +1234,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
     } else {
-      d = decide_tx_ipv4(t, T, r0[r], r1[r], (uint32_t)i);
+      d = decide_tx_ipv4(t, T, r0[r], r1[r], (uint32_t)i, ins);
     }
     if (r1[r].w) d |= USN_F_FRAG1;                         // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge

@@ -87,7 +87,7 @@ struct TxArgs {
   uint32_t epoch;             /* 1..65535 */
   uint4 *learned;             /* items appended by tx_decide: {frame, kind 0 mac | 1 rule},
                                  {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
-  uint32_t *counters;         /* [0] learned pairs, [1] overflow flag */
+  uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with items */
   uint32_t learned_cap;
   const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
   uint32_t bridge_mask;
