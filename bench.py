@@ -64,7 +64,8 @@ def main():
         dist_mod.init_process_group("gloo")
         dist = dist_mod
 
-    defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20}
+    defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20,
+                "c1fixed": 1 << 20}
     n = args.frames or defaults[args.config]
     S = max(1, args.streams)
     Qt = max(S, args.queues - args.queues % S)   # rx queues in total

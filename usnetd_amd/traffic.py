@@ -277,7 +277,12 @@ def c4tx(n=1 << 18, seed=6, host_at=None):
                   bridge=[bytes(m) for m in bridged])
 
 
-CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4tx": c4tx}
+def c1fixed(n=1 << 16, seed=1):
+    """c1 with one 5-tuple (pkt-gen style): nearly every frame is a cache hit."""
+    return c1(n=n, variant="fixed", seed=seed)
+
+
+CONFIGS = {"c1": c1, "c1fixed": c1fixed, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4tx": c4tx}
 
 
 def config(name, n=None, seed=None, **kw):
