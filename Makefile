@@ -5,7 +5,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 CSRC := usnetd_amd/csrc
 LIB := usnetd_amd/libusn.so
-OBJS := build/usn_device.o build/usn_host.o
+OBJS := build/usn_device.o build/usn_device512.o build/usn_host.o
 
 DAEMON := usnetd_amd/bin/usnetd
 
@@ -20,6 +20,10 @@ $(DAEMON): usnetd_amd/daemon/usnetd.cpp usnetd_amd/daemon/messages.hpp usnetd_am
 build/usn_device.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/usn_device512.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 -c -o $@ $<
 
 build/usn_host.o: $(CSRC)/usn_host.cpp $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
 	@mkdir -p build
@@ -47,11 +51,11 @@ clean:
 
 # A/B experiment builds (tools/abl.py): build/abl/<variant>/libusn.so,
 # one variant per line of tools/abl_variants.txt: "<name> <extra hipcc flags>"
-abl: build/usn_host.o
+abl: build/usn_host.o build/usn_device512.o
 	@while read -r name flags; do \
 	  case "$$name" in ''|'#'*) continue;; esac; \
 	  mkdir -p build/abl/$$name; echo "variant $$name: $$flags"; \
 	  $(HIPCC) $(HIPFLAGS) $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip || exit 1; \
-	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/usn_host.o || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/usn_device512.o build/usn_host.o || exit 1; \
 	done < tools/abl_variants.txt
 .PHONY: abl

@@ -109,18 +109,25 @@ def main():
     rdesc = [C.byref(r.desc) for r in results]
     joins = [ctx.event() for _ in streams]
 
-    def launch(i, per=P, count=None):
-        """Launch i: `count` (default per) batches of one stream's queues."""
-        if per == 1:
+    def launch(i, per=P, count=None, one_queue=False):
+        """Launch i on stream i % S: `count` (default per) batches of that
+        stream's queues.  one_queue: the single-queue reference (stream 0,
+        one batch per launch, batches in rotation)."""
+        if one_queue:
             rc = single(h, bdesc[i % nb], rdesc[i % nb], stream)
         else:
             si = i % S
-            g = groups[((i // S) % R, si)]
-            rc = multi(h, g[0], g[1], count or per, streams[si])
+            r = (i // S) % R
+            if per == 1:
+                k = r * Qt + si * P
+                rc = single(h, bdesc[k], rdesc[k], streams[si])
+            else:
+                g = groups[(r, si)]
+                rc = multi(h, g[0], g[1], count or per, streams[si])
         if rc:
             lib.check(rc, "usn_classify")
 
-    def timed(steps, per):
+    def timed(steps, per, one_queue=False):
         """Exactly `steps` batches, `per` per launch (the last launch takes the rest)."""
         full, rest = divmod(steps, per)
         for x in streams:
@@ -133,9 +140,9 @@ def main():
         for x in streams[1:]:
             ctx.wait_event(x, ev0)
         for i in range(full):
-            launch(i, per)
+            launch(i, per, one_queue=one_queue)
         if rest:
-            launch(full, per, rest)
+            launch(full, per, rest, one_queue=one_queue)
         for x, ej in zip(streams[1:], joins[1:]):
             ctx.record(ej, x)
             ctx.wait_event(stream, ej)
@@ -182,7 +189,7 @@ def main():
     # the same batches one per launch (single rx queue), for reference
     single_mpps = None
     if P > 1 and args.steps >= 4:
-        w1, _, d1 = timed(max(4, args.steps // 2), 1)
+        w1, _, d1 = timed(max(4, args.steps // 2), 1, one_queue=True)
         single_mpps = round(d1 * n / w1 / 1e6, 1)
 
     total_frames = world * done * n

@@ -29,7 +29,16 @@
 #include "usn_internal.h"
 #include "usn_kernels.h"
 
-namespace usn {
+/* The file is compiled twice into libusn.so: namespace usn (256 threads per
+ * tile) and, for rule tables in global memory, usn_t512 (-DUSN_NTHREADS=512
+ * -DUSN_NS=usn_t512: twice the waves per tile, half the probe chains per
+ * lane). */
+#ifndef USN_NS
+#define USN_NS usn
+#endif
+
+namespace USN_NS {
+using namespace ::usn;
 
 #define TILE USN_TILE
 #ifndef USN_NTHREADS
@@ -77,6 +86,10 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #define STAMP(k) do { } while (0)
 #define STAMP_DECL
 #define STAMP_FLUSH() do { } while (0)
+#endif
+
+#ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
+#define USN_ABL_NOTAGS 0
 #endif
 
 #ifndef USN_LOAD_NT
@@ -146,11 +159,34 @@ __device__ __forceinline__ bool slot_is(const uint4 &t, uint32_t x, uint32_t y, 
   return ((t.x ^ x) | (t.y ^ y) | (t.z ^ z) | ((t.w ^ meta) & USN_KEY_META_MASK)) == 0u;
 }
 
-/* One exact-match probe: the home bucket (one 64-byte line) is checked with
- * selects; the chain is followed only when that bucket is full and holds no
- * match (rare at load <= 1/2).  Returns the slot's meta word, 0 = miss. */
-__device__ __forceinline__ uint32_t probe(const uint4 *T, uint32_t bmask, uint32_t x, uint32_t y,
-                                          uint32_t z, uint32_t meta) {
+/* One exact-match probe.  LDS table: the home bucket (one 64-byte line) is
+ * checked with selects; the chain is followed only when that bucket is full
+ * and holds no match (rare at load <= 1/2).  Global table (TAGGED): one
+ * 16-byte tag line per bucket, then only the slot whose tag matches -- two
+ * 16-byte L2 requests per hit, one per miss, instead of four.  Returns the
+ * slot's meta word, 0 = miss. */
+template <bool TAGGED>
+__device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uint32_t bmask,
+                                          uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
+  if (TAGGED && !USN_ABL_NOTAGS) {
+    const uint32_t h = usn_key_hash(x, y, z, meta);
+    const uint32_t tg = usn_key_tag(h);
+    uint32_t b = h & bmask;
+    for (uint32_t it = 0; it <= bmask; ++it) {
+      const uint4 tv = tags[b];
+      uint32_t mm = (tv.x == tg ? 1u : 0u) | (tv.y == tg ? 2u : 0u) | (tv.z == tg ? 4u : 0u) |
+                    (tv.w == tg ? 8u : 0u);
+      while (mm) {   // verify: two keys of one bucket may share a tag
+        const uint32_t j = (uint32_t)__builtin_ctz(mm);
+        const uint4 sl = T[b * 4 + j];
+        if (slot_is(sl, x, y, z, meta)) return sl.w;
+        mm &= mm - 1;
+      }
+      if (tv.w == 0u) return 0u;   // bucket not full: the key would be in it
+      b = (b + 1) & bmask;
+    }
+    return 0u;
+  }
   uint32_t b = usn_key_hash(x, y, z, meta) & bmask;
   const uint4 *s = T + b * 4;
   uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
@@ -173,6 +209,7 @@ __device__ __forceinline__ uint32_t probe(const uint4 *T, uint32_t bmask, uint32
  * ARP/EAPOL -> FLOOD, loopback -> DROP, else get_endpoint (endpoint.rs:307-338:
  * key1 = with src, key2 = without, only on a key1 miss; a hit on a NIC-owned
  * rule or on the source itself is None with no retry), else DHCP / DROP. */
+template <bool TAGGED>
 __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs &a,
                                               const Parsed &p) {
   const bool has = p.has_ports != 0;
@@ -181,11 +218,11 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
   w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
 #else
   if (a.probe_mask & 1u)
-    w1 = probe(T, a.bucket_mask, p.dst, p.src, has ? (p.dport | (p.sport << 16)) : 0u,
+    w1 = probe<TAGGED>(T, a.tags, a.bucket_mask, p.dst, p.src, has ? (p.dport | (p.sport << 16)) : 0u,
                usn_key_meta(p.proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT)
                                          : USN_WANT_SRC));
   if (a.probe_mask & 2u)
-    w2 = probe(T, a.bucket_mask, p.dst, 0u, has ? p.dport : 0u,
+    w2 = probe<TAGGED>(T, a.tags, a.bucket_mask, p.dst, 0u, has ? p.dport : 0u,
                usn_key_meta(p.proto, has ? USN_WANT_DPORT : 0u));
 #endif
   const uint32_t w = w1 ? w1 : w2;
@@ -446,12 +483,13 @@ __device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *sc
 }
 
 /* Decision for a carried PacketInfo X under the current table (rx). */
+template <bool TAGGED>
 __device__ uint32_t decide_info_rx(const uint4 *T, const ClassifyArgs &a, const uint32_t *info) {
   Parsed p;
   p.status = 1; p.i0 = info[0]; p.src = info[1]; p.dst = info[2]; p.ports = info[3];
   p.proto = (info[0] >> 8) & 0xFFu; p.has_ports = (info[0] >> 16) & 1u;
   p.sport = info[3] & 0xFFFFu; p.dport = info[3] >> 16; p.frag_first = 0;
-  return decide_rx(T, a, p);
+  return decide_rx<TAGGED>(T, a, p);
 }
 
 /* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
@@ -576,7 +614,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       const uint32_t st = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
       if ((st & USN_CS_VALID) &&
-          ((decide_info_rx(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
+          ((decide_info_rx<!LDS>(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
         flags |= USN_S_STALE;
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
@@ -617,7 +655,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #endif
     Parsed p;
     parse(q[r], len[r], fp[r], p);
-    dec[r] = decide_rx(T, a, p);
+    dec[r] = decide_rx<!LDS>(T, a, p);
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
     uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
                    : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
@@ -1026,7 +1064,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
         uint4 r0 = make_uint4(p.i0, p.src, p.dst, p.ports);
         uint32_t x, y, z, meta;
         want_key(r0, x, y, z, meta);
-        if (!probe(T, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
+        if (!probe<!LDS>(T, a.tags, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
@@ -1133,6 +1171,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
 /* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
  * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
  * by a frame <= i. */
+template <bool TAGGED>
 __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
                                    const uint4 &r1, uint32_t i, uint32_t ins) {
   const ClassifyArgs &a = t.a;
@@ -1145,7 +1184,7 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   if (!d_in) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
   uint32_t x, y, z, meta;
   key1_of(r0, x, y, z, meta);
-  uint32_t w = (a.probe_mask & 1u) ? probe(T, a.bucket_mask, x, y, z, meta) : 0u;
+  uint32_t w = (a.probe_mask & 1u) ? probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta) : 0u;
   if (!w && (ins & 2u)) {   // a rule learned by a frame <= i is owned by S (so excluded)
     const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                               usn_key_fp48(x, y, z, meta),
@@ -1159,7 +1198,7 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   }
   const bool has = (r0.x >> 16) & 1u;
   if (!w && (a.probe_mask & 2u))
-    w = probe(T, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
+    w = probe<TAGGED>(T, a.tags, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
               usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u));
   const uint32_t owner = w >> 16;
   const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
@@ -1209,7 +1248,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     uint32_t hd = S->cin_dst;
     if (before) {
       const uint4 h0 = t.rec[2 * (size_t)(before - 1)], h1 = t.rec[2 * (size_t)(before - 1) + 1];
-      hd = decide_tx_ipv4(t, T, h0, h1, before - 1, ins);
+      hd = decide_tx_ipv4<!LDS>(t, T, h0, h1, before - 1, ins);
     }
     s_head = hd;
   }
@@ -1234,7 +1273,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
     } else {
-      d = decide_tx_ipv4(t, T, r0[r], r1[r], (uint32_t)i, ins);
+      d = decide_tx_ipv4<!LDS>(t, T, r0[r], r1[r], (uint32_t)i, ins);
     }
     if (r1[r].w) d |= USN_F_FRAG1;                         // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge
@@ -1404,11 +1443,11 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
   return hipGetLastError();
 }
 
-}  // namespace usn
+}  // namespace USN_NS
 
 #if USN_STAMPS
 extern "C" int usn_debug_stamps(void *host, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(usn::usn_stamp_buf), bytes, 0,
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(USN_NS::usn_stamp_buf), bytes, 0,
                                   hipMemcpyDeviceToHost);
 }
 #endif

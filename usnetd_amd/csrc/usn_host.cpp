@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -145,6 +146,7 @@ struct ParsedH {   // host-side extract_pkt_info result
 struct usn_ctx {
   int device = 0;
   int n_cu = 0;
+  int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
   std::mutex mu;
   std::vector<Ep> eps = std::vector<Ep>(USN_MAX_ENDPOINTS);
   uint32_t n_ep = 0;   // max id + 1
@@ -157,10 +159,13 @@ struct usn_ctx {
   /* host image of the device table; inserts go straight into it while the
    * load stays <= 1/2 (tx learning adds rules in bulk), removals rebuild */
   std::vector<uint4> img;
+  std::vector<uint32_t> img_tags;   // per slot: usn_key_tag of its key, 0 = empty
   bool img_valid = false;
   uint32_t img_pmask = 0;
   uint4 *d_table = nullptr;
   size_t d_table_cap = 0;
+  uint4 *d_tags = nullptr;
+  size_t d_tags_cap = 0;
   uint32_t table_slots = 0, bucket_mask = 0;
   uint32_t probe_mask = 0;   // key shapes present in the table (ClassifyArgs::probe_mask)
   bool bridge_dirty = true;
@@ -213,13 +218,15 @@ void img_put(usn_ctx *c, const WantKey &k, uint16_t owner) {
   const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
   const uint32_t meta = usn_key_meta(k.proto, k.present);
   const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
-  uint32_t b = usn_key_hash(k.dst, k.src, z, meta) & (nb - 1);
+  const uint32_t h = usn_key_hash(k.dst, k.src, z, meta);
+  uint32_t b = h & (nb - 1);
   for (;;) {
     uint4 *s = &c->img[(size_t)b * 4];
     for (int j = 0; j < 4; ++j)
       if (!(s[j].w & USN_SLOT_VALID)) {
         s[j] = make_uint4(k.dst, k.src, z,
                           meta | (nic ? USN_SLOT_NICOWNER : 0u) | ((uint32_t)owner << 16));
+        c->img_tags[(size_t)b * 4 + j] = usn_key_tag(h);
         c->img_pmask |= shape_bits(k);
         return;
       }
@@ -240,6 +247,7 @@ int rebuild_table(usn_ctx *c) {
     const uint32_t n = (uint32_t)c->rules.size();
     const uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
     c->img.assign((size_t)nb * 4, make_uint4(0, 0, 0, 0));
+    c->img_tags.assign((size_t)nb * 4, 0u);
     c->img_pmask = 0;
     for (const auto &kv : c->rules) img_put(c, kv.first, kv.second.owner);
     c->img_valid = true;
@@ -253,6 +261,14 @@ int rebuild_table(usn_ctx *c) {
     c->d_table_cap = bytes;
   }
   HIPCHK(hipMemcpy(c->d_table, c->img.data(), bytes, hipMemcpyHostToDevice));
+  const size_t tbytes = c->img_tags.size() * 4;
+  if (tbytes > c->d_tags_cap) {
+    if (c->d_tags) HIPCHK(hipFree(c->d_tags));
+    c->d_tags = nullptr;
+    HIPCHK(hipMalloc(&c->d_tags, tbytes));
+    c->d_tags_cap = tbytes;
+  }
+  HIPCHK(hipMemcpy(c->d_tags, c->img_tags.data(), tbytes, hipMemcpyHostToDevice));
   c->table_slots = (uint32_t)c->img.size();
   c->bucket_mask = (uint32_t)(c->img.size() / 4) - 1;
   c->probe_mask = c->img_pmask;
@@ -498,6 +514,7 @@ int usn_ctx_create(int hip_device, usn_ctx **out) {
   if (!c) return USN_ENOMEM;
   c->device = hip_device;
   c->n_cu = prop.multiProcessorCount;
+  if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
   *out = c;
   return USN_OK;
 }
@@ -509,6 +526,7 @@ void usn_ctx_destroy(usn_ctx *c) {
   (void)hipDeviceSynchronize();
   if (c->d_table) (void)hipFree(c->d_table);
   if (c->d_bridge) (void)hipFree(c->d_bridge);
+  if (c->d_tags) (void)hipFree(c->d_tags);
   if (c->d_bridge_set) (void)hipFree(c->d_bridge_set);
   for (void *p : {(void *)c->tx.rec, (void *)c->tx.aux, (void *)c->tx.macset,
                   (void *)c->tx.ruleset, (void *)c->tx.learned, (void *)c->tx.counters,
@@ -747,6 +765,7 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   a.summary = r->summary;
   a.host_list = r->host_list;
   a.table = c->d_table;
+  a.tags = c->d_tags;
   a.bucket_mask = c->bucket_mask;
   a.table_slots = c->table_slots;
   a.bridge = c->d_bridge;
@@ -763,6 +782,10 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   a.probe_mask = c->probe_mask;
   return USN_OK;
 }
+
+/* global-memory tables above this many slots (256 KiB) classify with 512
+ * threads per tile (A/B: c5's 65536 rules 1.55x faster; c4's 4096 equal) */
+#define USN_T512_MIN_SLOTS 16384u
 
 static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
   if (!b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
@@ -898,6 +921,10 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
     c->tx.decisions = r[0].decisions;
+  } else if (c->t512 == 1 || (c->t512 < 0 &&
+                                !usn::table_fits_lds(m.b[0].nbins, m.b[0].table_slots) &&
+                                m.b[0].table_slots > USN_T512_MIN_SLOTS)) {
+    HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
   } else {
     HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }

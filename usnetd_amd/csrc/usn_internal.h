@@ -12,6 +12,10 @@
  * Option::None differ from Some(0) exactly as derive(Eq) on Want does.
  * The table is rebuilt from the host registry on every change (no
  * tombstones), so a probe ends at the first bucket that has a free slot.
+ * Tables too large for LDS also get a tag array: one 16-byte line per
+ * bucket holding the four slots' 32-bit key tags (usn_key_tag of the bucket
+ * hash), so a global-memory probe is one 16-byte load plus one 16-byte slot
+ * load on a tag match, instead of four slot loads.
  *
  * PacketInfo (pkt.rs:11-22) as 4 words, compared whole for the 1-entry
  * decision cache (endpoint.rs:186-191, derive(PartialEq)):
@@ -66,6 +70,9 @@ USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) 
   h ^= h >> 15;
   return h;
 }
+
+/* 32-bit tag of a key in the tag array of a global-memory table (0 = empty) */
+USN_HD uint32_t usn_key_tag(uint32_t h) { return h | 1u; }
 
 /* MAC (48 bits) set hash, shared by the host bridge-set build and the device probe */
 USN_HD uint32_t usn_mac_hash(uint64_t m) {

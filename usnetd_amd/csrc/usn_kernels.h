@@ -31,6 +31,7 @@ struct ClassifyArgs {
   uint32_t *host_list;      /* per tile USN_TILE slots */
   /* rule table: nbuckets * 4 slots of uint4 */
   const uint4 *table;
+  const uint4 *tags;        /* per bucket: the 4 slots' key tags (global-memory probes) */
   uint32_t bucket_mask;
   uint32_t table_slots;
   /* inner L2 bridge (tx): MACs in the low 48 bits */
@@ -107,5 +108,11 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
 hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
 
 }  // namespace usn
+
+/* the same kernels at 512 threads per tile (a second compilation of
+ * usn_device.hip): faster when the rule table lives in global memory */
+namespace usn_t512 {
+hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
+}
 
 #endif
