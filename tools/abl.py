@@ -32,20 +32,36 @@ def main():
                     help="round-robin batches over S streams, one NIC rx queue (source) each")
     ap.add_argument("--multi", type=int, default=1,
                     help="classify Q batches of Q distinct rx queues per launch (usn_classify_multi)")
+    ap.add_argument("--private", dest="shared", action="store_false",
+                    help="each variant allocates its own batches (default: shared buffers)")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     names = a.variants or sorted(os.listdir(os.path.join(ROOT, "build", "abl")))
     cfgs = [traffic.config(a.config, n=a.frames, seed=17 * k + 2) for k in range(a.batches)]
     runs = {}
+    first = None
     for nm in names:
         path = os.path.join(ROOT, "build", "abl", nm, "libusn.so")
         ctx = lib.Ctx(0, libpath=path)
         traffic.install_ctx(ctx, cfgs[0])
         nq = max(a.streams, a.multi)
         nics = [0] + list(traffic.extra_nics(cfgs[0], nq - 1, ctx))
-        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k % nq], stride=c.stride)
-              for k, c in enumerate(cfgs)]
-        rs = [lib.DeviceResult(ctx, a.frames) for _ in cfgs]
+        # parity check: batch 0 into a private result of this variant
+        chk_b = lib.DeviceBatch(ctx, cfgs[0].frames, cfgs[0].lens, nics[0], stride=cfgs[0].stride)
+        chk_r = lib.DeviceResult(ctx, a.frames)
+        cs = ctx.stream()
+        lib.check(ctx.L.usn_classify(ctx.h, C.byref(chk_b.desc), C.byref(chk_r.desc), cs))
+        ctx.sync(cs)
+        chk = chk_r.decisions()
+        if first is None or not a.shared:
+            bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k % nq], stride=c.stride)
+                  for k, c in enumerate(cfgs)]
+            rs = [lib.DeviceResult(ctx, a.frames) for _ in cfgs]
+            first = (bs, rs)
+        else:
+            # the same device buffers for every variant: a variant's speed must not
+            # depend on where its own allocations landed in HBM
+            bs, rs = first
         s = ctx.stream()
         ss = [s] + [ctx.stream() for _ in range(a.streams - 1)]
         evs = [(ctx.event(), ctx.event()) for _ in range(a.launches)]
@@ -57,7 +73,7 @@ def main():
                 ba = (lib.Batch * a.multi)(*[bs[g * a.multi + j].desc for j in range(a.multi)])
                 ra = (lib.Result * a.multi)(*[rs[g * a.multi + j].desc for j in range(a.multi)])
                 groups.append((ba, ra))
-        runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, ss=ss, evs=evs, e0=e0, e1=e1, per=[], b2b=[],
+        runs[nm] = dict(ctx=ctx, bs=bs, rs=rs, s=s, chk=chk, ss=ss, evs=evs, e0=e0, e1=e1, per=[], b2b=[],
                         ejoin=[ctx.event() for _ in ss], groups=groups)
     for rnd in range(a.rounds):
         for nm in names:
@@ -104,7 +120,7 @@ def main():
     out = {}
     for nm in names:
         R = runs[nm]
-        d = R["rs"][0].decisions()
+        d = R["chk"]
         if ref is None:
             ref = d
         same = bool(((d ^ ref) & lib.PARITY_MASK).max() == 0) if d.shape == ref.shape else False

@@ -3,10 +3,9 @@
  *
  * classify: one workgroup (256 threads, 4 waves) per tile of USN_TILE = 1024
  * frames, one frame per lane per round, four rounds.  Per frame:
- *   1. the 64-byte header window + the 2-byte length; for the dense layout
- *      (64-byte stride) four fully coalesced 1 KiB wave loads per round and a
- *      wave-private transpose through LDS; every load of a lane is issued
- *      before any is consumed;
+ *   1. the 64-byte header window + the 2-byte length: windows stream into a
+ *      wave-private LDS stage by LDS-DMA (glds, non-temporal), one round in
+ *      flight while the previous one is decided;
  *   2. extract_pkt_info in registers, branch-free    /root/reference/src/pkt.rs:158-218
  *   3. get_endpoint: exact-match probes of the bucketed rule table (LDS copy
  *      when it fits, else L2-resident), only for key shapes the table holds
@@ -45,12 +44,6 @@ using namespace ::usn;
 #define USN_NTHREADS 256
 #endif
 #define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
-/* tiles per workgroup: workgroup g takes tiles g, g + grid, ... (grid =
- * ceil(tiles / USN_TPW)); each next tile's round 0 is loaded during the
- * previous tile's ordering phase */
-#ifndef USN_TPW
-#define USN_TPW 1
-#endif
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
 #define MAX_NBITS 10   /* nbins <= 1024 */
@@ -133,13 +126,26 @@ __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint
   const bool ip = eth && et == 0x0800u && len >= 34 &&               // Ipv4Packet::check_len
                   n >= hl && hl <= tl && n >= tl;
   const bool later = ip && (ff & 0x1FFFu) != 0;                      // frag_offset() > 0
-  const bool pp = pr == 6u || pr == 17u || pr == 0x21u || pr == 0x84u || pr == 0x88u;
+  // protocol_has_ports: pr in {6, 17, 33, 132, 136} as two bit-set tests
+  // (an || chain of compares became a branch tree)
+  const uint32_t ph = pr ^ 0x80u;
+  const uint32_t pp_lo = (uint32_t)(0x200020040ull >> (pr & 63u)) & (uint32_t)(pr < 64u);
+  const uint32_t pp_hi = (0x110u >> (ph & 31u)) & (uint32_t)(ph < 32u);
+  const bool pp = ((pp_lo | pp_hi) & 1u) != 0u;
   const bool has = ip && !later && pp && (tl - hl) > 4u;             // pkt.rs:128-133, 179
-  uint32_t a = w8, b = w9;                                           // ports at bytes 34..37
-  if (has && ihl != 5u) {                                            // ports at 14+hl (rare)
-    a = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
-    b = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
+  // ports at bytes 34..37, or at 14+hl when IHL != 5 (rare: reloaded).  The
+  // reload goes to its own registers (defaults are constants, so nothing
+  // waits on this round's headers before the branch) and is waited for in
+  // the branch: a wait after the join would be vmcnt(0) on every path and
+  // drain the next round's prefetch.
+  uint32_t ra = 0, rb = 0;
+  const bool reload = has && ihl != 5u;
+  if (reload) {
+    ra = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
+    rb = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
+    __builtin_amdgcn_s_waitcnt(0);
   }
+  const uint32_t a = reload ? ra : w8, b = reload ? rb : w9;
   p.sport = has ? be16lo(a >> 16) : 0u;
   p.dport = has ? be16lo(b) : 0u;
   p.ports = p.sport | (p.dport << 16);
@@ -157,6 +163,19 @@ __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint
 __device__ __forceinline__ bool slot_is(const uint4 &t, uint32_t x, uint32_t y, uint32_t z,
                                         uint32_t meta) {
   return ((t.x ^ x) | (t.y ^ y) | (t.z ^ z) | ((t.w ^ meta) & USN_KEY_META_MASK)) == 0u;
+}
+
+/* Meta word of the slot of a bucket that holds the key, or 0.  A key sits in
+ * at most one slot, so the four masked words are OR-ed: all four slots are
+ * read and compared unconditionally (a ?: chain let the compiler turn the
+ * later slot reads into dependent branches). */
+__device__ __forceinline__ uint32_t bucket_hit(const uint4 &s0, const uint4 &s1, const uint4 &s2,
+                                               const uint4 &s3, uint32_t x, uint32_t y, uint32_t z,
+                                               uint32_t meta) {
+  return (s0.w & (0u - (uint32_t)slot_is(s0, x, y, z, meta))) |
+         (s1.w & (0u - (uint32_t)slot_is(s1, x, y, z, meta))) |
+         (s2.w & (0u - (uint32_t)slot_is(s2, x, y, z, meta))) |
+         (s3.w & (0u - (uint32_t)slot_is(s3, x, y, z, meta)));
 }
 
 /* One exact-match probe.  LDS table: the home bucket (one 64-byte line) is
@@ -190,15 +209,13 @@ __device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uin
   uint32_t b = usn_key_hash(x, y, z, meta) & bmask;
   const uint4 *s = T + b * 4;
   uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-  uint32_t hit = slot_is(s0, x, y, z, meta) ? s0.w : slot_is(s1, x, y, z, meta) ? s1.w
-               : slot_is(s2, x, y, z, meta) ? s2.w : slot_is(s3, x, y, z, meta) ? s3.w : 0u;
+  uint32_t hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
   if (!hit && (s3.w & USN_SLOT_VALID)) {
     for (uint32_t it = 0; it < bmask; ++it) {
       b = (b + 1) & bmask;
       s = T + b * 4;
       s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
-      hit = slot_is(s0, x, y, z, meta) ? s0.w : slot_is(s1, x, y, z, meta) ? s1.w
-          : slot_is(s2, x, y, z, meta) ? s2.w : slot_is(s3, x, y, z, meta) ? s3.w : 0u;
+      hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
       if (hit || !(s3.w & USN_SLOT_VALID)) break;
     }
   }
@@ -247,11 +264,18 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
   return d;
 }
 
+/* bin of a decision: its endpoint, else NIC / FLOOD / DROP after the
+ * endpoints.  Classes 2, 3, 0 map to offsets 0, 1, 2 as (c + 2) & 3: one
+ * select, no divergent branch (a branch here kept the compiler from
+ * overlapping the loads ahead of it). */
+static_assert(USN_CLS_DROP == 0 && USN_CLS_EP == 1 && USN_CLS_NIC == 2 && USN_CLS_FLOOD == 3,
+              "dec_bin's class arithmetic");
+static_assert(USN_BIN_NIC(0) == 0 && USN_BIN_FLOOD(0) == 1 && USN_BIN_DROP(0) == 2, "bin order");
 __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
   const uint32_t c = USN_DEC_CLASS(d);
-  return c == USN_CLS_EP ? USN_DEC_EP(d)
-       : c == USN_CLS_NIC ? USN_BIN_NIC(n_ep)
-       : c == USN_CLS_FLOOD ? USN_BIN_FLOOD(n_ep) : USN_BIN_DROP(n_ep);
+  const uint32_t other = n_ep + ((c + 2u) & 3u);
+  const uint32_t m = 0u - (uint32_t)(c == USN_CLS_EP);   // mask form: stays a select
+  return other ^ ((other ^ USN_DEC_EP(d)) & m);
 }
 
 /* --------------------------------------------------------------------------- */
@@ -261,7 +285,6 @@ struct Lds {
   uint16_t *bstart;   // [nbins]: tile totals, then bin start slots
   uint16_t *order;    // [TILE]
   uint32_t *scratch;  // [16]
-  uint4 *stage;       // dense layout: 4 KiB per wave for the header transpose
   uint4 *table;       // staged rule table (optional)
 };
 
@@ -272,17 +295,14 @@ __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins) {
   return (b + 15) & ~(size_t)15;
 }
 
-#define STAGE_BYTES ((NTHREADS / 64) * 4096)
-
-__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, bool dense = false) {
+__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins) {
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
   L.bstart = L.cnt + (size_t)NSEG * nbins;
   const size_t off = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
   L.order = reinterpret_cast<uint16_t *>(smem + off);
   L.scratch = reinterpret_cast<uint32_t *>(L.order + TILE);
-  L.stage = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
-  L.table = L.stage + (dense ? (NTHREADS / 64) * 256 : 0);
+  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
   return L;
 }
 
@@ -499,109 +519,134 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
   return 4 * f + (j ^ ((f >> 2) & 3u));
 }
 
-/* Header loads of one round.  DENSE: 64 contiguous 64-byte frames per wave,
- * 4 fully coalesced 1 KiB wave loads; part lane&3 of frame 16k + lane/4
- * arrives in lane (transposed through LDS later).  Else one 64-byte window
- * per lane. */
-template <bool DENSE>
-__device__ __forceinline__ void issue_round(const ClassifyArgs &a, uint64_t base, uint32_t r,
-                                            uint32_t wave, uint32_t lane, const uint8_t *fp,
-                                            uint4 (&q)[4]) {
-  if (DENSE) {
-    const uint64_t f0 = base + r * NTHREADS + wave * 64;
-    const uint4 *chunk = reinterpret_cast<const uint4 *>(a.frames + f0 * 64);
+/* ---- header loads -----------------------------------------------------------
+ * GLDS (fixed-stride layouts, the default): LDS-DMA (`global_load_lds_dwordx4`)
+ * with the non-temporal hint straight into a wave-private stage of
+ * USN_GLDS_DEPTH rounds x 64 frames x 64 B.  No VGPRs are held for data in
+ * flight, and it is the fastest way found to stream the windows
+ * (tools/hbm_floor.hip, 8M frames per launch: 100-103 us vs 113 us for
+ * per-lane 16-byte register loads; register loads with nt: 199 us).
+ * glds writes LDS lane-linearly (base + 16 x lane), so each lane's SOURCE is
+ * the chunk that belongs at its slot: lane L of instruction k fills slot
+ * 64k + L = stage_slot(f, p) with f = 16k + L/4, p = (L & 3) ^ ((f >> 2) & 3),
+ * and every lane then reads its own frame's parts conflict-free.
+ * LANE (offsets layout, strides that are not 16-byte multiples): one 64-byte
+ * window per lane with 16-byte register loads, one round in flight ahead. */
+#ifndef USN_GLDS_DEPTH
+#define USN_GLDS_DEPTH 1
+#endif
+#define GD USN_GLDS_DEPTH
+#define NWAVES (NTHREADS / 64)
+#define STAGE_ROUND_SLOTS 256u   /* 16-byte slots per wave and round: 64 frames x 4 */
+#define GLDS_NT 2                /* aux bits of the header glds: non-temporal */
+#ifndef USN_GLDS_ENABLE          /* A/B only: 0 = register loads for every layout */
+#define USN_GLDS_ENABLE 1
+#endif
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {   /* hipcc does not count LDS-DMA for LDS reads */
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+/* glds of round r of this wave's 64 frames into stage `st` (wave-uniform) */
+__device__ __forceinline__ void glds_round(const ClassifyArgs &a, uint64_t base, uint32_t nt,
+                                           uint32_t r, uint32_t wave, uint32_t lane, uint4 *st) {
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint64_t f = f0 + 16 * k + (lane >> 2);
-      q[k] = f < a.n ? ld_stream(chunk + 64 * k + lane) : make_uint4(0, 0, 0, 0);
-    }
-  } else {
-    const uint4 *w = reinterpret_cast<const uint4 *>(fp);
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(w + k);
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t f = 16 * k + (lane >> 2);
+    const uint32_t p = (lane & 3u) ^ ((f >> 2) & 3u);
+    uint32_t local = r * NTHREADS + wave * 64 + f;
+    local = local < nt ? local : nt - 1;          // tail tile: re-read the last frame
+    const uint8_t *src = a.frames + (base + local) * a.stride + p * 16;
+    __builtin_amdgcn_global_load_lds(src, (lds_void_t *)(st + 64 * k), 16, 0, GLDS_NT);
   }
 }
 
-/* --------------------------------------------------------------------------- */
-/* Addresses and lengths of rounds [r0, r1) of tile w of a launch; round-0
- * header loads too when r0 == 0. */
-template <bool DENSE>
-__device__ __forceinline__ void prefetch_tile(const MultiArgs &m, uint32_t w, uint32_t r0,
-                                              uint32_t r1, uint32_t tid, uint32_t wave,
-                                              uint32_t lane, uint4 (&q)[ROUNDS][4],
-                                              uint32_t (&len)[ROUNDS],
-                                              const uint8_t *(&fp)[ROUNDS]) {
+/* this lane's frame (parts 0..2: bytes 0..47; parse reads bytes 12..39) */
+__device__ __forceinline__ void stage_read(const uint4 *st, uint32_t lane, uint4 (&q)[4]) {
+#pragma unroll
+  for (uint32_t j = 0; j < 3; ++j) q[j] = st[stage_slot(lane, j)];
+  q[3] = make_uint4(0, 0, 0, 0);
+}
+
+/* LANE: this lane's 64-byte window of round r into registers */
+__device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
+  const uint4 *w = reinterpret_cast<const uint4 *>(fp);
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(w + k);
+}
+
+/* Which batch of a launch tile w belongs to: tile_base[] is increasing, so
+ * bi = #{k in [1, count): w >= tile_base[k]}.  Unrolled over USN_MAX_MULTI
+ * so the bases arrive in one scalar load, not a dependent load per step. */
+__device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
   uint32_t bi = 0;
-  for (uint32_t k = 1; k < m.count; ++k)
-    if (w >= m.tile_base[k]) bi = k;
-  const ClassifyArgs &a = m.b[bi];
-  const uint64_t base = (uint64_t)(w - m.tile_base[bi]) * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    if (r < r0 || r >= r1) continue;
-    const uint32_t local = r * NTHREADS + tid;
-    const uint64_t i = base + (local < nt ? local : 0);
-    fp[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-    len[r] = local < nt ? (uint32_t)a.lens[i] : 0u;
-  }
-  if (r0 == 0) issue_round<DENSE>(a, base, 0, wave, lane, fp[0], q[0]);
+  for (uint32_t k = 1; k < USN_MAX_MULTI; ++k)
+    bi += (k < m.count && w >= m.tile_base[k]) ? 1u : 0u;
+  return bi;
 }
 
-/* USN_TPW 1024-frame tiles per workgroup: w = blockIdx.x, + gridDim.x, ...;
- * the next tile's lengths and round-0 headers are issued before this tile's
- * ordering phase, so a workgroup never waits on HBM with nothing in flight.
- * (A loop with a run-time trip count doubled the VGPRs; the unrolled form
- * does not.) */
-template <bool LDS, bool DENSE>
+/* One workgroup per 1024-frame tile of a launch (several batches = drained
+ * rx rings may share one launch). */
+template <bool LDS, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   extern __shared__ __align__(16) uint8_t smem[];
-  const uint32_t total = m.tile_base[m.count];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Lds L = carve(smem, m.b[0].nbins, DENSE);   // bins and table are shared by the batches
+  __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
+  __shared__ uint32_t s_carry[8];
+  __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Lds L = carve(smem, m.b[0].nbins);   // bins and table are shared by the batches
+  const uint32_t bi = batch_of(m, blockIdx.x);
+  const ClassifyArgs &a = m.b[bi];
+  const uint32_t tile = blockIdx.x - m.tile_base[bi];
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);   // this wave's stage
   STAMP_DECL
   STAMP(0);
 
-  // ---- loads, oldest first: rule table (tiny, L2-resident), lengths, then
-  //      the headers of round 0; round r+1 is issued just before round r is
-  //      decided.  Waves issue in order, so a wave that queued all 16 header
-  //      loads up front would sit behind HBM back-pressure instead of computing
-  //      on data that has already arrived; 16 waves per CU x one 4 KiB round
-  //      in flight keep the CU's share of HBM busy.
-  uint4 q[ROUNDS][4];
+  // ---- loads, oldest first: lengths, rule table (L2-resident), headers.
+  //      Unpredicated at a clamped index: a load under `local < nt` made the
+  //      compiler wait for each before issuing the next; lanes past nt are
+  //      masked at use.
   uint32_t len[ROUNDS];
   const uint8_t *fp[ROUNDS];
-  uint4 tb0 = make_uint4(0, 0, 0, 0);   // first 256 slots staged through registers
-  if (LDS && tid < m.b[0].table_slots) tb0 = m.b[0].table[tid];
-  uint32_t w = blockIdx.x;
-  prefetch_tile<DENSE>(m, w, 0, ROUNDS, tid, wave, lane, q, len, fp);
-  __builtin_amdgcn_sched_barrier(0);
-  bool first = true;
+  if (!GLDS && a.offsets) {   // uniform; GLDS launches have no offsets array
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r)
+      fp[r] = a.frames + a.offsets[base + min(r * NTHREADS + tid, nt - 1)];
+  } else {
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r)
+      fp[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
   const uint4 *T = m.b[0].table;
-  if (LDS) {
-    if (tid < m.b[0].table_slots) L.table[tid] = tb0;
-    for (uint32_t k = tid + NTHREADS; k < m.b[0].table_slots; k += NTHREADS)
-      L.table[k] = m.b[0].table[k];
+  if (LDS) {   // table -> LDS by glds, 64 slots per instruction, waves in turn
+    const uint32_t slots = m.b[0].table_slots;
+    for (uint32_t c = wave; c * 64 < slots; c += NWAVES) {
+      const uint32_t sl = min(c * 64 + lane, slots - 1);
+      __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
+    }
     T = L.table;
   }
-  __shared__ uint32_t s_carry[8];
-  __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
-
+  uint4 q[ROUNDS][4];
+  if (GLDS) {
 #pragma unroll
-  for (uint32_t it = 0; it < USN_TPW; ++it) {
-  uint32_t bi = 0;                       // which batch of the launch (uniform)
-  for (uint32_t k = 1; k < m.count; ++k)
-    if (w >= m.tile_base[k]) bi = k;
-  const ClassifyArgs &a = m.b[bi];
-  const uint32_t tile = w - m.tile_base[bi];
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-
-  // later tiles: round 0 was prefetched during the previous ordering phase
-  if (!first) prefetch_tile<DENSE>(m, w, 1, ROUNDS, tid, wave, lane, q, len, fp);
-  first = false;
+    for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
+      glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
+  } else {
+    lane_round(fp[0], q[0]);
+  }
   STAMP(1);
-  // ---- while they fly: zero the segment counters
+  // ---- while they fly: zero the segment counters (the barrier also waits
+  //      for every load: table and round 0 are in LDS / registers after it)
   for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
   if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
@@ -611,15 +656,15 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   if (tile == 0) {
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
-      const uint32_t st = s_carry[0], dst = s_carry[1];
+      const uint32_t cst = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
-      if ((st & USN_CS_VALID) &&
+      if ((cst & USN_CS_VALID) &&
           ((decide_info_rx<!LDS>(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
         flags |= USN_S_STALE;
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
       usn_summary *S = a.summary;
-      S->cin_state = st; S->cin_dst = dst;
+      S->cin_state = cst; S->cin_dst = dst;
       for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
       S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
     }
@@ -628,7 +673,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
   STAMP(3);
 
-  // ---- parse + decide
+  // ---- parse + decide, the next round's headers in flight meanwhile
   uint32_t dec[ROUNDS], bins[ROUNDS];
   uint32_t differs = 0;          // stale mode: bit r = touching frame whose info != carried
   uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
@@ -636,25 +681,34 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    if (r + 1 < ROUNDS) {        // one round of headers in flight ahead of the one decided
+    uint4 *sb = st + (r % GD) * STAGE_ROUND_SLOTS;
+    if (GLDS) {
+      // round r landed: only the rounds issued after it may still fly (4 glds each)
+      constexpr uint32_t kAfterMax = GD - 1;
+      const uint32_t after = min(kAfterMax, ROUNDS - 1 - r);
+      if (r > 0) {
+        if (after >= 3) vm_wait<12>();
+        else if (after == 2) vm_wait<8>();
+        else if (after == 1) vm_wait<4>();
+        else vm_wait<0>();
+      }
+      stage_read(sb, lane, q[r]);
+      if (r + GD < ROUNDS) {
+        lgkm_wait0();          // this round's reads are done before its buffer is refilled
+        glds_round(a, base, nt, r + GD, wave, lane, sb);
+      }
+    } else if (r + 1 < ROUNDS) {   // one round of headers in flight ahead of the one decided
       __builtin_amdgcn_sched_barrier(0);
-      issue_round<DENSE>(a, base, r + 1, wave, lane, fp[r + 1], q[r + 1]);
+      lane_round(fp[r + 1], q[r + 1]);
       __builtin_amdgcn_sched_barrier(0);
-    }
-    if (DENSE) {   // wave-private transpose through LDS: lane <- its own frame
-      uint4 *st = L.stage + wave * 256;
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) st[stage_slot(16 * k + (lane >> 2), lane & 3)] = q[r][k];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) q[r][k] = st[stage_slot(lane, k)];
     }
 #if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
     dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
-                       (q[r][0].x ^ q[r][1].y ^ q[r][2].z ^ q[r][3].w ^ len[r]) & 0xFFFFu);
+                       (q[r][0].w ^ q[r][1].y ^ q[r][2].x ^ q[r][2].y ^ len[r]) & 0xFFFFu);
     continue;
 #endif
     Parsed p;
-    parse(q[r], len[r], fp[r], p);
+    parse(q[r], local < nt ? len[r] : 0u, fp[r], p);
     dec[r] = decide_rx<!LDS>(T, a, p);
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
     uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
@@ -668,7 +722,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
                             p.dst == s_carry[4] && p.ports == s_carry[5]))
       differs |= 1u << r;        // later fragments also stop the device prefix
     if (r == 0) STAMP(4);
-
   }
   STAMP(5);
 
@@ -730,14 +783,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     }
   }
 
-  // ---- the next tile's lengths and round-0 headers fly during the ordering
-  const uint32_t wn = w + gridDim.x;
-  if (it + 1 < USN_TPW && wn < total) {
-    __builtin_amdgcn_sched_barrier(0);
-    prefetch_tile<DENSE>(m, wn, 0, 1, tid, wave, lane, q, len, fp);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
   STAMP(6);
   // ---- stable per-endpoint order of the tile
   uint32_t cls[4] = {0, 0, 0, 0};
@@ -775,10 +820,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
   STAMP(11);
-  if (wn >= total) break;
-  w = wn;
-  __syncthreads();   // s_misc / counters are reused by the next tile
-  }
   STAMP_FLUSH();
 }
 
@@ -798,7 +839,8 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    bins[r] = dec_bin(local < nt ? a.decisions[base + local] : 0u, a.n_ep);
+    const uint32_t d = a.decisions[base + (local < nt ? local : 0)];   // unpredicated load
+    bins[r] = dec_bin(local < nt ? d : 0u, a.n_ep);
   }
   __syncthreads();
   uint32_t cls[4] = {0, 0, 0, 0};
@@ -1099,7 +1141,12 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    r0[r] = local < nt ? t.rec[2 * (base + local)] : make_uint4(0, 0, 0, 0);
+    r0[r] = t.rec[2 * (base + (local < nt ? local : 0))];   // unpredicated: loads overlap
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) r0[r] = make_uint4(0, 0, 0, 0);
     srec[local] = r0[r];
     v[r] = (local < nt && tx_touch(r0[r])) ? local + 1 : 0u;
   }
@@ -1237,9 +1284,12 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     const uint64_t i = base + (local < nt ? local : 0);
-    r0[r] = local < nt ? t.rec[2 * i] : make_uint4(0, 0, 0, 0);
-    r1[r] = local < nt ? t.rec[2 * i + 1] : make_uint4(0, 0, 0, 0);
+    r0[r] = t.rec[2 * i];        // unpredicated (clamped index): the loads overlap
+    r1[r] = t.rec[2 * i + 1];
   }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r)
+    if (r * NTHREADS + tid >= nt) { r0[r] = make_uint4(0, 0, 0, 0); r1[r] = make_uint4(0, 0, 0, 0); }
   const uint32_t before = prev_tiles_last(t.aux, tile, 1);   // 1 + index, 0 = none
   const uint32_t ins = __builtin_amdgcn_readfirstlane(t.counters[2]);   // sets with items
   __syncthreads();
@@ -1387,7 +1437,7 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const dim3 g(a.ntiles), b(NTHREADS);
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
   const size_t core = lds_core_bytes(a.nbins);
-  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds, false);
+  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds);
   const size_t scan_lds =
       with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
   if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
@@ -1400,38 +1450,44 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
 }
 
 /* --------------------------------------------------------------------------- */
+/* The classify kernel's header stage (static LDS; GLDS only). */
+#define STAGE_BYTES_GLDS ((size_t)NWAVES * GD * STAGE_ROUND_SLOTS * 16)
+
+/* LDS copy of the rule table, rounded up to whole 64-slot glds chunks. */
+static inline size_t table_lds_bytes(uint32_t table_slots) {
+  return (size_t)((table_slots + 63) & ~63u) * 16;
+}
+
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots) {
   return (size_t)table_slots * 16 <= LDS_TABLE_MAX_BYTES &&
-         lds_core_bytes(nbins) + STAGE_BYTES + (size_t)table_slots * 16 <= 64u * 1024u;
+         lds_core_bytes(nbins) + STAGE_BYTES_GLDS + table_lds_bytes(table_slots) <= 64u * 1024u;
 }
 
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense) {
-  return lds_core_bytes(nbins) + (dense ? STAGE_BYTES : 0) +
-         (table_in_lds ? (size_t)table_slots * 16 : 0);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds) {
+  return lds_core_bytes(nbins) + (table_in_lds ? table_lds_bytes(table_slots) : 0);
 }
 
-/* The dense-layout transpose (coalesced 1 KiB loads + LDS transpose) is an
- * experiment: with launches overlapping, per-lane loads (no LDS traffic) were
- * faster (tools/abl.py, 3 streams: 13.8 vs 15.2 us per 1M frames). */
-#ifndef USN_DENSE
-#define USN_DENSE 0
-#endif
+/* glds needs 16-byte aligned sources: every window start of every batch. */
+static bool glds_layout(const MultiArgs &m) {
+  for (uint32_t k = 0; k < m.count; ++k) {
+    const ClassifyArgs &b = m.b[k];
+    if (b.offsets != nullptr || b.stride % 16 != 0 || (reinterpret_cast<uintptr_t>(b.frames) & 15))
+      return false;
+  }
+  return true;
+}
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
-  bool dense = USN_DENSE != 0;
-  for (uint32_t k = 0; k < m.count; ++k)
-    dense = dense && m.b[k].stride == 64 && m.b[k].offsets == nullptr;
-  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, dense);
-  uint32_t grid = tiles;
-  grid = (tiles + USN_TPW - 1) / USN_TPW;
-  const dim3 g(grid), b(NTHREADS);
-  if (in_lds && dense) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
+  const bool glds = USN_GLDS_ENABLE && glds_layout(m);
+  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds);
+  const dim3 g(tiles), b(NTHREADS);
+  if (in_lds && glds) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
   else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);
-  else if (dense) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, m);
+  else if (glds) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, m);
   else hipLaunchKernelGGL((classify_rx_kernel<false, false>), g, b, lds, stream, m);
   return hipGetLastError();
 }

@@ -100,7 +100,7 @@ struct TxArgs {
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool dense);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds);
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
