@@ -178,6 +178,34 @@ __device__ __forceinline__ uint32_t bucket_hit(const uint4 &s0, const uint4 &s1,
          (s3.w & (0u - (uint32_t)slot_is(s3, x, y, z, meta)));
 }
 
+/* The four slots of a bucket.  From LDS by inline asm: the classify kernel
+ * has LDS-DMA (glds) writes in flight while it probes, and hipcc cannot tell
+ * that the table does not alias the DMA's stage, so plain LDS reads got an
+ * s_waitcnt vmcnt(0) that drained the next round's headers.  The asm waits
+ * for its own reads (lgkmcnt) and nothing else. */
+template <bool IN_LDS>
+__device__ __forceinline__ void load_bucket(const uint4 *s, uint4 &s0, uint4 &s1, uint4 &s2,
+                                            uint4 &s3) {
+  if (IN_LDS) {
+    const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint4 *)s;
+    v4u32 a0, a1, a2, a3;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:16\n\t"
+        "ds_read_b128 %2, %4 offset:32\n\t"
+        "ds_read_b128 %3, %4 offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(addr));
+    s0 = make_uint4(a0.x, a0.y, a0.z, a0.w);
+    s1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
+    s2 = make_uint4(a2.x, a2.y, a2.z, a2.w);
+    s3 = make_uint4(a3.x, a3.y, a3.z, a3.w);
+  } else {
+    s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
+  }
+}
+
 /* One exact-match probe.  LDS table: the home bucket (one 64-byte line) is
  * checked with selects; the chain is followed only when that bucket is full
  * and holds no match (rare at load <= 1/2).  Global table (TAGGED): one
@@ -208,13 +236,14 @@ __device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uin
   }
   uint32_t b = usn_key_hash(x, y, z, meta) & bmask;
   const uint4 *s = T + b * 4;
-  uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+  uint4 s0, s1, s2, s3;
+  load_bucket<!TAGGED>(s, s0, s1, s2, s3);   // !TAGGED: the table is in LDS
   uint32_t hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
   if (!hit && (s3.w & USN_SLOT_VALID)) {
     for (uint32_t it = 0; it < bmask; ++it) {
       b = (b + 1) & bmask;
       s = T + b * 4;
-      s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
+      load_bucket<!TAGGED>(s, s0, s1, s2, s3);
       hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
       if (hit || !(s3.w & USN_SLOT_VALID)) break;
     }
@@ -288,21 +317,23 @@ struct Lds {
   uint4 *table;       // staged rule table (optional)
 };
 
-__host__ __device__ inline size_t lds_core_bytes(uint32_t nbins) {
-  size_t b = (size_t)NSEG * nbins * 2 + (size_t)nbins * 2;
-  b = (b + 15) & ~(size_t)15;
-  b += TILE * 2 + 16 * 4;
-  return (b + 15) & ~(size_t)15;
+/* cnt | bstart | scratch[16] | order[TILE] (unless the caller keeps the
+ * order row elsewhere) | table */
+__host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) {
+  const size_t b = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
+  return b + 16 * 4;
 }
-
-__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins) {
+__host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_order = true) {
+  return lds_head_bytes(nbins) + (own_order ? TILE * 2 : 0);
+}
+__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, uint16_t *order = nullptr) {
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
   L.bstart = L.cnt + (size_t)NSEG * nbins;
   const size_t off = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
-  L.order = reinterpret_cast<uint16_t *>(smem + off);
-  L.scratch = reinterpret_cast<uint32_t *>(L.order + TILE);
-  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins));
+  L.scratch = reinterpret_cast<uint32_t *>(smem + off);
+  L.order = order ? order : reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
+  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins, order == nullptr));
   return L;
 }
 
@@ -386,58 +417,111 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     if (local < nt && rank[r] == 0) L.cnt[bins[r] * NSEG + s] = (uint16_t)__popcll(same);
   }
   __syncthreads();
-  // each thread owns a contiguous chunk of bins: column scan over the 16
-  // segments (cnt[s][b] := frames of bin b in earlier segments), then one
-  // block scan of (present << 16 | total) gives bin starts and run indices
-  const uint32_t per = (nbins + NTHREADS - 1) / NTHREADS;
-  const uint32_t b0 = tid * per;
-  uint32_t packed = 0;
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t b = b0 + k;
-    if (b >= nbins) break;
-    // the 16 u16 counts of bin b are 32 contiguous bytes: two 16-byte LDS
-    // reads, an exclusive prefix in registers, two 16-byte writes
-    uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
-    uint32_t w[8];
-    const uint4 r0 = row[0], r1 = row[1];
-    w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
-    w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
-    uint32_t acc = 0;
-#pragma unroll
-    for (uint32_t k2 = 0; k2 < 8; ++k2) {
-      const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
-      w[k2] = acc | ((acc + lo) << 16);
-      acc += lo + hi;
-    }
-    row[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    row[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    L.bstart[b] = (uint16_t)acc;
-    packed += acc | (acc ? 0x10000u : 0u);
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan(packed, L.scratch, &total);
   uint32_t *rdst = runs_out + (size_t)tile * TILE;
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t b = b0 + k;
-    if (b >= nbins) break;
-    const uint32_t c = L.bstart[b];
-    const uint32_t start = run & 0xFFFFu;
-    L.bstart[b] = (uint16_t)start;
-    if (c) rdst[run >> 16] = (b << 16) | start;
-    run += c | (c ? 0x10000u : 0u);
-    // NIC, FLOOD, DROP totals (selects: a runtime index would put cls in scratch)
-    cls[1] = b == n_ep ? c : cls[1];
-    cls[2] = b == n_ep + 1 ? c : cls[2];
-    cls[3] = b == n_ep + 2 ? c : cls[3];
-  }
-  __syncthreads();
+  uint32_t n_runs;
+  if (nbins <= 64) {
+    // one wave does all of it, lane b for bin b: column scan of the bin's 16
+    // segment counts, a wave scan of (present << 16 | total) for the bin
+    // starts and run indices, and the start folded into the row, so the
+    // scatter below reads one word per frame.  Two barriers fewer than the
+    // block-wide form.
+    if (wave == 0) {
+      const uint32_t b = lane;
+      uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
+      if (b < nbins) {
+        const uint4 r0 = row[0], r1 = row[1];
+        w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
+        w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
+      }
+      uint32_t acc = 0;
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local < nt) {
-      const uint32_t s = r * (NTHREADS / 64) + wave;
-      const uint32_t b = bins[r];
-      L.order[L.bstart[b] + L.cnt[b * NSEG + s] + rank[r]] = (uint16_t)local;
+      for (uint32_t k2 = 0; k2 < 8; ++k2) {
+        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
+        w[k2] = acc | ((acc + lo) << 16);
+        acc += lo + hi;
+      }
+      const uint32_t packed = acc | (acc ? 0x10000u : 0u);
+      const uint32_t inc = wave_incl_scan(packed, lane);
+      const uint32_t run = inc - packed;
+      const uint32_t start = run & 0xFFFFu;
+      if (b < nbins) {
+        const uint32_t st2 = start | (start << 16);
+#pragma unroll
+        for (uint32_t k2 = 0; k2 < 8; ++k2) w[k2] += st2;
+        row[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        row[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        if (acc) rdst[run >> 16] = (b << 16) | start;
+      }
+      cls[1] = b == n_ep ? acc : 0u;
+      cls[2] = b == n_ep + 1 ? acc : 0u;
+      cls[3] = b == n_ep + 2 ? acc : 0u;
+      if (lane == 63) L.scratch[15] = inc >> 16;
+    }
+    __syncthreads();
+    n_runs = L.scratch[15];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      if (local < nt) {
+        const uint32_t s = r * (NTHREADS / 64) + wave;
+        L.order[L.cnt[bins[r] * NSEG + s] + rank[r]] = (uint16_t)local;
+      }
+    }
+  } else {
+    // each thread owns a contiguous chunk of bins: column scan over the 16
+    // segments (cnt[s][b] := frames of bin b in earlier segments), then one
+    // block scan of (present << 16 | total) gives bin starts and run indices
+    const uint32_t per = (nbins + NTHREADS - 1) / NTHREADS;
+    const uint32_t b0 = tid * per;
+    uint32_t packed = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = b0 + k;
+      if (b >= nbins) break;
+      // the 16 u16 counts of bin b are 32 contiguous bytes: two 16-byte LDS
+      // reads, an exclusive prefix in registers, two 16-byte writes
+      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
+      uint32_t w[8];
+      const uint4 r0 = row[0], r1 = row[1];
+      w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
+      w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
+      uint32_t acc = 0;
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 8; ++k2) {
+        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
+        w[k2] = acc | ((acc + lo) << 16);
+        acc += lo + hi;
+      }
+      row[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      row[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      L.bstart[b] = (uint16_t)acc;
+      packed += acc | (acc ? 0x10000u : 0u);
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan(packed, L.scratch, &total);
+    n_runs = total >> 16;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = b0 + k;
+      if (b >= nbins) break;
+      const uint32_t c = L.bstart[b];
+      const uint32_t start = run & 0xFFFFu;
+      L.bstart[b] = (uint16_t)start;
+      if (c) rdst[run >> 16] = (b << 16) | start;
+      run += c | (c ? 0x10000u : 0u);
+      // NIC, FLOOD, DROP totals (selects: a runtime index would put cls in scratch)
+      cls[1] = b == n_ep ? c : cls[1];
+      cls[2] = b == n_ep + 1 ? c : cls[2];
+      cls[3] = b == n_ep + 2 ? c : cls[3];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      if (local < nt) {
+        const uint32_t s = r * (NTHREADS / 64) + wave;
+        const uint32_t b = bins[r];
+        L.order[L.bstart[b] + L.cnt[b * NSEG + s] + rank[r]] = (uint16_t)local;
+      }
     }
   }
   __syncthreads();
@@ -454,7 +538,7 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
     for (uint32_t k = 0; k < ROUNDS; ++k)
       if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
   }
-  return total >> 16;
+  return n_runs;
 }
 
 /* --------------------------------------------------------------------------- */
@@ -600,7 +684,10 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Lds L = carve(smem, m.b[0].nbins);   // bins and table are shared by the batches
+  // bins and table are shared by the batches.  GLDS: the order row lives in
+  // the header stage, free once every round is decided (the sort starts after
+  // a barrier), so eight workgroups fit a CU's LDS instead of seven.
+  const Lds L = carve(smem, m.b[0].nbins, GLDS ? reinterpret_cast<uint16_t *>(s_stage) : nullptr);
   const uint32_t bi = batch_of(m, blockIdx.x);
   const ClassifyArgs &a = m.b[bi];
   const uint32_t tile = blockIdx.x - m.tile_base[bi];
@@ -1437,7 +1524,7 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const dim3 g(a.ntiles), b(NTHREADS);
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
   const size_t core = lds_core_bytes(a.nbins);
-  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds);
+  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds, false);
   const size_t scan_lds =
       with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
   if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
@@ -1463,8 +1550,9 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_slots) {
          lds_core_bytes(nbins) + STAGE_BYTES_GLDS + table_lds_bytes(table_slots) <= 64u * 1024u;
 }
 
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds) {
-  return lds_core_bytes(nbins) + (table_in_lds ? table_lds_bytes(table_slots) : 0);
+/* dynamic LDS of the classify kernels; glds: the order row is in the stage */
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool glds) {
+  return lds_core_bytes(nbins, !glds) + (table_in_lds ? table_lds_bytes(table_slots) : 0);
 }
 
 /* glds needs 16-byte aligned sources: every window start of every batch. */
@@ -1483,7 +1571,7 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds);
+  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, glds);
   const dim3 g(tiles), b(NTHREADS);
   if (in_lds && glds) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
   else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);

@@ -787,6 +787,16 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
  * threads per tile (A/B: c5's 65536 rules 1.55x faster; c4's 4096 equal) */
 #define USN_T512_MIN_SLOTS 16384u
 
+/* 512 threads per tile (two rounds per lane) when the table is in LDS for
+ * both builds (c1/c2: 3 % faster), never when only the 256-thread build can
+ * keep it in LDS (its stage is half as big; c3: 2 % slower in L2), and for
+ * large global tables. */
+static bool use_t512(uint32_t nbins, uint32_t slots) {
+  if (usn_t512::table_fits_lds(nbins, slots)) return true;
+  if (usn::table_fits_lds(nbins, slots)) return false;
+  return slots > USN_T512_MIN_SLOTS;
+}
+
 static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
   if (!b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
   if ((b->stride == 0) == (b->offsets == nullptr)) return USN_EINVAL;
@@ -921,9 +931,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
     c->tx.decisions = r[0].decisions;
-  } else if (c->t512 == 1 || (c->t512 < 0 &&
-                                !usn::table_fits_lds(m.b[0].nbins, m.b[0].table_slots) &&
-                                m.b[0].table_slots > USN_T512_MIN_SLOTS)) {
+  } else if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_slots))) {
     HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
   } else {
     HIPCHK(usn::launch_classify(m, (hipStream_t)stream));

@@ -100,7 +100,7 @@ struct TxArgs {
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool glds);
 bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
@@ -110,9 +110,10 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
 }  // namespace usn
 
 /* the same kernels at 512 threads per tile (a second compilation of
- * usn_device.hip): faster when the rule table lives in global memory */
+ * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
+bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
 }
 
 #endif
