@@ -31,6 +31,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
     ablmulti) step ablmulti_${NMULTI:-4}_${NSTREAMS:-1} 600 python tools/abl.py --multi ${NMULTI:-4} --streams ${NSTREAMS:-1} --batches ${NBATCH:-8} --json gpurun_out/ablmulti.json ${ABL_VARIANTS:-base loadonly} ;;
     hostio) step hostio 300 python tools/hostio.py ${HOSTIO_ARGS:-} ;;
     txbench) step txbench 600 python tools/txbench.py ${TXB_ARGS:-} ;;
+    txab)   # tx A/B: the same txbench per A/B build (make abl)
+      for v in ${TXAB_VARIANTS:-base t512}; do
+        step txab_$v 300 python tools/txbench.py 1048576 12 1 build/abl/$v/libusn.so
+      done ;;
     allcfg) step allcfg 1100 python tools/all_configs.py ${ALLCFG_ARGS:-} ;;
     txprof) rm -rf gpurun_out/txprof; step txprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/txprof -o run -- python3 tools/txbench.py ${TXB_ARGS:-} ;;
     ablsmall) step ablsmall 600 python tools/abl.py --frames 131072 --batches 1 --json gpurun_out/ablsmall.json ;;

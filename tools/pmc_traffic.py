@@ -17,12 +17,13 @@ import sys
 
 def per_dispatch(d, counter, frames):
     """Counter values of the classify dispatches covering `frames` frames
-    (grid = frames / 4 threads: 256-thread workgroups of 1024 frames)."""
+    (1024-frame tiles: grid = frames / 4 threads for 256-thread workgroups,
+    frames / 2 for the 512-thread build)."""
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if ("classify_rx_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter
-                    and int(r["Grid_Size"]) == frames // 4):
+                    and int(r["Grid_Size"]) in (frames // 4, frames // 2)):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
