@@ -31,6 +31,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
     ablmulti) step ablmulti_${NMULTI:-4}_${NSTREAMS:-1} 600 python tools/abl.py --multi ${NMULTI:-4} --streams ${NSTREAMS:-1} --batches ${NBATCH:-8} --json gpurun_out/ablmulti.json ${ABL_VARIANTS:-base loadonly} ;;
     hostio) step hostio 300 python tools/hostio.py ${HOSTIO_ARGS:-} ;;
     txbench) step txbench 600 python tools/txbench.py ${TXB_ARGS:-} ;;
+    ablcfg)  # rx A/B of ABL_VARIANTS per config of ABL_CFGS (one process per config)
+      for c in ${ABL_CFGS:-c4 c5}; do
+        step abl_$c 600 python tools/abl.py --config $c --rounds 3 --json gpurun_out/abl_$c.json ${ABL_VARIANTS:-old new}
+      done ;;
     txab)   # tx A/B: the same txbench per A/B build (make abl)
       for v in ${TXAB_VARIANTS:-base t512}; do
         step txab_$v 300 python tools/txbench.py 1048576 12 1 build/abl/$v/libusn.so

@@ -89,6 +89,10 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #define USN_LOAD_NT 0
 #endif
 
+#ifndef USN_ABL_LOADONLY   /* A/B only: loads and stores, no parse/probe/decide */
+#define USN_ABL_LOADONLY 0
+#endif
+
 /* 16-byte header load (`nt` streaming hint only when USN_LOAD_NT) */
 __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
 #if USN_LOAD_NT
@@ -255,22 +259,39 @@ __device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uin
  * ARP/EAPOL -> FLOOD, loopback -> DROP, else get_endpoint (endpoint.rs:307-338:
  * key1 = with src, key2 = without, only on a key1 miss; a hit on a NIC-owned
  * rule or on the source itself is None with no retry), else DHCP / DROP. */
+/* key1 = to_match_want_with_src(true), key2 = (false) of a parsed frame (pkt.rs:96-113) */
+__device__ __forceinline__ void rx_keys(const Parsed &p, uint32_t &x1, uint32_t &y1, uint32_t &z1,
+                                        uint32_t &m1, uint32_t &x2, uint32_t &y2, uint32_t &z2,
+                                        uint32_t &m2) {
+  const bool has = p.has_ports != 0;
+  x1 = p.dst; y1 = p.src; z1 = has ? (p.dport | (p.sport << 16)) : 0u;
+  m1 = usn_key_meta(p.proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT) : USN_WANT_SRC);
+  x2 = p.dst; y2 = 0u; z2 = has ? p.dport : 0u;
+  m2 = usn_key_meta(p.proto, has ? USN_WANT_DPORT : 0u);
+}
+
+/* the decision from the two probe results (w1 = key1's slot meta, w2 = key2's) */
+__device__ __forceinline__ uint32_t decide_rx_w(const ClassifyArgs &a, const Parsed &p, uint32_t w1,
+                                                uint32_t w2);
+
 template <bool TAGGED>
 __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs &a,
                                               const Parsed &p) {
-  const bool has = p.has_ports != 0;
   uint32_t w1 = 0, w2 = 0;
 #if USN_ABL_NOPROBE   /* ablation build only: no table probes */
   w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
 #else
-  if (a.probe_mask & 1u)
-    w1 = probe<TAGGED>(T, a.tags, a.bucket_mask, p.dst, p.src, has ? (p.dport | (p.sport << 16)) : 0u,
-               usn_key_meta(p.proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT)
-                                         : USN_WANT_SRC));
-  if (a.probe_mask & 2u)
-    w2 = probe<TAGGED>(T, a.tags, a.bucket_mask, p.dst, 0u, has ? p.dport : 0u,
-               usn_key_meta(p.proto, has ? USN_WANT_DPORT : 0u));
+  uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+  rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
+  if (a.probe_mask & 1u) w1 = probe<TAGGED>(T, a.tags, a.bucket_mask, x1, y1, z1, m1);
+  if (a.probe_mask & 2u) w2 = probe<TAGGED>(T, a.tags, a.bucket_mask, x2, y2, z2, m2);
 #endif
+  return decide_rx_w(a, p, w1, w2);
+}
+
+__device__ __forceinline__ uint32_t decide_rx_w(const ClassifyArgs &a, const Parsed &p, uint32_t w1,
+                                                uint32_t w2) {
+  const bool has = p.has_ports != 0;
   const uint32_t w = w1 ? w1 : w2;
   const uint32_t owner = w >> 16;
   const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
@@ -310,18 +331,30 @@ __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
 /* --------------------------------------------------------------------------- */
 /* LDS layout of a block                                                        */
 struct Lds {
-  uint16_t *cnt;      // [nbins][NSEG]: per-segment counts, then segment prefixes
-  uint16_t *bstart;   // [nbins]: tile totals, then bin start slots
-  uint16_t *order;    // [TILE]
+  uint16_t *cnt;      // [rows][NSEG]: per-segment counts, then segment prefixes
+  uint16_t *bstart;   // [nbins]: tile totals, then bin starts (64 < nbins <= RADIX_MIN)
   uint32_t *scratch;  // [16]
+  uint32_t *keys;     // [TILE] (bin << 16 | index) between radix passes (> RADIX_MIN)
+  uint16_t *order;    // [TILE]
   uint4 *table;       // staged rule table (optional)
 };
 
-/* cnt | bstart | scratch[16] | order[TILE] (unless the caller keeps the
- * order row elsewhere) | table */
+/* Up to USN_RADIX_MIN_BINS bins the tile is counted per (bin, segment); with
+ * more it is sorted by 6-bit digits of the bin (tile_order_radix, one counter
+ * row per digit value).  A/B (c4: 261 bins, c5: 1005): the direct form costs
+ * in proportion to the bins, the radix passes a constant; they meet near 450. */
+#define USN_RADIX_MIN_BINS 512u
+__host__ __device__ inline bool radix_bins(uint32_t nbins) { return nbins > USN_RADIX_MIN_BINS; }
+__host__ __device__ inline uint32_t cnt_rows(uint32_t nbins) { return radix_bins(nbins) ? 64 : nbins; }
+__host__ __device__ inline size_t cnt_bytes(uint32_t nbins) {
+  const size_t b = (size_t)NSEG * cnt_rows(nbins) * 2 + (nbins > 64 && !radix_bins(nbins) ? nbins * 2 : 0);
+  return (b + 15) & ~(size_t)15;
+}
+
+/* cnt | bstart | scratch[16] | keys[TILE] (radix) | order[TILE] (unless the
+ * caller keeps the order row elsewhere) | table */
 __host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) {
-  const size_t b = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
-  return b + 16 * 4;
+  return cnt_bytes(nbins) + 16 * 4 + (radix_bins(nbins) ? (size_t)TILE * 4 : 0);
 }
 __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_order = true) {
   return lds_head_bytes(nbins) + (own_order ? TILE * 2 : 0);
@@ -329,9 +362,9 @@ __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_order 
 __device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, uint16_t *order = nullptr) {
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
-  L.bstart = L.cnt + (size_t)NSEG * nbins;
-  const size_t off = ((size_t)NSEG * nbins * 2 + (size_t)nbins * 2 + 15) & ~(size_t)15;
-  L.scratch = reinterpret_cast<uint32_t *>(smem + off);
+  L.bstart = L.cnt + (size_t)NSEG * cnt_rows(nbins);
+  L.scratch = reinterpret_cast<uint32_t *>(smem + cnt_bytes(nbins));
+  L.keys = radix_bins(nbins) ? L.scratch + 16 : nullptr;
   L.order = order ? order : reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
   L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins, order == nullptr));
   return L;
@@ -398,6 +431,95 @@ __device__ __forceinline__ uint64_t match_bin(uint32_t b, uint64_t valid, uint32
   return same;
 }
 
+/* Stable sort of a tile with more than 64 bins: LSD radix passes over 6-bit
+ * digits of the bin.  Each pass is the <=64-bin counting sort of tile_order
+ * (bit-sliced ballots, one wave scans the 64 digit rows) and moves the keys
+ * (bin << 16 | tile-local index) to their sorted slots in L.keys.  The direct
+ * form's [bin][segment] counters grow with the endpoints (16 K counters, 32
+ * KiB to zero and scan per tile at 1000 endpoints); these stay 64 x 16.
+ * Leaves the order row in L.order, writes the runs, returns their number;
+ * cls[1..3] get this thread's NIC / FLOOD / DROP frames.  L.cnt is zero on
+ * entry and on return. */
+__device__ uint32_t tile_order_radix(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbits,
+                                     uint32_t n_ep, const Lds &L, uint32_t *rdst, uint32_t cls[4]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t key[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) key[r] = (bins[r] << 16) | (r * NTHREADS + tid);
+  for (uint32_t shift = 0; shift < nbits; shift += 6) {
+    uint32_t dg[ROUNDS], rank[ROUNDS];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      const uint32_t s = r * (NTHREADS / 64) + wave;       // 64-slot segment, slot order
+      dg[r] = (key[r] >> (16 + shift)) & 63u;
+      const uint64_t same = match_bin(dg[r], __ballot(local < nt), 6);
+      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+      if (local < nt && rank[r] == 0) L.cnt[dg[r] * NSEG + s] = (uint16_t)__popcll(same);
+    }
+    __syncthreads();
+    if (wave == 0) {   // lane d: segment prefixes of digit d plus the digit's start
+      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + lane * NSEG);
+      const uint4 r0 = row[0], r1 = row[1];
+      uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      uint32_t acc = 0;
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 8; ++k2) {
+        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
+        w[k2] = acc | ((acc + lo) << 16);
+        acc += lo + hi;
+      }
+      const uint32_t start = wave_incl_scan(acc, lane) - acc;
+      const uint32_t st2 = start | (start << 16);
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < 8; ++k2) w[k2] += st2;
+      row[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      row[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      const uint32_t s = r * (NTHREADS / 64) + wave;
+      if (local < nt) L.keys[L.cnt[dg[r] * NSEG + s] + rank[r]] = key[r];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 64 * NSEG; i += NTHREADS) L.cnt[i] = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) key[r] = L.keys[r * NTHREADS + tid];   // slots >= nt unused
+    __syncthreads();
+  }
+  // sorted keys in L.keys[0, nt): the order row, and a run wherever the bin changes
+  const uint32_t p0 = tid * ROUNDS;
+  uint32_t kb[ROUNDS], starts = 0;
+  uint32_t prev = (p0 > 0 && p0 <= nt) ? (L.keys[p0 - 1] >> 16) : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t k = 0; k < ROUNDS; ++k) {
+    const uint32_t p = p0 + k;
+    kb[k] = 0xFFFFFFFFu;
+    if (p < nt) {
+      const uint32_t kv = L.keys[p];
+      kb[k] = kv >> 16;
+      L.order[p] = (uint16_t)(kv & 0xFFFFu);
+      starts += kb[k] != prev ? 1u : 0u;
+      prev = kb[k];
+      cls[1] += kb[k] == n_ep ? 1u : 0u;
+      cls[2] += kb[k] == n_ep + 1 ? 1u : 0u;
+      cls[3] += kb[k] == n_ep + 2 ? 1u : 0u;
+    }
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan(starts, L.scratch, &total);
+  prev = (p0 > 0 && p0 <= nt) ? (L.keys[p0 - 1] >> 16) : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t k = 0; k < ROUNDS; ++k) {
+    const uint32_t p = p0 + k;
+    if (p < nt && kb[k] != prev) rdst[run++] = (kb[k] << 16) | p;
+    if (p < nt) prev = kb[k];
+  }
+  return total;
+}
+
 /* Stable counting sort of the tile by bin, written out as the tile's order
  * (tile-local indices) and bin runs.  bins[r] belongs to tile-local frame
  * r*256 + tid (valid when < nt).  L.cnt must be zero on entry.  Returns the
@@ -407,19 +529,20 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
                                uint32_t nbits, uint32_t n_ep, const Lds &L, uint32_t tile,
                                uint16_t *order_out, uint32_t *runs_out, uint32_t cls[4]) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t rank[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const uint32_t s = r * (NTHREADS / 64) + wave;         // 64-frame segment, index order
-    const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
-    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-    if (local < nt && rank[r] == 0) L.cnt[bins[r] * NSEG + s] = (uint16_t)__popcll(same);
-  }
-  __syncthreads();
   uint32_t *rdst = runs_out + (size_t)tile * TILE;
   uint32_t n_runs;
-  if (nbins <= 64) {
+  if (nbins <= USN_RADIX_MIN_BINS) {
+    uint32_t rank[ROUNDS];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      const uint32_t s = r * (NTHREADS / 64) + wave;         // 64-frame segment, index order
+      const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
+      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+      if (local < nt && rank[r] == 0) L.cnt[bins[r] * NSEG + s] = (uint16_t)__popcll(same);
+    }
+    __syncthreads();
+    if (nbins <= 64) {
     // one wave does all of it, lane b for bin b: column scan of the bin's 16
     // segment counts, a wave scan of (present << 16 | total) for the bin
     // starts and run indices, and the start folded into the row, so the
@@ -468,7 +591,7 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
         L.order[L.cnt[bins[r] * NSEG + s] + rank[r]] = (uint16_t)local;
       }
     }
-  } else {
+    } else {
     // each thread owns a contiguous chunk of bins: column scan over the 16
     // segments (cnt[s][b] := frames of bin b in earlier segments), then one
     // block scan of (present << 16 | total) gives bin starts and run indices
@@ -523,6 +646,9 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
         L.order[L.bstart[b] + L.cnt[b * NSEG + s] + rank[r]] = (uint16_t)local;
       }
     }
+    }
+  } else {
+    n_runs = tile_order_radix(bins, nt, nbits, n_ep, L, rdst, cls);
   }
   __syncthreads();
   uint16_t *dst = order_out + (size_t)tile * TILE;
@@ -734,7 +860,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   STAMP(1);
   // ---- while they fly: zero the segment counters (the barrier also waits
   //      for every load: table and round 0 are in LDS / registers after it)
-  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
+  for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
   if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
   STAMP(2);
@@ -921,7 +1047,7 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   __shared__ uint32_t s_cls[4];
   if (tid < 4) s_cls[tid] = 0;
-  for (uint32_t i = tid; i < NSEG * a.nbins; i += NTHREADS) L.cnt[i] = 0;
+  for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
   uint32_t bins[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -1157,7 +1283,6 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     if (local >= nt) continue;
-    const uint64_t i = base + local;
     const uint8_t *fp = fps[r];
     const uint4 *q = qq[r];
     const uint32_t len = ll[r];
@@ -1189,21 +1314,21 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
                             p.dport == 67u && (p.dst & 0xFFu) == 255u;
       if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
-      if (!listening && !dhcp_req) {
-        uint4 r0 = make_uint4(p.i0, p.src, p.dst, p.ports);
+      if (!listening && !dhcp_req) {   // the answer key is learned unless the table has it
         uint32_t x, y, z, meta;
-        want_key(r0, x, y, z, meta);
+        want_key(make_uint4(p.i0, p.src, p.dst, p.ports), x, y, z, meta);
         if (!probe<!LDS>(T, a.tags, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
+    if (p.status == 1u && p.frag_first) f |= TXR_FRAG1;
     uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
     if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
     r0.x = (r0.x & TXR_I0_MASK) | f;
-    uint4 r1 = make_uint4((uint32_t)smac, (uint32_t)(smac >> 32) | ((uint32_t)dmac << 16),
-                          (uint32_t)(dmac >> 16), p.status == 1u ? p.frag_first : 0u);
-    t.rec[2 * i] = r0;
-    t.rec[2 * i + 1] = r1;
+    const uint64_t i = base + local;
+    t.rec[i] = r0;
+    t.rec[a.n + i] = make_uint4((uint32_t)smac, (uint32_t)(smac >> 32) | ((uint32_t)dmac << 16),
+                                (uint32_t)(dmac >> 16), 0u);
     if (touch) last = local + 1;
   }
   if (last) atomicMax(&s_last, last);
@@ -1228,7 +1353,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    r0[r] = t.rec[2 * (base + (local < nt ? local : 0))];   // unpredicated: loads overlap
+    r0[r] = t.rec[base + (local < nt ? local : 0)];   // unpredicated: loads overlap
   }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -1254,7 +1379,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
       const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
       const uint32_t info0 = fl & TXR_I0_MASK;
       if (k1) {
-        const uint4 pr = prev[r] ? srec[prev[r] - 1] : t.rec[2 * (size_t)(k1 - 1)];
+        const uint4 pr = prev[r] ? srec[prev[r] - 1] : t.rec[k1 - 1];
         const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == r0[r].y &&
                           pr.z == r0[r].z && pr.w == r0[r].w;
         if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
@@ -1265,12 +1390,12 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
       }
     }
     if (hit) fl |= TXR_HIT;
-    if (fl != r0[r].x) t.rec[2 * i].x = fl;
+    if (fl != r0[r].x) t.rec[i].x = fl;
     if (!hit) last_nh = local + 1;
     if (hit || (fl & TXR_HOST)) continue;
     // this frame really learns: first occurrence per item
     if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
-      const uint4 r1 = t.rec[2 * i + 1];
+      const uint4 r1 = t.rec[a.n + i];
       if (fl & TXR_LEARNMAC) {
         const uint64_t m = rec_smac(r1);
         unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
@@ -1305,35 +1430,43 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
 /* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
  * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
  * by a frame <= i. */
-template <bool TAGGED>
-__device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
-                                   const uint4 &r1, uint32_t i, uint32_t ins) {
-  const ClassifyArgs &a = t.a;
-  const uint32_t fl = r0.x;
-  const uint64_t dmac = rec_dmac(r1);
+/* dmac in the inner bridge: in the snapshot, or learned by a frame <= i
+ * (endpoint.rs:254); r1 is read only when this batch learned a MAC */
+__device__ __forceinline__ bool tx_dmac_in(const TxArgs &t, uint32_t fl, const uint4 &r1, uint32_t i,
+                                           uint32_t ins) {
   bool d_in = (fl & TXR_DMAC_IN) != 0;
-  if (!d_in && (ins & 1u))                             // learned by a frame <= i ?
+  if (!d_in && (ins & 1u)) {
+    const uint64_t dmac = rec_dmac(r1);
     d_in = slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, dmac, usn_mac_hash(dmac)),
                       t.epoch) <= i;
-  if (!d_in) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
-  uint32_t x, y, z, meta;
-  key1_of(r0, x, y, z, meta);
-  uint32_t w = (a.probe_mask & 1u) ? probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta) : 0u;
-  if (!w && (ins & 2u)) {   // a rule learned by a frame <= i is owned by S (so excluded)
-    const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
-                                              usn_key_fp48(x, y, z, meta),
-                                              usn_key_hash(x, y, z, meta));
-    if (slot_first(slot, t.epoch) <= i) {
-      if (slot[2] != (((unsigned long long)y << 32) | x) ||
-          slot[3] != (((unsigned long long)meta << 32) | z))
-        atomicOr(t.counters + 1, 2u);                // fingerprint collision: host redoes
-      w = USN_SLOT_VALID | (a.src << 16);
-    }
   }
-  const bool has = (r0.x >> 16) & 1u;
-  if (!w && (a.probe_mask & 2u))
-    w = probe<TAGGED>(T, a.tags, a.bucket_mask, r0.z, 0u, has ? (r0.w >> 16) : 0u,
-              usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u));
+  return d_in;
+}
+
+/* key1 = a rule learned by a frame <= i: it is owned by S (so excluded) */
+__device__ __forceinline__ uint32_t tx_learned_key1(const TxArgs &t, uint32_t x, uint32_t y, uint32_t z,
+                                                    uint32_t meta, uint32_t i) {
+  const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
+                                            usn_key_fp48(x, y, z, meta), usn_key_hash(x, y, z, meta));
+  if (slot_first(slot, t.epoch) > i) return 0u;
+  if (slot[2] != (((unsigned long long)y << 32) | x) ||
+      slot[3] != (((unsigned long long)meta << 32) | z))
+    atomicOr(t.counters + 1, 2u);                      // fingerprint collision: host redoes
+  return USN_SLOT_VALID | (t.a.src << 16);
+}
+
+/* key2 = to_match_want_with_src(false) */
+__device__ __forceinline__ void key2_of(const uint4 &r0, uint32_t &x, uint32_t &y, uint32_t &z,
+                                        uint32_t &meta) {
+  const uint32_t has = (r0.x >> 16) & 1u;
+  x = r0.z;
+  y = 0u;
+  z = has ? (r0.w >> 16) : 0u;
+  meta = usn_key_meta((r0.x >> 8) & 0xFFu, has ? USN_WANT_DPORT : 0u);
+}
+
+/* the decision from get_endpoint's result w (endpoint.rs:256-284) */
+__device__ __forceinline__ uint32_t tx_lookup_dec(const ClassifyArgs &a, uint32_t fl, uint32_t w) {
   const uint32_t owner = w >> 16;
   const bool excl = w && ((w & USN_SLOT_NICOWNER) || owner == a.src);
   if (w && !excl) return usn_mkdec(USN_CLS_EP, USN_R_NONE, owner);
@@ -1341,6 +1474,23 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
     return usn_mkdec(USN_CLS_DROP, USN_R_DHCP_NONE, 0xFFFFu) |
            (a.next_dhcp_set ? (USN_F_DHCP | USN_F_HOST) : 0u);
   return usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
+}
+
+template <bool TAGGED>
+__device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
+                                   const uint4 &r1, uint32_t i, uint32_t ins) {
+  const ClassifyArgs &a = t.a;
+  const uint32_t fl = r0.x;
+  if (!tx_dmac_in(t, fl, r1, i, ins)) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // :254-255
+  uint32_t x, y, z, meta;
+  key1_of(r0, x, y, z, meta);
+  uint32_t w = (a.probe_mask & 1u) ? probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta) : 0u;
+  if (!w && (ins & 2u)) w = tx_learned_key1(t, x, y, z, meta, i);
+  if (!w && (a.probe_mask & 2u)) {
+    key2_of(r0, x, y, z, meta);
+    w = probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta);
+  }
+  return tx_lookup_dec(a, fl, w);
 }
 
 /* tx_decide + tx_fill in one launch: non-hit decisions into LDS, then every
@@ -1365,26 +1515,29 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     T = L.table;
   }
   if (tid < 8) s_misc[tid] = 0;
-  for (uint32_t k = tid; k < NSEG * a.nbins; k += NTHREADS) L.cnt[k] = 0;
+  for (uint32_t k = tid; k < NSEG * cnt_rows(a.nbins); k += NTHREADS) L.cnt[k] = 0;
+  // which device sets hold items: r1 (the MACs) is needed only when a MAC set
+  // does (the dmac test, the first learner's smac)
+  const uint32_t ins = __builtin_amdgcn_readfirstlane(t.counters[2]);
   uint4 r0[ROUNDS], r1[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     const uint64_t i = base + (local < nt ? local : 0);
-    r0[r] = t.rec[2 * i];        // unpredicated (clamped index): the loads overlap
-    r1[r] = t.rec[2 * i + 1];
+    r0[r] = t.rec[i];            // unpredicated (clamped index): the loads overlap
+    r1[r] = make_uint4(0, 0, 0, 0);
+    if (ins & 1u) r1[r] = t.rec[a.n + i];
   }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r)
     if (r * NTHREADS + tid >= nt) { r0[r] = make_uint4(0, 0, 0, 0); r1[r] = make_uint4(0, 0, 0, 0); }
   const uint32_t before = prev_tiles_last(t.aux, tile, 1);   // 1 + index, 0 = none
-  const uint32_t ins = __builtin_amdgcn_readfirstlane(t.counters[2]);   // sets with items
   __syncthreads();
   if (tid == 0) {
     const usn_summary *S = a.summary;
     uint32_t hd = S->cin_dst;
     if (before) {
-      const uint4 h0 = t.rec[2 * (size_t)(before - 1)], h1 = t.rec[2 * (size_t)(before - 1) + 1];
+      const uint4 h0 = t.rec[before - 1], h1 = t.rec[a.n + before - 1];
       hd = decide_tx_ipv4<!LDS>(t, T, h0, h1, before - 1, ins);
     }
     s_head = hd;
@@ -1412,7 +1565,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     } else {
       d = decide_tx_ipv4<!LDS>(t, T, r0[r], r1[r], (uint32_t)i, ins);
     }
-    if (r1[r].w) d |= USN_F_FRAG1;                         // first fragment: remembered (host map)
+    if (fl & TXR_FRAG1) d |= USN_F_FRAG1;                  // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge
     if (touch && !(fl & (TXR_HIT | TXR_HOST)) && (fl & (TXR_LEARNMAC | TXR_LEARNRULE))) {
       bool learned = false;

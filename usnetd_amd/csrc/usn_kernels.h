@@ -65,9 +65,12 @@ struct MultiArgs {
 };
 
 /* ---- tx direction (a non-NIC source sends): four launches ---------------- */
-/* per-frame record (2 x uint4), written by tx_scan:
- *   r0 = {i0 | TXR_* flags, src, dst, ports}
- *   r1 = {smac[0..3], smac[4..5] | dmac[0..1] << 16, dmac[2..5], 0}          */
+/* per-frame record, two planes of n uint4 written by tx_scan:
+ *   rec[i]     r0 = {i0 | TXR_* flags, src, dst, ports}
+ *   rec[n + i] r1 = {smac[0..3], smac[4..5] | dmac[0..1] << 16, dmac[2..5], 0}
+ * r0 is all a frame's decision needs unless this batch learns a MAC (the
+ * dmac test) or the frame is the first to learn one (its smac); in steady
+ * state tx_hits and tx_decide read 16 B per frame, not 32.                   */
 #define TXR_TOUCH_SHIFT 20u    /* 2 bits: 0 none, 1 retains, 2 leaves None, 3 unknown */
 #define TXR_LEARNMAC (1u << 22)  /* unicast smac not in the bridge snapshot */
 #define TXR_LEARNRULE (1u << 23) /* answer key not listened, not in the table snapshot */
@@ -76,11 +79,12 @@ struct MultiArgs {
 #define TXR_DMAC_IN (1u << 26)
 #define TXR_HIT (1u << 27)       /* 1-entry cache hit (set by tx_hits) */
 #define TXR_DHCPANS (1u << 28)
+#define TXR_FRAG1 (1u << 29)     /* first fragment: extract_pkt_info remembers it (host map) */
 #define TXR_I0_MASK 0x1FFFFu
 
 struct TxArgs {
   ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
-  uint4 *rec;                 /* n x 2 */
+  uint4 *rec;                 /* 2 planes of n: r0 at [i], r1 at [n + i] */
   uint32_t *aux;              /* per tile x 4: [0] 1+last touching, [1] 1+last non-hit touching */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
