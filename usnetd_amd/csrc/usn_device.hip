@@ -1708,11 +1708,16 @@ size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_ld
   return lds_core_bytes(nbins, !glds) + (table_in_lds ? table_lds_bytes(table_slots) : 0);
 }
 
-/* glds needs 16-byte aligned sources: every window start of every batch. */
+/* glds needs 16-byte aligned sources: every window start of every batch.
+ * Only dense slots use it: at a 2048-byte stride (c3, netmap-sized slots)
+ * per-lane register loads were 8 % faster (A/B 40.9 vs 44.3 us per 1M frames),
+ * at 64 bytes glds is (c2). */
+#define USN_GLDS_MAX_STRIDE 128u
 static bool glds_layout(const MultiArgs &m) {
   for (uint32_t k = 0; k < m.count; ++k) {
     const ClassifyArgs &b = m.b[k];
-    if (b.offsets != nullptr || b.stride % 16 != 0 || (reinterpret_cast<uintptr_t>(b.frames) & 15))
+    if (b.offsets != nullptr || b.stride % 16 != 0 || b.stride > USN_GLDS_MAX_STRIDE ||
+        (reinterpret_cast<uintptr_t>(b.frames) & 15))
       return false;
   }
   return true;
