@@ -220,21 +220,30 @@ template <bool TAGGED>
 __device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uint32_t bmask,
                                           uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
   if (TAGGED && !USN_ABL_NOTAGS) {
+    // the home bucket's tag line and the next one are loaded together: at
+    // load <= 1/4 a chain rarely passes two buckets, so a wave seldom waits
+    // for a straggler lane's third dependent load
     const uint32_t h = usn_key_hash(x, y, z, meta);
     const uint32_t tg = usn_key_tag(h);
     uint32_t b = h & bmask;
-    for (uint32_t it = 0; it <= bmask; ++it) {
-      const uint4 tv = tags[b];
-      uint32_t mm = (tv.x == tg ? 1u : 0u) | (tv.y == tg ? 2u : 0u) | (tv.z == tg ? 4u : 0u) |
-                    (tv.w == tg ? 8u : 0u);
-      while (mm) {   // verify: two keys of one bucket may share a tag
-        const uint32_t j = (uint32_t)__builtin_ctz(mm);
-        const uint4 sl = T[b * 4 + j];
-        if (slot_is(sl, x, y, z, meta)) return sl.w;
-        mm &= mm - 1;
+    for (uint32_t it = 0; it <= bmask; it += 2) {
+      const uint32_t b2 = (b + 1) & bmask;
+      const uint4 tv = tags[b], tv2 = tags[b2];
+#pragma unroll
+      for (uint32_t half = 0; half < 2; ++half) {
+        const uint4 &t4 = half ? tv2 : tv;
+        const uint32_t bb = half ? b2 : b;
+        uint32_t mm = (t4.x == tg ? 1u : 0u) | (t4.y == tg ? 2u : 0u) | (t4.z == tg ? 4u : 0u) |
+                      (t4.w == tg ? 8u : 0u);
+        while (mm) {   // verify: two keys of one bucket may share a tag
+          const uint32_t j = (uint32_t)__builtin_ctz(mm);
+          const uint4 sl = T[bb * 4 + j];
+          if (slot_is(sl, x, y, z, meta)) return sl.w;
+          mm &= mm - 1;
+        }
+        if (t4.w == 0u) return 0u;   // bucket not full: the key would be in it
       }
-      if (tv.w == 0u) return 0u;   // bucket not full: the key would be in it
-      b = (b + 1) & bmask;
+      b = (b2 + 1) & bmask;
     }
     return 0u;
   }

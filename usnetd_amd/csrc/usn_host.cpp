@@ -196,6 +196,8 @@ struct usn_ctx {
 
 namespace {
 
+#define USN_LDS_RULES_MAX 1024u   /* 2048 slots = 32 KiB: the LDS table's limit */
+
 uint32_t next_pow2(uint32_t v) {
   uint32_t p = 1;
   while (p < v) p <<= 1;
@@ -234,18 +236,31 @@ void img_put(usn_ctx *c, const WantKey &k, uint16_t owner) {
   }
 }
 
+/* Buckets of the table image for n rules.  Up to 1024 rules (2048 slots:
+ * the table is staged into LDS) the load is <= 1/2.  Larger tables are probed
+ * in global memory, where a wave waits for its slowest lane's chain: there the
+ * load is <= 1/4, and a probe reads its home bucket's tag line and the next
+ * one together, so a chain past two buckets is rare. */
+uint32_t image_buckets(uint64_t n) {
+  if (n <= USN_LDS_RULES_MAX) return next_pow2(std::max<uint32_t>(2, (uint32_t)((2 * n + 3) / 4)));
+  return next_pow2((uint32_t)n);
+}
+bool image_has_room(const usn_ctx *c, uint64_t n) {
+  return (uint64_t)image_buckets(n) * 4 <= c->img.size();
+}
+
 /* registry insert; keeps the host image current when it can */
 void rule_insert(usn_ctx *c, const WantKey &k, Rule r) {
   c->rules[k] = r;
   c->table_dirty = true;
-  if (c->img_valid && 2 * c->rules.size() <= c->img.size()) img_put(c, k, r.owner);
+  if (c->img_valid && image_has_room(c, c->rules.size())) img_put(c, k, r.owner);
   else c->img_valid = false;
 }
 
 int rebuild_table(usn_ctx *c) {
   if (!c->img_valid) {
     const uint32_t n = (uint32_t)c->rules.size();
-    const uint32_t nb = next_pow2(std::max<uint32_t>(2, (2 * n + 3) / 4));   // load <= 50 %
+    const uint32_t nb = image_buckets(n);
     c->img.assign((size_t)nb * 4, make_uint4(0, 0, 0, 0));
     c->img_tags.assign((size_t)nb * 4, 0u);
     c->img_pmask = 0;
