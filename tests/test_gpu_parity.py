@@ -63,10 +63,15 @@ def _oracle_lists(d, n_ep):
     return out
 
 
-@pytest.mark.parametrize("name,n", [("c1", 50000), ("c2", 1 << 20), ("c3", 1 << 17),
-                                    ("c4", 1 << 18), ("c5", 1 << 20)])
-def test_config_parity(name, n, coracle_mod):
+@pytest.mark.parametrize("name,n,t512", [
+    ("c1", 50000, None), ("c2", 1 << 20, None), ("c3", 1 << 17, None), ("c4", 1 << 18, None),
+    ("c5", 1 << 20, None),
+    # ragged last tiles; c5's 1005 bins take the radix order in both builds
+    ("c3", 5003, None), ("c4", 70001, None), ("c5", 100003, "0"), ("c5", 100003, "1")])
+def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     from usnetd_amd import lib, traffic
+    if t512 is not None:   # USN_T512 (read at context creation): force one build
+        monkeypatch.setenv("USN_T512", t512)
     cfg = traffic.config(name, n=n)
     o = coracle_mod.Oracle()
     coracle_mod.install_oracle(o, cfg)
