@@ -57,7 +57,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
       rm -rf gpurun_out/pmcf gpurun_out/pmcw
       step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf -o run -- python3 bench.py --steps 64 --warmup 8 --no-cpu-baseline --launch-probe 0
       step pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw -o run -- python3 bench.py --steps 64 --warmup 8 --no-cpu-baseline --launch-probe 0
-      step pmctraffic 60 python3 tools/pmc_traffic.py gpurun_out/pmcf gpurun_out/pmcw ${PMC_FRAMES:-4194304} gpurun_out/pmc_c2.json ;;
+      step pmctraffic 60 python3 tools/pmc_traffic.py gpurun_out/pmcf gpurun_out/pmcw ${PMC_FRAMES:-8388608} gpurun_out/pmc_c2.json ;;
   esac
 done
 echo "=== done"
