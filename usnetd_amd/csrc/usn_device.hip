@@ -1257,6 +1257,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
   if (tid == 0) s_last = 0;
   __syncthreads();
   if (tile == 0) {   // carried-in cache of this source, for tx_hits / tx_fill
+    if (tid < 4) t.counters[tid] = 0;   // learned count, flags, sets used: read from tx_hits on
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
       usn_summary *S = a.summary;

@@ -1095,8 +1095,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_mask = c->bridge_mask;
     t.listen = c->tx.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
-    HIPCHK(hipMemsetAsync(c->tx.counters, 0, 4 * sizeof(uint32_t), (hipStream_t)stream));
-    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));
+    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tx_scan zeroes t.counters
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
     c->tx.decisions = r[0].decisions;
