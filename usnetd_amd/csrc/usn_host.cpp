@@ -304,6 +304,11 @@ struct usn_ctx {
     int src = -1;
     const uint32_t *decisions = nullptr;
   } tx;
+  /* pinned staging for usn_finalize's small reads (summary, tile headers,
+   * tx counters): async copies and one stream sync instead of three
+   * synchronous pageable copies */
+  uint8_t *h_stage = nullptr;
+  size_t h_stage_cap = 0;
 };
 
 namespace {
@@ -701,6 +706,7 @@ void usn_ctx_destroy(usn_ctx *c) {
                   (void *)c->tx.ruleset, (void *)c->tx.learned, (void *)c->tx.counters,
                   (void *)c->tx.listen})
     if (p) (void)hipFree(p);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   delete c;
 }
 
@@ -1169,6 +1175,33 @@ bool retains(uint32_t d) {
 
 /* the per-tile host lists of a result, merged in frame order: one copy per
  * listed tile, or one bulk copy of the whole area when many tiles list frames */
+/* summary + tile headers (+ the tx counters when cnt) of a classified batch,
+ * through the context's pinned staging buffer on stream s */
+int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
+                      usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt) {
+  const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
+  const size_t need = sizeof(usn_summary) + tb + 16;
+  if (need > c->h_stage_cap) {
+    if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    const size_t cap = std::max<size_t>(need, 64 * 1024);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), cap, hipHostMallocDefault));
+    c->h_stage_cap = cap;
+  }
+  uint8_t *p = c->h_stage;
+  HIPCHK(hipMemcpyAsync(p, r->summary, sizeof(usn_summary), hipMemcpyDeviceToHost, s));
+  if (tb) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary), r->tiles, tb, hipMemcpyDeviceToHost, s));
+  if (cnt)
+    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, c->tx.counters, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(&sum, p, sizeof sum);
+  th.resize(ntiles);
+  if (tb) std::memcpy(th.data(), p + sizeof(usn_summary), tb);
+  if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, 16);
+  return USN_OK;
+}
+
 int fetch_host_lists(const usn_result *r, const std::vector<usn_tile_hdr> &th,
                      std::vector<uint32_t> &hosts) {
   const uint32_t ntiles = (uint32_t)th.size();
@@ -1215,11 +1248,12 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   const int src = b->src_endpoint;
   Ep &S = c->eps[src];
   usn_summary sum;
-  HIPCHK(hipMemcpy(&sum, r->summary, sizeof sum, hipMemcpyDeviceToHost));
-  std::vector<usn_tile_hdr> th(ntiles);
-  HIPCHK(hipMemcpy(th.data(), r->tiles, ntiles * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+  std::vector<usn_tile_hdr> th;
   uint32_t cnt[4];
-  HIPCHK(hipMemcpy(cnt, c->tx.counters, sizeof cnt, hipMemcpyDeviceToHost));
+  {
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt);
+    if (e) return e;
+  }
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
   fi.flags = sum.flags;
@@ -1410,9 +1444,11 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   }
   const uint32_t ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
   usn_summary sum;
-  HIPCHK(hipMemcpy(&sum, r->summary, sizeof sum, hipMemcpyDeviceToHost));
-  std::vector<usn_tile_hdr> th(ntiles);
-  HIPCHK(hipMemcpy(th.data(), r->tiles, ntiles * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+  std::vector<usn_tile_hdr> th;
+  {
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr);
+    if (e) return e;
+  }
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
   fi.flags = sum.flags;
