@@ -1101,11 +1101,18 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
  * =========================================================================== */
 
 __device__ __forceinline__ uint32_t tx_touch(const uint4 &r0) { return (r0.x >> TXR_TOUCH_SHIFT) & 3u; }
+/* r1 = the frame's first 16 bytes (dmac, smac, ethertype), re-read from the
+ * batch where a later pass needs the MACs: rarer than writing a MAC record
+ * for every frame in tx_scan */
+__device__ __forceinline__ uint4 frame_head(const ClassifyArgs &a, uint64_t i) {
+  const uint8_t *fp = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
+  return *reinterpret_cast<const uint4 *>(fp);
+}
 __device__ __forceinline__ uint64_t rec_smac(const uint4 &r1) {
-  return (uint64_t)r1.x | ((uint64_t)(r1.y & 0xFFFFu) << 32);
+  return (uint64_t)(r1.y >> 16) | ((uint64_t)r1.z << 16);
 }
 __device__ __forceinline__ uint64_t rec_dmac(const uint4 &r1) {
-  return (uint64_t)(r1.y >> 16) | ((uint64_t)r1.z << 16);
+  return (uint64_t)r1.x | ((uint64_t)(r1.y & 0xFFFFu) << 32);
 }
 
 __device__ __forceinline__ bool bridge_has(const unsigned long long *set, uint32_t mask, uint64_t mac) {
@@ -1337,8 +1344,6 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
     r0.x = (r0.x & TXR_I0_MASK) | f;
     const uint64_t i = base + local;
     t.rec[i] = r0;
-    t.rec[a.n + i] = make_uint4((uint32_t)smac, (uint32_t)(smac >> 32) | ((uint32_t)dmac << 16),
-                                (uint32_t)(dmac >> 16), 0u);
     if (touch) last = local + 1;
   }
   if (last) atomicMax(&s_last, last);
@@ -1405,7 +1410,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
     if (hit || (fl & TXR_HOST)) continue;
     // this frame really learns: first occurrence per item
     if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
-      const uint4 r1 = t.rec[a.n + i];
+      const uint4 r1 = frame_head(a, i);
       if (fl & TXR_LEARNMAC) {
         const uint64_t m = rec_smac(r1);
         unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
@@ -1536,7 +1541,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     const uint64_t i = base + (local < nt ? local : 0);
     r0[r] = t.rec[i];            // unpredicated (clamped index): the loads overlap
     r1[r] = make_uint4(0, 0, 0, 0);
-    if (ins & 1u) r1[r] = t.rec[a.n + i];
+    if (ins & 1u) r1[r] = frame_head(a, i);
   }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r)
@@ -1547,7 +1552,8 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     const usn_summary *S = a.summary;
     uint32_t hd = S->cin_dst;
     if (before) {
-      const uint4 h0 = t.rec[before - 1], h1 = t.rec[a.n + before - 1];
+      const uint4 h0 = t.rec[before - 1];
+      const uint4 h1 = (ins & 1u) ? frame_head(a, before - 1) : make_uint4(0, 0, 0, 0);
       hd = decide_tx_ipv4<!LDS>(t, T, h0, h1, before - 1, ins);
     }
     s_head = hd;

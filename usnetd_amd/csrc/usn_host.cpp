@@ -990,7 +990,7 @@ static int tx_prepare(usn_ctx *c, uint64_t n, uint32_t ntiles) {
     if (T.rec) HIPCHK(hipFree(T.rec));
     if (T.learned) HIPCHK(hipFree(T.learned));
     T.rec = nullptr; T.learned = nullptr;
-    HIPCHK(hipMalloc(&T.rec, n * 2 * sizeof(uint4)));
+    HIPCHK(hipMalloc(&T.rec, n * sizeof(uint4)));
     HIPCHK(hipMalloc(&T.learned, n * 4 * sizeof(uint4)));   // <= 2 items of 2 x uint4 per frame
     T.rec_frames = n;
     T.learned_cap = (uint32_t)(2 * n);

@@ -84,7 +84,7 @@ struct MultiArgs {
 
 struct TxArgs {
   ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
-  uint4 *rec;                 /* 2 planes of n: r0 at [i], r1 at [n + i] */
+  uint4 *rec;                 /* n records r0 (the MACs are re-read from the frames) */
   uint32_t *aux;              /* per tile x 4: [0] 1+last touching, [1] 1+last non-hit touching */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
