@@ -358,9 +358,12 @@ void img_put(usn_ctx *c, const WantKey &k, uint16_t owner) {
  * in global memory, where a wave waits for its slowest lane's chain: there the
  * load is <= 1/4, and a probe reads its home bucket's tag line and the next
  * one together, so a chain past two buckets is rare. */
+#ifndef USN_GLOBAL_BUCKET_SHIFT
+#define USN_GLOBAL_BUCKET_SHIFT 0   /* A/B knob: global tables get n >> shift buckets */
+#endif
 uint32_t image_buckets(uint64_t n) {
   if (n <= USN_LDS_RULES_MAX) return next_pow2(std::max<uint32_t>(2, (uint32_t)((2 * n + 3) / 4)));
-  return next_pow2((uint32_t)n);
+  return next_pow2(std::max<uint32_t>(512, (uint32_t)(n >> USN_GLOBAL_BUCKET_SHIFT)));
 }
 bool image_has_room(const usn_ctx *c, uint64_t n) {
   return (uint64_t)image_buckets(n) * 4 <= c->img.size();
