@@ -1365,6 +1365,10 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
   uint4 *srec = L.table;   // the tile's first record words, for the previous-frame compares
   uint4 r0[ROUNDS];
   uint32_t v[ROUNDS], prev[ROUNDS];
+  // last touching frame of the earlier tiles, and its record: independent of
+  // this tile's records, so their loads overlap the tile's
+  const uint32_t before = prev_tiles_last(t.aux, tile, 0);   // 1 + index, 0 = none
+  const uint4 brec = t.rec[before ? before - 1 : 0];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
@@ -1379,7 +1383,6 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
   }
   tile_prefix_max(v, L, prev);   // its barriers also publish srec
   const usn_summary *S = a.summary;
-  const uint32_t before = prev_tiles_last(t.aux, tile, 0);   // last touching frame of earlier tiles
   uint32_t last_nh = 0;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -1394,7 +1397,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
       const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
       const uint32_t info0 = fl & TXR_I0_MASK;
       if (k1) {
-        const uint4 pr = prev[r] ? srec[prev[r] - 1] : t.rec[k1 - 1];
+        const uint4 pr = prev[r] ? srec[prev[r] - 1] : brec;
         const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == r0[r].y &&
                           pr.z == r0[r].z && pr.w == r0[r].w;
         if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
