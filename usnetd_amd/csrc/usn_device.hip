@@ -84,6 +84,9 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
 #define USN_ABL_NOTAGS 0
 #endif
+#ifndef USN_ABL_NOHEAD   /* A/B only: tx_decide without the run-head recompute (wrong results) */
+#define USN_ABL_NOHEAD 0
+#endif
 
 #ifndef USN_LOAD_NT
 #define USN_LOAD_NT 0
@@ -1554,7 +1557,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
   if (tid == 0) {
     const usn_summary *S = a.summary;
     uint32_t hd = S->cin_dst;
-    if (before) {
+    if (before && !USN_ABL_NOHEAD) {   // (A/B only: NOHEAD measures the recompute)
       const uint4 h0 = t.rec[before - 1];
       const uint4 h1 = (ins & 1u) ? frame_head(a, before - 1) : make_uint4(0, 0, 0, 0);
       hd = decide_tx_ipv4<!LDS>(t, T, h0, h1, before - 1, ins);
