@@ -84,6 +84,9 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
 #define USN_ABL_NOTAGS 0
 #endif
+#ifndef USN_ABL_TXNOPROBE   /* A/B only: tx kernels without rule-table probes (wrong results) */
+#define USN_ABL_TXNOPROBE 0
+#endif
 #ifndef USN_ABL_NOHEAD   /* A/B only: tx_decide without the run-head recompute (wrong results) */
 #define USN_ABL_NOHEAD 0
 #endif
@@ -1337,7 +1340,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       if (!listening && !dhcp_req) {   // the answer key is learned unless the table has it
         uint32_t x, y, z, meta;
         want_key(make_uint4(p.i0, p.src, p.dst, p.ports), x, y, z, meta);
-        if (!probe<!LDS>(T, a.tags, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
+        if (!USN_ABL_TXNOPROBE && !probe<!LDS>(T, a.tags, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
@@ -1505,6 +1508,7 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   if (!tx_dmac_in(t, fl, r1, i, ins)) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // :254-255
   uint32_t x, y, z, meta;
   key1_of(r0, x, y, z, meta);
+  if (USN_ABL_TXNOPROBE) return usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);
   uint32_t w = (a.probe_mask & 1u) ? probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta) : 0u;
   if (!w && (ins & 2u)) w = tx_learned_key1(t, x, y, z, meta, i);
   if (!w && (a.probe_mask & 2u)) {
