@@ -309,6 +309,8 @@ struct usn_ctx {
    * synchronous pageable copies */
   uint8_t *h_stage = nullptr;
   size_t h_stage_cap = 0;
+  uint32_t *h_lists = nullptr;   // pinned: the host lists of a batch with many listed tiles
+  size_t h_lists_cap = 0;
 };
 
 namespace {
@@ -710,6 +712,7 @@ void usn_ctx_destroy(usn_ctx *c) {
                   (void *)c->tx.listen})
     if (p) (void)hipFree(p);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_lists) (void)hipHostFree(c->h_lists);
   delete c;
 }
 
@@ -1205,8 +1208,8 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   return USN_OK;
 }
 
-int fetch_host_lists(const usn_result *r, const std::vector<usn_tile_hdr> &th,
-                     std::vector<uint32_t> &hosts) {
+int fetch_host_lists(usn_ctx *c, const usn_result *r, const std::vector<usn_tile_hdr> &th,
+                     std::vector<uint32_t> &hosts, hipStream_t s) {
   const uint32_t ntiles = (uint32_t)th.size();
   uint32_t listed = 0;
   size_t total = 0;
@@ -1216,12 +1219,20 @@ int fetch_host_lists(const usn_result *r, const std::vector<usn_tile_hdr> &th,
   }
   hosts.clear();
   hosts.reserve(total);
-  if (listed > 32) {
-    std::vector<uint32_t> all((size_t)ntiles * USN_TILE);
-    HIPCHK(hipMemcpy(all.data(), r->host_list, all.size() * 4, hipMemcpyDeviceToHost));
+  if (listed > 32) {   // every tile's list area in one copy, through pinned memory
+    const size_t bytes = (size_t)ntiles * USN_TILE * 4;
+    if (bytes > c->h_lists_cap) {
+      if (c->h_lists) HIPCHK(hipHostFree(c->h_lists));
+      c->h_lists = nullptr;
+      c->h_lists_cap = 0;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_lists), bytes, hipHostMallocDefault));
+      c->h_lists_cap = bytes;
+    }
+    HIPCHK(hipMemcpyAsync(c->h_lists, r->host_list, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint32_t *all = c->h_lists;
     for (uint32_t t = 0; t < ntiles; ++t)
-      hosts.insert(hosts.end(), all.begin() + (size_t)t * USN_TILE,
-                   all.begin() + (size_t)t * USN_TILE + th[t].n_host);
+      hosts.insert(hosts.end(), all + (size_t)t * USN_TILE, all + (size_t)t * USN_TILE + th[t].n_host);
   } else {
     for (uint32_t t = 0; t < ntiles; ++t) {
       if (!th[t].n_host) continue;
@@ -1231,7 +1242,36 @@ int fetch_host_lists(const usn_result *r, const std::vector<usn_tile_hdr> &th,
                        th[t].n_host * 4, hipMemcpyDeviceToHost));
     }
   }
-  std::sort(hosts.begin(), hosts.end());
+  /* frame order: a tile lists only its own frames (in atomic order), so the
+   * tiles' segments are already in order and each is ordered by itself, by a
+   * 1024-bit map when it is long.  Anything else falls back to a full sort. */
+  size_t at = 0;
+  bool full_sort = false;
+  for (uint32_t t = 0; t < ntiles && !full_sort; ++t) {
+    const uint32_t m = th[t].n_host;
+    if (!m) continue;
+    uint32_t *seg = hosts.data() + at;
+    at += m;
+    const uint64_t lo = (uint64_t)t * USN_TILE;
+    uint64_t bits[USN_TILE / 64] = {0};
+    uint32_t pop = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint64_t o = (uint64_t)seg[k] - lo;
+      if (seg[k] < lo || o >= USN_TILE) { full_sort = true; break; }
+      pop += (bits[o >> 6] >> (o & 63) & 1) ? 0u : 1u;
+      bits[o >> 6] |= 1ull << (o & 63);
+    }
+    if (full_sort) break;
+    if (m < 64 || pop != m) {   // short, or a frame listed twice (not expected)
+      std::sort(seg, seg + m);
+      continue;
+    }
+    uint32_t k = 0;
+    for (uint32_t w = 0; w < USN_TILE / 64; ++w)
+      for (uint64_t bb = bits[w]; bb; bb &= bb - 1)
+        seg[k++] = (uint32_t)(lo + w * 64 + (uint32_t)__builtin_ctzll(bb));
+  }
+  if (full_sort) std::sort(hosts.begin(), hosts.end());
   return USN_OK;
 }
 
@@ -1257,13 +1297,14 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt);
     if (e) return e;
   }
+  clk.mark("state");
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
   fi.flags = sum.flags;
   for (uint32_t t = 0; t < ntiles; ++t)
     for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
   std::vector<uint32_t> hosts;
-  int st = fetch_host_lists(r, th, hosts);
+  int st = fetch_host_lists(c, r, th, hosts, s);
   if (st) return st;
   clk.mark("summary");
   if (hosts.empty() && cnt[0] == 0 && cnt[1] == 0) {   // nothing learned, nothing ordered
@@ -1459,7 +1500,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
   std::vector<uint32_t> hosts;
   {
-    const int e = fetch_host_lists(r, th, hosts);
+    const int e = fetch_host_lists(c, r, th, hosts, s);
     if (e) return e;
   }
   const bool stale_walk = (sum.flags & USN_S_STALE) && sum.first_break < b->n;
