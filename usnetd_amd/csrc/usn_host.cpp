@@ -311,6 +311,8 @@ struct usn_ctx {
   size_t h_stage_cap = 0;
   uint32_t *h_lists = nullptr;   // pinned: the host lists of a batch with many listed tiles
   size_t h_lists_cap = 0;
+  uint4 *h_items = nullptr;      // pinned: a tx batch's learned list
+  size_t h_items_cap = 0;
 };
 
 namespace {
@@ -713,6 +715,7 @@ void usn_ctx_destroy(usn_ctx *c) {
     if (p) (void)hipFree(p);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
+  if (c->h_items) (void)hipHostFree(c->h_items);
   delete c;
 }
 
@@ -1322,9 +1325,21 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       if (hv.dec[j] & USN_F_HOST) { h = j; break; }
   /* learned items and first fragments before h, in frame order */
   const uint32_t nl = std::min(cnt[0], c->tx.learned_cap);
-  std::vector<uint4> items((size_t)nl * 2);
-  if (nl) HIPCHK(hipMemcpy(items.data(), c->tx.learned, items.size() * sizeof(uint4),
-                           hipMemcpyDeviceToHost));
+  const uint4 *items = nullptr;   // the learned list, through pinned memory
+  if (nl) {
+    const size_t bytes = (size_t)nl * 2 * sizeof(uint4);
+    if (bytes > c->h_items_cap) {
+      if (c->h_items) HIPCHK(hipHostFree(c->h_items));
+      c->h_items = nullptr;
+      c->h_items_cap = 0;
+      const size_t cap = bytes + bytes / 2;   // counts vary per batch: no re-pin every time
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_items), cap, hipHostMallocDefault));
+      c->h_items_cap = cap;
+    }
+    HIPCHK(hipMemcpyAsync(c->h_items, c->tx.learned, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    items = c->h_items;
+  }
   clk.mark("items");
   struct Ev { uint64_t idx; uint32_t kind; uint4 key; };   // kind 0 mac, 1 rule, 2 frag1
   std::vector<Ev> evs;
