@@ -2,14 +2,27 @@
 """bench.py -- device-resident usnetd match-path throughput on MI355X.
 
 Metric (BASELINE.json): Mpkts/s of device-resident L4 classification of 64 B
-frames, and the achieved HBM GB/s of the classify kernel against the gfx950
-peak.  One step = one usn_classify pass over one batch of the configuration
-the metric is quoted on (BASELINE.json configs[1] = "c2": 1M x 64 B IPv4/UDP
-frames, 16-rule endpoint table), frames already resident in HBM.  Batches
-rotate over --batches distinct buffers (> 256 MiB in total) so the Infinity
-Cache cannot serve them.  Multi-GPU: one process per GPU, each classifying its
-own batches with a replicated rule table ("replicas only", weak scaling; no
-collective on the data path -- gloo carries only the timing barrier/max).
+frames, and the classify kernel's achieved HBM GB/s against the gfx950 peak.
+
+Workload: BASELINE.json configs[4] ("c5"), the configuration the north star
+reports at 1, 2, 4 and 8 GPUs: 64 B IPv4 TCP/UDP frames, a 65 536-rule table
+(16 IPs x 2048 listening ports + 32 768 connected 5-tuples, L2/MALL-resident),
+1 000 endpoints, 8M frames per drained rx ring.  Frames are resident in HBM
+when the timed region starts.  At N=1 the line also carries configs[1] ("c2":
+1M x 64 B frames, 16 rules) under the key "c2", measured the same way.
+
+One step = one poll round: every rx queue the rank owns is drained once (one
+batch per queue, the reference's Endpoint::forward drain of each readable
+ring, /root/reference/src/main.rs:1029-1046), classified on the device with
+usn_classify_multi (up to 8 rings per launch, 2 HIP streams).  c5: 2 queues of
+8M frames per rank = 16M frames per step; c2: 16 queues of 1M.
+
+Multi-GPU: one process per GPU (torchrun), "replicas only": each rank owns a
+disjoint block of the node's rx queues (usnetd_amd.shard.rank_queues) and a
+replica of the rule table; no collective on the data path (gloo carries the
+barrier and the max-over-ranks time).  --strong fixes the whole job's frames
+per step at 64M (c5) and splits the queues over the ranks; the default is
+weak scaling (fixed queues per rank).
 
 Usage: python bench.py [--gpus N --steps K --warmup W] (torchrun for N > 1)
 """
@@ -29,25 +42,244 @@ sys.path.insert(0, ROOT)
 
 ALGO_BYTES = 64 + 2 + 4 + 2   # header window + length + decision + order index per frame
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+LAUNCH_FRAMES = 1 << 23       # frames per launch the rings are grouped to (8 x 1M, or 1 x 8M)
+ROTATE_BYTES = 1 << 30        # distinct batch bytes per rank, > the 256 MiB Infinity Cache
+STRONG_FRAMES = 1 << 26       # --strong: 64M frames per step for the whole job
+METRIC = "Mpkts/s device-resident L4 classify @64B frames; HBM GB/s vs roofline"
+DEFAULT_FRAMES = {"c1": 1 << 20, "c1fixed": 1 << 20, "c2": 1 << 20, "c3": 1 << 18, "c4": 1 << 20,
+                  "c5": 1 << 23}
 
 
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c5")
     ap.add_argument("--frames", type=int, default=0, help="frames per batch (default: config's)")
-    ap.add_argument("--batches", type=int, default=5, help="distinct rotating batches")
+    ap.add_argument("--queues", type=int, default=0,
+                    help="rx queues per rank (default: 8 rings' worth of launches on 2 streams)")
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: 64M frames per step for the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--launch-probe", type=int, default=100, help="per-launch event pairs")
-    ap.add_argument("--queues", type=int, default=16,
-                    help="NIC rx queues (sources) drained per poll round")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams; stream s owns queues [s*Q/S, (s+1)*Q/S) and classifies "
-                         "their drained rings with one usn_classify_multi launch per round")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c2 line at N=1")
+    ap.add_argument("--launch-probe", type=int, default=60, help="per-launch event pairs")
     return ap.parse_args()
+
+
+class Run:
+    """The rank's rx queues of one config, resident in HBM, and the launches
+    of one poll round."""
+
+    def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong):
+        from usnetd_amd import shard, traffic
+        self.L, self.ctx, self.name, self.n = L, ctx, name, n
+        S = max(1, streams)
+        P = max(1, min(8, LAUNCH_FRAMES // n))           # rings per launch
+        if strong:
+            total_q = max(world, STRONG_FRAMES // n)
+            mine = shard.rank_queues(total_q, world, rank)
+        else:
+            q = queues or P * S
+            total_q = q * world
+            mine = shard.rank_queues(total_q, world, rank)
+        self.queues = mine                                # global queue ids of this rank
+        Q = len(mine)
+        S = min(S, Q)
+        P = min(P, -(-Q // S))
+        self.P, self.S, self.Q = P, S, Q
+        # launches of one poll round: stream s takes queues s, s+S, ... in groups of P
+        per_stream = [list(range(s, Q, S)) for s in range(S)]
+        self.launches = []                                # (stream index, [local queue])
+        for s in range(S):
+            qs = per_stream[s]
+            for k in range(0, len(qs), P):
+                self.launches.append((s, qs[k:k + P]))
+        # rotation: R rounds of distinct batches per queue (> 256 MiB in all)
+        cfg0 = None
+        self.batches, self.results = [], []
+        frame_bytes = None
+        R = 1
+        for rnd in range(64):
+            if rnd >= R:
+                break
+            for j, gq in enumerate(mine):
+                cfg = traffic.config(name, n=n, seed=shard.queue_seed(gq, rnd))
+                if cfg0 is None:
+                    cfg0 = cfg
+                    traffic.install_ctx(ctx, cfg)
+                    self.nics = [cfg.src] + traffic.extra_nics(cfg, Q - 1, ctx)
+                    frame_bytes = n * cfg.stride
+                    R = max(1, -(-ROTATE_BYTES // (frame_bytes * Q)))
+                self.batches.append(_batch(ctx, cfg, self.nics[j]))
+                self.results.append(_result(ctx, n))
+                del cfg
+        self.R = R
+        self.cfg0 = cfg0
+        self.rotating_bytes = int(R * Q * (frame_bytes + 2 * n))
+        self.streams = [ctx.stream() for _ in range(S)]
+        self.joins = [ctx.event() for _ in range(S)]
+        self.ev0, self.ev1 = ctx.event(), ctx.event()
+        self.groups = []                                  # per round, per launch: (stream, ptrs)
+        for rnd in range(R):
+            gl = []
+            for s, qs in self.launches:
+                ks = [rnd * Q + j for j in qs]
+                ba = (_lib().Batch * len(ks))(*[self.batches[k].desc for k in ks])
+                ra = (_lib().Result * len(ks))(*[self.results[k].desc for k in ks])
+                gl.append((s, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(ks), ba, ra))
+            self.groups.append(gl)
+        self.h = ctx.h
+
+    def frames_per_step(self):
+        return self.Q * self.n
+
+    def step(self, i, stream_override=None):
+        multi = self.L.usn_classify_multi
+        for s, ba, ra, cnt, _, _ in self.groups[i % self.R]:
+            st = self.streams[s] if stream_override is None else stream_override
+            rc = multi(self.h, ba, ra, cnt, st)
+            if rc:
+                _lib().check(rc, "usn_classify_multi")
+
+    def timed(self, steps, dist):
+        ctx = self.ctx
+        for x in self.streams:
+            ctx.sync(x)
+        if dist:
+            dist.barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        main = self.streams[0]
+        ctx.record(self.ev0, main)
+        for x in self.streams[1:]:
+            ctx.wait_event(x, self.ev0)
+        for i in range(steps):
+            self.step(i)
+        for x, ej in zip(self.streams[1:], self.joins[1:]):
+            ctx.record(ej, x)
+            ctx.wait_event(main, ej)
+        ctx.record(self.ev1, main)
+        ctx.sync(main)
+        ctx.sync()
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        return t1 - t0, ctx.elapsed_ms(self.ev0, self.ev1)
+
+    def launch_probe(self, count):
+        """Median duration of one launch (HIP events on the stream it runs on):
+        the first launch group of the round, back to back on one stream, so no
+        launch shares the GPU with another and none starts from an idle GPU."""
+        ctx = self.ctx
+        st = self.streams[0]
+        evs = [(ctx.event(), ctx.event()) for _ in range(count)]
+        for x in self.streams:
+            ctx.sync(x)
+        for i, (ea, eb) in enumerate(evs):
+            _, ba, ra, cnt, _, _ = self.groups[i % self.R][0]
+            ctx.record(ea, st)
+            rc = self.L.usn_classify_multi(self.h, ba, ra, cnt, st)
+            if rc:
+                _lib().check(rc, "usn_classify_multi")
+            ctx.record(eb, st)
+        ctx.sync(st)
+        ms = [ctx.elapsed_ms(a, b) for a, b in evs]
+        frames = self.groups[0][0][3] * self.n
+        return float(np.median(ms)), frames
+
+    def finalize_all(self):
+        """usn_finalize of every batch of the last rotation: the ordered host
+        stage has nothing to do on these configs (no fragments, DHCP, stale
+        caches); counted and reported."""
+        host_frames, flags, cls = 0, 0, [0, 0, 0, 0]
+        for x in self.streams:
+            self.ctx.sync(x)
+        for k in range(len(self.batches)):
+            info = self.ctx.finalize(self.batches[k], self.results[k], self.streams[0])
+            host_frames += info.n_host
+            flags |= info.flags
+            cls = [x + y for x, y in zip(cls, info.class_count)]
+        return host_frames, flags, cls
+
+    def free(self):
+        for b in self.batches:
+            b.free()
+        for r in self.results:
+            r.free()
+
+
+def _lib():
+    from usnetd_amd import lib
+    return lib
+
+
+def _batch(ctx, cfg, src):
+    return _lib().DeviceBatch(ctx, cfg.frames, cfg.lens, src, stride=cfg.stride)
+
+
+def _result(ctx, n):
+    return _lib().DeviceResult(ctx, n)
+
+
+def measure(run, args, dist, world):
+    from usnetd_amd import shard
+    for i in range(args.warmup):
+        run.step(i)
+    wall, ev_ms = run.timed(args.steps, dist)
+    elapsed = shard.max_over_ranks(wall, dist)
+    kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
+    host_frames, flags, cls = run.finalize_all()
+    frames = world * args.steps * run.frames_per_step()
+    achieved = ALGO_BYTES * probe_frames / (kern_ms * 1e-3) / 1e9 if kern_ms else None
+    roof = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": None,
+        "kernel": "classify_rx_kernel",
+        "kernel_us_median": round(kern_ms * 1e3, 3) if kern_ms else None,
+        "frames_per_launch": probe_frames,
+        "algo_bytes_per_frame": ALGO_BYTES,
+        "achieved_basis": "algorithmic bytes of one launch / its median duration (HIP events on "
+                          "its stream, launches serialised on one stream)",
+        # the timed region (launches overlapping on the streams): per GPU,
+        # algorithmic bytes of all its frames / the timed region's wall time
+        "achieved_steady_state": round(ALGO_BYTES * args.steps * run.frames_per_step() / elapsed
+                                       / 1e9, 1),
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % run.name)
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                pm = json.load(fh)
+            if int(pm.get("frames_per_launch", -1)) == probe_frames:
+                roof["traffic"] = pm.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(pmc, ROOT)
+        except (OSError, ValueError):
+            pass
+    return {
+        "value": round(frames / elapsed / 1e6, 2),
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "event_ms_per_step": round(ev_ms / args.steps, 5),
+        "frames_per_step_per_gpu": run.frames_per_step(),
+        "host_stage_frames": int(host_frames),
+        "summary_flags": int(flags),
+        "class_count_last_rotation": [int(x) for x in cls],
+        "roofline": roof,
+    }
+
+
+def workload(run, strong):
+    cfg = run.cfg0
+    return ("%s: %d x %dB frames per drained rx ring, %d-rule endpoint table, %d endpoints, NIC rx; "
+            "step = one poll round of %d rx queues per GPU (%d rings per launch, %d streams)%s"
+            % (run.name, run.n, int(cfg.lens[0]), len(cfg.rules), len(cfg.endpoints), run.Q, run.P,
+               run.S, "; strong scaling: 64M frames per step in all" if strong else ""))
 
 
 def main():
@@ -55,217 +287,71 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    from usnetd_amd import lib, shard, traffic
+    from usnetd_amd import lib
     L = lib.load()            # the HIP runtime is loaded here, before torch (if any)
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist_mod
         dist_mod.init_process_group("gloo")
         dist = dist_mod
-
-    defaults = {"c2": 1 << 20, "c5": 1 << 23, "c3": 1 << 18, "c4": 1 << 20, "c1": 1 << 20,
-                "c1fixed": 1 << 20}
-    n = args.frames or defaults[args.config]
-    S = max(1, args.streams)
-    Qt = max(S, args.queues - args.queues % S)   # rx queues in total
-    P = min(8, Qt // S)                           # queues (batches) per launch
-    Qt = P * S
-    R = max(2, -(-args.batches // Qt))            # rounds of distinct batches rotated through
-    nb = R * Qt
-    device = local
-    if world > 1:   # one rank per GPU; more ranks than GPUs (a rehearsal) share them round-robin
-        import torch
         ndev = torch.cuda.device_count()   # counts without initialising the GPU
-        if ndev > 0:
+        if ndev > 0:                       # more ranks than GPUs (a rehearsal): round-robin
             device = local % ndev
     ctx = lib.Ctx(device)
-    batches, results, cfg0 = [], [], None
-    nics = None
-    for k in range(nb):
-        cfg = traffic.config(args.config, n=n, seed=shard.batch_seed(rank, k))
-        if k == 0:
-            cfg0 = cfg
-            traffic.install_ctx(ctx, cfg)
-            nics = [cfg.src] + traffic.extra_nics(cfg, Qt - 1, ctx)
-        batches.append(lib.DeviceBatch(ctx, cfg.frames, cfg.lens, nics[k % Qt], stride=cfg.stride))
-        results.append(lib.DeviceResult(ctx, n))
-        if k:
-            del cfg
-    streams = [ctx.stream() for _ in range(S)]
-    stream = streams[0]
-    h = ctx.h
-    # launch (round r, stream s): the batches of queues [sP, sP+P) of round r
-    groups = {}
-    for r in range(R):
-        for si in range(S):
-            ks = [r * Qt + si * P + j for j in range(P)]
-            ba = (lib.Batch * P)(*[batches[k].desc for k in ks])
-            ra = (lib.Result * P)(*[results[k].desc for k in ks])
-            groups[(r, si)] = (C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), ba, ra)
-    multi = L.usn_classify_multi
-    single = L.usn_classify
-    bdesc = [C.byref(b.desc) for b in batches]
-    rdesc = [C.byref(r.desc) for r in results]
-    joins = [ctx.event() for _ in streams]
-
-    def launch(i, per=P, count=None, one_queue=False):
-        """Launch i on stream i % S: `count` (default per) batches of that
-        stream's queues.  one_queue: the single-queue reference (stream 0,
-        one batch per launch, batches in rotation)."""
-        if one_queue:
-            rc = single(h, bdesc[i % nb], rdesc[i % nb], stream)
-        else:
-            si = i % S
-            r = (i // S) % R
-            if per == 1:
-                k = r * Qt + si * P
-                rc = single(h, bdesc[k], rdesc[k], streams[si])
-            else:
-                g = groups[(r, si)]
-                rc = multi(h, g[0], g[1], count or per, streams[si])
-        if rc:
-            lib.check(rc, "usn_classify")
-
-    def timed(steps, per, one_queue=False):
-        """Exactly `steps` batches, `per` per launch (the last launch takes the rest)."""
-        full, rest = divmod(steps, per)
-        for x in streams:
-            ctx.sync(x)
-        if dist:
-            dist.barrier()
-        ctx.sync()
-        t0 = time.perf_counter()
-        ctx.record(ev0, stream)
-        for x in streams[1:]:
-            ctx.wait_event(x, ev0)
-        for i in range(full):
-            launch(i, per, one_queue=one_queue)
-        if rest:
-            launch(full, per, rest, one_queue=one_queue)
-        for x, ej in zip(streams[1:], joins[1:]):
-            ctx.record(ej, x)
-            ctx.wait_event(stream, ej)
-        ctx.record(ev1, stream)
-        ctx.sync(stream)
-        ctx.sync()
-        t1 = time.perf_counter()
-        if dist:
-            dist.barrier()
-        return t1 - t0, ctx.elapsed_ms(ev0, ev1), steps
-
-    ev0, ev1 = ctx.event(), ctx.event()
-    for i in range(-(-args.warmup // P)):
-        launch(i)
-    wall, ev_ms, done = timed(args.steps, P)
-    elapsed = shard.max_over_ranks(wall, dist)
-
-    # every batch of the last rotation: the ordered host stage had nothing to do
-    host_frames, flags = 0, 0
-    cls = [0, 0, 0, 0]
-    for x in streams:
-        ctx.sync(x)
-    for k in range(nb):
-        info = ctx.finalize(batches[k], results[k], streams[(k % Qt) // P])
-        host_frames += info.n_host
-        flags |= info.flags
-        cls = [x + y for x, y in zip(cls, info.class_count)]
-
-    # per-launch kernel duration (HIP events on the launch stream): the same
-    # launches back to back on ONE stream, so no launch shares the GPU with
-    # another (stream order serialises them) and none starts from an idle GPU
-    probe = []
-    evs = [(ctx.event(), ctx.event()) for _ in range(args.launch_probe)]
-    for x in streams:
-        ctx.sync(x)
-    for i, (ea, eb) in enumerate(evs):
-        ctx.record(ea, stream)
-        g = groups[((i // S) % R, i % S)]
-        rc = multi(h, g[0], g[1], P, stream)
-        if rc:
-            lib.check(rc, "usn_classify_multi")
-        ctx.record(eb, stream)
-    ctx.sync(stream)
-    for ea, eb in evs:
-        probe.append(ctx.elapsed_ms(ea, eb))
-    kern_ms = float(np.median(probe)) if probe else ev_ms / max(1, done // P)
-    achieved = ALGO_BYTES * n * P / (kern_ms * 1e-3) / 1e9
-
-    # the same batches one per launch (single rx queue), for reference
-    single_mpps = None
-    if P > 1 and args.steps >= 4:
-        w1, _, d1 = timed(max(4, args.steps // 2), 1, one_queue=True)
-        single_mpps = round(d1 * n / w1 / 1e6, 1)
-
-    total_frames = world * done * n
-    value = total_frames / elapsed / 1e6
+    n = args.frames or DEFAULT_FRAMES[args.config]
+    run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong)
+    res = measure(run, args, dist, world)
     out = {
-        "metric": "Mpkts/s device-resident L4 classify @64B frames; HBM GB/s vs roofline",
-        "value": round(value, 2),
+        "metric": METRIC,
+        "value": res["value"],
         "unit": "Mpkts/s",
         "n_gpus": world,
-        "steps": done,
+        "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / done, 5),
+        "ms_per_step": res["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic frames generated on the host (no captures), resident in HBM",
         "config": {
-            "workload": "%s: %d x 64B IPv4/UDP frames per batch (one drained rx ring), %d-rule "
-                        "endpoint table, NIC rx; %d rx queues on %d streams, %d rings per launch"
-                        % (args.config, n, len(cfg0.rules), Qt, S, P),
+            "workload": workload(run, args.strong),
             "frames_per_batch": n,
-            "rx_queues": Qt,
-            "streams": S,
-            "batches_per_launch": P,
-            "rotating_batches": nb,
-            "rotating_bytes": int(nb * (n * cfg0.stride + n * 2)),
+            "rx_queues_per_gpu": run.Q,
+            "streams": run.S,
+            "batches_per_launch": run.P,
+            "rotating_bytes_per_gpu": run.rotating_bytes,
             "parallelism": "replicas%d" % world,
-            "host_stage_frames": int(host_frames),
-            "summary_flags": int(flags),
-            "class_count_last_rotation": [int(x) for x in cls],
-            "event_ms_per_step": round(ev_ms / done, 5),
-            "single_queue_mpps": single_mpps,
+            "event_ms_per_step": res["event_ms_per_step"],
+            "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],
+            "host_stage_frames": res["host_stage_frames"],
+            "summary_flags": res["summary_flags"],
+            "class_count_last_rotation": res["class_count_last_rotation"],
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": "classify_rx_kernel",
-            "kernel_us_median": round(kern_ms * 1e3, 3),
-            "achieved_basis": "launches serialised on one stream (HIP events around each; no overlap)",
-            # the timed region's launches overlap on two streams: per GPU, algorithmic
-            # bytes of all its frames / the timed region's wall time
-            "achieved_steady_state": round(ALGO_BYTES * done * n / elapsed / 1e9, 1),
-            "batches_per_launch": P,
-            "algo_bytes_per_frame": ALGO_BYTES,
-        },
+        "roofline": res["roofline"],
         "cpu_baseline": None,
     }
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as fh:
-                pm = json.load(fh)
-            if int(pm.get("frames_per_launch", -1)) == n * P:
-                out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-                out["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
-        except Exception:
-            pass
+    cfg0 = run.cfg0
+    run.free()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
-        out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, n, args.cpu_seconds)
+        out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, args.cpu_seconds)
+    del cfg0
+    if world == 1 and not args.no_extra and args.config != "c2":
+        # configs[1] (the 1M x 64 B, 16-rule slice), measured the same way
+        ctx.close()
+        ctx = lib.Ctx(device)
+        r2 = Run(L, ctx, "c2", DEFAULT_FRAMES["c2"], 0, 1, 0, args.streams, False)
+        x = measure(r2, args, None, 1)
+        x["workload"] = workload(r2, False)
+        if not args.no_cpu_baseline:
+            x["cpu_baseline"] = cpu_baseline(r2.cfg0, min(args.cpu_seconds, 5.0))
+        r2.free()
+        out["c2"] = x
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for b in batches:
-        b.free()
-    for r in results:
-        r.free()
     ctx.close()
     if dist:
         dist.destroy_process_group()
@@ -273,7 +359,8 @@ def main():
 
 def cpu_baseline(cfg, seconds):
     """The sequential C oracle (restatement of the reference matcher, one
-    thread) timed on this host on the same batch, repeated for ~`seconds`."""
+    thread) timed on this host on the rank's first batch, repeated for about
+    `seconds` (at least one pass)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
     coracle.build()
@@ -308,7 +395,7 @@ def _cpu_worker(arg):
     return passes * cfg.n, time.perf_counter() - t0
 
 
-def cpu_baseline_ncores(name, n, seconds):
+def cpu_baseline_ncores(name, seconds):
     """SURVEY §8d's N-core variant: the sequential oracle sharded by rx queue,
     one process per core, N = the host CPUs this job may use (at most 16 on
     the GPU box).  Aggregate frames / slowest worker's time."""
@@ -318,7 +405,7 @@ def cpu_baseline_ncores(name, n, seconds):
     except AttributeError:
         ncores = os.cpu_count() or 1
     ncores = max(1, min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)), 16))
-    nshard = min(n, 1 << 18)   # each core's queue: a quarter-size batch keeps memory small
+    nshard = 1 << 18   # each core's queue: a quarter-million frames keeps memory small
     ctx = mp.get_context("spawn")
     with ctx.Pool(ncores) as pool:
         res = pool.map(_cpu_worker, [(name, nshard, 1000 + k, seconds) for k in range(ncores)])

@@ -33,10 +33,12 @@
 extern "C" {
 #endif
 
-#define USN_ABI_VERSION 1
-#define USN_WINDOW 64     /* header bytes read per frame (ports beyond it: slow path) */
+#define USN_ABI_VERSION 2
+#define USN_WINDOW 64     /* default readable header bytes at every frame start (usn_batch.window) */
+#define USN_WINDOW_MAX 80 /* the most extract_pkt_info ever reads: L4 ports of IHL 15 end at byte 78 */
 #define USN_TILE 1024     /* frames per tile of the per-endpoint order output */
-#define USN_MAX_ENDPOINTS 1021 /* endpoint ids 0..1020 (bins = endpoints + NIC + FLOOD + DROP) */
+#define USN_MAX_ENDPOINTS 4095 /* endpoint ids 0..4094 (0xFFFF = none); netmap pipe ids are 12 bits
+                                  (/root/reference/src/devices.rs:36-37) */
 
 /* status codes */
 #define USN_OK 0
@@ -67,6 +69,8 @@ extern "C" {
 #define USN_R_EXCLUDED 4u  /* get_endpoint hit a NIC or the source (endpoint.rs:328-336) */
 #define USN_R_FRAGMISS 5u  /* later fragment without a remembered first (pkt.rs:172-176) */
 #define USN_R_DHCP_NONE 6u /* DHCP answer, no rule, no next_dhcp (endpoint.rs:269-272) */
+#define USN_R_WINDOW 7u    /* device: L4 ports lie beyond usn_batch.window; usn_finalize resolves
+                              the frame from the host frame reader (usn_set_frame_reader) */
 #define USN_F_CACHE (1u << 24)   /* decision taken from the 1-entry cache (endpoint.rs:186-191) */
 #define USN_F_FRAG1 (1u << 25)   /* first fragment: remembered in the fragment map */
 #define USN_F_FRAGN (1u << 26)   /* later fragment: resolved through the fragment map */
@@ -101,13 +105,19 @@ typedef struct {
 /* ---- batch of frames (one drained rx ring of one source endpoint) -------- */
 typedef struct {
   const uint8_t *frames;   /* device: frame i starts at frames + i*stride or frames + offsets[i];
-                              16-byte aligned, USN_WINDOW readable bytes at every start */
+                              16-byte aligned, `window` readable bytes of frame i at every start */
   uint64_t stride;         /* > 0 selects the fixed-stride layout (netmap-slot like) */
   const uint64_t *offsets; /* device, or NULL when stride > 0 */
   const uint16_t *lens;    /* device: frame lengths (netmap_slot.len) */
   uint64_t n;              /* frames in the batch */
   uint16_t src_endpoint;   /* the endpoint whose ring was drained */
-  uint16_t _reserved[3];
+  uint16_t window;         /* bytes of frame i readable at its start, >= USN_WINDOW (0 means
+                              USN_WINDOW); with a stride, window <= stride.  A frame whose ports
+                              lie past the window (IPv4 with IHL >= 12 at window 64: pkt.rs:177-186
+                              reads 14+hl .. 18+hl) is never read past it: the kernel flags it
+                              USN_R_WINDOW | USN_F_HOST and usn_finalize resolves it from the host
+                              frame reader.  window >= USN_WINDOW_MAX never needs the reader. */
+  uint16_t _reserved[2];
 } usn_batch;
 
 /* Tile header: one per USN_TILE frames (written by the tile's workgroup only,
@@ -173,6 +183,26 @@ int usn_last_hip_error(void);
 #define USN_HOST_ONLY (-1)
 int usn_ctx_create(int hip_device, usn_ctx **out);
 void usn_ctx_destroy(usn_ctx *ctx);
+
+/* ---- several GPUs behind one registry (replicas only) -------
+ * One context, one match_register / bridge / fragment map / per-endpoint
+ * state (the reference's single daemon, main.rs:447-449), and one device
+ * replica of the rule image and bridge set per entry of hip_devices (the same
+ * device may appear twice).  Every registry or bridge change -- AddMatch,
+ * RemoveMatch, endpoint removal, usn_table_build / usn_bridge_set, and what a
+ * tx batch learned (applied by its usn_finalize, endpoint.rs:194-253) -- bumps
+ * the image version; a replica uploads the current version before its next
+ * batch (the table-version fence), and while a tx batch awaits usn_finalize
+ * every classify on every replica returns USN_EBUSY.  usn_classify /
+ * usn_classify_multi and the device plumbing calls act on the selected
+ * replica (0 after creation); usn_finalize finds the batch's replica itself.
+ * A source whose batches move to another replica carries its decision cache
+ * across through the host. */
+#define USN_MAX_REPLICAS 16
+int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out);
+int usn_ctx_replicas(usn_ctx *ctx);
+int usn_replica_select(usn_ctx *ctx, uint32_t replica);
+int usn_replica_device(usn_ctx *ctx, uint32_t replica);
 
 /* Endpoints::add / EntryChange::Add (main.rs:151-166).  for_nic = -1 iff NIC. */
 int usn_endpoint_add(usn_ctx *ctx, uint16_t id, int kind, int32_t for_nic);
@@ -243,6 +273,17 @@ int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t
  * n_host > 0 or flags != 0; calling it always is allowed. */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
                  usn_finalize_info *info);
+
+/* Host frame reader for frames whose ports lie past usn_batch.window: copies
+ * up to `cap` bytes (cap >= USN_WINDOW_MAX) of frame `index` of the batch of
+ * `src_endpoint` being finalized into `out`, returns the bytes copied (the
+ * frame length when shorter) or a negative value on failure.  Called only
+ * from usn_finalize, on the calling thread.  Without a reader, usn_finalize
+ * of a batch holding such frames returns USN_EINVAL before any side effect
+ * (their decisions stay USN_R_WINDOW drops).  NULL fn unregisters. */
+typedef int (*usn_frame_reader)(void *user, uint16_t src_endpoint, uint64_t index, uint8_t *out,
+                                uint32_t cap);
+int usn_set_frame_reader(usn_ctx *ctx, usn_frame_reader fn, void *user);
 
 /* Forget the carried decision cache of one endpoint (last_pkt = None). */
 int usn_cache_clear(usn_ctx *ctx, uint16_t endpoint);

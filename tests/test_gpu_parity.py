@@ -29,7 +29,7 @@ def _gpu():
 def test_library_is_native_and_gfx950():
     from usnetd_amd import lib
     ctx = lib.Ctx(0)
-    assert lib.load().usn_abi_version() == 1
+    assert lib.load().usn_abi_version() == 2
     ctx.close()
 
 
@@ -67,12 +67,17 @@ def _oracle_lists(d, n_ep):
     ("c1", 50000, None), ("c2", 1 << 20, None), ("c3", 1 << 17, None), ("c4", 1 << 18, None),
     ("c5", 1 << 20, None),
     # ragged last tiles; c5's 1005 bins take the radix order in both builds
-    ("c3", 5003, None), ("c4", 70001, None), ("c5", 100003, "0"), ("c5", 100003, "1")])
+    ("c3", 5003, None), ("c4", 70001, None), ("c5", 100003, "0"), ("c5", 100003, "1"),
+    # 4093 pipes + NIC + host ring: the whole 12-bit endpoint id space (4098 bins, 3 radix passes)
+    ("c5-4093", 300007, None)])
 def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     from usnetd_amd import lib, traffic
     if t512 is not None:   # USN_T512 (read at context creation): force one build
         monkeypatch.setenv("USN_T512", t512)
-    cfg = traffic.config(name, n=n)
+    kw = {}
+    if name == "c5-4093":
+        name, kw = "c5", {"n_ep": 4093}
+    cfg = traffic.config(name, n=n, **kw)
     o = coracle_mod.Oracle()
     coracle_mod.install_oracle(o, cfg)
     want = o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)

@@ -2,10 +2,12 @@
 
 Replicas only: each rank owns disjoint rx queues (sources) and a replica of
 the rule table.  The per-rank classifier here is the C oracle standing in for
-the device (the GPU path is covered by tests/test_gpu_parity.py); what is
-tested is the partitioning: every queue is classified exactly once, the
-union of the ranks' per-queue decision streams equals a single process
-classifying every queue, and the timing reduction is a max over ranks."""
+the device (the same ranks on the GPU, through the product: tests/
+test_gpu_multiproc.py); what is tested is the partition bench.py uses
+(shard.rank_queues, shard.queue_seed): every queue is classified exactly
+once, the union of the ranks' per-queue decision streams equals a single
+process classifying every queue, and the timing reduction is a max over
+ranks."""
 import os
 import socket
 
@@ -38,7 +40,7 @@ def _classify_queues(queues, n):
             o.add_endpoint(first + q - 1, 0, -1)
     for q in queues:
         src = 0 if q == 0 else first + q - 1
-        cfg = traffic.config("c2", n=n, seed=shard.batch_seed(0, 1 + q))
+        cfg = traffic.config("c2", n=n, seed=shard.queue_seed(q, 0))   # as bench.py's Run
         d = o.forward_batch(src, cfg.frames, cfg.lens, stride=cfg.stride)
         out[q] = d.tolist()
     return out

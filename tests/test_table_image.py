@@ -1,0 +1,155 @@
+"""CPU tests of the device rule image (perfect hash, usn_internal.h), built
+from the registry by the product library on a registry-only context
+(USN_HOST_ONLY) and probed on the host with the device's own hash functions
+(test hook usn_debug_image_probe, which computes exactly what ph_probe in
+usn_device.hip computes).
+
+The image must answer get_endpoint's two exact-match lookups
+(/root/reference/src/endpoint.rs:307-338): every rule key1 or key2 can hit is
+found with its owner; nothing else is (other Want shapes never match a frame,
+SURVEY.md A.3.6); and a probe reads one displacement and one slot."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from usnetd_amd import lib, traffic
+
+VALID = 1 << 11
+META_MASK = 0x0FFF
+
+
+def _ctx():
+    L = lib.load()
+    h = C.c_void_p()
+    assert L.usn_ctx_create(-1, C.byref(h)) == 0
+    L.usn_debug_image_probe.restype = C.c_int64
+    L.usn_debug_image_probe.argtypes = [C.c_void_p, C.c_int] + [C.c_uint32] * 4
+    L.usn_debug_image_info.argtypes = [C.c_void_p, C.c_void_p]
+    return L, h.value
+
+
+def _packed(w):
+    """(table, x, y, z, meta) of a Want as the device packs it."""
+    p = w.present & 7
+    z = (w.dst_port if p & 1 else 0) | ((w.src_port if p & 4 else 0) << 16)
+    y = w.src_addr if p & 2 else 0
+    meta = (w.protocol & 0xFF) | (p << 8) | VALID
+    table = 0 if p in (2, 7) else 1 if p in (0, 1) else -1
+    return table, w.dst_addr, y, z, meta
+
+
+def _info(L, h):
+    out = (C.c_uint32 * 6)()
+    assert L.usn_debug_image_info(h, out) == 0
+    return list(out)
+
+
+def test_image_finds_every_rule_c5():
+    L, h = _ctx()
+    cfg = traffic.config("c5", n=16)
+    for eid, kind, for_nic in cfg.endpoints:
+        assert L.usn_endpoint_add(h, eid, kind, -1 if for_nic is None else for_nic) == 0
+    ws = []
+    for w, owner, sticky in cfg.rules:
+        want = lib.make_want(w["dst"], w["proto"], w["dport"], w["src"], w["sport"])
+        assert L.usn_add_match(h, C.byref(want), owner, int(sticky)) == 1
+        ws.append((want, owner))
+    m0, g0, m1, g1, units, pmask = _info(L, h)
+    assert pmask == 3
+    assert m0 >= 32768 and m1 >= 32768 and m0 < 32768 / 0.8 and m1 < 32768 / 0.8
+    assert units * 16 < 1.4 * 2 ** 20            # the c5 image is L2-resident
+    for want, owner in ws:
+        t, x, y, z, meta = _packed(want)
+        got = L.usn_debug_image_probe(h, t, x, y, z, meta)
+        assert got and (got >> 16) == owner and (got & META_MASK) == meta
+        # never in the other table
+        assert L.usn_debug_image_probe(h, 1 - t, x, y, z, meta) == 0
+    rng = np.random.default_rng(3)
+    for _ in range(20000):   # random keys of both shapes miss
+        x = int(rng.integers(0, 2 ** 32))
+        z = int(rng.integers(0, 2 ** 32))
+        assert L.usn_debug_image_probe(h, 0, x, 7, z, 6 | (7 << 8) | VALID) == 0
+        assert L.usn_debug_image_probe(h, 1, x, 0, z & 0xFFFF, 17 | (1 << 8) | VALID) == 0
+    L.usn_ctx_destroy(h)
+
+
+def test_image_shapes_owner_flags_and_updates():
+    """Other Want shapes stay out of the image; NIC-owned rules carry the NIC
+    bit (the exclusion of endpoint.rs:328-336); the image follows AddMatch /
+    RemoveMatch / endpoint removal."""
+    L, h = _ctx()
+    assert L.usn_endpoint_add(h, 0, 0, -1) == 0      # NIC
+    assert L.usn_endpoint_add(h, 1, 1, 0) == 0       # host ring
+    assert L.usn_endpoint_add(h, 2, 2, 0) == 0       # pipe
+    w_listen = lib.make_want("10.0.0.1", 6, 80)
+    w_icmp = lib.make_want("10.0.0.1", 1)
+    w_conn = lib.make_want("10.0.0.1", 6, 80, "10.9.9.9", 4444)
+    w_src_only = lib.make_want("10.0.0.1", 1, None, "10.9.9.9")
+    w_odd = lib.make_want("10.0.0.1", 6, 80, "10.9.9.9")           # dport+src, no sport
+    for w, o in ((w_listen, 1), (w_icmp, 2), (w_conn, 2), (w_src_only, 1), (w_odd, 2)):
+        assert L.usn_add_match(h, C.byref(w), o, 0) == 1
+    for w, o in ((w_listen, 1), (w_icmp, 2), (w_conn, 2), (w_src_only, 1)):
+        t, x, y, z, meta = _packed(w)
+        got = L.usn_debug_image_probe(h, t, x, y, z, meta)
+        assert (got >> 16) == o and not got & (1 << 12)
+    t, x, y, z, meta = _packed(w_odd)
+    assert t == -1
+    assert L.usn_debug_image_probe(h, 0, x, y, z, meta) == 0
+    assert L.usn_debug_image_probe(h, 1, x, y, z, meta) == 0
+    # RemoveMatch drops the key from the image
+    assert L.usn_remove_match(h, C.byref(w_conn), 2) == 1
+    t, x, y, z, meta = _packed(w_conn)
+    assert L.usn_debug_image_probe(h, t, x, y, z, meta) == 0
+    # endpoint removal drops its rules
+    assert L.usn_endpoint_remove(h, 1) == 0
+    t, x, y, z, meta = _packed(w_listen)
+    assert L.usn_debug_image_probe(h, t, x, y, z, meta) == 0
+    t, x, y, z, meta = _packed(w_icmp)
+    assert (L.usn_debug_image_probe(h, t, x, y, z, meta) >> 16) == 2
+    # a NIC-owned rule (usn_table_build can install one) carries the NIC bit
+    rules = np.zeros(1, lib.RULE_DTYPE)
+    rules[0] = (lib.ip2int("10.0.0.2"), 0, 53, 0, 17, 1, 0)
+    assert L.usn_table_build(h, rules.ctypes.data, 1) == 1
+    got = L.usn_debug_image_probe(h, 1, lib.ip2int("10.0.0.2"), 0, 53, 17 | (1 << 8) | VALID)
+    assert got & (1 << 12) and (got >> 16) == 0
+    L.usn_ctx_destroy(h)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 300000])
+def test_image_bulk_sizes(n):
+    """usn_table_build of n random connected 5-tuples and listening ports:
+    every key found, load <= 0.86, displacement groups of ~4."""
+    L, h = _ctx()
+    assert L.usn_endpoint_add(h, 0, 0, -1) == 0
+    for e in range(1, 9):
+        assert L.usn_endpoint_add(h, e, 2, 0) == 0
+    rng = np.random.default_rng(n)
+    rules = np.zeros(n, lib.RULE_DTYPE)
+    rules["dst_addr"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    conn = rng.random(n) < 0.5
+    rules["src_addr"] = np.where(conn, rng.integers(0, 2 ** 32, n, dtype=np.uint64), 0)
+    rules["dst_port"] = rng.integers(0, 65536, n)
+    rules["src_port"] = np.where(conn, rng.integers(0, 65536, n), 0)
+    rules["protocol"] = rng.choice([6, 17], n)
+    rules["present"] = np.where(conn, 7, 1)
+    rules["endpoint"] = rng.integers(1, 9, n)
+    got_n = L.usn_table_build(h, rules.ctypes.data, n)
+    assert got_n >= 1
+    m0, g0, m1, g1, units, pmask = _info(L, h)
+    n_conn, n_list = int(conn.sum()), int((~conn).sum())
+    if n > 100:
+        assert m0 <= n_conn / 0.84 + 2 and m1 <= n_list / 0.84 + 2
+        assert g0 == (n_conn + 3) // 4 and g1 == (n_list + 3) // 4
+    idx = rng.choice(n, min(n, 5000), replace=False)
+    for i in idx:
+        r = rules[i]
+        p = int(r["present"])
+        t = 0 if p == 7 else 1
+        z = int(r["dst_port"]) | (int(r["src_port"]) << 16 if p == 7 else 0)
+        meta = int(r["protocol"]) | (p << 8) | VALID
+        got = L.usn_debug_image_probe(h, t, int(r["dst_addr"]), int(r["src_addr"]), z, meta)
+        assert got, i
+        # duplicates keep the first owner (HashMap::entry().or_insert)
+        assert (got >> 16) in range(1, 9)
+    L.usn_ctx_destroy(h)

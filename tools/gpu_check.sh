@@ -53,6 +53,17 @@ for s in ${STEPS:-tests smoke bench prof}; do
         step pmc$i 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python3 tools/kbench.py ${KB_ARGS:-c2 1048576 30}
       done
       step pmcsum 60 python3 tools/pmc_summary.py gpurun_out/pmc ;;
+    pmccfg)  # per config: kernel trace + FETCH_SIZE / WRITE_SIZE / L2 hit-miss passes (kbench launches)
+      for c in ${PMC_CFGS:-c3 c4 c5}; do
+        rm -rf gpurun_out/pmccfg/$c
+        step kt_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmccfg/$c/kt -o run -- python3 tools/kbench.py $c ${KB_FRAMES:-1048576} 40
+        j=0
+        for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+          j=$((j+1))
+          step pmc_${c}_$j 300 timeout -s KILL 240 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmccfg/$c/p$j -o run -- python3 tools/kbench.py $c ${KB_FRAMES:-1048576} 30
+        done
+        step pmcsum_$c 60 python3 tools/pmc_summary.py gpurun_out/pmccfg/$c/p1 gpurun_out/pmccfg/$c/p2 gpurun_out/pmccfg/$c/p3 gpurun_out/pmccfg/$c/p4
+      done ;;
     traffic)
       rm -rf gpurun_out/pmcf gpurun_out/pmcw
       step pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf -o run -- python3 bench.py --steps 64 --warmup 8 --no-cpu-baseline --launch-probe 0

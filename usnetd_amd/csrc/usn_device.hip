@@ -46,8 +46,10 @@ using namespace ::usn;
 #define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
-#define MAX_NBITS 10   /* nbins <= 1024 */
-#define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule tables up to 2048 slots live in LDS */
+#define MAX_NBITS 13   /* nbins <= USN_MAX_ENDPOINTS + 3 <= 8192 */
+#define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule images up to 32 KiB live in LDS */
+/* the LDS copy of the image, rounded up to whole 64-unit glds chunks */
+__host__ __device__ inline uint32_t table_lds_units(uint32_t units) { return (units + 63) & ~63u; }
 
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
@@ -114,16 +116,19 @@ __device__ __forceinline__ uint32_t be16lo(uint32_t v) {  // bytes [0,1] of v as
 }
 
 struct Parsed {
-  uint32_t status;   // 0 parse fail, 1 IPv4, 2 ARP, 3 EAPOL, 4 later fragment
+  uint32_t status;   // 0 parse fail, 1 IPv4, 2 ARP, 3 EAPOL, 4 later fragment,
+                     // 5 IPv4 whose L4 ports lie past the batch window (the host parses it)
   uint32_t i0, src, dst, ports;   // PacketInfo words (usn_internal.h)
   uint32_t sport, dport, proto, has_ports, frag_first;
 };
 
 /* extract_pkt_info (pkt.rs:158-218) with smoltcp 0.7.0's EthernetFrame /
  * Ipv4Packet::new_checked length rules, computed for every lane with selects
- * (no divergent early exits).  q = 64-byte window as little-endian words. */
+ * (no divergent early exits).  q = 64-byte window as little-endian words;
+ * `window` = readable bytes at `frame` (never read past: a frame whose ports
+ * end beyond it gets status 5). */
 __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint8_t *frame,
-                                      Parsed &p) {
+                                      uint32_t window, Parsed &p) {
   const uint32_t w3 = q[0].w, w4 = q[1].x, w5 = q[1].y, w6 = q[1].z, w7 = q[1].w;
   const uint32_t w8 = q[2].x, w9 = q[2].y;
   const uint32_t et = be16lo(w3);                                    // bytes 12..13
@@ -149,7 +154,8 @@ __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint
   // the branch: a wait after the join would be vmcnt(0) on every path and
   // drain the next round's prefetch.
   uint32_t ra = 0, rb = 0;
-  const bool reload = has && ihl != 5u;
+  const bool beyond = has && 18u + hl > window;                      // ports at 14+hl..17+hl
+  const bool reload = has && ihl != 5u && !beyond;
   if (reload) {
     ra = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
     rb = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
@@ -165,7 +171,7 @@ __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint
   p.dst = __builtin_bswap32(__builtin_amdgcn_alignbyte(w8, w7, 2));  // bytes 30..33
   p.frag_first = (!(ff & 0x4000u) && (ff & 0x2000u)) ? 1u : 0u;      // pkt.rs:198
   const bool arp = eth && et == 0x0806u, eapol = eth && et == 0x888Eu;
-  p.status = arp ? 2u : eapol ? 3u : !ip ? 0u : later ? 4u : 1u;
+  p.status = arp ? 2u : eapol ? 3u : !ip ? 0u : later ? 4u : beyond ? 5u : 1u;
   p.i0 = arp ? USN_INFO_ARP : eapol ? USN_INFO_EAPOL
        : (p.status == 1u ? (USN_INFO_IPV4 | (pr << 8) | (p.has_ports << 16)) : 0u);
 }
@@ -175,99 +181,94 @@ __device__ __forceinline__ bool slot_is(const uint4 &t, uint32_t x, uint32_t y, 
   return ((t.x ^ x) | (t.y ^ y) | (t.z ^ z) | ((t.w ^ meta) & USN_KEY_META_MASK)) == 0u;
 }
 
-/* Meta word of the slot of a bucket that holds the key, or 0.  A key sits in
- * at most one slot, so the four masked words are OR-ed: all four slots are
- * read and compared unconditionally (a ?: chain let the compiler turn the
- * later slot reads into dependent branches). */
-__device__ __forceinline__ uint32_t bucket_hit(const uint4 &s0, const uint4 &s1, const uint4 &s2,
-                                               const uint4 &s3, uint32_t x, uint32_t y, uint32_t z,
-                                               uint32_t meta) {
-  return (s0.w & (0u - (uint32_t)slot_is(s0, x, y, z, meta))) |
-         (s1.w & (0u - (uint32_t)slot_is(s1, x, y, z, meta))) |
-         (s2.w & (0u - (uint32_t)slot_is(s2, x, y, z, meta))) |
-         (s3.w & (0u - (uint32_t)slot_is(s3, x, y, z, meta)));
+/* ---- rule lookups: the perfect-hash image (usn_internal.h) ----------------
+ * A key's probe reads one 16-bit displacement and exactly ONE 16-byte slot,
+ * hit or miss: no chains, no tag line.  In LDS (small images) both reads are
+ * inline asm: the classify kernel has LDS-DMA header writes in flight, and
+ * hipcc cannot tell that the image does not alias the DMA's stage, so plain
+ * LDS reads got an s_waitcnt vmcnt(0) that drained the next round's headers;
+ * the asm waits for its own reads (lgkmcnt) and nothing else. */
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void *)p;
 }
 
-/* The four slots of a bucket.  From LDS by inline asm: the classify kernel
- * has LDS-DMA (glds) writes in flight while it probes, and hipcc cannot tell
- * that the table does not alias the DMA's stage, so plain LDS reads got an
- * s_waitcnt vmcnt(0) that drained the next round's headers.  The asm waits
- * for its own reads (lgkmcnt) and nothing else. */
+struct PhKeyH {        // a key's hashes for one table
+  uint32_t grp, h2;
+};
+
+__device__ __forceinline__ PhKeyH ph_hash(const usn_ph_table &t, uint32_t x, uint32_t y,
+                                          uint32_t z, uint32_t meta) {
+  PhKeyH k;
+  k.grp = usn_mulhi32(usn_ph_h1(x, y, z, meta, t.seed), t.g);
+  k.h2 = usn_key_hash2(x, y, z, meta, t.seed);
+  return k;
+}
+
+__device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t y, uint32_t z,
+                                           uint32_t meta) {
+  return slot_is(sl, x, y, z, meta) ? sl.w : 0u;
+}
+
+/* Both keys of a frame, issued together: two displacement reads, then two
+ * slot reads (one round trip each for the global image).  use1/use2 are
+ * wave-uniform (the image's probe_mask); w = the slot's meta word, 0 = miss. */
 template <bool IN_LDS>
-__device__ __forceinline__ void load_bucket(const uint4 *s, uint4 &s0, uint4 &s1, uint4 &s2,
-                                            uint4 &s3) {
+__device__ __forceinline__ void ph_probe2(const uint4 *T, const ClassifyArgs &a, bool use1,
+                                          bool use2, uint32_t x1, uint32_t y1, uint32_t z1,
+                                          uint32_t m1, uint32_t x2, uint32_t y2, uint32_t z2,
+                                          uint32_t m2, uint32_t &w1, uint32_t &w2) {
+  const PhKeyH k1 = ph_hash(a.ph[0], x1, y1, z1, m1);
+  const PhKeyH k2 = ph_hash(a.ph[1], x2, y2, z2, m2);
+  const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+  w1 = 0u;
+  w2 = 0u;
   if (IN_LDS) {
-    const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint4 *)s;
-    v4u32 a0, a1, a2, a3;
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:16\n\t"
-        "ds_read_b128 %2, %4 offset:32\n\t"
-        "ds_read_b128 %3, %4 offset:48\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
-        : "v"(addr));
-    s0 = make_uint4(a0.x, a0.y, a0.z, a0.w);
-    s1 = make_uint4(a1.x, a1.y, a1.z, a1.w);
-    s2 = make_uint4(a2.x, a2.y, a2.z, a2.w);
-    s3 = make_uint4(a3.x, a3.y, a3.z, a3.w);
+    // an unused table's reads go to index 0 of the image (always present)
+    const uint32_t di1 = use1 ? a.ph[0].disp_off + k1.grp : 0u;
+    const uint32_t di2 = use2 ? a.ph[1].disp_off + k2.grp : 0u;
+    uint32_t d1, d2;
+    asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(d1), "=&v"(d2)
+                 : "v"(lds_addr(D + di1)), "v"(lds_addr(D + di2)));
+    const uint32_t si1 = use1 ? a.ph[0].slot_off + usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u;
+    const uint32_t si2 = use2 ? a.ph[1].slot_off + usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u;
+    v4u32 s1, s2;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(s1), "=&v"(s2)
+                 : "v"(lds_addr(T + si1)), "v"(lds_addr(T + si2)));
+    if (use1) w1 = ph_hit(make_uint4(s1.x, s1.y, s1.z, s1.w), x1, y1, z1, m1);
+    if (use2) w2 = ph_hit(make_uint4(s2.x, s2.y, s2.z, s2.w), x2, y2, z2, m2);
   } else {
-    s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
+    uint32_t d1 = 0, d2 = 0;
+    if (use1) d1 = D[a.ph[0].disp_off + k1.grp];
+    if (use2) d2 = D[a.ph[1].disp_off + k2.grp];
+    uint4 s1 = make_uint4(0, 0, 0, 0), s2 = make_uint4(0, 0, 0, 0);
+    if (use1) s1 = T[a.ph[0].slot_off + usn_ph_slot(k1.h2, d1, a.ph[0].m)];
+    if (use2) s2 = T[a.ph[1].slot_off + usn_ph_slot(k2.h2, d2, a.ph[1].m)];
+    if (use1) w1 = ph_hit(s1, x1, y1, z1, m1);
+    if (use2) w2 = ph_hit(s2, x2, y2, z2, m2);
   }
 }
 
-/* One exact-match probe.  LDS table: the home bucket (one 64-byte line) is
- * checked with selects; the chain is followed only when that bucket is full
- * and holds no match (rare at load <= 1/2).  Global table (TAGGED): one
- * 16-byte tag line per bucket, then only the slot whose tag matches -- two
- * 16-byte L2 requests per hit, one per miss, instead of four.  Returns the
- * slot's meta word, 0 = miss. */
-template <bool TAGGED>
-__device__ __forceinline__ uint32_t probe(const uint4 *T, const uint4 *tags, uint32_t bmask,
-                                          uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
-  if (TAGGED && !USN_ABL_NOTAGS) {
-    // the home bucket's tag line and the next one are loaded together: at
-    // load <= 1/4 a chain rarely passes two buckets, so a wave seldom waits
-    // for a straggler lane's third dependent load
-    const uint32_t h = usn_key_hash(x, y, z, meta);
-    const uint32_t tg = usn_key_tag(h);
-    uint32_t b = h & bmask;
-    for (uint32_t it = 0; it <= bmask; it += 2) {
-      const uint32_t b2 = (b + 1) & bmask;
-      const uint4 tv = tags[b], tv2 = tags[b2];
-#pragma unroll
-      for (uint32_t half = 0; half < 2; ++half) {
-        const uint4 &t4 = half ? tv2 : tv;
-        const uint32_t bb = half ? b2 : b;
-        uint32_t mm = (t4.x == tg ? 1u : 0u) | (t4.y == tg ? 2u : 0u) | (t4.z == tg ? 4u : 0u) |
-                      (t4.w == tg ? 8u : 0u);
-        while (mm) {   // verify: two keys of one bucket may share a tag
-          const uint32_t j = (uint32_t)__builtin_ctz(mm);
-          const uint4 sl = T[bb * 4 + j];
-          if (slot_is(sl, x, y, z, meta)) return sl.w;
-          mm &= mm - 1;
-        }
-        if (t4.w == 0u) return 0u;   // bucket not full: the key would be in it
-      }
-      b = (b2 + 1) & bmask;
-    }
-    return 0u;
+/* One key in table `tb` (0 = K1, 1 = K2); 0 when the table is empty. */
+template <bool IN_LDS>
+__device__ __forceinline__ uint32_t ph_probe1(const uint4 *T, const ClassifyArgs &a, uint32_t tb,
+                                              uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
+  const usn_ph_table &t = a.ph[tb];
+  if (!(a.probe_mask & (1u << tb))) return 0u;
+  const PhKeyH k = ph_hash(t, x, y, z, meta);
+  const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+  if (IN_LDS) {
+    uint32_t d;
+    asm volatile("ds_read_u16 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
+                 : "v"(lds_addr(D + t.disp_off + k.grp)));
+    v4u32 sv;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(sv)
+                 : "v"(lds_addr(T + t.slot_off + usn_ph_slot(k.h2, d, t.m))));
+    return ph_hit(make_uint4(sv.x, sv.y, sv.z, sv.w), x, y, z, meta);
   }
-  uint32_t b = usn_key_hash(x, y, z, meta) & bmask;
-  const uint4 *s = T + b * 4;
-  uint4 s0, s1, s2, s3;
-  load_bucket<!TAGGED>(s, s0, s1, s2, s3);   // !TAGGED: the table is in LDS
-  uint32_t hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
-  if (!hit && (s3.w & USN_SLOT_VALID)) {
-    for (uint32_t it = 0; it < bmask; ++it) {
-      b = (b + 1) & bmask;
-      s = T + b * 4;
-      load_bucket<!TAGGED>(s, s0, s1, s2, s3);
-      hit = bucket_hit(s0, s1, s2, s3, x, y, z, meta);
-      if (hit || !(s3.w & USN_SLOT_VALID)) break;
-    }
-  }
-  return hit;
+  const uint32_t d = D[t.disp_off + k.grp];
+  return ph_hit(T[t.slot_off + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
 }
 
 /* find_forward for a NIC source (incoming == true), cache handled outside:
@@ -289,7 +290,7 @@ __device__ __forceinline__ void rx_keys(const Parsed &p, uint32_t &x1, uint32_t 
 __device__ __forceinline__ uint32_t decide_rx_w(const ClassifyArgs &a, const Parsed &p, uint32_t w1,
                                                 uint32_t w2);
 
-template <bool TAGGED>
+template <bool IN_LDS>
 __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs &a,
                                               const Parsed &p) {
   uint32_t w1 = 0, w2 = 0;
@@ -298,8 +299,8 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs
 #else
   uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
   rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
-  if (a.probe_mask & 1u) w1 = probe<TAGGED>(T, a.tags, a.bucket_mask, x1, y1, z1, m1);
-  if (a.probe_mask & 2u) w2 = probe<TAGGED>(T, a.tags, a.bucket_mask, x2, y2, z2, m2);
+  ph_probe2<IN_LDS>(T, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
+                    y2, z2, m2, w1, w2);
 #endif
   return decide_rx_w(a, p, w1, w2);
 }
@@ -321,10 +322,12 @@ __device__ __forceinline__ uint32_t decide_rx_w(const ClassifyArgs &a, const Par
   uint32_t d =
       p.status == 0u ? usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu)
       : p.status == 4u ? (usn_mkdec(USN_CLS_DROP, USN_R_FRAGMISS, 0xFFFFu) | USN_F_FRAGN | USN_F_HOST)
+      : p.status == 5u ? (usn_mkdec(USN_CLS_DROP, USN_R_WINDOW, 0xFFFFu) | USN_F_HOST)
       : p.status != 1u ? usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu)            // ARP/EAPOL
       : (p.dst >> 24) == 127u ? usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu)   // :205-208
                               : d_look;
   // a first fragment is remembered by extract_pkt_info before any decision
+  // (status 5: the host parses the frame and remembers it itself)
   if (p.status == 1u && p.frag_first) d |= USN_F_FRAG1 | USN_F_HOST;
   return d;
 }
@@ -728,13 +731,13 @@ __device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *sc
 }
 
 /* Decision for a carried PacketInfo X under the current table (rx). */
-template <bool TAGGED>
+template <bool IN_LDS>
 __device__ uint32_t decide_info_rx(const uint4 *T, const ClassifyArgs &a, const uint32_t *info) {
   Parsed p;
   p.status = 1; p.i0 = info[0]; p.src = info[1]; p.dst = info[2]; p.ports = info[3];
   p.proto = (info[0] >> 8) & 0xFFu; p.has_ports = (info[0] >> 16) & 1u;
   p.sport = info[3] & 0xFFFFu; p.dport = info[3] >> 16; p.frag_first = 0;
-  return decide_rx<TAGGED>(T, a, p);
+  return decide_rx<IN_LDS>(T, a, p);
 }
 
 /* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
@@ -857,7 +860,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
   const uint4 *T = m.b[0].table;
   if (LDS) {   // table -> LDS by glds, 64 slots per instruction, waves in turn
-    const uint32_t slots = m.b[0].table_slots;
+    const uint32_t slots = m.b[0].table_units;
     for (uint32_t c = wave; c * 64 < slots; c += NWAVES) {
       const uint32_t sl = min(c * 64 + lane, slots - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
@@ -887,7 +890,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       const uint32_t cst = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
       if ((cst & USN_CS_VALID) &&
-          ((decide_info_rx<!LDS>(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
+          ((decide_info_rx<LDS>(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
         flags |= USN_S_STALE;
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
@@ -936,10 +939,10 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     continue;
 #endif
     Parsed p;
-    parse(q[r], local < nt ? len[r] : 0u, fp[r], p);
-    dec[r] = decide_rx<!LDS>(T, a, p);
+    parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
+    dec[r] = decide_rx<LDS>(T, a, p);
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
-    uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
+    uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                    : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
     if (local >= nt) touch = 0;
     if (touch) {
@@ -1262,7 +1265,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   const uint4 *T = a.table;
   if (LDS) {
-    for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    for (uint32_t k = tid; k < a.table_units; k += NTHREADS) L.table[k] = a.table[k];
     T = L.table;
   }
   __shared__ uint32_t s_carry[8];
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
   /* the bridge snapshot set in LDS when small */
   const unsigned long long *BS = t.bridge_set;
   if (t.bridge_mask < TX_BRIDGE_LDS_SLOTS) {
-    unsigned long long *bs = reinterpret_cast<unsigned long long *>(L.table + (LDS ? a.table_slots : 0));
+    unsigned long long *bs = reinterpret_cast<unsigned long long *>(L.table + (LDS ? table_lds_units(a.table_units) : 0));
     for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
     BS = bs;
   }
@@ -1310,11 +1313,11 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
     const uint4 *q = qq[r];
     const uint32_t len = ll[r];
     Parsed p;
-    parse(q, len, fp, p);
+    parse(q, len, fp, a.window, p);
     const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
     const uint64_t smac = (uint64_t)(q[0].y >> 16) | ((uint64_t)q[0].z << 16);
     const bool loop = p.status == 1u && (p.dst >> 24) == 127u;
-    const uint32_t touch = p.status == 0u ? 0u : p.status == 4u ? 3u
+    const uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                          : (p.status == 1u && !loop) ? 1u : 2u;
     uint32_t f = (touch << TXR_TOUCH_SHIFT);
     if (touch == 1u || touch == 2u) {
@@ -1325,6 +1328,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
     }
     if (touch == 3u) f |= TXR_HOST;                           // later fragment: map lookup
+    if (p.status == 5u) f |= TXR_WINDOW;                      // ports past the window
     if (touch == 1u) {
       // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
       bool listening = false;
@@ -1340,7 +1344,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       if (!listening && !dhcp_req) {   // the answer key is learned unless the table has it
         uint32_t x, y, z, meta;
         want_key(make_uint4(p.i0, p.src, p.dst, p.ports), x, y, z, meta);
-        if (!USN_ABL_TXNOPROBE && !probe<!LDS>(T, a.tags, a.bucket_mask, x, y, z, meta)) f |= TXR_LEARNRULE;
+        if (!USN_ABL_TXNOPROBE && !ph_probe1<LDS>(T, a, 0, x, y, z, meta)) f |= TXR_LEARNRULE;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
@@ -1500,7 +1504,7 @@ __device__ __forceinline__ uint32_t tx_lookup_dec(const ClassifyArgs &a, uint32_
   return usn_mkdec(USN_CLS_DROP, excl ? USN_R_EXCLUDED : USN_R_NOMATCH, 0xFFFFu);
 }
 
-template <bool TAGGED>
+template <bool IN_LDS>
 __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
                                    const uint4 &r1, uint32_t i, uint32_t ins) {
   const ClassifyArgs &a = t.a;
@@ -1509,11 +1513,11 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   uint32_t x, y, z, meta;
   key1_of(r0, x, y, z, meta);
   if (USN_ABL_TXNOPROBE) return usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);
-  uint32_t w = (a.probe_mask & 1u) ? probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta) : 0u;
+  uint32_t w = ph_probe1<IN_LDS>(T, a, 0, x, y, z, meta);
   if (!w && (ins & 2u)) w = tx_learned_key1(t, x, y, z, meta, i);
   if (!w && (a.probe_mask & 2u)) {
     key2_of(r0, x, y, z, meta);
-    w = probe<TAGGED>(T, a.tags, a.bucket_mask, x, y, z, meta);
+    w = ph_probe1<IN_LDS>(T, a, 1, x, y, z, meta);
   }
   return tx_lookup_dec(a, fl, w);
 }
@@ -1531,12 +1535,12 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
   const uint32_t tile = blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  uint32_t *sdec = reinterpret_cast<uint32_t *>(L.table + (LDS ? a.table_slots : 0));
+  uint32_t *sdec = reinterpret_cast<uint32_t *>(L.table + (LDS ? table_lds_units(a.table_units) : 0));
   __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   __shared__ uint32_t s_head;      // decision of the last non-hit touching frame before the tile
   const uint4 *T = a.table;
   if (LDS) {
-    for (uint32_t k = tid; k < a.table_slots; k += NTHREADS) L.table[k] = a.table[k];
+    for (uint32_t k = tid; k < a.table_units; k += NTHREADS) L.table[k] = a.table[k];
     T = L.table;
   }
   if (tid < 8) s_misc[tid] = 0;
@@ -1564,7 +1568,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     if (before && !USN_ABL_NOHEAD) {   // (A/B only: NOHEAD measures the recompute)
       const uint4 h0 = t.rec[before - 1];
       const uint4 h1 = (ins & 1u) ? frame_head(a, before - 1) : make_uint4(0, 0, 0, 0);
-      hd = decide_tx_ipv4<!LDS>(t, T, h0, h1, before - 1, ins);
+      hd = decide_tx_ipv4<LDS>(t, T, h0, h1, before - 1, ins);
     }
     s_head = hd;
   }
@@ -1581,7 +1585,9 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     if (touch == 0u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
     } else if (fl & TXR_HOST) {
-      d = usn_mkdec(USN_CLS_DROP, touch == 3u ? USN_R_FRAGMISS : USN_R_NOMATCH, 0xFFFFu) | USN_F_HOST;
+      d = usn_mkdec(USN_CLS_DROP, (fl & TXR_WINDOW) ? USN_R_WINDOW : touch == 3u ? USN_R_FRAGMISS
+                                                                          : USN_R_NOMATCH, 0xFFFFu) |
+          USN_F_HOST;
     } else if (fl & TXR_HIT) {
       d = USN_F_CACHE;                                     // the run head's, below
     } else if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) {
@@ -1589,7 +1595,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
     } else {
-      d = decide_tx_ipv4<!LDS>(t, T, r0[r], r1[r], (uint32_t)i, ins);
+      d = decide_tx_ipv4<LDS>(t, T, r0[r], r1[r], (uint32_t)i, ins);
     }
     if (fl & TXR_FRAG1) d |= USN_F_FRAG1;                  // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge
@@ -1701,9 +1707,9 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const ClassifyArgs &a = t.a;
   if (a.ntiles == 0) return hipSuccess;
   const dim3 g(a.ntiles), b(NTHREADS);
-  const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
+  const bool in_lds = table_fits_lds(a.nbins, a.table_units);
   const size_t core = lds_core_bytes(a.nbins);
-  const size_t with_table = classify_lds_bytes(a.nbins, a.table_slots, in_lds, false);
+  const size_t with_table = classify_lds_bytes(a.nbins, a.table_units, in_lds, false);
   const size_t scan_lds =
       with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
   if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
@@ -1720,18 +1726,18 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
 #define STAGE_BYTES_GLDS ((size_t)NWAVES * GD * STAGE_ROUND_SLOTS * 16)
 
 /* LDS copy of the rule table, rounded up to whole 64-slot glds chunks. */
-static inline size_t table_lds_bytes(uint32_t table_slots) {
-  return (size_t)((table_slots + 63) & ~63u) * 16;
+static inline size_t table_lds_bytes(uint32_t table_units) {
+  return (size_t)table_lds_units(table_units) * 16;
 }
 
-bool table_fits_lds(uint32_t nbins, uint32_t table_slots) {
-  return (size_t)table_slots * 16 <= LDS_TABLE_MAX_BYTES &&
-         lds_core_bytes(nbins) + STAGE_BYTES_GLDS + table_lds_bytes(table_slots) <= 64u * 1024u;
+bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
+  return (size_t)table_units * 16 <= LDS_TABLE_MAX_BYTES &&
+         lds_core_bytes(nbins) + STAGE_BYTES_GLDS + table_lds_bytes(table_units) <= 64u * 1024u;
 }
 
 /* dynamic LDS of the classify kernels; glds: the order row is in the stage */
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool glds) {
-  return lds_core_bytes(nbins, !glds) + (table_in_lds ? table_lds_bytes(table_slots) : 0);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds) {
+  return lds_core_bytes(nbins, !glds) + (table_in_lds ? table_lds_bytes(table_units) : 0);
 }
 
 /* glds needs 16-byte aligned sources: every window start of every batch.
@@ -1753,9 +1759,9 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
-  const bool in_lds = table_fits_lds(a.nbins, a.table_slots);
+  const bool in_lds = table_fits_lds(a.nbins, a.table_units);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds_bytes(a.nbins, a.table_slots, in_lds, glds);
+  const size_t lds = classify_lds_bytes(a.nbins, a.table_units, in_lds, glds);
   const dim3 g(tiles), b(NTHREADS);
   if (in_lds && glds) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
   else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);

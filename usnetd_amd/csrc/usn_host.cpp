@@ -239,6 +239,7 @@ struct Ep {
 /* carried decision cache of one source endpoint */
 struct Chain {
   bool device_chain = false;        // previous result on the device is authoritative
+  uint32_t replica = 0;             // where the source's last batch was classified
   const usn_tile_hdr *tiles = nullptr;
   uint32_t ntiles = 0;
   const usn_summary *summary = nullptr;
@@ -255,9 +256,38 @@ struct ParsedH {   // host-side extract_pkt_info result
 
 }  // namespace
 
-struct usn_ctx {
+/* One device copy of the shared state (a usn_ctx group has one per GPU):
+ * the rule image and bridge set at the version it last uploaded, and the
+ * device scratch of a tx batch classified on it. */
+struct Replica {
   int device = 0;
   int n_cu = 0;
+  uint4 *d_table = nullptr;
+  size_t d_table_cap = 0;
+  uint64_t table_version = 0;    // image version on the device (0 = none)
+  uint64_t *d_bridge = nullptr;
+  size_t d_bridge_cap = 0;
+  unsigned long long *d_bridge_set = nullptr;   // open addressing, bit 63 = used
+  size_t d_bridge_set_cap = 0;
+  uint64_t bridge_version = 0;
+  /* tx scratch */
+  uint4 *rec = nullptr;
+  uint64_t rec_frames = 0;
+  uint32_t *aux = nullptr;
+  uint32_t aux_tiles = 0;
+  unsigned long long *macset = nullptr, *ruleset = nullptr;
+  uint32_t set_slots = 0;
+  uint4 *learned = nullptr;
+  uint32_t learned_cap = 0;
+  uint32_t *counters = nullptr;
+  uint32_t *listen = nullptr;
+  size_t listen_cap = 0;
+  uint32_t epoch = 0;
+};
+
+struct usn_ctx {
+  int device = 0;        // the selected replica's device (plumbing calls)
+  uint32_t sel = 0;      // selected replica (usn_replica_select)
   int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
   std::mutex mu;
   std::vector<Ep> eps = std::vector<Ep>(USN_MAX_ENDPOINTS);
@@ -266,42 +296,24 @@ struct usn_ctx {
   std::vector<uint64_t> bridge;
   std::unordered_map<FragKey, FragVal, FragHash> frags;
   std::vector<Chain> chains = std::vector<Chain>(USN_MAX_ENDPOINTS);
-  /* device table snapshot */
+  std::vector<Replica> reps;
+  /* host image of the device rule table (perfect hash, usn_internal.h),
+   * rebuilt from the registry when it changed; every replica uploads the
+   * current version before its next batch (the table-version fence) */
   bool table_dirty = true;
-  /* host image of the device table; inserts go straight into it while the
-   * load stays <= 1/2 (tx learning adds rules in bulk), removals rebuild */
-  std::vector<uint4> img;
-  std::vector<uint32_t> img_tags;   // per slot: usn_key_tag of its key, 0 = empty
-  bool img_valid = false;
-  uint32_t img_pmask = 0;
-  uint4 *d_table = nullptr;
-  size_t d_table_cap = 0;
-  uint4 *d_tags = nullptr;
-  size_t d_tags_cap = 0;
-  uint32_t table_slots = 0, bucket_mask = 0;
-  uint32_t probe_mask = 0;   // key shapes present in the table (ClassifyArgs::probe_mask)
+  uint64_t table_version = 0;
+  std::vector<uint4> img;          // the whole image in 16-byte units
+  usn_ph_table img_t[2] = {};
+  uint32_t probe_mask = 0;   // tables holding rules (ClassifyArgs::probe_mask)
   bool bridge_dirty = true;
-  uint64_t *d_bridge = nullptr;
-  size_t d_bridge_cap = 0;
-  unsigned long long *d_bridge_set = nullptr;   // open addressing, bit 63 = used
-  size_t d_bridge_set_cap = 0;
+  uint64_t bridge_version = 0;
+  std::vector<unsigned long long> bridge_set;
   uint32_t bridge_mask = 0;
-  /* tx scratch (one tx batch in flight per context) */
+  /* the tx batch in flight (one per context: it changes shared state) */
   struct Tx {
-    uint4 *rec = nullptr;
-    uint64_t rec_frames = 0;
-    uint32_t *aux = nullptr;
-    uint32_t aux_tiles = 0;
-    unsigned long long *macset = nullptr, *ruleset = nullptr;
-    uint32_t set_slots = 0;
-    uint4 *learned = nullptr;
-    uint32_t learned_cap = 0;
-    uint32_t *counters = nullptr;
-    uint32_t *listen = nullptr;
-    size_t listen_cap = 0;
-    uint32_t epoch = 0;
     bool pending = false;   // classified, not finalized: registry not final
     int src = -1;
+    uint32_t replica = 0;
     const uint32_t *decisions = nullptr;
   } tx;
   /* pinned staging for usn_finalize's small reads (summary, tile headers,
@@ -313,11 +325,12 @@ struct usn_ctx {
   size_t h_lists_cap = 0;
   uint4 *h_items = nullptr;      // pinned: a tx batch's learned list
   size_t h_items_cap = 0;
+  /* host frame reader: frames whose ports lie past the batch window */
+  usn_frame_reader reader = nullptr;
+  void *reader_user = nullptr;
 };
 
 namespace {
-
-#define USN_LDS_RULES_MAX 1024u   /* 2048 slots = 32 KiB: the LDS table's limit */
 
 uint32_t next_pow2(uint32_t v) {
   uint32_t p = 1;
@@ -325,60 +338,21 @@ uint32_t next_pow2(uint32_t v) {
   return p;
 }
 
-/* key shapes key1/key2 can take (ClassifyArgs::probe_mask): key1
- * (to_match_want_with_src(true)) always has src and both ports or neither;
- * key2 has neither src nor src_port.  Other shapes never match. */
-uint32_t shape_bits(const WantKey &k) {
-  uint32_t m = 0;
+/* Which table of the device image a registry key belongs to: key1
+ * (to_match_want_with_src(true), pkt.rs:96-113) always has src and both
+ * ports or neither -> K1; key2 has neither src nor src_port -> K2.  A rule of
+ * any other shape can never be hit by a frame and is left out (-1). */
+int image_table(const WantKey &k) {
   if (k.present == USN_WANT_SRC || k.present == (USN_WANT_SRC | USN_WANT_DPORT | USN_WANT_SPORT))
-    m |= 1u;
-  if (k.present == 0 || k.present == USN_WANT_DPORT) m |= 2u;
-  return m;
+    return 0;
+  if (k.present == 0 || k.present == USN_WANT_DPORT) return 1;
+  return -1;
 }
 
-void img_put(usn_ctx *c, const WantKey &k, uint16_t owner) {
-  const uint32_t nb = (uint32_t)(c->img.size() / 4);
-  const uint32_t z = (uint32_t)k.dport | ((uint32_t)k.sport << 16);
-  const uint32_t meta = usn_key_meta(k.proto, k.present);
-  const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
-  const uint32_t h = usn_key_hash(k.dst, k.src, z, meta);
-  uint32_t b = h & (nb - 1);
-  for (;;) {
-    uint4 *s = &c->img[(size_t)b * 4];
-    for (int j = 0; j < 4; ++j)
-      if (!(s[j].w & USN_SLOT_VALID)) {
-        s[j] = make_uint4(k.dst, k.src, z,
-                          meta | (nic ? USN_SLOT_NICOWNER : 0u) | ((uint32_t)owner << 16));
-        c->img_tags[(size_t)b * 4 + j] = usn_key_tag(h);
-        c->img_pmask |= shape_bits(k);
-        return;
-      }
-    b = (b + 1) & (nb - 1);
-  }
-}
-
-/* Buckets of the table image for n rules.  Up to 1024 rules (2048 slots:
- * the table is staged into LDS) the load is <= 1/2.  Larger tables are probed
- * in global memory, where a wave waits for its slowest lane's chain: there the
- * load is <= 1/4, and a probe reads its home bucket's tag line and the next
- * one together, so a chain past two buckets is rare. */
-#ifndef USN_GLOBAL_BUCKET_SHIFT
-#define USN_GLOBAL_BUCKET_SHIFT 0   /* A/B knob: global tables get n >> shift buckets */
-#endif
-uint32_t image_buckets(uint64_t n) {
-  if (n <= USN_LDS_RULES_MAX) return next_pow2(std::max<uint32_t>(2, (uint32_t)((2 * n + 3) / 4)));
-  return next_pow2(std::max<uint32_t>(512, (uint32_t)(n >> USN_GLOBAL_BUCKET_SHIFT)));
-}
-bool image_has_room(const usn_ctx *c, uint64_t n) {
-  return (uint64_t)image_buckets(n) * 4 <= c->img.size();
-}
-
-/* registry insert; keeps the host image current when it can */
+/* registry insert: the device image is rebuilt before the next batch */
 void rule_insert(usn_ctx *c, const WantKey &k, Rule r) {
   c->rules[k] = r;
   c->table_dirty = true;
-  if (c->img_valid && image_has_room(c, c->rules.size())) img_put(c, k, r.owner);
-  else c->img_valid = false;
 }
 
 /* USN_PROFILE_HOST=1: per-stage wall times of the host stages on stderr */
@@ -396,95 +370,221 @@ struct StageClock {
   }
 };
 
-/* the registry slot of k and, while inserts go straight into the image, its
- * image bucket: both are random lines in tables of 10^7..10^8 B */
-void prefetch_rule(const usn_ctx *c, const WantKey &k) {
-  c->rules.prefetch(k);
-  if (c->img_valid && !c->img.empty()) {
-    const size_t b = (WantHash()(k) & (c->img.size() / 4 - 1)) * 4;
-    __builtin_prefetch(&c->img[b], 1);
-    __builtin_prefetch(&c->img_tags[b], 1);
+/* the registry slot of k: a random line in a table of 10^7..10^8 B */
+void prefetch_rule(const usn_ctx *c, const WantKey &k) { c->rules.prefetch(k); }
+
+/* ---- perfect-hash image (hash and displace) ---------------------------------
+ * n keys go to m = n / USN_PH_LOAD slots through g = n / USN_PH_GROUP groups.
+ * Groups are placed largest first; each takes the smallest displacement d
+ * that sends all its keys to free, distinct slots (usn_ph_slot).  Lookups
+ * then read one displacement and exactly one slot. */
+#ifndef USN_PH_LOAD
+#define USN_PH_LOAD 0.85
+#endif
+#ifndef USN_PH_GROUP
+#define USN_PH_GROUP 4
+#endif
+
+struct PhKey {
+  uint4 e;         // x, y, z, meta | NICOWNER | owner << 16
+  uint32_t h2, grp;
+};
+
+bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed,
+              std::vector<uint4> &slots, std::vector<uint16_t> &disp) {
+  const uint32_t n = (uint32_t)keys.size();
+  for (PhKey &k : keys) {
+    const uint32_t meta = k.e.w & USN_KEY_META_MASK;
+    k.grp = usn_mulhi32(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed), g);
+    k.h2 = usn_key_hash2(k.e.x, k.e.y, k.e.z, meta, seed);
   }
+  /* members of each group (counting sort), then groups by size, largest first */
+  std::vector<uint32_t> start(g + 1, 0), member(n);
+  for (const PhKey &k : keys) start[k.grp + 1]++;
+  uint32_t maxsz = 0;
+  for (uint32_t i = 0; i < g; ++i) maxsz = std::max(maxsz, start[i + 1]);
+  for (uint32_t i = 0; i < g; ++i) start[i + 1] += start[i];
+  {
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) member[fill[keys[i].grp]++] = i;
+  }
+  std::vector<uint32_t> bysz(maxsz + 2, 0), order(g);
+  for (uint32_t i = 0; i < g; ++i) bysz[maxsz - (start[i + 1] - start[i]) + 1]++;
+  for (uint32_t s = 0; s <= maxsz; ++s) bysz[s + 1] += bysz[s];
+  for (uint32_t i = 0; i < g; ++i) order[bysz[maxsz - (start[i + 1] - start[i])]++] = i;
+  slots.assign(m, make_uint4(0, 0, 0, 0));
+  disp.assign(g, 0);
+  std::vector<uint8_t> used(m, 0);
+  uint32_t pos[64];
+  for (uint32_t gi : order) {
+    const uint32_t a = start[gi], sz = start[gi + 1] - a;
+    if (sz == 0) break;             // the rest are empty
+    if (sz > 64) return false;
+    uint32_t d = 0;
+    for (; d < 65536; ++d) {
+      bool ok = true;
+      for (uint32_t j = 0; j < sz && ok; ++j) {
+        const uint32_t p = usn_ph_slot(keys[member[a + j]].h2, d, m);
+        if (used[p]) { ok = false; break; }
+        for (uint32_t q = 0; q < j; ++q)
+          if (pos[q] == p) { ok = false; break; }
+        pos[j] = p;
+      }
+      if (ok) break;
+    }
+    if (d == 65536) return false;
+    disp[gi] = (uint16_t)d;
+    for (uint32_t j = 0; j < sz; ++j) {
+      used[pos[j]] = 1;
+      slots[pos[j]] = keys[member[a + j]].e;
+    }
+  }
+  return true;
 }
 
-int rebuild_table(usn_ctx *c) {
-  StageClock clk("rebuild_table");
-  if (!c->img_valid) {
-    const uint32_t n = (uint32_t)c->rules.size();
-    const uint32_t nb = image_buckets(n);
-    c->img.assign((size_t)nb * 4, make_uint4(0, 0, 0, 0));
-    c->img_tags.assign((size_t)nb * 4, 0u);
-    c->img_pmask = 0;
-    /* the image is ~10^8 B at 10^6 rules: prefetch the bucket 16 entries ahead */
-    auto ahead = c->rules.begin();
-    for (int k = 0; k < 16 && ahead != c->rules.end(); ++k) ++ahead;
-    for (const auto &kv : c->rules) {
-      if (ahead != c->rules.end()) {
-        const WantKey &a = ahead->first;
-        const uint32_t hb = usn_key_hash(a.dst, a.src, (uint32_t)a.dport | ((uint32_t)a.sport << 16),
-                                         usn_key_meta(a.proto, a.present)) & (nb - 1);
-        __builtin_prefetch(&c->img[(size_t)hb * 4], 1);
-        __builtin_prefetch(&c->img_tags[(size_t)hb * 4], 1);
-        ++ahead;
-      }
-      img_put(c, kv.first, kv.second.owner);
+/* one table of the image: m, g, seed and its slots / displacements */
+bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
+              std::vector<uint16_t> &disp) {
+  const uint32_t n = (uint32_t)keys.size();
+  t = usn_ph_table{};
+  slots.clear();
+  disp.clear();
+  if (n == 0) return true;
+  double load = USN_PH_LOAD;
+  for (uint32_t attempt = 0; attempt < 12; ++attempt) {
+    if (attempt && attempt % 3 == 0) load *= 0.9;
+    const uint32_t m = std::max<uint32_t>(n + 1, (uint32_t)((double)n / load) + 1);
+    const uint32_t g = std::max<uint32_t>(1, (n + USN_PH_GROUP - 1) / USN_PH_GROUP);
+    const uint32_t seed = 0x9E3779B9u * (attempt + 1);
+    if (ph_place(keys, m, g, seed, slots, disp)) {
+      t.m = m;
+      t.g = g;
+      t.seed = seed;
+      return true;
     }
-    c->img_valid = true;
-    clk.mark("image");
   }
-  const size_t bytes = c->img.size() * sizeof(uint4);
-  HIPCHK(hipDeviceSynchronize());   // no in-flight batch may read the old snapshot
-  if (bytes > c->d_table_cap) {
-    if (c->d_table) HIPCHK(hipFree(c->d_table));
-    c->d_table = nullptr;
-    HIPCHK(hipMalloc(&c->d_table, bytes));
-    c->d_table_cap = bytes;
+  return false;
+}
+
+/* The host image of the registry: [K1 slots][K2 slots][K1 disp][K2 disp],
+ * each part starting on a 16-byte unit. */
+int build_image(usn_ctx *c) {
+  StageClock clk("build_image");
+  std::vector<PhKey> keys[2];
+  for (const auto &kv : c->rules) {
+    const WantKey &k = kv.first;
+    const int t = image_table(k);
+    if (t < 0) continue;
+    const uint16_t owner = kv.second.owner;
+    const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
+    PhKey pk;
+    pk.e = make_uint4(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
+                      usn_key_meta(k.proto, k.present) | (nic ? USN_SLOT_NICOWNER : 0u) |
+                          ((uint32_t)owner << 16));
+    pk.h2 = pk.grp = 0;
+    keys[t].push_back(pk);
   }
-  HIPCHK(hipMemcpy(c->d_table, c->img.data(), bytes, hipMemcpyHostToDevice));
-  const size_t tbytes = c->img_tags.size() * 4;
-  if (tbytes > c->d_tags_cap) {
-    if (c->d_tags) HIPCHK(hipFree(c->d_tags));
-    c->d_tags = nullptr;
-    HIPCHK(hipMalloc(&c->d_tags, tbytes));
-    c->d_tags_cap = tbytes;
-  }
-  HIPCHK(hipMemcpy(c->d_tags, c->img_tags.data(), tbytes, hipMemcpyHostToDevice));
-  c->table_slots = (uint32_t)c->img.size();
-  c->bucket_mask = (uint32_t)(c->img.size() / 4) - 1;
-  c->probe_mask = c->img_pmask;
+  clk.mark("keys");
+  std::vector<uint4> slots[2];
+  std::vector<uint16_t> disp[2];
+  usn_ph_table t[2];
+  for (int i = 0; i < 2; ++i)
+    if (!ph_build(keys[i], t[i], slots[i], disp[i])) return USN_ENOMEM;
+  clk.mark("place");
+  const uint32_t u0 = t[0].m, u1 = t[1].m;
+  const uint32_t d0 = (t[0].g + 7) / 8, d1 = (t[1].g + 7) / 8;   // 8 u16 per 16-byte unit
+  c->img.assign((size_t)u0 + u1 + d0 + d1 + 1, make_uint4(0, 0, 0, 0));
+  std::copy(slots[0].begin(), slots[0].end(), c->img.begin());
+  std::copy(slots[1].begin(), slots[1].end(), c->img.begin() + u0);
+  uint16_t *dp = reinterpret_cast<uint16_t *>(c->img.data() + u0 + u1);
+  std::copy(disp[0].begin(), disp[0].end(), dp);
+  std::copy(disp[1].begin(), disp[1].end(), dp + (size_t)d0 * 8);
+  t[0].slot_off = 0;
+  t[1].slot_off = u0;
+  t[0].disp_off = (u0 + u1) * 8;
+  t[1].disp_off = (u0 + u1 + d0) * 8;
+  c->img_t[0] = t[0];
+  c->img_t[1] = t[1];
+  c->probe_mask = (keys[0].empty() ? 0u : 1u) | (keys[1].empty() ? 0u : 2u);
   c->table_dirty = false;
+  ++c->table_version;
+  clk.mark("image");
+  return USN_OK;
+}
+
+/* the image probe as the device computes it (usn_device.hip ph_probe) */
+uint32_t image_probe(const usn_ctx *c, int table, uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
+  const usn_ph_table &t = c->img_t[table];
+  if (!t.m) return 0;
+  const uint32_t grp = usn_mulhi32(usn_ph_h1(x, y, z, meta, t.seed), t.g);
+  const uint16_t d = reinterpret_cast<const uint16_t *>(c->img.data())[t.disp_off + grp];
+  const uint4 s = c->img[t.slot_off + usn_ph_slot(usn_key_hash2(x, y, z, meta, t.seed), d, t.m)];
+  const bool hit = s.x == x && s.y == y && s.z == z && ((s.w ^ meta) & USN_KEY_META_MASK) == 0;
+  return hit ? s.w : 0u;
+}
+
+/* the replica's device table at the current image version; no batch still
+ * in flight on that device may read the old one */
+int upload_table(usn_ctx *c, Replica &R) {
+  if (c->table_dirty) {
+    const int s = build_image(c);
+    if (s) return s;
+  }
+  if (R.table_version == c->table_version) return USN_OK;
+  StageClock clk("upload_table");
+  const size_t bytes = c->img.size() * sizeof(uint4);
+  HIPCHK(hipSetDevice(R.device));
+  HIPCHK(hipDeviceSynchronize());
+  if (bytes > R.d_table_cap) {
+    if (R.d_table) HIPCHK(hipFree(R.d_table));
+    R.d_table = nullptr;
+    HIPCHK(hipMalloc(&R.d_table, bytes));
+    R.d_table_cap = bytes;
+  }
+  HIPCHK(hipMemcpy(R.d_table, c->img.data(), bytes, hipMemcpyHostToDevice));
+  R.table_version = c->table_version;
   clk.mark("upload");
   return USN_OK;
 }
 
-int rebuild_bridge(usn_ctx *c) {
-  const size_t bytes = std::max<size_t>(8, c->bridge.size() * 8);
-  HIPCHK(hipDeviceSynchronize());
-  if (bytes > c->d_bridge_cap) {
-    if (c->d_bridge) HIPCHK(hipFree(c->d_bridge));
-    c->d_bridge = nullptr;
-    HIPCHK(hipMalloc(&c->d_bridge, bytes));
-    c->d_bridge_cap = bytes;
-  }
-  if (!c->bridge.empty())
-    HIPCHK(hipMemcpy(c->d_bridge, c->bridge.data(), c->bridge.size() * 8, hipMemcpyHostToDevice));
-  /* membership set for tx_scan (innerl2bridge.contains, endpoint.rs:195, 254) */
+/* membership set of innerl2bridge (endpoint.rs:195, 254) for tx_scan */
+void build_bridge_set(usn_ctx *c) {
   const uint32_t slots = next_pow2(std::max<uint32_t>(16, 2 * (uint32_t)c->bridge.size()));
-  std::vector<unsigned long long> set(slots, 0ull);
+  c->bridge_set.assign(slots, 0ull);
   for (uint64_t m : c->bridge) {
     uint32_t h = usn_mac_hash(m) & (slots - 1);
-    while ((set[h] >> 63) && (set[h] & 0xFFFFFFFFFFFFull) != m) h = (h + 1) & (slots - 1);
-    set[h] = (1ull << 63) | m;
+    while ((c->bridge_set[h] >> 63) && (c->bridge_set[h] & 0xFFFFFFFFFFFFull) != m)
+      h = (h + 1) & (slots - 1);
+    c->bridge_set[h] = (1ull << 63) | m;
   }
-  if (slots * 8ull > c->d_bridge_set_cap) {
-    if (c->d_bridge_set) HIPCHK(hipFree(c->d_bridge_set));
-    c->d_bridge_set = nullptr;
-    HIPCHK(hipMalloc(&c->d_bridge_set, slots * 8ull));
-    c->d_bridge_set_cap = slots * 8ull;
-  }
-  HIPCHK(hipMemcpy(c->d_bridge_set, set.data(), slots * 8ull, hipMemcpyHostToDevice));
   c->bridge_mask = slots - 1;
   c->bridge_dirty = false;
+  ++c->bridge_version;
+}
+
+int upload_bridge(usn_ctx *c, Replica &R) {
+  if (c->bridge_dirty) build_bridge_set(c);
+  if (R.bridge_version == c->bridge_version) return USN_OK;
+  HIPCHK(hipSetDevice(R.device));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t bytes = std::max<size_t>(8, c->bridge.size() * 8);
+  if (bytes > R.d_bridge_cap) {
+    if (R.d_bridge) HIPCHK(hipFree(R.d_bridge));
+    R.d_bridge = nullptr;
+    HIPCHK(hipMalloc(&R.d_bridge, bytes));
+    R.d_bridge_cap = bytes;
+  }
+  if (!c->bridge.empty())
+    HIPCHK(hipMemcpy(R.d_bridge, c->bridge.data(), c->bridge.size() * 8, hipMemcpyHostToDevice));
+  const size_t sb = c->bridge_set.size() * 8ull;
+  if (sb > R.d_bridge_set_cap) {
+    if (R.d_bridge_set) HIPCHK(hipFree(R.d_bridge_set));
+    R.d_bridge_set = nullptr;
+    HIPCHK(hipMalloc(&R.d_bridge_set, sb));
+    R.d_bridge_set_cap = sb;
+  }
+  HIPCHK(hipMemcpy(R.d_bridge_set, c->bridge_set.data(), sb, hipMemcpyHostToDevice));
+  R.bridge_version = c->bridge_version;
   return USN_OK;
 }
 
@@ -684,35 +784,66 @@ int usn_ctx_create(int hip_device, usn_ctx **out) {
     *out = c;
     return USN_OK;
   }
+  return usn_ctx_create_group(&hip_device, 1, out);
+}
+
+int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
+  if (!out || !hip_devices || n == 0 || n > USN_MAX_REPLICAS) return USN_EINVAL;
+  *out = nullptr;
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
-  if (hip_device < 0 || hip_device >= ndev) return USN_ENODEV;
-  hipDeviceProp_t prop;
-  HIPCHK(hipGetDeviceProperties(&prop, hip_device));
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return USN_ENODEV;
-  HIPCHK(hipSetDevice(hip_device));
+  std::vector<Replica> reps(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const int d = hip_devices[i];
+    if (d < 0 || d >= ndev) return USN_ENODEV;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, d));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return USN_ENODEV;
+    reps[i].device = d;
+    reps[i].n_cu = prop.multiProcessorCount;
+  }
+  HIPCHK(hipSetDevice(hip_devices[0]));
   usn_ctx *c = new (std::nothrow) usn_ctx();
   if (!c) return USN_ENOMEM;
-  c->device = hip_device;
-  c->n_cu = prop.multiProcessorCount;
+  c->reps.swap(reps);
+  c->device = hip_devices[0];
   if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
   *out = c;
   return USN_OK;
 }
 
+int usn_ctx_replicas(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  return (int)c->reps.size();
+}
+
+int usn_replica_select(usn_ctx *c, uint32_t replica) {
+  if (!c) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
+  if (replica >= c->reps.size()) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->sel = replica;
+  c->device = c->reps[replica].device;
+  HIPCHK(hipSetDevice(c->device));
+  return USN_OK;
+}
+
+int usn_replica_device(usn_ctx *c, uint32_t replica) {
+  if (!c) return USN_EINVAL;
+  if (replica >= c->reps.size()) return USN_EINVAL;
+  return c->reps[replica].device;
+}
+
 void usn_ctx_destroy(usn_ctx *c) {
   if (!c) return;
-  if (c->device < 0) { delete c; return; }
-  (void)hipSetDevice(c->device);
-  (void)hipDeviceSynchronize();
-  if (c->d_table) (void)hipFree(c->d_table);
-  if (c->d_bridge) (void)hipFree(c->d_bridge);
-  if (c->d_tags) (void)hipFree(c->d_tags);
-  if (c->d_bridge_set) (void)hipFree(c->d_bridge_set);
-  for (void *p : {(void *)c->tx.rec, (void *)c->tx.aux, (void *)c->tx.macset,
-                  (void *)c->tx.ruleset, (void *)c->tx.learned, (void *)c->tx.counters,
-                  (void *)c->tx.listen})
-    if (p) (void)hipFree(p);
+  for (Replica &R : c->reps) {
+    (void)hipSetDevice(R.device);
+    (void)hipDeviceSynchronize();
+    for (void *p : {(void *)R.d_table, (void *)R.d_bridge, (void *)R.d_bridge_set, (void *)R.rec,
+                    (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
+                    (void *)R.counters, (void *)R.listen})
+      if (p) (void)hipFree(p);
+  }
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
   if (c->h_items) (void)hipHostFree(c->h_items);
@@ -747,7 +878,6 @@ int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
     if (it->second.owner == id) {
       it = c->rules.erase(it);
       c->table_dirty = true;
-      c->img_valid = false;
     } else {
       ++it;
     }
@@ -783,7 +913,6 @@ int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
   if (it->second.owner != requester) return USN_EPERM;               // main.rs:612-616
   c->rules.erase(it);
   c->table_dirty = true;
-  c->img_valid = false;
   return 1;
 }
 
@@ -869,7 +998,6 @@ int usn_table_build(usn_ctx *c, const usn_rule *rules, uint32_t n) {
   for (int e = 0; e < USN_MAX_ENDPOINTS; ++e)
     if (c->eps[e].used && c->eps[e].kind == USN_EP_NIC) cache_clear(c, e);
   c->table_dirty = true;
-  c->img_valid = false;
   return (int)c->rules.size();
 }
 
@@ -885,6 +1013,42 @@ int usn_frag_clear(usn_ctx *c) {
   std::lock_guard<std::mutex> g(c->mu);
   if (c->tx.pending) return USN_EBUSY;
   c->frags.clear();
+  return USN_OK;
+}
+
+int usn_set_frame_reader(usn_ctx *c, usn_frame_reader fn, void *user) {
+  if (!c) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->reader = fn;
+  c->reader_user = user;
+  return USN_OK;
+}
+
+/* Test hook (not in the public header): the device image's lookup of one
+ * packed key, computed on the host image (table 0 = K1, 1 = K2).  Builds
+ * the image if the registry changed.  Returns the slot's meta word, 0 = miss. */
+int64_t usn_debug_image_probe(usn_ctx *c, int table, uint32_t x, uint32_t y, uint32_t z,
+                              uint32_t meta) {
+  if (!c || table < 0 || table > 1) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->table_dirty) {
+    const int s = build_image(c);
+    if (s) return s;
+  }
+  return (int64_t)image_probe(c, table, x, y, z, meta);
+}
+
+/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask}. */
+int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
+  if (!c || !out6) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->table_dirty) {
+    const int s = build_image(c);
+    if (s) return s;
+  }
+  out6[0] = c->img_t[0].m; out6[1] = c->img_t[0].g;
+  out6[2] = c->img_t[1].m; out6[3] = c->img_t[1].g;
+  out6[4] = (uint32_t)c->img.size(); out6[5] = c->probe_mask;
   return USN_OK;
 }
 
@@ -934,7 +1098,8 @@ int usn_result_bind(void *mem, size_t bytes, uint64_t n, usn_result *out) {
 }
 
 /* ---- the hot path ----------------------------------------------------------- */
-static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, ClassifyArgs &a) {
+static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn_result *r,
+                     ClassifyArgs &a) {
   std::memset(&a, 0, sizeof a);
   a.frames = b->frames;
   a.stride = b->stride;
@@ -942,17 +1107,18 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   a.lens = b->lens;
   a.n = b->n;
   a.ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
+  a.window = b->window ? b->window : USN_WINDOW;
   a.decisions = r->decisions;
   a.order = r->order;
   a.runs = r->runs;
   a.tiles = r->tiles;
   a.summary = r->summary;
   a.host_list = r->host_list;
-  a.table = c->d_table;
-  a.tags = c->d_tags;
-  a.bucket_mask = c->bucket_mask;
-  a.table_slots = c->table_slots;
-  a.bridge = c->d_bridge;
+  a.table = R.d_table;
+  a.table_units = (uint32_t)c->img.size();
+  a.ph[0] = c->img_t[0];
+  a.ph[1] = c->img_t[1];
+  a.bridge = R.d_bridge;
   a.n_bridge = (uint32_t)c->bridge.size();
   const Ep &S = c->eps[b->src_endpoint];
   a.src = b->src_endpoint;
@@ -967,34 +1133,34 @@ static int fill_args(usn_ctx *c, const usn_batch *b, const usn_result *r, Classi
   return USN_OK;
 }
 
-/* global-memory tables above this many slots (256 KiB) classify with 512
- * threads per tile (A/B: c5's 65536 rules 1.55x faster; c4's 4096 equal) */
-#define USN_T512_MIN_SLOTS 16384u
-
-/* 512 threads per tile (two rounds per lane) when the table is in LDS for
- * both builds (c1/c2: 3 % faster), never when only the 256-thread build can
- * keep it in LDS (its stage is half as big; c3: 2 % slower in L2), and for
- * large global tables. */
-static bool use_t512(uint32_t nbins, uint32_t slots) {
-  if (usn_t512::table_fits_lds(nbins, slots)) return true;
-  if (usn::table_fits_lds(nbins, slots)) return false;
-  return slots > USN_T512_MIN_SLOTS;
+/* 512 threads per tile (two rounds per lane) when the rule image is in LDS
+ * for both builds (c1/c2: 3 % faster), never when only the 256-thread build
+ * can keep it in LDS (its stage is half as big), and for global images
+ * above USN_T512_MIN_UNITS 16-byte units. */
+#ifndef USN_T512_MIN_UNITS
+#define USN_T512_MIN_UNITS 16384u
+#endif
+static bool use_t512(uint32_t nbins, uint32_t units) {
+  if (usn_t512::table_fits_lds(nbins, units)) return true;
+  if (usn::table_fits_lds(nbins, units)) return false;
+  return units > USN_T512_MIN_UNITS;
 }
 
 static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
   if (!b || !r || !b->frames || !b->lens || b->n == 0 || r->n < b->n) return USN_EINVAL;
   if ((b->stride == 0) == (b->offsets == nullptr)) return USN_EINVAL;
-  if (b->stride && (b->stride % 16 != 0 || b->stride < USN_WINDOW)) return USN_EINVAL;
+  const uint32_t window = b->window ? b->window : USN_WINDOW;
+  if (window < USN_WINDOW) return USN_EINVAL;   // the header loads read 64 bytes
+  if (b->stride && (b->stride % 16 != 0 || b->stride < window)) return USN_EINVAL;
   if (((uintptr_t)b->frames & 15) != 0) return USN_EINVAL;
   if (b->n > 0xFFFFFFFFull) return USN_ERANGE;
   if (b->src_endpoint >= USN_MAX_ENDPOINTS || !c->eps[b->src_endpoint].used) return USN_EINVAL;
   return USN_OK;
 }
 
-/* device scratch of a tx batch of n frames; the epoch-tagged sets are
- * cleared only when (re)allocated or when the 16-bit epoch wraps */
-static int tx_prepare(usn_ctx *c, uint64_t n, uint32_t ntiles) {
-  usn_ctx::Tx &T = c->tx;
+/* device scratch of a tx batch of n frames on replica R; the epoch-tagged
+ * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
+static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
   if (n > T.rec_frames) {
     if (T.rec) HIPCHK(hipFree(T.rec));
     if (T.learned) HIPCHK(hipFree(T.learned));
@@ -1032,7 +1198,7 @@ static int tx_prepare(usn_ctx *c, uint64_t n, uint32_t ntiles) {
 }
 
 /* S.listening as {dst, proto | has_port << 8 | port << 16} words on the device */
-static int tx_listen(usn_ctx *c, const Ep &S, uint32_t &n_listen) {
+static int tx_listen(Replica &T, const Ep &S, uint32_t &n_listen) {
   std::vector<uint32_t> v;
   for (const Listen &l : S.listening) {
     v.push_back(l.dst);
@@ -1040,20 +1206,56 @@ static int tx_listen(usn_ctx *c, const Ep &S, uint32_t &n_listen) {
   }
   n_listen = (uint32_t)S.listening.size();
   if (v.empty()) return USN_OK;
-  if (v.size() * 4 > c->tx.listen_cap) {
-    if (c->tx.listen) HIPCHK(hipFree(c->tx.listen));
-    c->tx.listen = nullptr;
-    HIPCHK(hipMalloc(&c->tx.listen, v.size() * 4));
-    c->tx.listen_cap = v.size() * 4;
+  if (v.size() * 4 > T.listen_cap) {
+    if (T.listen) HIPCHK(hipFree(T.listen));
+    T.listen = nullptr;
+    HIPCHK(hipMalloc(&T.listen, v.size() * 4));
+    T.listen_cap = v.size() * 4;
   }
-  HIPCHK(hipMemcpy(c->tx.listen, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.listen, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  return USN_OK;
+}
+
+/* A source's carried cache whose last batch ran on another replica (another
+ * device): resolve it on the host from that batch's summary and tile headers,
+ * as the kernel's resolve_carry would. */
+static int chain_to_host(usn_ctx *c, Chain &ch) {
+  HIPCHK(hipSetDevice(c->reps[ch.replica].device));
+  usn_summary ps;
+  HIPCHK(hipMemcpy(&ps, ch.summary, sizeof ps, hipMemcpyDeviceToHost));
+  uint32_t st = 0, dst = 0, info[4] = {0, 0, 0, 0};
+  if (ps.flags & USN_S_COUT) {
+    st = ps.cout_state; dst = ps.cout_dst;
+    std::memcpy(info, ps.cout_info, 16);
+  } else {
+    std::vector<usn_tile_hdr> th(ch.ntiles);
+    if (ch.ntiles)
+      HIPCHK(hipMemcpy(th.data(), ch.tiles, ch.ntiles * sizeof(usn_tile_hdr), hipMemcpyDeviceToHost));
+    int best = -1;
+    for (uint32_t t = 0; t < ch.ntiles; ++t)
+      if (th[t].last_state & USN_TS_HAS) best = (int)t;
+    if (best >= 0) {
+      const usn_tile_hdr &h = th[best];
+      if ((h.last_state & USN_TS_RETAINED) && !(h.last_state & USN_TS_UNKNOWN)) {
+        st = USN_CS_VALID; dst = h.last_dst;
+        std::memcpy(info, h.last_info, 16);
+      }
+    } else {
+      st = ps.cin_state; dst = ps.cin_dst;
+      std::memcpy(info, ps.cin_info, 16);
+    }
+  }
+  ch.device_chain = false;
+  ch.state = st;
+  ch.dst = dst;
+  std::memcpy(ch.info, info, 16);
   return USN_OK;
 }
 
 int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t count,
                        void *stream) {
   if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
-  if (c->device < 0) return USN_ENODEV;
+  if (c->reps.empty()) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
   if (c->tx.pending) return USN_EBUSY;
   bool tx = false;
@@ -1065,15 +1267,23 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       if (b[j].src_endpoint == b[k].src_endpoint) return USN_EINVAL;   // one batch per source
   }
   if (tx && count != 1) return USN_EINVAL;   // a tx batch changes shared state: alone
-  HIPCHK(hipSetDevice(c->device));
-  if (c->table_dirty) { int s = rebuild_table(c); if (s) return s; }
-  if (c->bridge_dirty) { int s = rebuild_bridge(c); if (s) return s; }
+  const uint32_t rep = c->sel;
+  Replica &R = c->reps[rep];
+  /* the table-version fence: this replica sees every registry and bridge
+   * change made before this call */
+  { int s = upload_table(c, R); if (s) return s; }
+  { int s = upload_bridge(c, R); if (s) return s; }
+  for (uint32_t k = 0; k < count; ++k) {
+    Chain &ch = c->chains[b[k].src_endpoint];
+    if (ch.device_chain && ch.replica != rep) { int s = chain_to_host(c, ch); if (s) return s; }
+  }
+  HIPCHK(hipSetDevice(R.device));
   usn::MultiArgs m;
   std::memset(&m, 0, sizeof m);
   m.count = count;
   for (uint32_t k = 0; k < count; ++k) {
     ClassifyArgs &a = m.b[k];
-    fill_args(c, &b[k], &r[k], a);
+    fill_args(c, R, &b[k], &r[k], a);
     Chain &ch = c->chains[b[k].src_endpoint];
     if (ch.device_chain) {
       a.carry_mode = usn::CARRY_CHAIN;
@@ -1090,31 +1300,32 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   }
   if (tx) {
     const usn_batch &tb = b[0];
-    int st = tx_prepare(c, tb.n, m.b[0].ntiles);
+    int st = tx_prepare(R, tb.n, m.b[0].ntiles);
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
     t.a = m.b[0];
-    st = tx_listen(c, c->eps[tb.src_endpoint], t.n_listen);
+    st = tx_listen(R, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
-    t.rec = c->tx.rec;
-    t.aux = c->tx.aux;
-    t.macset = c->tx.macset;
-    t.ruleset = c->tx.ruleset;
-    t.macset_mask = t.ruleset_mask = c->tx.set_slots - 1;
-    t.epoch = c->tx.epoch;
-    t.learned = c->tx.learned;
-    t.counters = c->tx.counters;
-    t.learned_cap = c->tx.learned_cap;
-    t.bridge_set = c->d_bridge_set;
+    t.rec = R.rec;
+    t.aux = R.aux;
+    t.macset = R.macset;
+    t.ruleset = R.ruleset;
+    t.macset_mask = t.ruleset_mask = R.set_slots - 1;
+    t.epoch = R.epoch;
+    t.learned = R.learned;
+    t.counters = R.counters;
+    t.learned_cap = R.learned_cap;
+    t.bridge_set = R.d_bridge_set;
     t.bridge_mask = c->bridge_mask;
-    t.listen = c->tx.listen;
+    t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
     HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tx_scan zeroes t.counters
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
+    c->tx.replica = rep;
     c->tx.decisions = r[0].decisions;
-  } else if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_slots))) {
+  } else if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units))) {
     HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
   } else {
     HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
@@ -1122,6 +1333,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   for (uint32_t k = 0; k < count; ++k) {
     Chain &ch = c->chains[b[k].src_endpoint];
     ch.device_chain = true;
+    ch.replica = rep;
     ch.tiles = r[k].tiles;
     ch.ntiles = m.b[k].ntiles;
     ch.summary = r[k].summary;
@@ -1135,6 +1347,27 @@ int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
 
 /* ---- ordered host stage --------------------------------------------------- */
 namespace {
+
+uint32_t batch_window(const usn_batch *b) { return b->window ? b->window : USN_WINDOW; }
+
+/* extract_pkt_info would read the L4 ports (pkt.rs:177-186, bytes 14+hl ..
+ * 17+hl) past the first `have` bytes of this frame: the kernel's status 5 */
+bool ports_past(const uint8_t *f, uint32_t len, uint32_t have) {
+  if (len < 34 || be16(f + 12) != 0x0800) return false;
+  const uint32_t n = len - 14, hl = (f[14] & 0x0Fu) * 4, tl = be16(f + 16);
+  if (n < hl || hl > tl || n < tl || (be16(f + 20) & 0x1FFF)) return false;
+  const uint32_t proto = f[23];
+  const bool pp = proto == 6 || proto == 17 || proto == 0x21 || proto == 0x84 || proto == 0x88;
+  return pp && (tl - hl) > 4 && 18 + hl > have;
+}
+
+/* frames the device left to the host because their ports lie past the
+ * window need the host frame reader */
+bool needs_reader(const std::vector<uint32_t> &dec, const std::vector<uint32_t> &hosts) {
+  for (uint32_t j : hosts)
+    if (USN_DEC_REASON(dec[j]) == USN_R_WINDOW && (dec[j] & USN_F_HOST)) return true;
+  return false;
+}
 
 struct HostView {   // lazily fetched device data of one batch
   usn_ctx *c;
@@ -1159,7 +1392,9 @@ struct HostView {   // lazily fetched device data of one batch
     have_lens = true;
     return USN_OK;
   }
-  /* frame bytes [0, max(64, min(len, 80))) of frame i */
+  /* the bytes of frame i that extract_pkt_info reads: the batch window from
+   * the device, or, when its ports lie past the window, min(len, 80) bytes
+   * from the host frame reader (usn_set_frame_reader) */
   int frame(uint64_t i, std::vector<uint8_t> &buf, uint32_t &len) {
     int s = fetch_lens();
     if (s) return s;
@@ -1167,9 +1402,14 @@ struct HostView {   // lazily fetched device data of one batch
     uint64_t off;
     if (b->offsets) HIPCHK(hipMemcpy(&off, b->offsets + i, 8, hipMemcpyDeviceToHost));
     else off = i * b->stride;
-    const uint32_t want = std::max<uint32_t>(USN_WINDOW, std::min<uint32_t>(len, 80));
-    buf.assign(want, 0);
-    HIPCHK(hipMemcpy(buf.data(), b->frames + off, want, hipMemcpyDeviceToHost));
+    const uint32_t have = std::min<uint32_t>(batch_window(b), USN_WINDOW_MAX);
+    buf.assign(USN_WINDOW_MAX, 0);
+    HIPCHK(hipMemcpy(buf.data(), b->frames + off, have, hipMemcpyDeviceToHost));
+    if (ports_past(buf.data(), len, have)) {
+      if (!c->reader) return USN_EINVAL;
+      const int got = c->reader(c->reader_user, b->src_endpoint, i, buf.data(), USN_WINDOW_MAX);
+      if (got < 0 || (uint32_t)got < std::min<uint32_t>(len, USN_WINDOW_MAX)) return USN_EINVAL;
+    }
     return USN_OK;
   }
 };
@@ -1187,7 +1427,8 @@ bool retains(uint32_t d) {
 /* summary + tile headers (+ the tx counters when cnt) of a classified batch,
  * through the context's pinned staging buffer on stream s */
 int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
-                      usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt) {
+                      usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
+                      const uint32_t *d_counters = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
   const size_t need = sizeof(usn_summary) + tb + 16;
   if (need > c->h_stage_cap) {
@@ -1202,7 +1443,7 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   HIPCHK(hipMemcpyAsync(p, r->summary, sizeof(usn_summary), hipMemcpyDeviceToHost, s));
   if (tb) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary), r->tiles, tb, hipMemcpyDeviceToHost, s));
   if (cnt)
-    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, c->tx.counters, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, 16, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   std::memcpy(&sum, p, sizeof sum);
   th.resize(ntiles);
@@ -1293,11 +1534,12 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   const uint32_t ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
   const int src = b->src_endpoint;
   Ep &S = c->eps[src];
+  Replica &R = c->reps[c->tx.replica];
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[4];
   {
-    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt);
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters);
     if (e) return e;
   }
   clk.mark("state");
@@ -1317,6 +1559,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   HostView hv{c, b, r, s, {}, {}, false, false};
   st = hv.fetch_dec();
   if (st) return st;
+  if (!c->reader && needs_reader(hv.dec, hosts)) return USN_EINVAL;   // before any side effect
   clk.mark("decisions");
   uint64_t h = n;
   if (cnt[1]) h = 0;
@@ -1324,7 +1567,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     for (uint32_t j : hosts)
       if (hv.dec[j] & USN_F_HOST) { h = j; break; }
   /* learned items and first fragments before h, in frame order */
-  const uint32_t nl = std::min(cnt[0], c->tx.learned_cap);
+  const uint32_t nl = std::min(cnt[0], R.learned_cap);
   const uint4 *items = nullptr;   // the learned list, through pinned memory
   if (nl) {
     const size_t bytes = (size_t)nl * 2 * sizeof(uint4);
@@ -1336,7 +1579,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_items), cap, hipHostMallocDefault));
       c->h_items_cap = cap;
     }
-    HIPCHK(hipMemcpyAsync(c->h_items, c->tx.learned, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_items, R.learned, bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     items = c->h_items;
   }
@@ -1427,10 +1670,11 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       break;
     }
     /* frames [h, n): one strided gather of their header windows */
-    const uint32_t W = 80;
+    const uint32_t W = USN_WINDOW_MAX;
     std::vector<uint8_t> win;
     const bool strided = b->stride != 0;
-    const uint32_t width = strided ? (uint32_t)std::min<uint64_t>(b->stride, W) : 0;
+    const uint32_t width =
+        strided ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(b->stride, batch_window(b)), W) : 0;
     st = hv.fetch_lens();
     if (st) return st;
     if (strided) {
@@ -1441,7 +1685,8 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     std::vector<uint32_t> out(n - h);
     for (uint64_t j = h; j < n; ++j) {
       const uint8_t *fp;
-      if (strided && (hv.lens[j] <= width || width == W)) {
+      if (strided && (hv.lens[j] <= width || width == W ||
+                      !ports_past(win.data() + (size_t)(j - h) * W, hv.lens[j], width))) {
         fp = win.data() + (size_t)(j - h) * W;
         len = hv.lens[j];
       } else {
@@ -1461,7 +1706,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     fi.n_host = (uint32_t)(n - h);
     HIPCHK(hipMemcpy(r->decisions + h, out.data(), out.size() * 4, hipMemcpyHostToDevice));
     ClassifyArgs a;
-    fill_args(c, b, r, a);
+    fill_args(c, R, b, r, a);
     HIPCHK(usn::launch_resort(a, (uint32_t)(h / USN_TILE), ntiles, s));
     usn_summary o = sum;
     o.flags |= USN_S_COUT;
@@ -1477,10 +1722,12 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
 
 int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
                  usn_finalize_info *info) {
-  if (!c || !b || !r || b->n == 0) return USN_EINVAL;
-  if (c->device < 0) return USN_ENODEV;
+  if (!c || !b || !r || b->n == 0 || b->src_endpoint >= USN_MAX_ENDPOINTS) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  const bool txb = c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions;
+  const uint32_t rep = txb ? c->tx.replica : c->chains[b->src_endpoint].replica;
+  HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
   if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
@@ -1527,6 +1774,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HostView hv{c, b, r, s, {}, {}, false, false};
   int st = hv.fetch_dec();
   if (st) return st;
+  if (!c->reader && needs_reader(hv.dec, hosts)) return USN_EINVAL;   // before any side effect
   std::vector<uint8_t> buf;
   uint32_t len = 0;
   std::vector<char> dirty(ntiles, 0);
@@ -1605,7 +1853,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   if (st) return st;
   /* patched tiles: rebuild their order / runs / counts */
   ClassifyArgs a;
-  fill_args(c, b, r, a);
+  fill_args(c, c->reps[rep], b, r, a);
   for (uint32_t t = 0; t < ntiles;) {
     if (!dirty[t]) { ++t; continue; }
     uint32_t e = t;

@@ -71,6 +71,50 @@ USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) 
   return h;
 }
 
+/* ---- perfect-hash rule image (hash-and-displace) ------------------------
+ * The device image holds two tables: K1 = the rules key1 can hit (present
+ * SRC or SRC|DPORT|SPORT), K2 = the rules key2 can hit (present 0 or DPORT);
+ * rules of any other shape never match a frame and are not in the image.
+ * Each table: m slots (16 B, the packed key above) and g 16-bit displacements.
+ * A key's group is mulhi(h1, g); its slot is usn_ph_slot(h2, disp[group], m),
+ * so a probe is one displacement read and ONE slot read, hit or miss. */
+USN_HD uint32_t usn_mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+USN_HD uint32_t usn_fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+/* second key hash, independent of usn_key_hash (other multipliers) */
+USN_HD uint32_t usn_key_hash2(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uint32_t seed) {
+  uint32_t h = (x ^ seed) * 0xCC9E2D51u;
+  h = usn_rotl32(h, 15) ^ (y * 0x1B873593u);
+  h = usn_rotl32(h, 13) * 5u + 0xE6546B64u;
+  h ^= usn_rotl32(z * 0x85EBCA77u, 17);
+  h ^= (meta + seed) * 0x165667B1u;
+  return usn_fmix32(h);
+}
+USN_HD uint32_t usn_ph_h1(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uint32_t seed) {
+  return usn_key_hash(x, y ^ seed, z, meta);
+}
+USN_HD uint32_t usn_ph_slot(uint32_t h2, uint32_t d, uint32_t m) {
+  return usn_mulhi32(usn_fmix32(h2 + d * 0x9E3779B9u), m);
+}
+
+/* one table of the image, in 16-byte units / u16 units from the image base */
+typedef struct {
+  uint32_t slot_off;   /* first slot (16-B units) */
+  uint32_t m;          /* slots */
+  uint32_t disp_off;   /* first displacement (u16 units) */
+  uint32_t g;          /* groups */
+  uint32_t seed;
+  uint32_t _pad[3];
+} usn_ph_table;
+
 /* 32-bit tag of a key in the tag array of a global-memory table (0 = empty) */
 USN_HD uint32_t usn_key_tag(uint32_t h) { return h | 1u; }
 

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "../../include/usn_classify.h"
+#include "usn_internal.h"
 
 namespace usn {
 
@@ -22,6 +23,7 @@ struct ClassifyArgs {
   const uint16_t *lens;
   uint64_t n;
   uint32_t ntiles;
+  uint32_t window;          /* readable bytes at every frame start (usn_batch.window) */
   /* outputs */
   uint32_t *decisions;
   uint16_t *order;
@@ -29,11 +31,10 @@ struct ClassifyArgs {
   usn_tile_hdr *tiles;
   usn_summary *summary;
   uint32_t *host_list;      /* per tile USN_TILE slots */
-  /* rule table: nbuckets * 4 slots of uint4 */
+  /* rule image (usn_internal.h): K1 / K2 perfect-hash tables in one buffer */
   const uint4 *table;
-  const uint4 *tags;        /* per bucket: the 4 slots' key tags (global-memory probes) */
-  uint32_t bucket_mask;
-  uint32_t table_slots;
+  uint32_t table_units;     /* 16-byte units of the whole image */
+  usn_ph_table ph[2];       /* K1 (key1 shapes), K2 (key2 shapes) */
   /* inner L2 bridge (tx): MACs in the low 48 bits */
   const uint64_t *bridge;
   uint32_t n_bridge;
@@ -44,7 +45,7 @@ struct ClassifyArgs {
   uint32_t nbins;           /* endpoints + 3 */
   uint32_t nbits;           /* bits to tell bins apart (ceil log2 nbins) */
   uint32_t n_ep;            /* endpoints (bin of NIC) */
-  uint32_t probe_mask;      /* bit0: rules key1 can hit exist; bit1: rules key2 can hit */
+  uint32_t probe_mask;      /* bit0: K1 holds rules; bit1: K2 holds rules */
   uint32_t next_dhcp_set;   /* the source's next_dhcp_endpoint is Some: DHCP answers need the host */
   /* carried 1-entry decision cache */
   uint32_t carry_mode;
@@ -80,6 +81,7 @@ struct MultiArgs {
 #define TXR_HIT (1u << 27)       /* 1-entry cache hit (set by tx_hits) */
 #define TXR_DHCPANS (1u << 28)
 #define TXR_FRAG1 (1u << 29)     /* first fragment: extract_pkt_info remembers it (host map) */
+#define TXR_WINDOW (1u << 30)    /* L4 ports lie past the batch window: the host reads the frame */
 #define TXR_I0_MASK 0x1FFFFu
 
 struct TxArgs {
@@ -104,8 +106,8 @@ struct TxArgs {
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
-size_t classify_lds_bytes(uint32_t nbins, uint32_t table_slots, bool table_in_lds, bool glds);
-bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
+size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds);
+bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
 /* Rebuild order/runs/counts of tiles [t0, t1) from the (patched) decisions. */
@@ -117,7 +119,7 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
-bool table_fits_lds(uint32_t nbins, uint32_t table_slots);
+bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }
 
 #endif

@@ -804,6 +804,7 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
     std::memset(&b, 0, sizeof b);
     b.frames = d_hdr_ + (size_t)s.start * HDR;
     b.stride = HDR;
+    b.window = HDR;                // whole 128-byte windows: never past USN_WINDOW_MAX
     b.lens = d_lens_ + s.start;
     b.n = s.n;
     b.src_endpoint = s.dev->id;

@@ -16,7 +16,9 @@ LIB_PATH = os.path.join(HERE, "libusn.so")
 
 USN_TILE = 1024
 USN_WINDOW = 64
-USN_MAX_ENDPOINTS = 1021
+USN_WINDOW_MAX = 80
+USN_MAX_ENDPOINTS = 4095
+R_WINDOW = 7
 PARITY_MASK = 0x00FFFFFF
 EP_NIC, EP_HOST, EP_PIPE, EP_UDS = 0, 1, 2, 3
 CLS_DROP, CLS_EP, CLS_NIC, CLS_FLOOD = 0, 1, 2, 3
@@ -41,7 +43,12 @@ class Want(C.Structure):
 class Batch(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("stride", C.c_uint64), ("offsets", C.c_void_p),
                 ("lens", C.c_void_p), ("n", C.c_uint64), ("src_endpoint", C.c_uint16),
-                ("_reserved", C.c_uint16 * 3)]
+                ("window", C.c_uint16), ("_reserved", C.c_uint16 * 2)]
+
+
+# int (*usn_frame_reader)(void *user, uint16_t src, uint64_t index, uint8_t *out, uint32_t cap)
+FRAME_READER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint16, C.c_uint64, C.POINTER(C.c_uint8),
+                           C.c_uint32)
 
 
 class Result(C.Structure):
@@ -110,8 +117,16 @@ def load(path: str | None = None):
         "usn_event_elapsed_ms": ([P, P, P, C.POINTER(C.c_float)], I),
         "usn_stream_wait_event": ([P, P, P], I),
         "usn_classify_multi": ([P, P, P, U32, P], I),
+        "usn_set_frame_reader": ([P, FRAME_READER, P], I),
+        "usn_ctx_create_group": ([P, U32, C.POINTER(P)], I),
+        "usn_ctx_replicas": ([P], I), "usn_replica_select": ([P, U32], I),
+        "usn_replica_device": ([P, U32], I),
     }
+    optional = {"usn_set_frame_reader", "usn_ctx_create_group", "usn_ctx_replicas",
+                "usn_replica_select", "usn_replica_device"}   # A/B builds of older ABI versions lack these
     for name, (args, res) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -128,7 +143,8 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
             "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
             "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi",
-            "usn_bridge_set", "usn_table_build"]
+            "usn_bridge_set", "usn_table_build", "usn_set_frame_reader", "usn_ctx_create_group",
+            "usn_ctx_replicas", "usn_replica_select", "usn_replica_device"]
 
 
 def check(rc, what=""):
@@ -206,12 +222,28 @@ class DevBuf:
 class Ctx:
     """One usn_ctx bound to one gfx950 device (the daemon's match state)."""
 
-    def __init__(self, device: int = 0, libpath: str | None = None):
+    def __init__(self, device: int = 0, libpath: str | None = None, devices=None):
+        """devices: a list of HIP devices -> one registry with a device
+        replica per entry (usn_ctx_create_group); replica 0 is selected."""
         self.L = load(libpath)
         h = C.c_void_p()
-        check(self.L.usn_ctx_create(device, C.byref(h)), "usn_ctx_create")
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            check(self.L.usn_ctx_create_group(C.cast(arr, C.c_void_p), len(devices), C.byref(h)),
+                  "usn_ctx_create_group")
+            device = devices[0]
+        else:
+            check(self.L.usn_ctx_create(device, C.byref(h)), "usn_ctx_create")
         self.h = h.value
         self.device = device
+
+    def replicas(self) -> int:
+        return check(self.L.usn_ctx_replicas(self.h), "usn_ctx_replicas")
+
+    def select(self, replica: int):
+        """Classify and device plumbing act on this replica from now on."""
+        check(self.L.usn_replica_select(self.h, replica), "usn_replica_select")
+        self.device = check(self.L.usn_replica_device(self.h, replica), "usn_replica_device")
 
     def close(self):
         if self.h:
@@ -275,6 +307,25 @@ class Ctx:
     def cache_clear(self, eid):
         check(self.L.usn_cache_clear(self.h, eid), "usn_cache_clear")
 
+    def set_frame_reader(self, fn):
+        """fn(src_endpoint, index) -> bytes of that frame of the batch being
+        finalized (the host copy, whole or its first USN_WINDOW_MAX bytes);
+        None unregisters.  The ctypes callback is kept alive on the Ctx."""
+        if fn is None:
+            self._reader = None
+            check(self.L.usn_set_frame_reader(self.h, FRAME_READER(), None), "usn_set_frame_reader")
+            return
+
+        def cb(user, src, index, out, cap):
+            try:
+                data = bytes(fn(int(src), int(index)))[:cap]
+            except Exception:
+                return -1
+            C.memmove(out, data, len(data))
+            return len(data)
+        self._reader = FRAME_READER(cb)
+        check(self.L.usn_set_frame_reader(self.h, self._reader, None), "usn_set_frame_reader")
+
     # --- plumbing ---------------------------------------------------------------
     def alloc(self, nbytes) -> DevBuf:
         return DevBuf(self, nbytes)
@@ -322,7 +373,10 @@ class DeviceBatch:
     """Frames + lengths resident in HBM (one drained rx ring)."""
 
     def __init__(self, ctx: Ctx, frames: np.ndarray, lens: np.ndarray, src: int,
-                 stride: int = 0, offsets: np.ndarray | None = None, pad: int = USN_WINDOW):
+                 stride: int = 0, offsets: np.ndarray | None = None, pad: int = USN_WINDOW,
+                 window: int | None = None):
+        """window: readable bytes of each frame at its start (usn_batch.window);
+        default min(stride, 2048) for strided layouts, USN_WINDOW for offsets."""
         frames = np.ascontiguousarray(frames, dtype=np.uint8).reshape(-1)
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         self.n = int(lens.shape[0])
@@ -336,6 +390,9 @@ class DeviceBatch:
         self.desc.lens = self.lbuf.ptr
         self.desc.n = self.n
         self.desc.src_endpoint = src
+        if window is None:
+            window = min(int(stride), 2048) if offsets is None and stride else USN_WINDOW
+        self.desc.window = window
         if offsets is not None:
             offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
             self.obuf = ctx.alloc(offsets.nbytes)

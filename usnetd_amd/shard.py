@@ -19,6 +19,13 @@ def rank_queues(total_queues: int, world: int, rank: int) -> list[int]:
     return list(range(start, start + per + (1 if rank < extra else 0)))
 
 
+def queue_seed(queue: int, rnd: int) -> int:
+    """Seed of the synthetic traffic of global rx queue `queue` in rotation
+    round `rnd` (distinct across queues, hence across ranks; the rule table of
+    a config does not depend on it)."""
+    return 7919 * queue + 17 * rnd + 2
+
+
 def batch_seed(rank: int, k: int) -> int:
     """Seed of the k-th synthetic batch generated on `rank` (distinct across ranks)."""
     return 1000 * rank + 17 * k + 2

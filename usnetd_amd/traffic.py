@@ -10,7 +10,9 @@
   c5  64 B, 65536 rules (16 IPs x 2048 listening ports + 32768 connected)
 
 Frames are generated directly into their HBM layout (fixed stride); every
-frame start has 64 readable bytes.  Data is synthetic (no captures).
+frame start has 64 readable bytes.  Data is synthetic (no captures).  A
+config's rule table is fixed (its own seed); `seed` varies only the traffic,
+so every rx queue of a bench hits the one installed table.
 """
 from __future__ import annotations
 
@@ -182,7 +184,7 @@ def _ipv4_mix(rng, n, ips, listen, conn, p_icmp, hit_rate=0.9):
 
 def c3(n=1 << 18, seed=3, stride=2048):
     rng = np.random.default_rng(seed)
-    ips, rules, listen, conn = _listen_conn_rules(rng, 504, 512, 8, 64)
+    ips, rules, listen, conn = _listen_conn_rules(np.random.default_rng(3), 504, 512, 8, 64)
     dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.10)
     sizes = rng.choice(np.array([64, 576, 1500]), size=n, p=[7 / 12, 4 / 12, 1 / 12])
     lens = sizes.astype(np.uint16)
@@ -192,7 +194,7 @@ def c3(n=1 << 18, seed=3, stride=2048):
 
 def c4(n=1 << 18, seed=4):
     rng = np.random.default_rng(seed)
-    ips, rules, listen, conn = _listen_conn_rules(rng, 2048 - 32, 2048, 32, 256)
+    ips, rules, listen, conn = _listen_conn_rules(np.random.default_rng(4), 2048 - 32, 2048, 32, 256)
     dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.1)
     lens = np.full(n, 64, np.uint16)
     H = build_ipv4(n, dst, src, proto, sport, dport, lens)
@@ -213,13 +215,16 @@ def c4(n=1 << 18, seed=4):
     return Config("c4", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(256), rules)
 
 
-def c5(n=1 << 23, seed=5):
+def c5(n=1 << 23, seed=5, n_ep=1000):
+    """n_ep: endpoints owning the rules (4093 fills the 12-bit netmap pipe id
+    space, USN_MAX_ENDPOINTS)."""
     rng = np.random.default_rng(seed)
-    ips, rules, listen, conn = _listen_conn_rules(rng, 16 * 2048, 32768, 16, 1000, icmp=False)
+    ips, rules, listen, conn = _listen_conn_rules(np.random.default_rng(5), 16 * 2048, 32768, 16, n_ep,
+                                                  icmp=False)
     dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.0)
     lens = np.full(n, 64, np.uint16)
     H = build_ipv4(n, dst, src, proto, sport, dport, lens)
-    return Config("c5", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(1000), rules)
+    return Config("c5", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(n_ep), rules)
 
 
 def c4tx(n=1 << 18, seed=6, host_at=None):
