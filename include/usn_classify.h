@@ -126,7 +126,8 @@ typedef struct {
   uint16_t n_frames;       /* frames in this tile */
   uint16_t n_runs;         /* entries of runs[] used by this tile */
   uint16_t n_host;         /* frames of this tile listed for the ordered host stage */
-  uint16_t _reserved;
+  uint16_t bin_nic;        /* bins of order/runs: endpoint ids 0..bin_nic-1, then bin_nic = NIC
+                              (Target::Nic, the source's NIC), bin_nic+1 = FLOOD, +2 = DROP */
   uint16_t class_count[4]; /* frames per decision class (before host fix-ups) */
   uint32_t last_state;     /* internal: 1-entry cache state after this tile */
   uint32_t last_dst;

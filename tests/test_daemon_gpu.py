@@ -42,12 +42,41 @@ def sock_has_more(sock):
     return bool(r)
 
 
-def test_daemon_forwards_like_the_oracle():
+def _pcap_frames(path):
+    """Frames of a libpcap file (Ethernet, the reference's PcapSink format)."""
+    import struct
+    data = open(path, "rb").read()
+    magic, _, _, _, _, snap, link = struct.unpack("<IHHiIII", data[:24])
+    assert magic == 0xA1B2C3D4 and link == 1
+    out, at = [], 24
+    while at + 16 <= len(data):
+        _, _, incl, orig = struct.unpack("<IIII", data[at:at + 16])
+        out.append(data[at + 16:at + 16 + incl])
+        assert incl == orig
+        at += 16 + incl
+    assert at == len(data)
+    return out
+
+
+def _subsequence(seq, of):
+    it = iter(of)
+    return all(any(x == y for y in it) for x in seq)
+
+
+@pytest.mark.parametrize("devices", [None, "0,0"], ids=["one-gpu", "two-replicas"])
+def test_daemon_forwards_like_the_oracle(devices, tmp_path):
+    """...and PCAP_LOG (src/main.rs:635-648, hook src/endpoint.rs:47-52) holds
+    every received frame, each source's in its order.  "two-replicas": the
+    daemon over USNETD_HIP_DEVICES=0,0 (one registry, two device copies of the
+    rule image; the NIC on one, nothing changes in what comes out)."""
     import coracle
     coracle.build()
-    d = Daemon({"INTERFACES": "eth0", "ADD_MACS": ",".join(MACS), "USNETD_MAX_BATCH": "64",
-                "USNETD_WRITE_WAIT_MS": "5000"},
-               control_only=False)
+    envs = {"INTERFACES": "eth0", "ADD_MACS": ",".join(MACS), "USNETD_MAX_BATCH": "64",
+            "USNETD_WRITE_WAIT_MS": "5000", "PCAP_LOG": str(tmp_path / "rx.pcap")}
+    if devices:
+        envs["USNETD_HIP_DEVICES"] = devices
+    d = Daemon(envs, control_only=False)
+    bursts = []
     try:
         assert d.p.poll() is None, d.log_text()
         wire = _sink(os.path.join(d.dir, "eth0.wire"))
@@ -78,6 +107,7 @@ def test_daemon_forwards_like_the_oracle():
         for burst in range(24):
             src = rng.choice([0, 0, 0, 1, 2, 3])
             frames = [randtraffic.rand_frame(rng, [1, 2]) for _ in range(rng.randrange(1, 80))]
+            bursts.append(frames)
             for f in frames:
                 dec = o.forward(src, f)
                 cls, ep = (dec >> 16) & 0xF, dec & 0xFFFF
@@ -115,3 +145,8 @@ def test_daemon_forwards_like_the_oracle():
     finally:
         rc = d.stop()
     assert rc == 0, d.log_text()[-3000:]
+    dumped = _pcap_frames(str(tmp_path / "rx.pcap"))
+    sent = [f for b in bursts for f in b]
+    assert sorted(dumped) == sorted(sent)
+    for b in bursts:
+        assert _subsequence(b, dumped)

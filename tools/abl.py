@@ -41,8 +41,21 @@ def main():
     runs = {}
     first = None
     for nm in names:
-        path = os.path.join(ROOT, "build", "abl", nm, "libusn.so")
+        # "build@ENV=VAL,ENV2=VAL": the build's library with context knobs set
+        # while its context is created (USN_PH_GROUP, USN_PH_LOAD, USN_T512)
+        build, _, knobs = nm.partition("@")
+        path = os.path.join(ROOT, "build", "abl", build, "libusn.so")
+        saved = {}
+        for kv in filter(None, knobs.split(",")):
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
         ctx = lib.Ctx(0, libpath=path)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         traffic.install_ctx(ctx, cfgs[0])
         nq = max(a.streams, a.multi)
         nics = [0] + list(traffic.extra_nics(cfgs[0], nq - 1, ctx))

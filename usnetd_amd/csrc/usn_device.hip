@@ -209,42 +209,61 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
   return slot_is(sl, x, y, z, meta) ? sl.w : 0u;
 }
 
+/* Where a probe reads the image from (template TM of the classify kernel):
+ * TM_GLOBAL  displacements and slots from global memory (L1/L2);
+ * TM_LDS     the whole image staged in LDS (small tables);
+ * TM_DISPLDS the displacement arrays staged in LDS, slots from global
+ *            memory: one L2 request per key. */
+#define TM_GLOBAL 0
+#define TM_LDS 1
+#define TM_DISPLDS 2
+
+#ifndef USN_PH_SEQ   /* A/B: key2 only after a key1 miss (one more round trip, fewer reads) */
+#define USN_PH_SEQ 0
+#endif
+
 /* Both keys of a frame, issued together: two displacement reads, then two
- * slot reads (one round trip each for the global image).  use1/use2 are
- * wave-uniform (the image's probe_mask); w = the slot's meta word, 0 = miss. */
-template <bool IN_LDS>
-__device__ __forceinline__ void ph_probe2(const uint4 *T, const ClassifyArgs &a, bool use1,
-                                          bool use2, uint32_t x1, uint32_t y1, uint32_t z1,
-                                          uint32_t m1, uint32_t x2, uint32_t y2, uint32_t z2,
-                                          uint32_t m2, uint32_t &w1, uint32_t &w2) {
+ * slot reads (one round trip each for a global image).  use1/use2 are
+ * wave-uniform (the image's probe_mask); w = the slot's meta word, 0 = miss.
+ * Dl: the LDS copy of the displacements, indexed like the image (TM_DISPLDS). */
+template <int TM>
+__device__ __forceinline__ void ph_probe2(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                          bool use1, bool use2, uint32_t x1, uint32_t y1,
+                                          uint32_t z1, uint32_t m1, uint32_t x2, uint32_t y2,
+                                          uint32_t z2, uint32_t m2, uint32_t &w1, uint32_t &w2) {
   const PhKeyH k1 = ph_hash(a.ph[0], x1, y1, z1, m1);
   const PhKeyH k2 = ph_hash(a.ph[1], x2, y2, z2, m2);
-  const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+  const uint16_t *D = TM == TM_DISPLDS ? Dl : reinterpret_cast<const uint16_t *>(T);
   w1 = 0u;
   w2 = 0u;
-  if (IN_LDS) {
-    // an unused table's reads go to index 0 of the image (always present)
-    const uint32_t di1 = use1 ? a.ph[0].disp_off + k1.grp : 0u;
-    const uint32_t di2 = use2 ? a.ph[1].disp_off + k2.grp : 0u;
-    uint32_t d1, d2;
+  uint32_t d1 = 0, d2 = 0;
+  if (TM != TM_GLOBAL) {
+    // an unused table's read goes to the first displacement (always present)
+    const uint32_t di1 = a.ph[0].disp_off + (use1 ? k1.grp : 0u);
+    const uint32_t di2 = a.ph[1].disp_off + (use2 ? k2.grp : 0u);
     asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(d1), "=&v"(d2)
                  : "v"(lds_addr(D + di1)), "v"(lds_addr(D + di2)));
-    const uint32_t si1 = use1 ? a.ph[0].slot_off + usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u;
-    const uint32_t si2 = use2 ? a.ph[1].slot_off + usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u;
+  } else {
+    if (use1) d1 = D[a.ph[0].disp_off + k1.grp];
+    if (use2) d2 = D[a.ph[1].disp_off + k2.grp];
+  }
+  const uint32_t si1 = a.ph[0].slot_off + (use1 ? usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u);
+  const uint32_t si2 = a.ph[1].slot_off + (use2 ? usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u);
+  if (TM == TM_LDS) {
     v4u32 s1, s2;
     asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(s1), "=&v"(s2)
                  : "v"(lds_addr(T + si1)), "v"(lds_addr(T + si2)));
     if (use1) w1 = ph_hit(make_uint4(s1.x, s1.y, s1.z, s1.w), x1, y1, z1, m1);
     if (use2) w2 = ph_hit(make_uint4(s2.x, s2.y, s2.z, s2.w), x2, y2, z2, m2);
+  } else if (USN_PH_SEQ) {
+    if (use1) w1 = ph_hit(T[si1], x1, y1, z1, m1);
+    if (use2 && !w1) w2 = ph_hit(T[si2], x2, y2, z2, m2);
   } else {
-    uint32_t d1 = 0, d2 = 0;
-    if (use1) d1 = D[a.ph[0].disp_off + k1.grp];
-    if (use2) d2 = D[a.ph[1].disp_off + k2.grp];
     uint4 s1 = make_uint4(0, 0, 0, 0), s2 = make_uint4(0, 0, 0, 0);
-    if (use1) s1 = T[a.ph[0].slot_off + usn_ph_slot(k1.h2, d1, a.ph[0].m)];
-    if (use2) s2 = T[a.ph[1].slot_off + usn_ph_slot(k2.h2, d2, a.ph[1].m)];
+    if (use1) s1 = T[si1];
+    if (use2) s2 = T[si2];
     if (use1) w1 = ph_hit(s1, x1, y1, z1, m1);
     if (use2) w2 = ph_hit(s2, x2, y2, z2, m2);
   }
@@ -290,17 +309,17 @@ __device__ __forceinline__ void rx_keys(const Parsed &p, uint32_t &x1, uint32_t 
 __device__ __forceinline__ uint32_t decide_rx_w(const ClassifyArgs &a, const Parsed &p, uint32_t w1,
                                                 uint32_t w2);
 
-template <bool IN_LDS>
-__device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const ClassifyArgs &a,
-                                              const Parsed &p) {
+template <int TM>
+__device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const uint16_t *Dl,
+                                              const ClassifyArgs &a, const Parsed &p) {
   uint32_t w1 = 0, w2 = 0;
 #if USN_ABL_NOPROBE   /* ablation build only: no table probes */
   w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
 #else
   uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
   rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
-  ph_probe2<IN_LDS>(T, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
-                    y2, z2, m2, w1, w2);
+  ph_probe2<TM>(T, Dl, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
+                y2, z2, m2, w1, w2);
 #endif
   return decide_rx_w(a, p, w1, w2);
 }
@@ -731,13 +750,14 @@ __device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *sc
 }
 
 /* Decision for a carried PacketInfo X under the current table (rx). */
-template <bool IN_LDS>
-__device__ uint32_t decide_info_rx(const uint4 *T, const ClassifyArgs &a, const uint32_t *info) {
+template <int TM>
+__device__ uint32_t decide_info_rx(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                   const uint32_t *info) {
   Parsed p;
   p.status = 1; p.i0 = info[0]; p.src = info[1]; p.dst = info[2]; p.ports = info[3];
   p.proto = (info[0] >> 8) & 0xFFu; p.has_ports = (info[0] >> 16) & 1u;
   p.sport = info[3] & 0xFFFFu; p.dport = info[3] >> 16; p.frag_first = 0;
-  return decide_rx<IN_LDS>(T, a, p);
+  return decide_rx<TM>(T, Dl, a, p);
 }
 
 /* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
@@ -820,7 +840,7 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 
 /* One workgroup per 1024-frame tile of a launch (several batches = drained
  * rx rings may share one launch). */
-template <bool LDS, bool GLDS>
+template <int TM, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
@@ -859,13 +879,16 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
   const uint4 *T = m.b[0].table;
-  if (LDS) {   // table -> LDS by glds, 64 slots per instruction, waves in turn
-    const uint32_t slots = m.b[0].table_units;
-    for (uint32_t c = wave; c * 64 < slots; c += NWAVES) {
-      const uint32_t sl = min(c * 64 + lane, slots - 1);
+  const uint16_t *Dl = nullptr;
+  if (TM != TM_GLOBAL) {   // image (or its displacements) -> LDS by glds, 64 units per instruction
+    const uint32_t u0 = TM == TM_LDS ? 0u : m.b[0].disp_unit;
+    const uint32_t units = m.b[0].table_units - u0;
+    for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
+      const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
     }
-    T = L.table;
+    if (TM == TM_LDS) T = L.table;
+    else Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)u0 * 8;
   }
   uint4 q[ROUNDS][4];
   if (GLDS) {
@@ -890,7 +913,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       const uint32_t cst = s_carry[0], dst = s_carry[1];
       uint32_t flags = 0;
       if ((cst & USN_CS_VALID) &&
-          ((decide_info_rx<LDS>(T, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
+          ((decide_info_rx<TM>(T, Dl, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
         flags |= USN_S_STALE;
       s_carry[6] = flags;
       s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
@@ -940,7 +963,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #endif
     Parsed p;
     parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
-    dec[r] = decide_rx<LDS>(T, a, p);
+    dec[r] = decide_rx<TM>(T, Dl, a, p);
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
     uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                    : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
@@ -1043,7 +1066,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     H->n_frames = (uint16_t)nt;
     H->n_runs = (uint16_t)n_runs;
     H->n_host = (uint16_t)s_misc[1];
-    H->_reserved = 0;
+    H->bin_nic = (uint16_t)a.n_ep;
     H->class_count[0] = (uint16_t)s_misc[5];                       // DROP bin
     H->class_count[2] = (uint16_t)s_misc[3];                       // NIC bin
     H->class_count[3] = (uint16_t)s_misc[4];                       // FLOOD bin
@@ -1694,7 +1717,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     H->n_frames = (uint16_t)nt;
     H->n_runs = (uint16_t)n_runs;
     H->n_host = (uint16_t)s_misc[1];
-    H->_reserved = 0;
+    H->bin_nic = (uint16_t)a.n_ep;
     H->class_count[0] = (uint16_t)s_misc[5];
     H->class_count[2] = (uint16_t)s_misc[3];
     H->class_count[3] = (uint16_t)s_misc[4];
@@ -1735,6 +1758,16 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
          lds_core_bytes(nbins) + STAGE_BYTES_GLDS + table_lds_bytes(table_units) <= 64u * 1024u;
 }
 
+/* where the classify kernel reads the image from (TM_*) */
+#ifndef USN_DISP_LDS_MAX
+#define USN_DISP_LDS_MAX (16u * 1024u)   /* displacement arrays up to this size go to LDS */
+#endif
+static int table_mode(const ClassifyArgs &a) {
+  if (table_fits_lds(a.nbins, a.table_units)) return TM_LDS;
+  const size_t disp = (size_t)(a.table_units - a.disp_unit) * 16;
+  return disp <= USN_DISP_LDS_MAX ? TM_DISPLDS : TM_GLOBAL;
+}
+
 /* dynamic LDS of the classify kernels; glds: the order row is in the stage */
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds) {
   return lds_core_bytes(nbins, !glds) + (table_in_lds ? table_lds_bytes(table_units) : 0);
@@ -1759,14 +1792,17 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
-  const bool in_lds = table_fits_lds(a.nbins, a.table_units);
+  const int tm = table_mode(a);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds_bytes(a.nbins, a.table_units, in_lds, glds);
+  const size_t lds = lds_core_bytes(a.nbins, !glds) +
+                     (tm == TM_LDS ? table_lds_bytes(a.table_units)
+                      : tm == TM_DISPLDS ? table_lds_bytes(a.table_units - a.disp_unit) : 0);
   const dim3 g(tiles), b(NTHREADS);
-  if (in_lds && glds) hipLaunchKernelGGL((classify_rx_kernel<true, true>), g, b, lds, stream, m);
-  else if (in_lds) hipLaunchKernelGGL((classify_rx_kernel<true, false>), g, b, lds, stream, m);
-  else if (glds) hipLaunchKernelGGL((classify_rx_kernel<false, true>), g, b, lds, stream, m);
-  else hipLaunchKernelGGL((classify_rx_kernel<false, false>), g, b, lds, stream, m);
+#define USN_LAUNCH(T_, G_) hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), g, b, lds, stream, m)
+  if (tm == TM_LDS) { if (glds) USN_LAUNCH(TM_LDS, true); else USN_LAUNCH(TM_LDS, false); }
+  else if (tm == TM_DISPLDS) { if (glds) USN_LAUNCH(TM_DISPLDS, true); else USN_LAUNCH(TM_DISPLDS, false); }
+  else { if (glds) USN_LAUNCH(TM_GLOBAL, true); else USN_LAUNCH(TM_GLOBAL, false); }
+#undef USN_LAUNCH
   return hipGetLastError();
 }
 

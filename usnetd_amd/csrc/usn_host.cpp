@@ -30,6 +30,14 @@
 
 using usn::ClassifyArgs;
 
+/* perfect-hash image geometry: slot load and keys per displacement group */
+#ifndef USN_PH_LOAD
+#define USN_PH_LOAD 0.85
+#endif
+#ifndef USN_PH_GROUP
+#define USN_PH_GROUP 4
+#endif
+
 namespace {
 
 thread_local int g_last_hip = 0;
@@ -289,6 +297,8 @@ struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
   uint32_t sel = 0;      // selected replica (usn_replica_select)
   int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
+  double ph_load = USN_PH_LOAD;   // perfect-hash image geometry (env knobs)
+  uint32_t ph_group = USN_PH_GROUP;
   std::mutex mu;
   std::vector<Ep> eps = std::vector<Ep>(USN_MAX_ENDPOINTS);
   uint32_t n_ep = 0;   // max id + 1
@@ -378,12 +388,18 @@ void prefetch_rule(const usn_ctx *c, const WantKey &k) { c->rules.prefetch(k); }
  * Groups are placed largest first; each takes the smallest displacement d
  * that sends all its keys to free, distinct slots (usn_ph_slot).  Lookups
  * then read one displacement and exactly one slot. */
-#ifndef USN_PH_LOAD
-#define USN_PH_LOAD 0.85
-#endif
-#ifndef USN_PH_GROUP
-#define USN_PH_GROUP 4
-#endif
+/* A/B knobs, read at context creation: USN_PH_LOAD (slot load), USN_PH_GROUP
+ * (keys per displacement) */
+double ph_load_knob() {
+  const char *e = std::getenv("USN_PH_LOAD");
+  const double v = e ? std::atof(e) : USN_PH_LOAD;
+  return v > 0.05 && v < 0.99 ? v : USN_PH_LOAD;
+}
+uint32_t ph_group_knob() {
+  const char *e = std::getenv("USN_PH_GROUP");
+  const int v = e ? std::atoi(e) : USN_PH_GROUP;
+  return v >= 1 && v <= 32 ? (uint32_t)v : USN_PH_GROUP;
+}
 
 struct PhKey {
   uint4 e;         // x, y, z, meta | NICOWNER | owner << 16
@@ -444,17 +460,17 @@ bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed,
 
 /* one table of the image: m, g, seed and its slots / displacements */
 bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
-              std::vector<uint16_t> &disp) {
+              std::vector<uint16_t> &disp, double load0, uint32_t group) {
   const uint32_t n = (uint32_t)keys.size();
   t = usn_ph_table{};
   slots.clear();
   disp.clear();
   if (n == 0) return true;
-  double load = USN_PH_LOAD;
+  double load = load0;
   for (uint32_t attempt = 0; attempt < 12; ++attempt) {
     if (attempt && attempt % 3 == 0) load *= 0.9;
     const uint32_t m = std::max<uint32_t>(n + 1, (uint32_t)((double)n / load) + 1);
-    const uint32_t g = std::max<uint32_t>(1, (n + USN_PH_GROUP - 1) / USN_PH_GROUP);
+    const uint32_t g = std::max<uint32_t>(1, (n + group - 1) / group);
     const uint32_t seed = 0x9E3779B9u * (attempt + 1);
     if (ph_place(keys, m, g, seed, slots, disp)) {
       t.m = m;
@@ -489,7 +505,7 @@ int build_image(usn_ctx *c) {
   std::vector<uint16_t> disp[2];
   usn_ph_table t[2];
   for (int i = 0; i < 2; ++i)
-    if (!ph_build(keys[i], t[i], slots[i], disp[i])) return USN_ENOMEM;
+    if (!ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, c->ph_group)) return USN_ENOMEM;
   clk.mark("place");
   const uint32_t u0 = t[0].m, u1 = t[1].m;
   const uint32_t d0 = (t[0].g + 7) / 8, d1 = (t[1].g + 7) / 8;   // 8 u16 per 16-byte unit
@@ -781,6 +797,8 @@ int usn_ctx_create(int hip_device, usn_ctx **out) {
     usn_ctx *c = new (std::nothrow) usn_ctx();
     if (!c) return USN_ENOMEM;
     c->device = -1;
+    c->ph_load = ph_load_knob();
+    c->ph_group = ph_group_knob();
     *out = c;
     return USN_OK;
   }
@@ -808,6 +826,8 @@ int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
   c->reps.swap(reps);
   c->device = hip_devices[0];
   if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
+  c->ph_load = ph_load_knob();
+  c->ph_group = ph_group_knob();
   *out = c;
   return USN_OK;
 }
@@ -1116,6 +1136,7 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   a.host_list = r->host_list;
   a.table = R.d_table;
   a.table_units = (uint32_t)c->img.size();
+  a.disp_unit = c->img_t[1].slot_off + c->img_t[1].m;
   a.ph[0] = c->img_t[0];
   a.ph[1] = c->img_t[1];
   a.bridge = R.d_bridge;
@@ -1469,8 +1490,9 @@ int fetch_host_lists(usn_ctx *c, const usn_result *r, const std::vector<usn_tile
       if (c->h_lists) HIPCHK(hipHostFree(c->h_lists));
       c->h_lists = nullptr;
       c->h_lists_cap = 0;
-      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_lists), bytes, hipHostMallocDefault));
-      c->h_lists_cap = bytes;
+      const size_t cap = bytes + bytes / 2;   // batch sizes vary: no re-pin every time
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_lists), cap, hipHostMallocDefault));
+      c->h_lists_cap = cap;
     }
     HIPCHK(hipMemcpyAsync(c->h_lists, r->host_list, bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1616,8 +1638,64 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     evs.swap(sorted);
   }
   std::vector<uint8_t> buf;
-  uint32_t len = 0;
   clk.mark("sort");
+  /* Every device read comes first: the frames the apply loop parses (first
+   * fragments), the last cache-touching frame before h and the frames
+   * [h, n).  A failure there leaves the registry, bridge and maps untouched
+   * (the batch's results stay unusable; nothing was learned). */
+  const uint32_t W = USN_WINDOW_MAX;
+  auto fetch = [&](uint64_t i, uint8_t *dst, uint32_t &l) -> int {
+    const int e = hv.frame(i, buf, l);
+    if (e) return e;
+    std::memcpy(dst, buf.data(), W);
+    return USN_OK;
+  };
+  std::vector<uint8_t> frag_bytes;      // kind-2 events' frames, in event order
+  std::vector<uint32_t> frag_lens;
+  for (const Ev &e : evs)
+    if (e.kind == 2) {
+      frag_bytes.resize(frag_bytes.size() + W);
+      frag_lens.push_back(0);
+      st = fetch(e.idx, frag_bytes.data() + frag_bytes.size() - W, frag_lens.back());
+      if (st) return st;
+    }
+  uint64_t walk = n;                    // the last touching frame before h, if it retains
+  std::vector<uint8_t> walk_bytes(W);
+  uint32_t walk_len = 0;
+  bool walk_none = false;               // a touching frame left last_pkt = None
+  std::vector<uint8_t> seq;             // frames [h, n), W bytes each
+  std::vector<uint32_t> seq_len;
+  if (h < n) {
+    for (uint64_t k = h; k > 0; --k) {
+      const uint32_t d = hv.dec[k - 1];
+      if (!touches(d)) continue;
+      if (!retains(d)) { walk_none = true; break; }
+      walk = k - 1;
+      st = fetch(walk, walk_bytes.data(), walk_len);
+      if (st) return st;
+      break;
+    }
+    const bool strided = b->stride != 0;
+    const uint32_t width =
+        strided ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(b->stride, batch_window(b)), W) : 0;
+    st = hv.fetch_lens();
+    if (st) return st;
+    seq.assign((size_t)(n - h) * W, 0);
+    seq_len.assign(n - h, 0);
+    if (strided)
+      HIPCHK(hipMemcpy2D(seq.data(), W, b->frames + h * b->stride, b->stride, width, n - h,
+                         hipMemcpyDeviceToHost));
+    for (uint64_t j = h; j < n; ++j) {
+      uint8_t *fp = seq.data() + (size_t)(j - h) * W;
+      if (strided && (hv.lens[j] <= width || width == W || !ports_past(fp, hv.lens[j], width))) {
+        seq_len[j - h] = hv.lens[j];
+      } else {
+        st = fetch(j, fp, seq_len[j - h]);
+        if (st) return st;
+      }
+    }
+  }
+  clk.mark("frames");
   auto ev_key = [](const Ev &e) {
     WantKey w;
     w.dst = e.key.x;
@@ -1631,13 +1709,13 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   constexpr size_t PF = 16;   // registry slots are random in a table of 10^6: prefetch ahead
   for (size_t k = 0; k < std::min(PF, evs.size()); ++k)
     if (evs[k].kind == 1) prefetch_rule(c, ev_key(evs[k]));
+  size_t kf = 0;
   for (size_t ke = 0; ke < evs.size(); ++ke) {
     const Ev &e = evs[ke];
     if (ke + PF < evs.size() && evs[ke + PF].kind == 1) prefetch_rule(c, ev_key(evs[ke + PF]));
     if (e.kind == 2) {                                   // extract_pkt_info side effect
-      st = hv.frame(e.idx, buf, len);
-      if (st) return st;
-      (void)host_parse(c, buf.data(), len);
+      (void)host_parse(c, frag_bytes.data() + kf * W, frag_lens[kf]);
+      ++kf;
     } else if (e.kind == 0) {                            // endpoint.rs:195-197
       const uint64_t m = (uint64_t)e.key.x | ((uint64_t)e.key.y << 32);
       if (!bridge_has(c, m)) { c->bridge.push_back(m); c->bridge_dirty = true; fi.n_learned++; }
@@ -1657,45 +1735,18 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     cs.valid = sum.cin_state & USN_CS_VALID;
     cs.dst = sum.cin_dst;
     std::memcpy(cs.info.w, sum.cin_info, 16);
-    for (uint64_t k = h; k > 0; --k) {
-      const uint32_t d = hv.dec[k - 1];
-      if (!touches(d)) continue;
-      if (!retains(d)) { cs.valid = false; break; }
-      st = hv.frame(k - 1, buf, len);
-      if (st) return st;
-      ParsedH p = host_parse(c, buf.data(), len);
+    if (walk_none) cs.valid = false;
+    if (walk < n) {
+      ParsedH p = host_parse(c, walk_bytes.data(), walk_len);
       cs.valid = true;
       cs.info = p.info;
-      cs.dst = d & USN_PARITY_MASK;
-      break;
-    }
-    /* frames [h, n): one strided gather of their header windows */
-    const uint32_t W = USN_WINDOW_MAX;
-    std::vector<uint8_t> win;
-    const bool strided = b->stride != 0;
-    const uint32_t width =
-        strided ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(b->stride, batch_window(b)), W) : 0;
-    st = hv.fetch_lens();
-    if (st) return st;
-    if (strided) {
-      win.assign((size_t)(n - h) * W, 0);
-      HIPCHK(hipMemcpy2D(win.data(), W, b->frames + h * b->stride, b->stride, width, n - h,
-                         hipMemcpyDeviceToHost));
+      cs.dst = hv.dec[walk] & USN_PARITY_MASK;
     }
     std::vector<uint32_t> out(n - h);
     for (uint64_t j = h; j < n; ++j) {
-      const uint8_t *fp;
-      if (strided && (hv.lens[j] <= width || width == W ||
-                      !ports_past(win.data() + (size_t)(j - h) * W, hv.lens[j], width))) {
-        fp = win.data() + (size_t)(j - h) * W;
-        len = hv.lens[j];
-      } else {
-        st = hv.frame(j, buf, len);
-        if (st) return st;
-        fp = buf.data();
-      }
       bool learned = false;
-      uint32_t d = host_step(c, src, fp, len, cs, learned) | USN_F_HOST;
+      uint32_t d = host_step(c, src, seq.data() + (size_t)(j - h) * W, seq_len[j - h], cs, learned) |
+                   USN_F_HOST;
       if (learned) { d |= USN_F_LEARN; fi.n_learned++; }
       const uint32_t old = hv.dec[j];
       if ((old & USN_PARITY_MASK) != (d & USN_PARITY_MASK)) fi.n_patched++;
@@ -1704,6 +1755,8 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       out[j - h] = d;
     }
     fi.n_host = (uint32_t)(n - h);
+    /* the registry is final from here on; a HIP failure below leaves this
+     * batch's device results unpatched (reported, not retried) */
     HIPCHK(hipMemcpy(r->decisions + h, out.data(), out.size() * 4, hipMemcpyHostToDevice));
     ClassifyArgs a;
     fill_args(c, R, b, r, a);

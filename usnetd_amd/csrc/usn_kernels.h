@@ -34,6 +34,7 @@ struct ClassifyArgs {
   /* rule image (usn_internal.h): K1 / K2 perfect-hash tables in one buffer */
   const uint4 *table;
   uint32_t table_units;     /* 16-byte units of the whole image */
+  uint32_t disp_unit;       /* first unit of the displacement arrays (the rest of the image) */
   usn_ph_table ph[2];       /* K1 (key1 shapes), K2 (key2 shapes) */
   /* inner L2 bridge (tx): MACs in the low 48 bits */
   const uint64_t *bridge;

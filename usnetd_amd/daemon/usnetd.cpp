@@ -139,6 +139,7 @@ struct Dev {
   sockaddr_un peer{};         // NIC / host ring: where frames are sent
   socklen_t peer_len = 0;
   int txfd = -1;              // NIC / host ring: socket connected to `peer` (lazily)
+  uint32_t rep = 0;           // the device replica its rings are classified on
   /* two result buffers per source: the carried cache reads the previous one */
   void *res[2] = {nullptr, nullptr};
   int cur = 0;
@@ -193,16 +194,19 @@ class Daemon {
   unsigned cleanup_secs_ = 90;
   int write_wait_ms_ = 5;     // USNETD_WRITE_WAIT_MS: back-pressure before a frame is dropped
 
-  /* data path buffers */
+  /* data path buffers, one set per device replica (USNETD_HIP_DEVICES) */
   static const uint32_t HDR = 128;        // header window stride on the device
   uint32_t max_batch_ = 4096;             // frames per source per round
-  void *stream_ = nullptr;
-  uint8_t *h_hdr_ = nullptr;              // pinned: headers of the round
-  uint16_t *h_lens_ = nullptr;
-  uint32_t *h_dec_ = nullptr;
-  uint8_t *d_hdr_ = nullptr;
-  uint16_t *d_lens_ = nullptr;
-  uint32_t round_cap_ = 0;
+  struct RepBuf {
+    void *stream = nullptr;
+    uint8_t *h_hdr = nullptr, *d_hdr = nullptr;   // headers of the round (pinned / device)
+    uint16_t *h_lens = nullptr, *d_lens = nullptr;
+    uint32_t cap = 0;                             // frames
+    uint8_t *h_out = nullptr;                     // pinned: tile headers, order, runs per source
+    size_t out_cap = 0;
+  };
+  std::vector<RepBuf> reps_;
+  uint32_t next_rep_ = 0;                 // endpoints are spread over the replicas round-robin
   std::vector<uint8_t> arena_;            // full frames of the round
   std::vector<size_t> off_;
   std::vector<uint32_t> len_;
@@ -235,7 +239,8 @@ class Daemon {
   /* data path */
   bool data_path_init();
   void forward_round(const std::vector<DevP> &ready);
-  int write_frame(const DevP &t, const uint8_t *p, uint32_t len);
+  int write_frames(const DevP &t, const std::vector<uint32_t> &idx);
+  bool select(uint32_t rep);
 };
 
 /* ---- configuration ------------------------------------------------------------- */
@@ -257,6 +262,9 @@ bool Daemon::iface_ipv4(const std::string &iface, uint32_t &ip) {
 }
 
 bool Daemon::register_dev(const DevP &d) {
+  /* every endpoint's rings go to one replica, round-robin: the registry is
+   * shared, so a sending endpoint may learn on any of them */
+  if (!reps_.empty()) d->rep = next_rep_++ % (uint32_t)reps_.size();
   const int st = usn_endpoint_add(ctx_, d->id, d->kind, d->for_nic);
   if (st != USN_OK) {
     LOGE("usn_endpoint_add(%u): %s", d->id, usn_strerror(st));
@@ -679,7 +687,10 @@ void Daemon::remove_dev(const DevP &d) {
   pipe_monitor_.erase(std::remove_if(pipe_monitor_.begin(), pipe_monitor_.end(),
                                      [&](const std::pair<uint64_t, DevP> &p) { return p.second == d; }),
                       pipe_monitor_.end());
-  for (void *r : d->res) if (r) usn_dev_free(ctx_, r);
+  if (d->res[0] || d->res[1]) {
+    select(d->rep);
+    for (void *r : d->res) if (r) usn_dev_free(ctx_, r);
+  }
   if (d->fd >= 0) close(d->fd);
   if (d->txfd >= 0) close(d->txfd);
   used_ids_[d->id] = 0;
@@ -707,17 +718,28 @@ void Daemon::apply_changes() {
 }
 
 /* ---- data path ------------------------------------------------------------------- */
+bool Daemon::select(uint32_t rep) {
+  const int st = usn_replica_select(ctx_, rep);
+  if (st != USN_OK) LOGE("usn_replica_select(%u): %s", rep, usn_strerror(st));
+  return st == USN_OK;
+}
+
 bool Daemon::data_path_init() {
-  if (usn_stream_create(ctx_, &stream_) != USN_OK) return false;
-  round_cap_ = 0;
+  const int n = usn_ctx_replicas(ctx_);
+  if (n <= 0) return false;
+  reps_.resize((size_t)n);
+  for (int r = 0; r < n; ++r)
+    if (!select((uint32_t)r) || usn_stream_create(ctx_, &reps_[r].stream) != USN_OK) return false;
   return true;
 }
 
-/* Endpoint write (EndpointDevice::write).  A full peer queue waits up to
- * USNETD_WRITE_WAIT_MS for room, then the frame is dropped with a debug log
- * (a full tx ring); a vanished client is Unaddressable (endpoint.rs:90-105)
- * and is removed after the round. */
-int Daemon::write_frame(const DevP &t, const uint8_t *p, uint32_t len) {
+/* Endpoint writes (EndpointDevice::write) of the frames `idx` (arena
+ * indices, in order) by sendmmsg.  A full peer queue gets up to
+ * USNETD_WRITE_WAIT_MS for room; frames that still do not fit are dropped
+ * with a debug log (a full tx ring).  Returns 1 when the client has vanished
+ * (Error::Unaddressable, endpoint.rs:90-105): it is removed after the round. */
+int Daemon::write_frames(const DevP &t, const std::vector<uint32_t> &idx) {
+  if (idx.empty()) return 0;
   int fd = t->fd;
   if (t->kind != USN_EP_UDS) {   // the wire / kernel side, connected for flow control
     if (t->txfd < 0) {
@@ -730,14 +752,39 @@ int Daemon::write_frame(const DevP &t, const uint8_t *p, uint32_t len) {
     }
     fd = t->txfd;
   }
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    const ssize_t r = send(fd, p, len, MSG_DONTWAIT | MSG_NOSIGNAL);
-    if (r == (ssize_t)len) { t->frames_out++; return 0; }
-    const int e = errno;
-    if (e == EAGAIN && attempt == 0 && write_wait_ms_ > 0) {
-      pollfd pf{fd, POLLOUT, 0};
-      poll(&pf, 1, write_wait_ms_);
+  static const size_t VLEN = 256;
+  std::vector<mmsghdr> msgs(std::min(idx.size(), VLEN));
+  std::vector<iovec> iov(msgs.size());
+  size_t done = 0;
+  int budget = write_wait_ms_;
+  while (done < idx.size()) {
+    const size_t k = std::min(idx.size() - done, VLEN);
+    for (size_t j = 0; j < k; ++j) {
+      const uint32_t i = idx[done + j];
+      iov[j].iov_base = arena_.data() + off_[i];
+      iov[j].iov_len = len_[i];
+      std::memset(&msgs[j], 0, sizeof msgs[j]);
+      msgs[j].msg_hdr.msg_iov = &iov[j];
+      msgs[j].msg_hdr.msg_iovlen = 1;
+    }
+    const int r = sendmmsg(fd, msgs.data(), (unsigned)k, MSG_DONTWAIT | MSG_NOSIGNAL);
+    if (r > 0) {
+      done += (size_t)r;
+      t->frames_out += (uint64_t)r;
       continue;
+    }
+    const int e = errno;
+    if (e == EAGAIN && budget > 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      pollfd pf{fd, POLLOUT, 0};
+      poll(&pf, 1, budget);
+      budget -= (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                    std::chrono::steady_clock::now() - t0).count() + 1;
+      continue;
+    }
+    if (e == EAGAIN) {
+      LOGD("endpoint %u: queue full, %zu frames dropped", t->id, idx.size() - done);
+      return 0;
     }
     LOGD("Write error %s for endpoint %u", std::strerror(e), t->id);
     if (t->kind == USN_EP_UDS && (e == ECONNREFUSED || e == EPIPE || e == ENOTCONN || e == ECONNRESET))
@@ -745,22 +792,32 @@ int Daemon::write_frame(const DevP &t, const uint8_t *p, uint32_t len) {
     if (t->kind != USN_EP_UDS && (e == ECONNREFUSED || e == ENOTCONN)) {   // peer went away
       close(t->txfd);
       t->txfd = -1;
+      return 0;
     }
-    return 0;
+    ++done;   // this frame cannot be sent (e.g. EMSGSIZE): skip it
   }
   return 0;
 }
 
 void Daemon::forward_round(const std::vector<DevP> &ready) {
   /* 1. drain every readable endpoint, in device order */
-  struct Src { DevP dev; uint32_t start, n; usn_result res; };
+  struct Src {
+    DevP dev;
+    uint32_t start, n;     // arena frames [start, start + n)
+    uint32_t dstart;       // first window in its replica's device buffer
+    size_t out_off;        // tile headers / order / runs in the replica's h_out
+    usn_batch b;
+    usn_result res;
+  };
   std::vector<Src> srcs;
   arena_.clear();
   off_.clear();
   len_.clear();
   static thread_local std::vector<uint8_t> buf(1 << 16);
   for (const DevP &d : ready) {
-    Src s{d, (uint32_t)len_.size(), 0, {}};
+    Src s{};
+    s.dev = d;
+    s.start = (uint32_t)len_.size();
     while (s.n < max_batch_) {
       const ssize_t r = recv(d->fd, buf.data(), buf.size(), MSG_DONTWAIT);
       if (r < 0) break;
@@ -773,84 +830,204 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
     d->frames_in += s.n;
     if (s.n) srcs.push_back(s);
   }
-  const uint32_t total = (uint32_t)len_.size();
-  if (!total) return;
-  /* 2. header windows + lengths to the device */
-  if (total > round_cap_) {
-    if (h_hdr_) { usn_host_free_pinned(ctx_, h_hdr_); usn_host_free_pinned(ctx_, h_lens_);
-                  usn_host_free_pinned(ctx_, h_dec_); usn_dev_free(ctx_, d_hdr_);
-                  usn_dev_free(ctx_, d_lens_); }
-    round_cap_ = std::max<uint32_t>(total, 4096);
-    usn_host_alloc_pinned(ctx_, (size_t)round_cap_ * HDR + 64, (void **)&h_hdr_);
-    usn_host_alloc_pinned(ctx_, (size_t)round_cap_ * 2, (void **)&h_lens_);
-    usn_host_alloc_pinned(ctx_, (size_t)round_cap_ * 4, (void **)&h_dec_);
-    usn_dev_alloc(ctx_, (size_t)round_cap_ * HDR + 64, (void **)&d_hdr_);
-    usn_dev_alloc(ctx_, (size_t)round_cap_ * 2, (void **)&d_lens_);
+  if (srcs.empty()) return;
+  /* 2. per replica: the header windows + lengths of its sources to its device */
+  const uint32_t R = (uint32_t)reps_.size();
+  std::vector<uint32_t> total(R, 0);
+  std::vector<size_t> outb(R, 0);
+  for (Src &s : srcs) {
+    const uint32_t r = s.dev->rep;
+    s.dstart = total[r];
+    total[r] += s.n;
+    const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
+    s.out_off = outb[r];
+    outb[r] += (size_t)nt * (sizeof(usn_tile_hdr) + USN_TILE * 2 + USN_TILE * 4);
   }
-  for (uint32_t i = 0; i < total; ++i) {
-    const uint32_t c = std::min<uint32_t>(len_[i], HDR);
-    std::memcpy(h_hdr_ + (size_t)i * HDR, arena_.data() + off_[i], c);
-    std::memset(h_hdr_ + (size_t)i * HDR + c, 0, HDR - c);
-    h_lens_[i] = (uint16_t)std::min<uint32_t>(len_[i], 0xFFFF);
+  for (uint32_t r = 0; r < R; ++r) {
+    RepBuf &B = reps_[r];
+    if (!total[r]) continue;
+    if (!select(r)) { end_ = true; return; }
+    if (total[r] > B.cap) {
+      if (B.h_hdr) {
+        usn_host_free_pinned(ctx_, B.h_hdr);
+        usn_host_free_pinned(ctx_, B.h_lens);
+        usn_dev_free(ctx_, B.d_hdr);
+        usn_dev_free(ctx_, B.d_lens);
+        B.h_hdr = B.d_hdr = nullptr;
+        B.h_lens = B.d_lens = nullptr;
+      }
+      B.cap = std::max<uint32_t>(total[r], 4096);
+      if (usn_host_alloc_pinned(ctx_, (size_t)B.cap * HDR + 64, (void **)&B.h_hdr) ||
+          usn_host_alloc_pinned(ctx_, (size_t)B.cap * 2, (void **)&B.h_lens) ||
+          usn_dev_alloc(ctx_, (size_t)B.cap * HDR + 64, (void **)&B.d_hdr) ||
+          usn_dev_alloc(ctx_, (size_t)B.cap * 2, (void **)&B.d_lens)) {
+        LOGE("data path buffers of replica %u: out of memory", r);
+        B.cap = 0;
+        end_ = true;
+        return;
+      }
+    }
+    if (outb[r] > B.out_cap) {
+      if (B.h_out) usn_host_free_pinned(ctx_, B.h_out);
+      B.h_out = nullptr;
+      B.out_cap = 0;
+      if (usn_host_alloc_pinned(ctx_, outb[r], (void **)&B.h_out)) {
+        LOGE("result staging of replica %u: out of memory", r);
+        end_ = true;
+        return;
+      }
+      B.out_cap = outb[r];
+    }
   }
-  usn_memcpy_h2d(ctx_, d_hdr_, h_hdr_, (size_t)total * HDR, stream_);
-  usn_memcpy_h2d(ctx_, d_lens_, h_lens_, (size_t)total * 2, stream_);
-  /* 3. classify in device order: consecutive NIC rings share one launch; a
-   *    sending endpoint's ring is classified alone (its learning is ordered) */
-  std::vector<usn_batch> bs(srcs.size());
-  for (size_t k = 0; k < srcs.size(); ++k) {
-    Src &s = srcs[k];
-    usn_batch &b = bs[k];
+  for (Src &s : srcs) {
+    RepBuf &B = reps_[s.dev->rep];
+    for (uint32_t j = 0; j < s.n; ++j) {
+      const uint32_t i = s.start + j, w = s.dstart + j;
+      const uint32_t c = std::min<uint32_t>(len_[i], HDR);
+      std::memcpy(B.h_hdr + (size_t)w * HDR, arena_.data() + off_[i], c);
+      std::memset(B.h_hdr + (size_t)w * HDR + c, 0, HDR - c);
+      B.h_lens[w] = (uint16_t)std::min<uint32_t>(len_[i], 0xFFFF);
+    }
+  }
+  for (uint32_t r = 0; r < R; ++r) {
+    if (!total[r]) continue;
+    RepBuf &B = reps_[r];
+    select(r);
+    usn_memcpy_h2d(ctx_, B.d_hdr, B.h_hdr, (size_t)total[r] * HDR, B.stream);
+    usn_memcpy_h2d(ctx_, B.d_lens, B.h_lens, (size_t)total[r] * 2, B.stream);
+  }
+  /* 3. batches and result buffers (two per source: the carried cache reads
+   *    the previous batch's result) */
+  for (Src &s : srcs) {
+    RepBuf &B = reps_[s.dev->rep];
+    usn_batch &b = s.b;
     std::memset(&b, 0, sizeof b);
-    b.frames = d_hdr_ + (size_t)s.start * HDR;
+    b.frames = B.d_hdr + (size_t)s.dstart * HDR;
     b.stride = HDR;
     b.window = HDR;                // whole 128-byte windows: never past USN_WINDOW_MAX
-    b.lens = d_lens_ + s.start;
+    b.lens = B.d_lens + s.dstart;
     b.n = s.n;
     b.src_endpoint = s.dev->id;
     Dev &d = *s.dev;
     d.cur ^= 1;
-    if (!d.res[d.cur]) usn_dev_alloc(ctx_, usn_result_bytes(max_batch_), &d.res[d.cur]);
+    if (!d.res[d.cur]) {
+      select(d.rep);
+      if (usn_dev_alloc(ctx_, usn_result_bytes(max_batch_), &d.res[d.cur]) != USN_OK) {
+        LOGE("result buffer of endpoint %u: out of memory", d.id);
+        end_ = true;
+        return;
+      }
+    }
     usn_result_bind(d.res[d.cur], usn_result_bytes(max_batch_), max_batch_, &s.res);
   }
-  for (size_t k = 0; k < srcs.size();) {
+  /* 4. classify in device order.  A run of consecutive NIC rings changes no
+   *    shared state: its rings go to their replicas' GPUs at once (up to 8
+   *    per launch), then are finalized in order.  A sending endpoint's ring
+   *    learns (endpoint.rs:194-253), so it is classified and finalized alone
+   *    before anything after it. */
+  int st = USN_OK;
+  for (size_t k = 0; k < srcs.size() && st == USN_OK;) {
     size_t e = k + 1;
     if (srcs[k].dev->kind == USN_EP_NIC)
-      while (e < srcs.size() && e - k < 8 && srcs[e].dev->kind == USN_EP_NIC) ++e;
-    std::vector<usn_result> rs;
-    for (size_t j = k; j < e; ++j) rs.push_back(srcs[j].res);
-    int st = usn_classify_multi(ctx_, &bs[k], rs.data(), (uint32_t)(e - k), stream_);
-    for (size_t j = k; j < e && st == USN_OK; ++j) {
-      usn_finalize_info info;
-      st = usn_finalize(ctx_, &bs[j], &rs[j - k], stream_, &info);
-      for (int c = 0; c < 4; ++c) class_count_[c] += info.class_count[c];
-      usn_memcpy_d2h(ctx_, h_dec_ + srcs[j].start, rs[j - k].decisions, (size_t)srcs[j].n * 4,
-                     stream_);
+      while (e < srcs.size() && srcs[e].dev->kind == USN_EP_NIC) ++e;
+    for (uint32_t r = 0; r < R && st == USN_OK; ++r) {
+      std::vector<usn_batch> bs;
+      std::vector<usn_result> rs;
+      auto flush = [&]() {
+        if (bs.empty()) return;
+        st = usn_classify_multi(ctx_, bs.data(), rs.data(), (uint32_t)bs.size(), reps_[r].stream);
+        bs.clear();
+        rs.clear();
+      };
+      for (size_t j = k; j < e && st == USN_OK; ++j) {
+        if (srcs[j].dev->rep != r) continue;
+        if (bs.empty() && !select(r)) { st = USN_EINVAL; break; }
+        bs.push_back(srcs[j].b);
+        rs.push_back(srcs[j].res);
+        if (bs.size() == 8) flush();
+      }
+      if (st == USN_OK) flush();
     }
-    if (st != USN_OK) {
-      LOGE("classify failed: %s (hip %d)", usn_strerror(st), usn_last_hip_error());
-      end_ = true;
-      return;
+    for (size_t j = k; j < e && st == USN_OK; ++j) {
+      Src &s = srcs[j];
+      RepBuf &B = reps_[s.dev->rep];
+      usn_finalize_info info;
+      std::memset(&info, 0, sizeof info);
+      st = usn_finalize(ctx_, &s.b, &s.res, B.stream, &info);
+      if (st != USN_OK) break;
+      for (int c = 0; c < 4; ++c) class_count_[c] += info.class_count[c];
+      /* the per-tile order output: tile headers, order rows, runs */
+      const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
+      uint8_t *o = B.h_out + s.out_off;
+      select(s.dev->rep);
+      usn_memcpy_d2h(ctx_, o, s.res.tiles, nt * sizeof(usn_tile_hdr), B.stream);
+      usn_memcpy_d2h(ctx_, o + nt * sizeof(usn_tile_hdr), s.res.order, (size_t)nt * USN_TILE * 2,
+                     B.stream);
+      usn_memcpy_d2h(ctx_, o + nt * (sizeof(usn_tile_hdr) + USN_TILE * 2), s.res.runs,
+                     (size_t)nt * USN_TILE * 4, B.stream);
     }
     k = e;
   }
-  usn_stream_sync(ctx_, stream_);
-  /* 4. deliver in frame order */
+  if (st != USN_OK) {
+    LOGE("classify failed: %s (hip %d)", usn_strerror(st), usn_last_hip_error());
+    end_ = true;
+    return;
+  }
+  for (uint32_t r = 0; r < R; ++r)
+    if (total[r]) { select(r); usn_stream_sync(ctx_, reps_[r].stream); }
+  /* 5. deliver, source by source, each target's frames in frame order with
+   *    one sendmmsg stream per target: the per-endpoint runs of the order
+   *    output, FLOOD (mirror_to_all, endpoint.rs:340-363: every endpoint but
+   *    the source) and Target::Nic merged in by frame index */
   std::vector<DevP> unaddressable;
+  std::vector<std::vector<uint32_t>> per(USN_MAX_ENDPOINTS);
+  std::vector<uint32_t> nic, flood, merged, tmp;
+  std::vector<uint16_t> touched;
   for (const Src &s : srcs) {
-    for (uint32_t i = s.start; i < s.start + s.n; ++i) {
-      const uint32_t d = h_dec_[i];
-      const uint32_t cls = USN_DEC_CLASS(d);
-      const uint8_t *p = arena_.data() + off_[i];
-      if (cls == USN_CLS_DROP) continue;
-      if (cls == USN_CLS_FLOOD) {   // mirror_to_all (endpoint.rs:340-363)
-        for (const DevP &t : devices_)
-          if (t != s.dev && write_frame(t, p, len_[i])) unaddressable.push_back(t);
-        continue;
+    const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
+    const uint8_t *o = reps_[s.dev->rep].h_out + s.out_off;
+    const usn_tile_hdr *th = reinterpret_cast<const usn_tile_hdr *>(o);
+    const uint16_t *order = reinterpret_cast<const uint16_t *>(o + nt * sizeof(usn_tile_hdr));
+    const uint32_t *runs =
+        reinterpret_cast<const uint32_t *>(o + nt * (sizeof(usn_tile_hdr) + USN_TILE * 2));
+    nic.clear();
+    flood.clear();
+    touched.clear();
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t nf = th[t].n_frames, nr = th[t].n_runs, bn = th[t].bin_nic;
+      for (uint32_t q = 0; q < nr; ++q) {
+        const uint32_t bin = runs[(size_t)t * USN_TILE + q] >> 16;
+        const uint32_t a = runs[(size_t)t * USN_TILE + q] & 0xFFFFu;
+        const uint32_t z = q + 1 < nr ? (runs[(size_t)t * USN_TILE + q + 1] & 0xFFFFu) : nf;
+        std::vector<uint32_t> *dst = bin < bn ? &per[bin] : bin == bn ? &nic : bin == bn + 1 ? &flood
+                                                                                          : nullptr;
+        if (!dst) continue;   // DROP
+        if (bin < bn && dst->empty()) touched.push_back((uint16_t)bin);
+        for (uint32_t p = a; p < z; ++p)
+          dst->push_back(s.start + t * USN_TILE + order[(size_t)t * USN_TILE + p]);
       }
-      DevP t = by_id(USN_DEC_EP(d));
-      if (t && write_frame(t, p, len_[i])) unaddressable.push_back(t);
     }
+    const uint32_t nic_id = (uint32_t)s.dev->for_nic;   // Target::Nic of a sending endpoint
+    for (const DevP &t : devices_) {
+      const bool fl = !flood.empty() && t != s.dev;
+      const bool ni = !nic.empty() && t->id == nic_id;
+      std::vector<uint32_t> &mine = per[t->id];
+      if (mine.empty() && !fl && !ni) continue;
+      const std::vector<uint32_t> *out = &mine;
+      if (fl || ni) {   // merge the sorted lists by frame index
+        const std::vector<uint32_t> &x = fl ? flood : nic;
+        merged.resize(mine.size() + x.size());
+        std::merge(mine.begin(), mine.end(), x.begin(), x.end(), merged.begin());
+        if (fl && ni) {
+          tmp.resize(merged.size() + nic.size());
+          std::merge(merged.begin(), merged.end(), nic.begin(), nic.end(), tmp.begin());
+          merged.swap(tmp);
+        }
+        out = &merged;
+      }
+      if (write_frames(t, *out)) unaddressable.push_back(t);
+    }
+    for (uint16_t b : touched) per[b].clear();
   }
   std::sort(unaddressable.begin(), unaddressable.end());
   unaddressable.erase(std::unique(unaddressable.begin(), unaddressable.end()), unaddressable.end());
@@ -880,11 +1057,22 @@ int Daemon::run(int argc, char **argv) {
     write_wait_ms_ = std::max(0, std::atoi(env("USNETD_WRITE_WAIT_MS").c_str()));
   if (has_env("USNETD_MAX_BATCH"))
     max_batch_ = (uint32_t)std::max(1L, std::strtol(env("USNETD_MAX_BATCH").c_str(), nullptr, 10));
-  const int dev = data_path_ ? std::atoi(env("USNETD_HIP_DEVICE", "0").c_str()) : USN_HOST_ONLY;
-  int st = usn_ctx_create(dev, &ctx_);
+  /* USNETD_HIP_DEVICES=0,1,...: one registry, a device replica per GPU; the
+   * NICs' rings are spread over them (USNETD_HIP_DEVICE: a single GPU) */
+  std::vector<int> devs;
+  if (data_path_) {
+    if (has_env("USNETD_HIP_DEVICES")) {
+      for (const std::string &x : split(env("USNETD_HIP_DEVICES"), ','))
+        if (!x.empty()) devs.push_back(std::atoi(x.c_str()));
+    } else {
+      devs.push_back(std::atoi(env("USNETD_HIP_DEVICE", "0").c_str()));
+    }
+  }
+  int st = data_path_ ? usn_ctx_create_group(devs.data(), (uint32_t)devs.size(), &ctx_)
+                      : usn_ctx_create(USN_HOST_ONLY, &ctx_);
   if (st != USN_OK) {
-    LOGE("usn_ctx_create(%d): %s -- the match path needs a gfx950 GPU "
-         "(USNETD_CONTROL_ONLY=1 runs the control plane alone)", dev, usn_strerror(st));
+    LOGE("usn_ctx_create: %s -- the match path needs a gfx950 GPU "
+         "(USNETD_CONTROL_ONLY=1 runs the control plane alone)", usn_strerror(st));
     return 1;
   }
   if (data_path_ && !data_path_init()) { LOGE("data path init failed"); return 1; }

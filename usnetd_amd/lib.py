@@ -63,7 +63,7 @@ class FinalizeInfo(C.Structure):
 
 
 TILE_HDR_DTYPE = np.dtype([("n_frames", "<u2"), ("n_runs", "<u2"), ("n_host", "<u2"),
-                           ("_r", "<u2"), ("class_count", "<u2", (4,)), ("last_state", "<u4"),
+                           ("bin_nic", "<u2"), ("class_count", "<u2", (4,)), ("last_state", "<u4"),
                            ("last_dst", "<u4"), ("last_idx", "<u4"), ("last_info", "<u4", (4,)),
                            ("_pad", "<u4")])
 SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames", "<u4"),
