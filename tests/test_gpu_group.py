@@ -85,7 +85,7 @@ def test_learned_rules_reach_the_other_replica(coracle_mod):
     want_r = o.forward_batch(0, ans, cfg.lens, stride=cfg.stride)
     got_r = rr.decisions()
     _same(got_r, want_r, "rx on replica 1")
-    to_host = int((((got_r >> 16) & 0xF) == 1) & ((got_r & 0xFFFF) == cfg.src)).sum()
+    to_host = int(((((got_r >> 16) & 0xF) == 1) & ((got_r & 0xFFFF) == cfg.src)).sum())
     assert to_host > 1000            # the learned answer rules route replies to the sender
     ctx.close()
 

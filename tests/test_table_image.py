@@ -119,7 +119,7 @@ def test_image_shapes_owner_flags_and_updates():
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 300000])
 def test_image_bulk_sizes(n):
     """usn_table_build of n random connected 5-tuples and listening ports:
-    every key found, load <= 0.86, displacement groups of ~4."""
+    every key found, load <= 0.86, displacement groups of ~8."""
     L, h = _ctx()
     assert L.usn_endpoint_add(h, 0, 0, -1) == 0
     for e in range(1, 9):
@@ -140,7 +140,7 @@ def test_image_bulk_sizes(n):
     n_conn, n_list = int(conn.sum()), int((~conn).sum())
     if n > 100:
         assert m0 <= n_conn / 0.84 + 2 and m1 <= n_list / 0.84 + 2
-        assert g0 == (n_conn + 3) // 4 and g1 == (n_list + 3) // 4
+        assert g0 == (n_conn + 7) // 8 and g1 == (n_list + 7) // 8
     idx = rng.choice(n, min(n, 5000), replace=False)
     for i in idx:
         r = rules[i]

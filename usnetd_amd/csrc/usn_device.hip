@@ -214,28 +214,28 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
  * TM_LDS     the whole image staged in LDS (small tables);
  * TM_DISPLDS the displacement arrays staged in LDS, slots from global
  *            memory: one L2 request per key. */
+#ifndef USN_LATE_DMA
+#define USN_LATE_DMA 1
+#endif
 #define TM_GLOBAL 0
 #define TM_LDS 1
 #define TM_DISPLDS 2
 
-#ifndef USN_PH_SEQ   /* A/B: key2 only after a key1 miss (one more round trip, fewer reads) */
-#define USN_PH_SEQ 0
-#endif
-
 /* Both keys of a frame, issued together: two displacement reads, then two
  * slot reads (one round trip each for a global image).  use1/use2 are
- * wave-uniform (the image's probe_mask); w = the slot's meta word, 0 = miss.
- * Dl: the LDS copy of the displacements, indexed like the image (TM_DISPLDS). */
-template <int TM>
-__device__ __forceinline__ void ph_probe2(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
-                                          bool use1, bool use2, uint32_t x1, uint32_t y1,
-                                          uint32_t z1, uint32_t m1, uint32_t x2, uint32_t y2,
-                                          uint32_t z2, uint32_t m2, uint32_t &w1, uint32_t &w2) {
+ * wave-uniform (the image's probe_mask).  ph_issue returns with the slot
+ * loads ISSUED (s1, s2 not yet waited for), so the caller can put the next
+ * round's header DMA behind them: the compiler's wait before the compare is
+ * then vmcnt(4), not a wait for the DMA.  Dl: the LDS copy of the
+ * displacements, indexed like the image (TM_DISPLDS). */
+template <int TM, bool ASM_SLOTS = false>
+__device__ __forceinline__ void ph_issue(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                         bool use1, bool use2, uint32_t x1, uint32_t y1,
+                                         uint32_t z1, uint32_t m1, uint32_t x2, uint32_t y2,
+                                         uint32_t z2, uint32_t m2, v4u32 &s1, v4u32 &s2) {
   const PhKeyH k1 = ph_hash(a.ph[0], x1, y1, z1, m1);
   const PhKeyH k2 = ph_hash(a.ph[1], x2, y2, z2, m2);
   const uint16_t *D = TM == TM_DISPLDS ? Dl : reinterpret_cast<const uint16_t *>(T);
-  w1 = 0u;
-  w2 = 0u;
   uint32_t d1 = 0, d2 = 0;
   if (TM != TM_GLOBAL) {
     // an unused table's read goes to the first displacement (always present)
@@ -245,28 +245,52 @@ __device__ __forceinline__ void ph_probe2(const uint4 *T, const uint16_t *Dl, co
                  : "=&v"(d1), "=&v"(d2)
                  : "v"(lds_addr(D + di1)), "v"(lds_addr(D + di2)));
   } else {
-    if (use1) d1 = D[a.ph[0].disp_off + k1.grp];
-    if (use2) d2 = D[a.ph[1].disp_off + k2.grp];
+    // branch-free: an unused table reads a valid address (the image always
+    // has a unit past its end), so the waits stay straight-line counts
+    d1 = D[a.ph[0].disp_off + (use1 ? k1.grp : 0u)];
+    d2 = D[a.ph[1].disp_off + (use2 ? k2.grp : 0u)];
   }
   const uint32_t si1 = a.ph[0].slot_off + (use1 ? usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u);
   const uint32_t si2 = a.ph[1].slot_off + (use2 ? usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u);
   if (TM == TM_LDS) {
-    v4u32 s1, s2;
     asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(s1), "=&v"(s2)
                  : "v"(lds_addr(T + si1)), "v"(lds_addr(T + si2)));
-    if (use1) w1 = ph_hit(make_uint4(s1.x, s1.y, s1.z, s1.w), x1, y1, z1, m1);
-    if (use2) w2 = ph_hit(make_uint4(s2.x, s2.y, s2.z, s2.w), x2, y2, z2, m2);
-  } else if (USN_PH_SEQ) {
-    if (use1) w1 = ph_hit(T[si1], x1, y1, z1, m1);
-    if (use2 && !w1) w2 = ph_hit(T[si2], x2, y2, z2, m2);
+  } else if (ASM_SLOTS) {
+    // issued here, waited for by ph_slots_wait: hipcc's own wait before the
+    // compare would be vmcnt(0), draining the header DMA issued after them
+    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
+                 : "=&v"(s1), "=&v"(s2)
+                 : "v"(T + si1), "v"(T + si2)
+                 : "memory");
   } else {
-    uint4 s1 = make_uint4(0, 0, 0, 0), s2 = make_uint4(0, 0, 0, 0);
-    if (use1) s1 = T[si1];
-    if (use2) s2 = T[si2];
-    if (use1) w1 = ph_hit(s1, x1, y1, z1, m1);
-    if (use2) w2 = ph_hit(s2, x2, y2, z2, m2);
+    const uint4 a1 = T[si1], a2 = T[si2];
+    s1 = v4u32{a1.x, a1.y, a1.z, a1.w};
+    s2 = v4u32{a2.x, a2.y, a2.z, a2.w};
   }
+}
+
+/* the two ASM_SLOTS loads of ph_issue have landed; `younger` = vector memory
+ * instructions issued after them (the next round's 4 header DMAs, or 0) */
+template <int YOUNGER>
+__device__ __forceinline__ void ph_slots_wait(v4u32 &s1, v4u32 &s2) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(s1), "+v"(s2) : "n"(YOUNGER) : "memory");
+}
+
+__device__ __forceinline__ uint32_t ph_hitv(const v4u32 &sl, uint32_t x, uint32_t y, uint32_t z,
+                                            uint32_t meta) {
+  return ph_hit(make_uint4(sl.x, sl.y, sl.z, sl.w), x, y, z, meta);
+}
+
+template <int TM>
+__device__ __forceinline__ void ph_probe2(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                          bool use1, bool use2, uint32_t x1, uint32_t y1,
+                                          uint32_t z1, uint32_t m1, uint32_t x2, uint32_t y2,
+                                          uint32_t z2, uint32_t m2, uint32_t &w1, uint32_t &w2) {
+  v4u32 s1, s2;
+  ph_issue<TM>(T, Dl, a, use1, use2, x1, y1, z1, m1, x2, y2, z2, m2, s1, s2);
+  w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
+  w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
 }
 
 /* One key in table `tb` (0 = K1, 1 = K2); 0 when the table is empty. */
@@ -842,6 +866,9 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
  * rx rings may share one launch). */
 template <int TM, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
+  // global-image probes: the next round's header DMA goes out after this
+  // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
+  constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
   __shared__ uint32_t s_carry[8];
@@ -947,7 +974,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
         else vm_wait<0>();
       }
       stage_read(sb, lane, q[r]);
-      if (r + GD < ROUNDS) {
+      if (!LATE_DMA && r + GD < ROUNDS) {
         lgkm_wait0();          // this round's reads are done before its buffer is refilled
         glds_round(a, base, nt, r + GD, wave, lane, sb);
       }
@@ -963,7 +990,40 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #endif
     Parsed p;
     parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
-    dec[r] = decide_rx<TM>(T, Dl, a, p);
+    if (LATE_DMA) {
+      // global probes: the slot loads first, then the next round's header DMA,
+      // so the wait for the slots does not also wait for the DMA
+      uint32_t w1 = 0, w2 = 0;
+#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
+      w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
+#else
+      uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+      rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
+      const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+      v4u32 s1, s2;
+      ph_issue<TM, true>(T, Dl, a, use1, use2, x1, y1, z1, m1, x2, y2, z2, m2, s1, s2);
+#endif
+      if (r + GD < ROUNDS) {
+        __builtin_amdgcn_sched_barrier(0);
+        lgkm_wait0();
+        glds_round(a, base, nt, r + GD, wave, lane, sb);
+        __builtin_amdgcn_sched_barrier(0);
+#if !USN_ABL_NOPROBE
+        ph_slots_wait<4>(s1, s2);   // the 4 header DMAs may still fly
+#endif
+      } else {
+#if !USN_ABL_NOPROBE
+        ph_slots_wait<0>(s1, s2);
+#endif
+      }
+#if !USN_ABL_NOPROBE
+      w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
+      w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
+#endif
+      dec[r] = decide_rx_w(a, p, w1, w2);
+    } else {
+      dec[r] = decide_rx<TM>(T, Dl, a, p);
+    }
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
     uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                    : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
@@ -1760,7 +1820,7 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
 
 /* where the classify kernel reads the image from (TM_*) */
 #ifndef USN_DISP_LDS_MAX
-#define USN_DISP_LDS_MAX (16u * 1024u)   /* displacement arrays up to this size go to LDS */
+#define USN_DISP_LDS_MAX (8u * 1024u)   /* displacement arrays up to this size go to LDS (c4: 1 KiB; A/B at c5's 16 KiB: the LDS copy halves the workgroups per CU and loses 6 %) */
 #endif
 static int table_mode(const ClassifyArgs &a) {
   if (table_fits_lds(a.nbins, a.table_units)) return TM_LDS;

@@ -35,7 +35,7 @@ using usn::ClassifyArgs;
 #define USN_PH_LOAD 0.85
 #endif
 #ifndef USN_PH_GROUP
-#define USN_PH_GROUP 4
+#define USN_PH_GROUP 8
 #endif
 
 namespace {
@@ -505,7 +505,10 @@ int build_image(usn_ctx *c) {
   std::vector<uint16_t> disp[2];
   usn_ph_table t[2];
   for (int i = 0; i < 2; ++i)
-    if (!ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, c->ph_group)) return USN_ENOMEM;
+    for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
+      if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp)) break;
+      if (grp <= 1) return USN_ENOMEM;
+    }
   clk.mark("place");
   const uint32_t u0 = t[0].m, u1 = t[1].m;
   const uint32_t d0 = (t[0].g + 7) / 8, d1 = (t[1].g + 7) / 8;   // 8 u16 per 16-byte unit
