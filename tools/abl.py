@@ -60,6 +60,7 @@ def main():
         nq = max(a.streams, a.multi)
         nics = [0] + list(traffic.extra_nics(cfgs[0], nq - 1, ctx))
         # parity check: batch 0 into a private result of this variant
+        print("variant %s: check launch" % nm, flush=True)
         chk_b = lib.DeviceBatch(ctx, cfgs[0].frames, cfgs[0].lens, nics[0], stride=cfgs[0].stride)
         chk_r = lib.DeviceResult(ctx, a.frames)
         cs = ctx.stream()

@@ -34,8 +34,9 @@ def main():
     ctx.sync(s)
     ntiles = (n + 1023) // 1024
     buf = np.zeros(16384 * 16, np.uint64)
-    ctx.L.usn_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
-    rc = ctx.L.usn_debug_stamps(buf.ctypes.data, buf.nbytes)
+    fn = ctx.L.usn_debug_stamps512 if os.environ.get("STAMPS512") == "1" else ctx.L.usn_debug_stamps
+    fn.argtypes = [C.c_void_p, C.c_size_t]
+    rc = fn(buf.ctypes.data, buf.nbytes)
     assert rc == 0, rc
     st = buf.reshape(16384, 16)[:ntiles, :12].astype(np.int64)
     t0 = st[:, 0].min()

@@ -97,6 +97,9 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #define USN_LOAD_NT 0
 #endif
 
+#ifndef USN_ABL_NOPROBE   /* A/B only: no rule-table probes (wrong results) */
+#define USN_ABL_NOPROBE 0
+#endif
 #ifndef USN_ABL_LOADONLY   /* A/B only: loads and stores, no parse/probe/decide */
 #define USN_ABL_LOADONLY 0
 #endif
@@ -217,6 +220,9 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_LATE_DMA
 #define USN_LATE_DMA 1
 #endif
+#ifndef USN_BATCH2
+#define USN_BATCH2 1
+#endif
 #define TM_GLOBAL 0
 #define TM_LDS 1
 #define TM_DISPLDS 2
@@ -280,6 +286,50 @@ __device__ __forceinline__ void ph_slots_wait(v4u32 &s1, v4u32 &s2) {
 __device__ __forceinline__ uint32_t ph_hitv(const v4u32 &sl, uint32_t x, uint32_t y, uint32_t z,
                                             uint32_t meta) {
   return ph_hit(make_uint4(sl.x, sl.y, sl.z, sl.w), x, y, z, meta);
+}
+
+/* Two-round batched probes (the 512-thread build, global image): both
+ * rounds' keys are formed first, then their four displacement reads fly
+ * together, then their four slot reads -- two round trips per wave for both
+ * rounds instead of two per round.  The loads are inline asm and every wait
+ * is an explicit count (hipcc's own waits would be vmcnt(0) and drain the
+ * next round's header DMA). */
+__device__ __forceinline__ void rx_keys(const Parsed &p, uint32_t &x1, uint32_t &y1, uint32_t &z1,
+                                        uint32_t &m1, uint32_t &x2, uint32_t &y2, uint32_t &z2,
+                                        uint32_t &m2);
+
+struct RoundKeys {
+  uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+  PhKeyH k1, k2;
+};
+
+__device__ __forceinline__ void round_keys(const ClassifyArgs &a, const Parsed &p, RoundKeys &k) {
+  rx_keys(p, k.x1, k.y1, k.z1, k.m1, k.x2, k.y2, k.z2, k.m2);
+  k.k1 = ph_hash(a.ph[0], k.x1, k.y1, k.z1, k.m1);
+  k.k2 = ph_hash(a.ph[1], k.x2, k.y2, k.z2, k.m2);
+}
+
+__device__ __forceinline__ void asm_disp2(const uint16_t *D, const ClassifyArgs &a, bool use1,
+                                          bool use2, const RoundKeys &k, uint32_t &d1,
+                                          uint32_t &d2) {
+  const uint16_t *p1 = D + a.ph[0].disp_off + (use1 ? k.k1.grp : 0u);
+  const uint16_t *p2 = D + a.ph[1].disp_off + (use2 ? k.k2.grp : 0u);
+  asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off"
+               : "=&v"(d1), "=&v"(d2) : "v"(p1), "v"(p2) : "memory");
+}
+
+__device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a, bool use1,
+                                          bool use2, const RoundKeys &k, uint32_t d1, uint32_t d2,
+                                          v4u32 &s1, v4u32 &s2) {
+  const uint4 *p1 = T + a.ph[0].slot_off + (use1 ? usn_ph_slot(k.k1.h2, d1, a.ph[0].m) : 0u);
+  const uint4 *p2 = T + a.ph[1].slot_off + (use2 ? usn_ph_slot(k.k2.h2, d2, a.ph[1].m) : 0u);
+  asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
+               : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
+}
+
+template <int YOUNGER>
+__device__ __forceinline__ void vm_wait2(uint32_t &d1, uint32_t &d2) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(d1), "+v"(d2) : "n"(YOUNGER) : "memory");
 }
 
 template <int TM>
@@ -844,6 +894,21 @@ __device__ __forceinline__ void stage_read(const uint4 *st, uint32_t lane, uint4
   q[3] = make_uint4(0, 0, 0, 0);
 }
 
+/* the same by inline asm: no vmcnt wait of hipcc's (which would also wait
+ * for asm probe loads in flight); the caller has waited for the DMA */
+__device__ __forceinline__ void stage_read_asm(const uint4 *st, uint32_t lane, uint4 (&q)[4]) {
+  v4u32 a0, a1, a2;
+  asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %5\n\t"
+               "s_waitcnt lgkmcnt(0)"
+               : "=&v"(a0), "=&v"(a1), "=&v"(a2)
+               : "v"(lds_addr(st + stage_slot(lane, 0))), "v"(lds_addr(st + stage_slot(lane, 1))),
+                 "v"(lds_addr(st + stage_slot(lane, 2))));
+  q[0] = make_uint4(a0.x, a0.y, a0.z, a0.w);
+  q[1] = make_uint4(a1.x, a1.y, a1.z, a1.w);
+  q[2] = make_uint4(a2.x, a2.y, a2.z, a2.w);
+  q[3] = make_uint4(0, 0, 0, 0);
+}
+
 /* LANE: this lane's 64-byte window of round r into registers */
 __device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
   const uint4 *w = reinterpret_cast<const uint4 *>(fp);
@@ -869,6 +934,9 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
   constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
+  // both rounds' probes batched (two rounds per lane, global image)
+  constexpr bool BATCH2 = GLDS && TM == TM_GLOBAL && ROUNDS == 2 && GD == 1 && USN_BATCH2 &&
+                          !USN_ABL_LOADONLY && !USN_ABL_NOPROBE;
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
   __shared__ uint32_t s_carry[8];
@@ -959,8 +1027,40 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   uint32_t differs = 0;          // stale mode: bit r = touching frame whose info != carried
   uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
   uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
+  Parsed pr[ROUNDS];
+  if (BATCH2) {
+    // round 0's headers are in the stage (the barrier above waited for them)
+    uint4 *sb = st;
+    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+    const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+    RoundKeys k0, k1;
+    uint32_t d01, d02, d11, d12;
+    v4u32 s01, s02, s11, s12;
+    stage_read_asm(sb, lane, q[0]);
+    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+    __builtin_amdgcn_sched_barrier(0);
+    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+    round_keys(a, pr[0], k0);
+    asm_disp2(D, a, use1, use2, k0, d01, d02);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<2>();                                               // round 1 landed (2 younger loads)
+    stage_read_asm(sb, lane, q[1]);
+    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+    round_keys(a, pr[1], k1);
+    asm_disp2(D, a, use1, use2, k1, d11, d12);
+    vm_wait2<2>(d01, d02);
+    asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
+    vm_wait2<2>(d11, d12);
+    asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
+    asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
+    dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
+                         use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
+    dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
+                         use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+  }
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
+  for (uint32_t r = 0; r < ROUNDS && !BATCH2; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     uint4 *sb = st + (r % GD) * STAGE_ROUND_SLOTS;
     if (GLDS) {
@@ -986,9 +1086,10 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
     dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
                        (q[r][0].w ^ q[r][1].y ^ q[r][2].x ^ q[r][2].y ^ len[r]) & 0xFFFFu);
+    pr[r] = Parsed{};   // defined (a parse failure): the touch pass below reads it
     continue;
 #endif
-    Parsed p;
+    Parsed &p = pr[r];
     parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
     if (LATE_DMA) {
       // global probes: the slot loads first, then the next round's header DMA,
@@ -1024,6 +1125,12 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     } else {
       dec[r] = decide_rx<TM>(T, Dl, a, p);
     }
+    if (r == 0) STAMP(4);
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    const Parsed &p = pr[r];
     // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
     uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                    : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
@@ -1035,7 +1142,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     if (stale && touch && !(touch == 1 && p.i0 == s_carry[2] && p.src == s_carry[3] &&
                             p.dst == s_carry[4] && p.ports == s_carry[5]))
       differs |= 1u << r;        // later fragments also stop the device prefix
-    if (r == 0) STAMP(4);
   }
   STAMP(5);
 
@@ -1876,7 +1982,12 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
 }  // namespace USN_NS
 
 #if USN_STAMPS
-extern "C" int usn_debug_stamps(void *host, size_t bytes) {
+#if USN_NTHREADS == 512
+#define USN_STAMPS_FN usn_debug_stamps512
+#else
+#define USN_STAMPS_FN usn_debug_stamps
+#endif
+extern "C" int USN_STAMPS_FN(void *host, size_t bytes) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(USN_NS::usn_stamp_buf), bytes, 0,
                                   hipMemcpyDeviceToHost);
 }
