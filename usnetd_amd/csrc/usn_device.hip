@@ -232,7 +232,7 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
  * wave-uniform (the image's probe_mask).  ph_issue returns with the slot
  * loads ISSUED (s1, s2 not yet waited for), so the caller can put the next
  * round's header DMA behind them: the compiler's wait before the compare is
- * then vmcnt(4), not a wait for the DMA.  Dl: the LDS copy of the
+ * then vmcnt(GLDS_PARTS), not a wait for the DMA.  Dl: the LDS copy of the
  * displacements, indexed like the image (TM_DISPLDS). */
 template <int TM, bool ASM_SLOTS = false>
 __device__ __forceinline__ void ph_issue(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
@@ -327,6 +327,16 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
 }
 
+/* TM_DISPLDS: both displacements from the LDS copy (indexed like the image) */
+__device__ __forceinline__ void lds_disp2(const uint16_t *Dl, const ClassifyArgs &a, bool use1,
+                                          bool use2, const RoundKeys &k, uint32_t &d1,
+                                          uint32_t &d2) {
+  const uint16_t *p1 = Dl + a.ph[0].disp_off + (use1 ? k.k1.grp : 0u);
+  const uint16_t *p2 = Dl + a.ph[1].disp_off + (use2 ? k.k2.grp : 0u);
+  asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(d1), "=&v"(d2) : "v"(lds_addr(p1)), "v"(lds_addr(p2)) : "memory");
+}
+
 template <int YOUNGER>
 __device__ __forceinline__ void vm_wait2(uint32_t &d1, uint32_t &d2) {
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(d1), "+v"(d2) : "n"(YOUNGER) : "memory");
@@ -362,6 +372,46 @@ __device__ __forceinline__ uint32_t ph_probe1(const uint4 *T, const ClassifyArgs
   }
   const uint32_t d = D[t.disp_off + k.grp];
   return ph_hit(T[t.slot_off + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
+}
+
+/* N probes issued together: all N displacement reads, then all N slot
+ * reads -- two round trips for the lot instead of two per key.  Keys
+ * [0, N1) go to table K1, the rest to K2; use[i] false (or an empty table)
+ * gives w[i] = 0 with a harmless read of the table's first entries.  IN_LDS:
+ * the image is the LDS copy. */
+template <bool IN_LDS, int N, int N1>
+__device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs &a,
+                                              const uint32_t (&x)[N], const uint32_t (&y)[N],
+                                              const uint32_t (&z)[N], const uint32_t (&m)[N],
+                                              const bool (&use)[N], uint32_t (&w)[N]) {
+  typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+  typedef __attribute__((address_space(3))) const v4u32 lds_v4;
+  const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+  PhKeyH k[N];
+  uint32_t d[N];
+  bool on[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
+    on[i] = use[i] && ((a.probe_mask >> (i < N1 ? 0 : 1)) & 1u);
+    k[i] = ph_hash(t, x[i], y[i], z[i], m[i]);
+    const uint32_t di = t.disp_off + (on[i] ? k[i].grp : 0u);
+    d[i] = IN_LDS ? (uint32_t)((lds_u16 *)D)[di] : (uint32_t)D[di];
+  }
+  uint4 sl[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
+    const uint32_t si = t.slot_off + (on[i] ? usn_ph_slot(k[i].h2, d[i], t.m) : 0u);
+    if (IN_LDS) {
+      const v4u32 v = ((lds_v4 *)T)[si];
+      sl[i] = make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+      sl[i] = T[si];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) w[i] = on[i] ? ph_hit(sl[i], x[i], y[i], z[i], m[i]) : 0u;
 }
 
 /* find_forward for a NIC source (incoming == true), cache handled outside:
@@ -462,22 +512,31 @@ __host__ __device__ inline size_t cnt_bytes(uint32_t nbins) {
   return (b + 15) & ~(size_t)15;
 }
 
-/* cnt | bstart | scratch[16] | keys[TILE] (radix) | order[TILE] (unless the
- * caller keeps the order row elsewhere) | table */
+/* cnt | bstart | scratch[16] | keys[TILE] (radix) | order[TILE] | table.
+ * A kernel with a header stage (the GLDS classify) passes it as `stage`: the
+ * order row and the radix keys then live there (the stage is free once every
+ * round is decided; the sort starts after a barrier), which leaves the
+ * dynamic LDS to the counters and the image. */
 __host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) {
   return cnt_bytes(nbins) + 16 * 4 + (radix_bins(nbins) ? (size_t)TILE * 4 : 0);
 }
-__host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_order = true) {
-  return lds_head_bytes(nbins) + (own_order ? TILE * 2 : 0);
+__host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_stage = true) {
+  return own_stage ? lds_head_bytes(nbins) + TILE * 2 : cnt_bytes(nbins) + 16 * 4;
 }
-__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, uint16_t *order = nullptr) {
+#define STAGE_SORT_BYTES (TILE * 2 + TILE * 4)   /* order row + radix keys in a stage */
+__device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, uint4 *stage = nullptr) {
   Lds L;
   L.cnt = reinterpret_cast<uint16_t *>(smem);
   L.bstart = L.cnt + (size_t)NSEG * cnt_rows(nbins);
   L.scratch = reinterpret_cast<uint32_t *>(smem + cnt_bytes(nbins));
-  L.keys = radix_bins(nbins) ? L.scratch + 16 : nullptr;
-  L.order = order ? order : reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
-  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins, order == nullptr));
+  if (stage) {
+    L.order = reinterpret_cast<uint16_t *>(stage);
+    L.keys = radix_bins(nbins) ? reinterpret_cast<uint32_t *>(L.order + TILE) : nullptr;
+  } else {
+    L.keys = radix_bins(nbins) ? L.scratch + 16 : nullptr;
+    L.order = reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
+  }
+  L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins, stage == nullptr));
   return L;
 }
 
@@ -834,24 +893,27 @@ __device__ uint32_t decide_info_rx(const uint4 *T, const uint16_t *Dl, const Cla
   return decide_rx<TM>(T, Dl, a, p);
 }
 
-/* Swizzled 16-byte slot of part j of frame f in a wave's 4 KiB stage: the
- * XOR with (f >> 2) & 3 makes both the linear writes and the per-frame reads
- * of ds_*_b128 bank-conflict free. */
+/* The stage holds bytes 0..47 of each frame (parse reads 12..39; the port
+ * words of longer IPv4 headers come from the frame itself): 16-byte part j
+ * of frame f at slot 3f + j of a wave's 3 KiB round stage.  glds writes it
+ * linearly, and the per-frame ds_read_b128s (a 12-dword stride) cover 16
+ * distinct 4-bank groups per 16 lanes: no bank conflicts either way. */
+#define GLDS_PARTS 3u
 __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
-  return 4 * f + (j ^ ((f >> 2) & 3u));
+  return GLDS_PARTS * f + j;
 }
 
 /* ---- header loads -----------------------------------------------------------
  * GLDS (fixed-stride layouts, the default): LDS-DMA (`global_load_lds_dwordx4`)
  * with the non-temporal hint straight into a wave-private stage of
- * USN_GLDS_DEPTH rounds x 64 frames x 64 B.  No VGPRs are held for data in
+ * USN_GLDS_DEPTH rounds x 64 frames x 48 B.  No VGPRs are held for data in
  * flight, and it is the fastest way found to stream the windows
  * (tools/hbm_floor.hip, 8M frames per launch: 100-103 us vs 113 us for
  * per-lane 16-byte register loads; register loads with nt: 199 us).
  * glds writes LDS lane-linearly (base + 16 x lane), so each lane's SOURCE is
  * the chunk that belongs at its slot: lane L of instruction k fills slot
- * 64k + L = stage_slot(f, p) with f = 16k + L/4, p = (L & 3) ^ ((f >> 2) & 3),
- * and every lane then reads its own frame's parts conflict-free.
+ * u = 64k + L = stage_slot(f, p) with f = u / 3, p = u % 3, and every lane
+ * then reads its own frame's parts.
  * LANE (offsets layout, strides that are not 16-byte multiples): one 64-byte
  * window per lane with 16-byte register loads, one round in flight ahead. */
 #ifndef USN_GLDS_DEPTH
@@ -859,7 +921,7 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #endif
 #define GD USN_GLDS_DEPTH
 #define NWAVES (NTHREADS / 64)
-#define STAGE_ROUND_SLOTS 256u   /* 16-byte slots per wave and round: 64 frames x 4 */
+#define STAGE_ROUND_SLOTS (64u * GLDS_PARTS)   /* 16-byte slots per wave and round */
 #define GLDS_NT 2                /* aux bits of the header glds: non-temporal */
 #ifndef USN_GLDS_ENABLE          /* A/B only: 0 = register loads for every layout */
 #define USN_GLDS_ENABLE 1
@@ -877,9 +939,9 @@ __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0
 __device__ __forceinline__ void glds_round(const ClassifyArgs &a, uint64_t base, uint32_t nt,
                                            uint32_t r, uint32_t wave, uint32_t lane, uint4 *st) {
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t f = 16 * k + (lane >> 2);
-    const uint32_t p = (lane & 3u) ^ ((f >> 2) & 3u);
+  for (uint32_t k = 0; k < GLDS_PARTS; ++k) {
+    const uint32_t u = 64 * k + lane;
+    const uint32_t f = u / GLDS_PARTS, p = u - GLDS_PARTS * f;
     uint32_t local = r * NTHREADS + wave * 64 + f;
     local = local < nt ? local : nt - 1;          // tail tile: re-read the last frame
     const uint8_t *src = a.frames + (base + local) * a.stride + p * 16;
@@ -935,7 +997,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
   constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
   // both rounds' probes batched (two rounds per lane, global image)
-  constexpr bool BATCH2 = GLDS && TM == TM_GLOBAL && ROUNDS == 2 && GD == 1 && USN_BATCH2 &&
+  constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1 && USN_BATCH2 &&
                           !USN_ABL_LOADONLY && !USN_ABL_NOPROBE;
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
@@ -943,10 +1005,10 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // bins and table are shared by the batches.  GLDS: the order row lives in
-  // the header stage, free once every round is decided (the sort starts after
-  // a barrier), so eight workgroups fit a CU's LDS instead of seven.
-  const Lds L = carve(smem, m.b[0].nbins, GLDS ? reinterpret_cast<uint16_t *>(s_stage) : nullptr);
+  // bins and table are shared by the batches.  GLDS: the order row and the
+  // radix keys live in the header stage (carve)
+  static_assert(!GLDS || NWAVES * GD * STAGE_ROUND_SLOTS * 16 >= STAGE_SORT_BYTES, "stage too small");
+  const Lds L = carve(smem, m.b[0].nbins, GLDS ? s_stage : nullptr);
   const uint32_t bi = batch_of(m, blockIdx.x);
   const ClassifyArgs &a = m.b[bi];
   const uint32_t tile = blockIdx.x - m.tile_base[bi];
@@ -1028,7 +1090,35 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
   uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
   Parsed pr[ROUNDS];
-  if (BATCH2) {
+  if (BATCH2 && TM == TM_DISPLDS) {
+    // displacements from LDS: one global round trip (the slots) per round,
+    // round 1's header DMA in flight under round 0's parse and slot loads
+    uint4 *sb = st;
+    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+    RoundKeys k0, k1;
+    uint32_t d01, d02, d11, d12;
+    v4u32 s01, s02, s11, s12;
+    stage_read_asm(sb, lane, q[0]);
+    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+    __builtin_amdgcn_sched_barrier(0);
+    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+    round_keys(a, pr[0], k0);
+    lds_disp2(Dl, a, use1, use2, k0, d01, d02);
+    asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<2>();                                               // round 1 landed (2 younger loads)
+    stage_read_asm(sb, lane, q[1]);
+    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+    round_keys(a, pr[1], k1);
+    lds_disp2(Dl, a, use1, use2, k1, d11, d12);
+    asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
+    asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
+    dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
+                         use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
+    dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
+                         use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+  } else if (BATCH2) {
     // round 0's headers are in the stage (the barrier above waited for them)
     uint4 *sb = st;
     const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
@@ -1064,13 +1154,13 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     const uint32_t local = r * NTHREADS + tid;
     uint4 *sb = st + (r % GD) * STAGE_ROUND_SLOTS;
     if (GLDS) {
-      // round r landed: only the rounds issued after it may still fly (4 glds each)
+      // round r landed: only the rounds issued after it may still fly (GLDS_PARTS glds each)
       constexpr uint32_t kAfterMax = GD - 1;
       const uint32_t after = min(kAfterMax, ROUNDS - 1 - r);
       if (r > 0) {
-        if (after >= 3) vm_wait<12>();
-        else if (after == 2) vm_wait<8>();
-        else if (after == 1) vm_wait<4>();
+        if (after >= 3) vm_wait<3 * GLDS_PARTS>();
+        else if (after == 2) vm_wait<2 * GLDS_PARTS>();
+        else if (after == 1) vm_wait<GLDS_PARTS>();
         else vm_wait<0>();
       }
       stage_read(sb, lane, q[r]);
@@ -1110,7 +1200,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
         glds_round(a, base, nt, r + GD, wave, lane, sb);
         __builtin_amdgcn_sched_barrier(0);
 #if !USN_ABL_NOPROBE
-        ph_slots_wait<4>(s1, s2);   // the 4 header DMAs may still fly
+        ph_slots_wait<GLDS_PARTS>(s1, s2);   // the next round's header DMAs may still fly
 #endif
       } else {
 #if !USN_ABL_NOPROBE
@@ -1493,22 +1583,34 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
     BS = bs;
   }
   __syncthreads();
+  // parse and flag every round; the answer-key probes of all rounds are then
+  // issued together (two round trips for the tile's four rounds)
+  const uint32_t lane = tid & 63;
   uint32_t last = 0;
+  uint4 rec[ROUNDS];
+  bool need[ROUNDS];
+  uint32_t kx[ROUNDS], ky[ROUNDS], kz[ROUNDS], km[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) continue;
-    const uint8_t *fp = fps[r];
     const uint4 *q = qq[r];
-    const uint32_t len = ll[r];
     Parsed p;
-    parse(q, len, fp, a.window, p);
+    parse(q, local < nt ? ll[r] : 0u, fps[r], a.window, p);
     const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
     const uint64_t smac = (uint64_t)(q[0].y >> 16) | ((uint64_t)q[0].z << 16);
     const bool loop = p.status == 1u && (p.dst >> 24) == 127u;
     const uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
                          : (p.status == 1u && !loop) ? 1u : 2u;
     uint32_t f = (touch << TXR_TOUCH_SHIFT);
+    uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
+    if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
+    // the frame before it in the tile (lane - 1) retains the same info: this
+    // one is a cache hit (or the host's, as that one is) and learns nothing,
+    // so its answer key need not be probed
+    const uint32_t i0 = r0.x & TXR_I0_MASK;
+    const uint32_t pi0 = __shfl_up(touch == 1u ? i0 : 0xFFFFFFFFu, 1, 64);
+    const uint32_t py = __shfl_up(r0.y, 1, 64), pz = __shfl_up(r0.z, 1, 64), pw = __shfl_up(r0.w, 1, 64);
+    const bool repeat = lane > 0 && touch == 1u && pi0 == i0 && py == r0.y && pz == r0.z && pw == r0.w;
     if (touch == 1u || touch == 2u) {
       const bool s_in = bridge_has(BS, t.bridge_mask, smac);
       const bool d_in = bridge_has(BS, t.bridge_mask, dmac);
@@ -1518,6 +1620,8 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
     }
     if (touch == 3u) f |= TXR_HOST;                           // later fragment: map lookup
     if (p.status == 5u) f |= TXR_WINDOW;                      // ports past the window
+    need[r] = false;
+    kx[r] = 0; ky[r] = 0; kz[r] = 0; km[r] = 0;
     if (touch == 1u) {
       // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
       bool listening = false;
@@ -1530,20 +1634,24 @@ __global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
       const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
                             p.dport == 67u && (p.dst & 0xFFu) == 255u;
       if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
-      if (!listening && !dhcp_req) {   // the answer key is learned unless the table has it
-        uint32_t x, y, z, meta;
-        want_key(make_uint4(p.i0, p.src, p.dst, p.ports), x, y, z, meta);
-        if (!USN_ABL_TXNOPROBE && !ph_probe1<LDS>(T, a, 0, x, y, z, meta)) f |= TXR_LEARNRULE;
+      if (!listening && !dhcp_req && !repeat) {   // learned unless the table has the answer key
+        want_key(make_uint4(p.i0, p.src, p.dst, p.ports), kx[r], ky[r], kz[r], km[r]);
+        need[r] = !USN_ABL_TXNOPROBE;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
     if (p.status == 1u && p.frag_first) f |= TXR_FRAG1;
-    uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
-    if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
-    r0.x = (r0.x & TXR_I0_MASK) | f;
-    const uint64_t i = base + local;
-    t.rec[i] = r0;
-    if (touch) last = local + 1;
+    r0.x = i0 | f;
+    rec[r] = r0;
+    if (local < nt && touch) last = local + 1;
+  }
+  uint32_t w[ROUNDS];
+  ph_probe_many<LDS, ROUNDS, ROUNDS>(T, a, kx, ky, kz, km, need, w);
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
+    if (local < nt) t.rec[base + local] = rec[r];
   }
   if (last) atomicMax(&s_last, last);
   __syncthreads();
@@ -1762,14 +1870,18 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     s_head = hd;
   }
   uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
+  // every decision but get_endpoint's first; then key1 and key2 of all the
+  // rounds that need get_endpoint are probed together (two round trips for
+  // the tile instead of up to four per round), then those decisions
+  bool use[2 * ROUNDS];
+  uint32_t kx[2 * ROUNDS], ky[2 * ROUNDS], kz[2 * ROUNDS], km[2 * ROUNDS], w[2 * ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    v[r] = 0;
-    dec[r] = 0;
-    if (local >= nt) continue;
-    const uint64_t i = base + local;
-    const uint32_t fl = r0[r].x, touch = tx_touch(r0[r]), kind = fl & 0xFFu;
+    const uint32_t fl = r0[r].x, touch = local < nt ? tx_touch(r0[r]) : 0u, kind = fl & 0xFFu;
+    use[r] = false; use[ROUNDS + r] = false;
+    kx[r] = ky[r] = kz[r] = km[r] = 0;
+    kx[ROUNDS + r] = ky[ROUNDS + r] = kz[ROUNDS + r] = km[ROUNDS + r] = 0;
     uint32_t d;
     if (touch == 0u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
@@ -1783,8 +1895,30 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
       d = usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
+    } else if (!tx_dmac_in(t, fl, r1[r], (uint32_t)(base + local), ins)) {
+      d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
     } else {
-      d = decide_tx_ipv4<LDS>(t, T, r0[r], r1[r], (uint32_t)i, ins);
+      d = usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);  // (the A/B no-probe build keeps it)
+      use[r] = use[ROUNDS + r] = !USN_ABL_TXNOPROBE;
+      key1_of(r0[r], kx[r], ky[r], kz[r], km[r]);
+      key2_of(r0[r], kx[ROUNDS + r], ky[ROUNDS + r], kz[ROUNDS + r], km[ROUNDS + r]);
+    }
+    dec[r] = d;
+  }
+  ph_probe_many<LDS, 2 * ROUNDS, ROUNDS>(T, a, kx, ky, kz, km, use, w);
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    v[r] = 0;
+    if (local >= nt) { dec[r] = 0; continue; }
+    const uint64_t i = base + local;
+    const uint32_t fl = r0[r].x, touch = tx_touch(r0[r]);
+    uint32_t d = dec[r];
+    if (use[r]) {   // key1, then a key1 learned by a frame <= i, then key2 (endpoint.rs:317-327)
+      uint32_t wr = w[r];
+      if (!wr && (ins & 2u)) wr = tx_learned_key1(t, kx[r], ky[r], kz[r], km[r], (uint32_t)i);
+      if (!wr) wr = w[ROUNDS + r];
+      d = tx_lookup_dec(a, fl, wr);
     }
     if (fl & TXR_FRAG1) d |= USN_F_FRAG1;                  // first fragment: remembered (host map)
     // the first frame that learns an item lists it for the host registry / bridge
@@ -1925,8 +2059,12 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
 }
 
 /* where the classify kernel reads the image from (TM_*) */
+/* displacement arrays up to this size go to LDS: up to 13 KiB the 512-thread
+ * kernel keeps 4 workgroups per CU, up to 26 KiB 3, and at 3 the LDS copy
+ * still beats global displacements at 4 (A/B, c5 16 KiB: 161.3 vs 174.2 us
+ * per 8M frames, profiles/r02d) */
 #ifndef USN_DISP_LDS_MAX
-#define USN_DISP_LDS_MAX (8u * 1024u)   /* displacement arrays up to this size go to LDS (c4: 1 KiB; A/B at c5's 16 KiB: the LDS copy halves the workgroups per CU and loses 6 %) */
+#define USN_DISP_LDS_MAX (26u * 1024u)
 #endif
 static int table_mode(const ClassifyArgs &a) {
   if (table_fits_lds(a.nbins, a.table_units)) return TM_LDS;

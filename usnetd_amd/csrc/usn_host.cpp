@@ -30,12 +30,18 @@
 
 using usn::ClassifyArgs;
 
-/* perfect-hash image geometry: slot load and keys per displacement group */
+/* perfect-hash image geometry: slot load and keys per displacement group.
+ * 10 keys per u16 displacement keep c5's two arrays (65536 keys) at 13 KiB,
+ * which the classify kernel stages in LDS at 4 workgroups per CU; 10-key
+ * groups need the slot load at 0.75 to place within u16 displacements.
+ * A/B, c5, 8M frames per launch: group 8 / load 0.85 with the displacements
+ * in global memory 174.2 us, the same in LDS (3 workgroups per CU) 161.3 us,
+ * group 10 / load 0.75 in LDS 156.5 us (profiles/r02d). */
 #ifndef USN_PH_LOAD
-#define USN_PH_LOAD 0.85
+#define USN_PH_LOAD 0.75
 #endif
 #ifndef USN_PH_GROUP
-#define USN_PH_GROUP 8
+#define USN_PH_GROUP 10
 #endif
 
 namespace {
