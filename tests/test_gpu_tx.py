@@ -54,11 +54,14 @@ def _run(cfg, coracle_mod, batches=2):
     return infos
 
 
-@pytest.mark.parametrize("n", [1500, 1 << 16, 1 << 18])
+@pytest.mark.parametrize("n", [1500, 1 << 16, 1 << 18, 1 << 20])
 def test_c4tx_parity(n, coracle_mod):
+    """Every batch is decided on the device (n_host == 0: no tile wait of the
+    one-launch tx kernel gave up, no set overflowed)."""
     from usnetd_amd import traffic
-    infos = _run(traffic.config("c4tx", n=n), coracle_mod)
-    assert infos[0].n_host == 0 and infos[0].n_learned > 0
+    infos = _run(traffic.config("c4tx", n=n), coracle_mod, batches=3)
+    assert infos[0].n_learned > 0
+    assert [i.n_host for i in infos] == [0, 0, 0]
 
 
 @pytest.mark.parametrize("n,at", [(5000, [2500]), (1 << 16, [0]), (1 << 16, [40000, 40001, 60000])])
@@ -190,3 +193,42 @@ def test_tx_tiny_and_tile_edges(n, coracle_mod):
     from usnetd_amd import traffic
     cfg = traffic.c4tx(n=n, seed=13)
     _check(cfg, coracle_mod)
+
+
+def test_tx_runs_across_tiles(coracle_mod):
+    """Runs of one repeated frame that cross tile boundaries (the run head's
+    decision reaches the next tiles: an IPv4 flow, an ARP flood), and whole
+    tiles without a cache-touching frame (the tile after looks further back)."""
+    from usnetd_amd import traffic
+    cfg = traffic.c4tx(n=9000, seed=14)
+    st = cfg.stride
+    V = cfg.frames[:cfg.n * st].reshape(cfg.n, st)
+    ip = np.nonzero((V[:, 12] == 8) & (V[:, 13] == 0))[0]
+    arp = np.nonzero((V[:, 12] == 8) & (V[:, 13] == 6))[0]
+    V[1000:1100] = V[ip[5]]                    # crosses 1024
+    V[2000:2200] = V[arp[3]]                   # crosses 2048
+    V[3000:3100] = V[ip[7]]                    # a run up to the garbage tiles
+    V[3100:5200, 12:14] = 0x12                 # no parse: tiles 4 (3072.. ) fully non-touching
+    V[5200:5300] = V[ip[7]]                    # the same flow again after them: a cache hit
+    V[8190:8200] = V[arp[4]]                   # crosses 8192
+    _check(cfg, coracle_mod)
+
+
+def test_tx_fixed_flow_all_hits(coracle_mod):
+    """One 5-tuple sent 200000 times by the host endpoint: every frame after
+    the first is a cache hit whose run head lies in tile 0."""
+    from usnetd_amd import traffic
+    cfg = traffic.config("c1", n=200000, variant="fixed")
+    info = _check(cfg, coracle_mod, src=1)
+    assert info.n_host == 0
+
+
+def test_tx_runs_host_free(coracle_mod):
+    """test_tx_runs_across_tiles' batch needs no host stage either."""
+    from usnetd_amd import traffic
+    cfg = traffic.c4tx(n=70000, seed=15)
+    st = cfg.stride
+    V = cfg.frames[:cfg.n * st].reshape(cfg.n, st)
+    V[3100:69000, 12:14] = 0x12                # 64+ tiles in a row without a touching frame
+    info = _check(cfg, coracle_mod)
+    assert info.n_host == 0

@@ -17,6 +17,11 @@ from usnetd_amd import lib, traffic  # noqa: E402
 NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided",
          "all rounds decided", "stores+hostlist+lastreduce", "-", "-", "-",
          "tile_order+cls", "header"]
+# c4tx: the one-launch tx kernel (stamps indexed by tile)
+TX_NAMES = ["start", "header loads + bridge", "parse, flags, probes", "LAST out, walk back",
+            "hits, claims, INS out", "look-back", "decisions", "fill, host list", "-", "-",
+            "tile_order+cls", "header"]
+TX_STEPS = [1, 2, 3, 4, 5, 6, 7, 10, 11]
 
 
 def main():
@@ -24,13 +29,18 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     path = os.path.join(ROOT, "build", "abl", "stamps", "libusn.so")
     ctx = lib.Ctx(0, libpath=path)
-    cfgs = [traffic.config(cfgname, n=n, seed=17 * k + 2) for k in range(5)]
+    # tx: one ring replayed (steady state: its answer rules are learned by the first pass)
+    cfgs = [traffic.config(cfgname, n=n, seed=6 if cfgname == "c4tx" else 17 * k + 2)
+            for k in range(5)]
     traffic.install_ctx(ctx, cfgs[0])
     bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
     rs = [lib.DeviceResult(ctx, n) for _ in cfgs]
     s = ctx.stream()
+    tx = cfgname == "c4tx"
     for i in range(40):
         lib.check(ctx.L.usn_classify(ctx.h, C.byref(bs[i % 5].desc), C.byref(rs[i % 5].desc), s))
+        if tx:
+            ctx.finalize(bs[i % 5], rs[i % 5], s)
     ctx.sync(s)
     ntiles = (n + 1023) // 1024
     buf = np.zeros(16384 * 16, np.uint64)
@@ -46,11 +56,15 @@ def main():
         us(np.percentile(st[:, 0] - t0, q)) for q in (50, 90, 100)))
     print("end   offset: median %.2f p90 %.2f max %.2f us" % tuple(
         us(np.percentile(st[:, 11] - t0, q)) for q in (50, 90, 100)))
-    for k in [1, 2, 3, 4, 5, 6, 10, 11]:
-        prev = {10: 6}.get(k, k - 1)
+    names, steps = (TX_NAMES, TX_STEPS) if tx else (NAMES, [1, 2, 3, 4, 5, 6, 10, 11])
+    for i, k in enumerate(steps):
+        prev = steps[i - 1] if i else 0
         d = st[:, k] - st[:, prev]
         print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % (
-            NAMES[k], us(np.median(d)), us(np.percentile(d, 90)), us(d.max())))
+            names[k], us(np.median(d)), us(np.percentile(d, 90)), us(d.max())))
+        e = st[:, k] - t0
+        print("  %-28s   (at: median %6.2f  p90 %6.2f  max %6.2f us)" % (
+            "", us(np.median(e)), us(np.percentile(e, 90)), us(e.max())))
     tot = st[:, 11] - st[:, 0]
     print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % ("TOTAL per block", us(np.median(tot)),
                                                         us(np.percentile(tot, 90)), us(tot.max())))

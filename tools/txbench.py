@@ -7,6 +7,7 @@ Usage: python tools/txbench.py [n] [batches] [distinct]
   distinct > 1 rotates over that many differently-seeded rings (new flows
   keep learning answer rules); 1 replays one ring (steady state: nothing new).
 """
+import ctypes as C
 import json
 import os
 import sys
@@ -43,6 +44,11 @@ def main():
         t1 = time.perf_counter()
         info = ctx.finalize(b, r, s)
         t2 = time.perf_counter()
+        dbg = (C.c_uint32 * 10)()
+        if hasattr(ctx.L, "usn_debug_tx_state"):
+            ctx.L.usn_debug_tx_state.argtypes = [C.c_void_p, C.c_void_p]
+        if hasattr(ctx.L, "usn_debug_tx_state") and ctx.L.usn_debug_tx_state(ctx.h, dbg) == 0:
+            print("tx state", list(dbg), flush=True)
         rows.append({"batch": k, "device_ms": round(ctx.elapsed_ms(*ev[k]), 4),
                      "classify_call_ms": round((t1 - t0) * 1e3, 3),
                      "finalize_ms": round((t2 - t1) * 1e3, 3),

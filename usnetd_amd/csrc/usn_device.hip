@@ -71,16 +71,18 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
     __builtin_amdgcn_sched_barrier(0);                                           \
   } while (0)
 #define STAMP_DECL unsigned long long stamp_t[12] = {0};
-#define STAMP_FLUSH()                                                            \
+#define STAMP_FLUSH_AT(slot)                                                     \
   do {                                                                           \
     if (threadIdx.x == 0)                                                        \
       for (int k_ = 0; k_ < 12; ++k_)                                            \
-        usn_stamp_buf[(blockIdx.x & 16383) * USN_NSTAMP + k_] = stamp_t[k_];     \
+        usn_stamp_buf[((slot) & 16383) * USN_NSTAMP + k_] = stamp_t[k_];         \
   } while (0)
+#define STAMP_FLUSH() STAMP_FLUSH_AT(blockIdx.x)
 #else
 #define STAMP(k) do { } while (0)
 #define STAMP_DECL
 #define STAMP_FLUSH() do { } while (0)
+#define STAMP_FLUSH_AT(slot) do { } while (0)
 #endif
 
 #ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
@@ -1419,6 +1421,18 @@ __device__ __forceinline__ void first_index_update(unsigned long long *w, uint32
   atomicMax(w, ((unsigned long long)epoch << 32) | (unsigned long long)(~idx));
 }
 
+/* The sets are written and read by tiles of the same launch: every access
+ * is an agent-scope atomic or an sc1 (write-through / L1- and stale-L2-free)
+ * load or store (MI355X guide, Guideline 16). */
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) unsigned long long *)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store((__attribute__((address_space(1))) unsigned long long *)p, v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
 /* Insert a 48-bit key into an epoch-tagged set (slot stride in u64 words). */
 __device__ __forceinline__ unsigned long long *set_claim(unsigned long long *set, uint32_t mask,
                                                          uint32_t stride, uint32_t epoch,
@@ -1450,7 +1464,7 @@ __device__ __forceinline__ const unsigned long long *set_find(const unsigned lon
   uint32_t h = home & mask;
   for (uint32_t it = 0; it <= mask; ++it) {
     const unsigned long long *slot = set + (size_t)h * stride;
-    const unsigned long long cur = slot[0];
+    const unsigned long long cur = ld_sc1(slot);
     if ((cur >> 48) != epoch) return nullptr;
     if (cur == key) return slot;
     h = (h + 1) & mask;
@@ -1461,7 +1475,7 @@ __device__ __forceinline__ const unsigned long long *set_find(const unsigned lon
 /* first index recorded in a set slot, or ~0 */
 __device__ __forceinline__ uint32_t slot_first(const unsigned long long *slot, uint32_t epoch) {
   if (!slot) return 0xFFFFFFFFu;
-  const unsigned long long v = slot[1];
+  const unsigned long long v = ld_sc1(slot + 1);
   return (uint32_t)(v >> 32) == epoch ? ~(uint32_t)v : 0xFFFFFFFFu;
 }
 
@@ -1521,236 +1535,7 @@ __device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t
   __syncthreads();
 }
 
-/* 1 + the batch-global index of the last frame before tile `tile` with aux
- * word `w` set (walks the earlier tiles' aux rows), or 0. */
-__device__ uint32_t prev_tiles_last(const uint32_t *aux, uint32_t tile, uint32_t w) {
-  for (int t = (int)tile - 1; t >= 0; --t) {
-    const uint32_t v = aux[t * 4 + w];
-    if (v) return (uint32_t)t * TILE + v;
-  }
-  return 0;
-}
-
 #define TX_BRIDGE_LDS_SLOTS 2048u   /* bridge sets up to 16 KiB are staged in LDS */
-
-template <bool LDS>
-__global__ __launch_bounds__(NTHREADS) void tx_scan_kernel(TxArgs t) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  const ClassifyArgs &a = t.a;
-  const Lds L = carve(smem, a.nbins);
-  const uint32_t tid = threadIdx.x;
-  const uint32_t tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  const uint4 *T = a.table;
-  if (LDS) {
-    for (uint32_t k = tid; k < a.table_units; k += NTHREADS) L.table[k] = a.table[k];
-    T = L.table;
-  }
-  __shared__ uint32_t s_carry[8];
-  __shared__ uint32_t s_last;
-  if (tid == 0) s_last = 0;
-  __syncthreads();
-  if (tile == 0) {   // carried-in cache of this source, for tx_hits / tx_fill
-    if (tid < 4) t.counters[tid] = 0;   // learned count, flags, sets used: read from tx_hits on
-    resolve_carry(a, s_carry, L.scratch);
-    if (tid == 0) {
-      usn_summary *S = a.summary;
-      S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
-      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
-      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
-      S->flags = 0; S->first_break = 0xFFFFFFFFu;
-    }
-  }
-  /* all header loads of the tile first (64 B x 4 frames per lane in flight) */
-  uint4 qq[ROUNDS][4];
-  uint32_t ll[ROUNDS];
-  const uint8_t *fps[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const uint64_t i = base + (local < nt ? local : 0);
-    fps[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
-    ll[r] = a.lens[i];
-  }
-  /* the bridge snapshot set in LDS when small */
-  const unsigned long long *BS = t.bridge_set;
-  if (t.bridge_mask < TX_BRIDGE_LDS_SLOTS) {
-    unsigned long long *bs = reinterpret_cast<unsigned long long *>(L.table + (LDS ? table_lds_units(a.table_units) : 0));
-    for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
-    BS = bs;
-  }
-  __syncthreads();
-  // parse and flag every round; the answer-key probes of all rounds are then
-  // issued together (two round trips for the tile's four rounds)
-  const uint32_t lane = tid & 63;
-  uint32_t last = 0;
-  uint4 rec[ROUNDS];
-  bool need[ROUNDS];
-  uint32_t kx[ROUNDS], ky[ROUNDS], kz[ROUNDS], km[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const uint4 *q = qq[r];
-    Parsed p;
-    parse(q, local < nt ? ll[r] : 0u, fps[r], a.window, p);
-    const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
-    const uint64_t smac = (uint64_t)(q[0].y >> 16) | ((uint64_t)q[0].z << 16);
-    const bool loop = p.status == 1u && (p.dst >> 24) == 127u;
-    const uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
-                         : (p.status == 1u && !loop) ? 1u : 2u;
-    uint32_t f = (touch << TXR_TOUCH_SHIFT);
-    uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
-    if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
-    // the frame before it in the tile (lane - 1) retains the same info: this
-    // one is a cache hit (or the host's, as that one is) and learns nothing,
-    // so its answer key need not be probed
-    const uint32_t i0 = r0.x & TXR_I0_MASK;
-    const uint32_t pi0 = __shfl_up(touch == 1u ? i0 : 0xFFFFFFFFu, 1, 64);
-    const uint32_t py = __shfl_up(r0.y, 1, 64), pz = __shfl_up(r0.z, 1, 64), pw = __shfl_up(r0.w, 1, 64);
-    const bool repeat = lane > 0 && touch == 1u && pi0 == i0 && py == r0.y && pz == r0.z && pw == r0.w;
-    if (touch == 1u || touch == 2u) {
-      const bool s_in = bridge_has(BS, t.bridge_mask, smac);
-      const bool d_in = bridge_has(BS, t.bridge_mask, dmac);
-      if (s_in) f |= TXR_SMAC_IN;
-      if (d_in) f |= TXR_DMAC_IN;
-      if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
-    }
-    if (touch == 3u) f |= TXR_HOST;                           // later fragment: map lookup
-    if (p.status == 5u) f |= TXR_WINDOW;                      // ports past the window
-    need[r] = false;
-    kx[r] = 0; ky[r] = 0; kz[r] = 0; km[r] = 0;
-    if (touch == 1u) {
-      // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
-      bool listening = false;
-      for (uint32_t k = 0; k < t.n_listen; ++k) {
-        const uint32_t ld = t.listen[2 * k], lw = t.listen[2 * k + 1];
-        const uint32_t lhas = (lw >> 8) & 1u;
-        listening |= ld == p.src && (lw & 0xFFu) == p.proto && lhas == p.has_ports &&
-                     (!lhas || (lw >> 16) == p.sport);
-      }
-      const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
-                            p.dport == 67u && (p.dst & 0xFFu) == 255u;
-      if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
-      if (!listening && !dhcp_req && !repeat) {   // learned unless the table has the answer key
-        want_key(make_uint4(p.i0, p.src, p.dst, p.ports), kx[r], ky[r], kz[r], km[r]);
-        need[r] = !USN_ABL_TXNOPROBE;
-      }
-      if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
-    }
-    if (p.status == 1u && p.frag_first) f |= TXR_FRAG1;
-    r0.x = i0 | f;
-    rec[r] = r0;
-    if (local < nt && touch) last = local + 1;
-  }
-  uint32_t w[ROUNDS];
-  ph_probe_many<LDS, ROUNDS, ROUNDS>(T, a, kx, ky, kz, km, need, w);
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
-    if (local < nt) t.rec[base + local] = rec[r];
-  }
-  if (last) atomicMax(&s_last, last);
-  __syncthreads();
-  if (tid == 0) t.aux[tile * 4 + 0] = s_last;
-}
-
-__global__ __launch_bounds__(NTHREADS) void tx_hits_kernel(TxArgs t) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  const ClassifyArgs &a = t.a;
-  const Lds L = carve(smem, a.nbins);
-  const uint32_t tid = threadIdx.x;
-  const uint32_t tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  __shared__ uint32_t s_last_nh, s_ins;
-  if (tid == 0) { s_last_nh = 0; s_ins = 0; }
-  uint32_t ins = 0;        // bit 0: a MAC was inserted, bit 1: a rule
-  uint4 *srec = L.table;   // the tile's first record words, for the previous-frame compares
-  uint4 r0[ROUNDS];
-  uint32_t v[ROUNDS], prev[ROUNDS];
-  // last touching frame of the earlier tiles, and its record: independent of
-  // this tile's records, so their loads overlap the tile's
-  const uint32_t before = prev_tiles_last(t.aux, tile, 0);   // 1 + index, 0 = none
-  const uint4 brec = t.rec[before ? before - 1 : 0];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    r0[r] = t.rec[base + (local < nt ? local : 0)];   // unpredicated: loads overlap
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) r0[r] = make_uint4(0, 0, 0, 0);
-    srec[local] = r0[r];
-    v[r] = (local < nt && tx_touch(r0[r])) ? local + 1 : 0u;
-  }
-  tile_prefix_max(v, L, prev);   // its barriers also publish srec
-  const usn_summary *S = a.summary;
-  uint32_t last_nh = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) continue;
-    const uint64_t i = base + local;
-    uint32_t fl = r0[r].x;
-    const uint32_t touch = tx_touch(r0[r]);
-    if (!touch) continue;
-    bool hit = false;
-    if (touch == 1u) {
-      const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
-      const uint32_t info0 = fl & TXR_I0_MASK;
-      if (k1) {
-        const uint4 pr = prev[r] ? srec[prev[r] - 1] : brec;
-        const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == r0[r].y &&
-                          pr.z == r0[r].z && pr.w == r0[r].w;
-        if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
-        else hit = same;
-      } else {
-        hit = (S->cin_state & USN_CS_VALID) && S->cin_info[0] == info0 && S->cin_info[1] == r0[r].y &&
-              S->cin_info[2] == r0[r].z && S->cin_info[3] == r0[r].w;
-      }
-    }
-    if (hit) fl |= TXR_HIT;
-    if (fl != r0[r].x) t.rec[i].x = fl;
-    if (!hit) last_nh = local + 1;
-    if (hit || (fl & TXR_HOST)) continue;
-    // this frame really learns: first occurrence per item
-    if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
-      const uint4 r1 = frame_head(a, i);
-      if (fl & TXR_LEARNMAC) {
-        const uint64_t m = rec_smac(r1);
-        unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
-                                             usn_mac_hash(m), t.counters + 1);
-        if (slot) first_index_update(slot + 1, t.epoch, (uint32_t)i);
-        ins |= 1u;
-      }
-      if (fl & TXR_LEARNRULE) {
-        uint32_t x, y, z, meta;
-        want_key(r0[r], x, y, z, meta);
-        const uint64_t fp = usn_key_fp48(x, y, z, meta);
-        unsigned long long *slot = set_claim(t.ruleset, t.ruleset_mask, 4, t.epoch, fp,
-                                             usn_key_hash(x, y, z, meta), t.counters + 1);
-        if (slot) {
-          slot[2] = ((unsigned long long)y << 32) | x;   // full key: collision check in tx_decide
-          slot[3] = ((unsigned long long)meta << 32) | z;
-          first_index_update(slot + 1, t.epoch, (uint32_t)i);
-        }
-        ins |= 2u;
-      }
-    }
-  }
-  if (last_nh) atomicMax(&s_last_nh, last_nh);
-  if (ins) atomicOr(&s_ins, ins);
-  __syncthreads();
-  if (tid == 0) {
-    t.aux[tile * 4 + 1] = s_last_nh;
-    if (s_ins) atomicOr(t.counters + 2, s_ins);   // which sets tx_decide must look in
-  }
-}
 
 /* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
  * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
@@ -1774,8 +1559,8 @@ __device__ __forceinline__ uint32_t tx_learned_key1(const TxArgs &t, uint32_t x,
   const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                             usn_key_fp48(x, y, z, meta), usn_key_hash(x, y, z, meta));
   if (slot_first(slot, t.epoch) > i) return 0u;
-  if (slot[2] != (((unsigned long long)y << 32) | x) ||
-      slot[3] != (((unsigned long long)meta << 32) | z))
+  if (ld_sc1(slot + 2) != (((unsigned long long)y << 32) | x) ||
+      ld_sc1(slot + 3) != (((unsigned long long)meta << 32) | z))
     atomicOr(t.counters + 1, 2u);                      // fingerprint collision: host redoes
   return USN_SLOT_VALID | (t.a.src << 16);
 }
@@ -1819,56 +1604,507 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   return tx_lookup_dec(a, fl, w);
 }
 
-/* tx_decide + tx_fill in one launch: non-hit decisions into LDS, then every
- * hit takes its run head's decision -- from LDS when the head is in the tile,
- * else from the one head before the tile (recomputed here from its record) or
- * the carried-in cache -- then the tile order and header. */
+/* ---- the tx batch in one launch ------------------------------------------
+ * A tile waits only on tiles with smaller indices, which are dispatched
+ * before it (blocks go out in index order, dealt round-robin over the XCDs;
+ * HIP does not promise it, so every wait is bounded: see below).  An
+ * ordered-ticket counter instead (one atomic per block on one word) spread
+ * the block starts over 12 us at 1024 blocks.  What crosses a tile boundary
+ * goes through per-tile aux granules: 8 bytes {epoch, value}, each written
+ * by ONE agent-scope (sc1, write-through) store and read by sc1 loads until
+ * its tag is the batch epoch, so a granule is its own flag (MI355X guide,
+ * Guideline 16 R2; no fences, no stale L1/L2 copies):
+ *   phase 1  parse, flags and the answer-key probes of the tile; publish its
+ *            last touching frame (LAST, LREC); take the last touching frame
+ *            before the tile from the tiles before; cache hits; the
+ *            first-occurrence claims of what the tile learns (atomics and
+ *            sc1 stores, drained by every wave); then publish the last
+ *            non-hit touching frame (HEAD, HREC) and INS, whose arrival also
+ *            says that the tile's claims are in the sets (R1)
+ *   phase 2  one wave waits for INS of every earlier tile; the run head
+ *            before the tile, decisions (get_endpoint probes batched; set
+ *            slots read sc1), run-head fill, learned list, order, header.
+ * A wait that outlasts TX_SPIN_TICKS marks the batch (counters[3] = epoch;
+ * later waits then give up at once): usn_finalize redoes it on the host. */
+#define TXG_LAST 0u    /* 1 + tile-local index of the last touching frame, 0 none */
+#define TXG_LREC 1u    /* 4 granules: its record (flags of the scan; zeros if none) */
+#define TXG_INS 5u     /* bit 0/1: the tile inserted MACs / rules, bit 2: a set overflowed */
+#define TXG_HEAD 6u    /* 1 + tile-local index of the last non-hit touching frame, 0 none */
+#define TXG_HREC 7u    /* 4 granules: its record (flags after the hit pass; zeros if none) */
+#define TXG_PINS 11u   /* INS of every tile up to and including this one */
+#define TXG_PHEAD 12u  /* 1 + batch index of the last non-hit touching frame up to this tile, 0 none */
+#define TXG_CIN 13u    /* tile 0: 6 granules, the carried-in cache {state, dst, info[4]} */
+#define TXG_EARLY 19u  /* bit 0/1: the tile has frames flagged to learn a MAC / rule (before
+                          the hit pass: a superset of what it inserts), out with LAST */
+#define TXG_PEARLY 20u /* EARLY of every tile up to and including this one */
+static_assert(TXG_CIN + 6 <= TXA_GRANULES, "aux granules");
+#define TX_SPIN_TICKS (200u * 100000u)   /* 200 ms of the 100 MHz real-time clock */
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ void g_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
+  __hip_atomic_store((gu64 *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_put4(unsigned long long *g, uint32_t epoch, const uint4 &v) {
+  g_put(g, epoch, v.x); g_put(g + 1, epoch, v.y); g_put(g + 2, epoch, v.z); g_put(g + 3, epoch, v.w);
+}
+__device__ __forceinline__ bool tx_timed_out(const TxArgs &t) {
+  return __hip_atomic_load((gu32 *)(t.counters + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+         t.epoch;
+}
+/* the values of granules g[0..N) once all carry the batch epoch (the N
+ * loads of a poll fly together); false after TX_SPIN_TICKS or once any wait
+ * of the batch has timed out */
+template <int N>
+__device__ bool g_getn(const unsigned long long *g, const TxArgs &t, uint32_t (&v)[N]) {
+  uint64_t t0 = 0;
+  for (uint32_t it = 0;; ++it) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const unsigned long long x =
+          __hip_atomic_load((gu64 *)(g + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[k] = (uint32_t)x;
+      ok &= (uint32_t)(x >> 32) == t.epoch;
+    }
+    if (ok) return true;
+    if (tx_timed_out(t)) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (it == 0) {
+      t0 = now;
+    } else if (now - t0 > TX_SPIN_TICKS) {
+      atomicMax(t.counters + 3, t.epoch);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+/* one read of granule g: true (and v) when it carries the batch epoch */
+__device__ __forceinline__ bool g_try(const unsigned long long *g, const TxArgs &t, uint32_t &v) {
+  const unsigned long long x = __hip_atomic_load((gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = (uint32_t)x;
+  return (uint32_t)(x >> 32) == t.epoch;
+}
+
+/* Tiles [0, tile): the OR of their INS and the last non-hit touching frame
+ * among them (1 + batch index, 0 none), once every one of them has published
+ * (INS comes after its claims landed).  All threads of the block: thread k
+ * reads the INS/HEAD granules of tiles tile-1-k, tile-1-k-NTHREADS, ... down
+ * to tile-TX_LOOKBACK, all loads of a poll together; the tiles below that are
+ * covered by the prefix (PINS/PHEAD) that tile tile-TX_LOOKBACK-1 published
+ * after its own look-back.  Results into *ins_out / *head_out (LDS, zeroed by
+ * the caller); false after a timeout. */
+#define TX_LB_PER_THREAD 4
+#define TX_LOOKBACK (NTHREADS * TX_LB_PER_THREAD)
+__device__ bool tx_lookback(const TxArgs &t, uint32_t tile, uint32_t *ins_out, uint32_t *head_out) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t ins = 0, head = 0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < TX_LB_PER_THREAD; ++k) {
+    const int u = (int)tile - 1 - (int)tid - k * (int)NTHREADS;
+    if (u < 0 || !ok) continue;
+    uint32_t v[2];
+    ok = g_getn<2>(t.aux + (size_t)u * TXA_GRANULES + TXG_INS, t, v);   // INS, HEAD
+    if (!ok) break;
+    ins |= v[0] & 3u;
+    const uint32_t h = min(v[1], (uint32_t)TILE);
+    if (h) head = max(head, (uint32_t)u * TILE + h);
+  }
+  const int below = (int)tile - 1 - (int)TX_LOOKBACK;   // the prefix of [0, below]
+  if (ok && tid == 0 && below >= 0) {
+    uint32_t v[2];
+    ok = g_getn<2>(t.aux + (size_t)below * TXA_GRANULES + TXG_PINS, t, v);   // PINS, PHEAD
+    if (ok) { ins |= v[0] & 3u; head = max(head, v[1]); }
+  }
+  if (ins) atomicOr(ins_out, ins);
+  if (head) atomicMax(head_out, head);
+  return ok;
+}
+
+/* The OR of EARLY over tiles [0, tile), the same way as tx_lookback (EARLY
+ * goes out long before INS: a tile whose predecessors flag nothing to learn
+ * need not wait for their claims). */
+__device__ bool tx_lookback_early(const TxArgs &t, uint32_t tile, uint32_t *early_out) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t e = 0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < TX_LB_PER_THREAD; ++k) {
+    const int u = (int)tile - 1 - (int)tid - k * (int)NTHREADS;
+    if (u < 0 || !ok) continue;
+    uint32_t v[1];
+    ok = g_getn<1>(t.aux + (size_t)u * TXA_GRANULES + TXG_EARLY, t, v);
+    if (ok) e |= v[0];
+  }
+  const int below = (int)tile - 1 - (int)TX_LOOKBACK;
+  if (ok && tid == 0 && below >= 0) {
+    uint32_t v[1];
+    ok = g_getn<1>(t.aux + (size_t)below * TXA_GRANULES + TXG_PEARLY, t, v);
+    if (ok) e |= v[0];
+  }
+  if (e) atomicOr(early_out, e);
+  return ok;
+}
+
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+/* tile 0's carried-in cache {state, dst, info[4]} (zeros after a timeout) */
+__device__ __forceinline__ void tx_load_cin(const TxArgs &t, uint32_t *cin) {
+  uint32_t v[6];
+  const bool ok = g_getn<6>(t.aux + TXG_CIN, t, v);
+  for (int k = 0; k < 6; ++k) cin[k] = ok ? v[k] : 0u;
+}
+
+/* the decision of a non-hit touching tx frame (the run head before a tile) */
 template <bool LDS>
-__global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
+__device__ uint32_t tx_nonhit_dec(const TxArgs &t, const uint4 *T, const uint4 &r0, const uint4 &r1,
+                                  uint32_t i, uint32_t ins) {
+  const uint32_t fl = r0.x, touch = tx_touch(r0), kind = fl & 0xFFu;
+  if (touch == 0u) return usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
+  if (fl & TXR_HOST)
+    return usn_mkdec(USN_CLS_DROP, (fl & TXR_WINDOW) ? USN_R_WINDOW : touch == 3u ? USN_R_FRAGMISS
+                                                                           : USN_R_NOMATCH, 0xFFFFu) |
+           USN_F_HOST;
+  if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) return usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
+  if (touch == 2u) return usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
+  return decide_tx_ipv4<LDS>(t, T, r0, r1, i, ins);
+}
+
+/* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge */
+__host__ __device__ inline size_t tx_lds_head(uint32_t nbins) {
+  return lds_core_bytes(nbins) + (size_t)TILE * 16 + (size_t)TILE * 4;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void tx_kernel(TxArgs t) {
   extern __shared__ __align__(16) uint8_t smem[];
   const ClassifyArgs &a = t.a;
   const Lds L = carve(smem, a.nbins);
+  uint4 *srec = reinterpret_cast<uint4 *>(smem + lds_core_bytes(a.nbins));   // the tile's records
+  uint32_t *sdec = reinterpret_cast<uint32_t *>(srec + TILE);               // its decisions
+  uint4 *stab = reinterpret_cast<uint4 *>(sdec + TILE);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  uint32_t *sdec = reinterpret_cast<uint32_t *>(L.table + (LDS ? table_lds_units(a.table_units) : 0));
+  __shared__ uint32_t s_last, s_lastnh, s_ins, s_ovf, s_insall, s_hidx, s_before, s_head;
+  __shared__ uint32_t s_early, s_early_all, s_slow;
+  __shared__ uint32_t s_cin[6];   // the carried-in cache {state, dst, info[4]} (tile 0's)
+  __shared__ uint4 s_brec;
+  __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
-  __shared__ uint32_t s_head;      // decision of the last non-hit touching frame before the tile
-  const uint4 *T = a.table;
-  if (LDS) {
-    for (uint32_t k = tid; k < a.table_units; k += NTHREADS) L.table[k] = a.table[k];
-    T = L.table;
+  if (tid == 0) {
+    s_last = 0; s_lastnh = 0; s_ins = 0; s_ovf = 0; s_insall = 0; s_hidx = 0; s_before = 0;
+    s_early = 0; s_early_all = 0; s_slow = 0;
   }
   if (tid < 8) s_misc[tid] = 0;
   for (uint32_t k = tid; k < NSEG * cnt_rows(a.nbins); k += NTHREADS) L.cnt[k] = 0;
-  // which device sets hold items: r1 (the MACs) is needed only when a MAC set
-  // does (the dmac test, the first learner's smac)
-  const uint32_t ins = __builtin_amdgcn_readfirstlane(t.counters[2]);
-  uint4 r0[ROUNDS], r1[ROUNDS];
+  __syncthreads();
+  const uint32_t tile = blockIdx.x;
+  STAMP_DECL
+  STAMP(0);   // tickets out of step with the host: the waits time out
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+  unsigned long long *aux = t.aux + (size_t)tile * TXA_GRANULES;
+  const uint4 *T = a.table;
+  if (LDS) {
+    for (uint32_t k = tid; k < a.table_units; k += NTHREADS) stab[k] = a.table[k];
+    T = stab;
+  }
+  if (tile == 0) {   // carried-in cache of this source; counters for phase 2 (all wait for tile 0)
+    if (tid < 3) __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    resolve_carry(a, s_carry, L.scratch);
+    if (tid == 0) {
+      for (int k = 0; k < 6; ++k) {
+        s_cin[k] = s_carry[k];
+        g_put(aux + TXG_CIN + k, t.epoch, s_carry[k]);
+      }
+      usn_summary *S = a.summary;
+      S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
+      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
+      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      S->flags = 0; S->first_break = 0xFFFFFFFFu;
+    }
+  }
+  /* all header loads of the tile first (64 B x 4 frames per lane in flight) */
+  uint4 qq[ROUNDS][4];
+  uint32_t ll[ROUNDS];
+  const uint8_t *fps[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     const uint64_t i = base + (local < nt ? local : 0);
-    r0[r] = t.rec[i];            // unpredicated (clamped index): the loads overlap
-    r1[r] = make_uint4(0, 0, 0, 0);
-    if (ins & 1u) r1[r] = frame_head(a, i);
-  }
+    fps[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r)
-    if (r * NTHREADS + tid >= nt) { r0[r] = make_uint4(0, 0, 0, 0); r1[r] = make_uint4(0, 0, 0, 0); }
-  const uint32_t before = prev_tiles_last(t.aux, tile, 1);   // 1 + index, 0 = none
+    for (uint32_t k = 0; k < 4; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
+    ll[r] = a.lens[i];
+  }
+  /* the bridge snapshot set in LDS when small */
+  const unsigned long long *BS = t.bridge_set;
+  if (t.bridge_mask < TX_BRIDGE_LDS_SLOTS) {
+    unsigned long long *bs = reinterpret_cast<unsigned long long *>(stab + (LDS ? table_lds_units(a.table_units) : 0));
+    for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
+    BS = bs;
+  }
+  __syncthreads();
+  STAMP(1);
+  // parse and flag every round; the answer-key probes of all rounds are then
+  // issued together (two round trips for the tile's four rounds)
+  uint32_t last = 0;
+  uint4 rec[ROUNDS];
+  // keys probed in phase 1: [0, R) answer keys (table K1), [R, 2R) key1 (K1)
+  // and [2R, 3R) key2 (K2) of the frames that will likely need get_endpoint
+  // (dmac in the bridge snapshot; phase 2 probes any other that turns out to)
+  constexpr int R3 = 3 * ROUNDS;
+  bool need[R3];
+  uint32_t ax[R3], ay[R3], az[R3], am[R3];
+#pragma unroll
+  for (int k = 0; k < R3; ++k) { need[k] = false; ax[k] = 0; ay[k] = 0; az[k] = 0; am[k] = 0; }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    const uint4 *q = qq[r];
+    Parsed p;
+    parse(q, local < nt ? ll[r] : 0u, fps[r], a.window, p);
+    const uint64_t dmac = (uint64_t)q[0].x | ((uint64_t)(q[0].y & 0xFFFFu) << 32);
+    const uint64_t smac = (uint64_t)(q[0].y >> 16) | ((uint64_t)q[0].z << 16);
+    const bool loop = p.status == 1u && (p.dst >> 24) == 127u;
+    const uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
+                         : (p.status == 1u && !loop) ? 1u : 2u;
+    uint32_t f = (touch << TXR_TOUCH_SHIFT);
+    uint4 r0 = make_uint4(p.status == 4u ? 0u : p.i0, p.src, p.dst, p.ports);
+    if (p.status != 1u) { r0.y = 0; r0.z = 0; r0.w = 0; }
+    // the frame before it in the tile (lane - 1) retains the same info: this
+    // one is a cache hit (or the host's, as that one is) and learns nothing,
+    // so its answer key need not be probed
+    const uint32_t i0 = r0.x & TXR_I0_MASK;
+    const uint32_t pi0 = __shfl_up(touch == 1u ? i0 : 0xFFFFFFFFu, 1, 64);
+    const uint32_t py = __shfl_up(r0.y, 1, 64), pz = __shfl_up(r0.z, 1, 64), pw = __shfl_up(r0.w, 1, 64);
+    const bool repeat = lane > 0 && touch == 1u && pi0 == i0 && py == r0.y && pz == r0.z && pw == r0.w;
+    if (touch == 1u || touch == 2u) {
+      const bool s_in = bridge_has(BS, t.bridge_mask, smac);
+      const bool d_in = bridge_has(BS, t.bridge_mask, dmac);
+      if (s_in) f |= TXR_SMAC_IN;
+      if (d_in) f |= TXR_DMAC_IN;
+      if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
+    }
+    if (touch == 3u) f |= TXR_HOST;                           // later fragment: map lookup
+    if (p.status == 5u) f |= TXR_WINDOW;                      // ports past the window
+    if (touch == 1u) {
+      // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
+      bool listening = false;
+      for (uint32_t k = 0; k < t.n_listen; ++k) {
+        const uint32_t ld = t.listen[2 * k], lw = t.listen[2 * k + 1];
+        const uint32_t lhas = (lw >> 8) & 1u;
+        listening |= ld == p.src && (lw & 0xFFu) == p.proto && lhas == p.has_ports &&
+                     (!lhas || (lw >> 16) == p.sport);
+      }
+      const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
+                            p.dport == 67u && (p.dst & 0xFFu) == 255u;
+      if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
+      if (!listening && !dhcp_req && !repeat) {   // learned unless the table has the answer key
+        want_key(make_uint4(p.i0, p.src, p.dst, p.ports), ax[r], ay[r], az[r], am[r]);
+        need[r] = !USN_ABL_TXNOPROBE;
+      }
+      if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
+    }
+    if (p.status == 1u && p.frag_first) f |= TXR_FRAG1;
+    r0.x = i0 | f;
+    rec[r] = r0;
+    if (local < nt && touch) last = local + 1;
+    const uint32_t kind = i0 & 0xFFu;
+    if (touch == 1u && !(f & TXR_HOST) && (f & TXR_DMAC_IN) && !repeat && kind != USN_INFO_ARP &&
+        kind != USN_INFO_EAPOL && !USN_ABL_TXNOPROBE) {
+      need[ROUNDS + r] = need[2 * ROUNDS + r] = true;
+      key1_of(r0, ax[ROUNDS + r], ay[ROUNDS + r], az[ROUNDS + r], am[ROUNDS + r]);
+      key2_of(r0, ax[2 * ROUNDS + r], ay[2 * ROUNDS + r], az[2 * ROUNDS + r], am[2 * ROUNDS + r]);
+    }
+  }
+  uint32_t w1e[ROUNDS], w2e[ROUNDS];   // key1 / key2 results, valid where need[R + r]
+  bool pre[ROUNDS];
+  {
+    uint32_t w[R3];
+    ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
+      pre[r] = need[ROUNDS + r];
+      w1e[r] = w[ROUNDS + r];
+      w2e[r] = w[2 * ROUNDS + r];
+    }
+  }
+
+  STAMP(2);
+  // ---- the tile's records in LDS; each frame's previous touching frame
+  uint32_t vt[ROUNDS], prev[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) rec[r] = make_uint4(0, 0, 0, 0);
+    srec[local] = rec[r];
+    vt[r] = (local < nt && tx_touch(rec[r])) ? local + 1 : 0u;
+    if (local < nt && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE)))
+      atomicOr(&s_early, ((rec[r].x & TXR_LEARNMAC) ? 1u : 0u) | ((rec[r].x & TXR_LEARNRULE) ? 2u : 0u));
+  }
+  if (last) atomicMax(&s_last, last);
+  tile_prefix_max(vt, L, prev);   // its barriers also publish srec and s_last
+  if (tid == 0) {
+    const uint32_t lt = s_last;
+    g_put4(aux + TXG_LREC, t.epoch, lt ? srec[lt - 1] : make_uint4(0, 0, 0, 0));
+    g_put(aux + TXG_LAST, t.epoch, lt);
+    g_put(aux + TXG_EARLY, t.epoch, s_early);
+    // the last touching frame before the tile (a tile without one is skipped)
+    uint32_t before = 0;
+    uint4 brec = make_uint4(0, 0, 0, 0);
+    for (int u = (int)tile - 1; u >= 0; --u) {
+      uint32_t v[5];   // LAST, LREC
+      if (!g_getn<5>(t.aux + (size_t)u * TXA_GRANULES + TXG_LAST, t, v)) break;
+      const uint32_t lu = min(v[0], (uint32_t)TILE);
+      if (lu) {
+        before = (uint32_t)u * TILE + lu;
+        brec = make_uint4(v[1], v[2], v[3], v[4]);
+        break;
+      }
+    }
+    s_before = before;
+    s_brec = brec;
+    if (tile > 0 && before == 0) tx_load_cin(t, s_cin);   // the first touching frame's cache
+  }
+  __syncthreads();
+  STAMP(3);
+  // ---- cache hits (endpoint.rs:186-191); what a frame really learns is
+  //      claimed in the epoch-tagged sets with its index (first occurrence wins)
+  const uint32_t before = s_before;
+  const uint4 brec = s_brec;
+  uint32_t last_nh = 0, ins = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint64_t i = base + local;
+    uint32_t fl = rec[r].x;
+    const uint32_t touch = tx_touch(rec[r]);
+    if (!touch) continue;
+    bool hit = false;
+    if (touch == 1u) {
+      const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
+      const uint32_t info0 = fl & TXR_I0_MASK;
+      if (k1) {
+        const uint4 pr = prev[r] ? srec[prev[r] - 1] : brec;
+        const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == rec[r].y &&
+                          pr.z == rec[r].z && pr.w == rec[r].w;
+        if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
+        else hit = same;
+      } else {
+        hit = (s_cin[0] & USN_CS_VALID) && s_cin[2] == info0 && s_cin[3] == rec[r].y &&
+              s_cin[4] == rec[r].z && s_cin[5] == rec[r].w;
+      }
+    }
+    if (hit) fl |= TXR_HIT;
+    rec[r].x = fl;
+    if (!hit) last_nh = local + 1;
+    if (hit || (fl & TXR_HOST)) continue;
+    if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
+      if (fl & TXR_LEARNMAC) {
+        const uint64_t m = rec_smac(frame_head(a, i));
+        unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
+                                             usn_mac_hash(m), &s_ovf);
+        if (slot) first_index_update(slot + 1, t.epoch, (uint32_t)i);
+        ins |= 1u;
+      }
+      if (fl & TXR_LEARNRULE) {
+        uint32_t x, y, z, meta;
+        want_key(rec[r], x, y, z, meta);
+        const uint64_t fp = usn_key_fp48(x, y, z, meta);
+        unsigned long long *slot = set_claim(t.ruleset, t.ruleset_mask, 4, t.epoch, fp,
+                                             usn_key_hash(x, y, z, meta), &s_ovf);
+        if (slot) {
+          st_sc1(slot + 2, ((unsigned long long)y << 32) | x);   // full key: collision check below
+          st_sc1(slot + 3, ((unsigned long long)meta << 32) | z);
+          first_index_update(slot + 1, t.epoch, (uint32_t)i);
+        }
+        ins |= 2u;
+      }
+    }
+  }
+  if (last_nh) atomicMax(&s_lastnh, last_nh);
+  if (ins) atomicOr(&s_ins, ins);
+  vm_drain();                  // this wave's claims (atomics, sc1 stores) have landed
+  __syncthreads();             // (and every frame has read srec)
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) srec[r * NTHREADS + tid] = rec[r];   // flags after the hit pass
+  __syncthreads();
+  if (tid == 0) {   // INS last: its arrival also says the claims above have landed (R1)
+    const uint32_t hn = s_lastnh;
+    g_put4(aux + TXG_HREC, t.epoch, hn ? srec[hn - 1] : make_uint4(0, 0, 0, 0));
+    g_put(aux + TXG_HEAD, t.epoch, hn);
+    g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
+  }
+  STAMP(4);
+  // ---- phase 2: the sets as every earlier frame left them, and the last
+  //      non-hit touching frame before the tile.  When no earlier tile
+  //      flagged anything to learn (EARLY, out with LAST), no earlier tile
+  //      claims: only the nearest tiles' HEAD is waited for.  Otherwise, or
+  //      when the head is further back, every earlier tile's INS (tx_lookback).
+  tx_lookback_early(t, tile, &s_early_all);
   __syncthreads();
   if (tid == 0) {
-    const usn_summary *S = a.summary;
-    uint32_t hd = S->cin_dst;
-    if (before && !USN_ABL_NOHEAD) {   // (A/B only: NOHEAD measures the recompute)
-      const uint4 h0 = t.rec[before - 1];
-      const uint4 h1 = (ins & 1u) ? frame_head(a, before - 1) : make_uint4(0, 0, 0, 0);
-      hd = decide_tx_ipv4<LDS>(t, T, h0, h1, before - 1, ins);
+    bool slow = s_early_all != 0;
+    if (!slow) {
+      uint32_t hx = 0;
+      int u = (int)tile - 1;
+      for (int steps = 0; u >= 0 && steps < 8; --u, ++steps) {
+        uint32_t v[1];
+        if (!g_getn<1>(t.aux + (size_t)u * TXA_GRANULES + TXG_HEAD, t, v)) break;
+        const uint32_t h = min(v[0], (uint32_t)TILE);
+        if (h) { hx = (uint32_t)u * TILE + h; break; }
+      }
+      if (hx || u < 0) s_hidx = hx;   // found, or none in the batch
+      else slow = true;               // further back than 8 tiles
+    }
+    s_slow = slow;
+  }
+  __syncthreads();
+  if (s_slow) {
+    tx_lookback(t, tile, &s_insall, &s_hidx);
+    __syncthreads();
+  }
+  if (tid == 0) {   // this tile's prefixes, for the tiles TX_LOOKBACK + 1 and more after it
+    const uint32_t own = s_lastnh;
+    g_put(aux + TXG_PINS, t.epoch, s_insall | s_ins);
+    g_put(aux + TXG_PHEAD, t.epoch, own ? (uint32_t)base + own : s_hidx);
+    g_put(aux + TXG_PEARLY, t.epoch, s_early_all | s_early);
+  }
+  const uint32_t insall = __builtin_amdgcn_readfirstlane(s_insall | s_ins);
+  if (tid == 0) {
+    if (s_ovf) atomicOr(t.counters + 1, 1u);
+    if (s_ins) atomicOr(t.counters + 2, s_ins);
+    // the decision of the run head before the tile: recomputed from its record
+    const uint32_t hx = s_hidx;
+    uint32_t hd = 0;
+    uint32_t hv[4];
+    if (!hx) {   // no non-hit touching frame before the tile: the carried-in cache's
+      if (tile > 0) tx_load_cin(t, s_cin);
+      hd = s_cin[1];
+    } else if (!USN_ABL_NOHEAD &&   // (A/B only: NOHEAD measures the recompute)
+               g_getn<4>(t.aux + (size_t)((hx - 1) / TILE) * TXA_GRANULES + TXG_HREC, t, hv)) {
+      const uint4 h0 = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+      const uint4 h1 = (insall & 1u) ? frame_head(a, hx - 1) : make_uint4(0, 0, 0, 0);
+      hd = tx_nonhit_dec<LDS>(t, T, h0, h1, hx - 1, insall);
     }
     s_head = hd;
   }
+  STAMP(5);
+  // MACs (dmac test, the first learner's smac) only when some frame <= this tile learned one
+  uint4 r1[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    r1[r] = make_uint4(0, 0, 0, 0);
+    if ((insall & 1u) && local < nt) r1[r] = frame_head(a, base + local);
+  }
+  const uint32_t ins_d = insall;
   uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
   // every decision but get_endpoint's first; then key1 and key2 of all the
   // rounds that need get_endpoint are probed together (two round trips for
@@ -1878,7 +2114,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    const uint32_t fl = r0[r].x, touch = local < nt ? tx_touch(r0[r]) : 0u, kind = fl & 0xFFu;
+    const uint32_t fl = rec[r].x, touch = local < nt ? tx_touch(rec[r]) : 0u, kind = fl & 0xFFu;
     use[r] = false; use[ROUNDS + r] = false;
     kx[r] = ky[r] = kz[r] = km[r] = 0;
     kx[ROUNDS + r] = ky[ROUNDS + r] = kz[ROUNDS + r] = km[ROUNDS + r] = 0;
@@ -1895,28 +2131,42 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
       d = usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
-    } else if (!tx_dmac_in(t, fl, r1[r], (uint32_t)(base + local), ins)) {
+    } else if (!tx_dmac_in(t, fl, r1[r], (uint32_t)(base + local), ins_d)) {
       d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
     } else {
       d = usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);  // (the A/B no-probe build keeps it)
-      use[r] = use[ROUNDS + r] = !USN_ABL_TXNOPROBE;
-      key1_of(r0[r], kx[r], ky[r], kz[r], km[r]);
-      key2_of(r0[r], kx[ROUNDS + r], ky[ROUNDS + r], kz[ROUNDS + r], km[ROUNDS + r]);
+      use[r] = !USN_ABL_TXNOPROBE;
+      use[ROUNDS + r] = use[r] && !pre[r];                   // not probed in phase 1
+      key1_of(rec[r], kx[r], ky[r], kz[r], km[r]);
+      key2_of(rec[r], kx[ROUNDS + r], ky[ROUNDS + r], kz[ROUNDS + r], km[ROUNDS + r]);
     }
     dec[r] = d;
   }
-  ph_probe_many<LDS, 2 * ROUNDS, ROUNDS>(T, a, kx, ky, kz, km, use, w);
+  {
+    bool late = false;
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) late |= use[ROUNDS + r];
+    if (__any(late)) {   // frames whose dmac a MAC learned earlier in the batch put on this path
+      bool u2[2 * ROUNDS];
+#pragma unroll
+      for (uint32_t r = 0; r < ROUNDS; ++r) { u2[r] = use[ROUNDS + r]; u2[ROUNDS + r] = use[ROUNDS + r]; }
+      ph_probe_many<LDS, 2 * ROUNDS, ROUNDS>(T, a, kx, ky, kz, km, u2, w);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r)
+      if (pre[r]) { w[r] = w1e[r]; w[ROUNDS + r] = w2e[r]; }
+  }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     v[r] = 0;
     if (local >= nt) { dec[r] = 0; continue; }
     const uint64_t i = base + local;
-    const uint32_t fl = r0[r].x, touch = tx_touch(r0[r]);
+    const uint32_t fl = rec[r].x, touch = tx_touch(rec[r]);
     uint32_t d = dec[r];
     if (use[r]) {   // key1, then a key1 learned by a frame <= i, then key2 (endpoint.rs:317-327)
       uint32_t wr = w[r];
-      if (!wr && (ins & 2u)) wr = tx_learned_key1(t, kx[r], ky[r], kz[r], km[r], (uint32_t)i);
+      if (!wr && (ins_d & 2u)) wr = tx_learned_key1(t, kx[r], ky[r], kz[r], km[r], (uint32_t)i);
       if (!wr) wr = w[ROUNDS + r];
       d = tx_lookup_dec(a, fl, wr);
     }
@@ -1940,13 +2190,13 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
       }
       if (fl & TXR_LEARNRULE) {
         uint32_t x, y, z, meta;
-        want_key(r0[r], x, y, z, meta);
+        want_key(rec[r], x, y, z, meta);
         const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                                   usn_key_fp48(x, y, z, meta),
                                                   usn_key_hash(x, y, z, meta));
         if (slot_first(slot, t.epoch) == (uint32_t)i) {
-          if (slot[2] != (((unsigned long long)y << 32) | x) ||
-              slot[3] != (((unsigned long long)meta << 32) | z))
+          if (ld_sc1(slot + 2) != (((unsigned long long)y << 32) | x) ||
+              ld_sc1(slot + 3) != (((unsigned long long)meta << 32) | z))
             atomicOr(t.counters + 1, 2u);
           const uint32_t pos = atomicAdd(t.counters, 1u);
           if (pos < t.learned_cap) {
@@ -1964,6 +2214,7 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     sdec[local] = d;
     v[r] = (touch && !(fl & TXR_HIT)) ? local + 1 : 0u;
   }
+  STAMP(6);
   tile_prefix_max(v, L, head);   // its barriers also publish sdec and s_head
   uint32_t my_last = 0, my_touch = 0, my_dec = 0, my_host = 0;
   uint4 my_info = make_uint4(0, 0, 0, 0);
@@ -1973,16 +2224,16 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
     const bool valid = local < nt;
-    if (valid && (r0[r].x & TXR_HIT)) {
+    if (valid && (rec[r].x & TXR_HIT)) {
       const uint32_t hd = head[r] ? sdec[head[r] - 1] : s_head;
       dec[r] = (hd & USN_PARITY_MASK) | USN_F_CACHE | (dec[r] & USN_F_FRAG1);
     }
     if (valid) a.decisions[base + local] = dec[r];
-    const uint32_t touch = valid ? tx_touch(r0[r]) : 0u;
+    const uint32_t touch = valid ? tx_touch(rec[r]) : 0u;
     if (touch) {
       my_last = local + 1; my_touch = touch; my_dec = dec[r];
-      my_host = (r0[r].x & TXR_HOST) != 0;
-      my_info = make_uint4(r0[r].x & TXR_I0_MASK, r0[r].y, r0[r].z, r0[r].w);
+      my_host = (rec[r].x & TXR_HOST) != 0;
+      my_info = make_uint4(rec[r].x & TXR_I0_MASK, rec[r].y, rec[r].z, rec[r].w);
     }
     bins[r] = dec_bin(dec[r], a.n_ep);
     const bool host = valid && (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_LEARN));
@@ -1996,9 +2247,11 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
   }
   __syncthreads();
+  STAMP(7);
   uint32_t cls[4] = {0, 0, 0, 0};
   const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
                                      a.runs, cls);
+  STAMP(10);
   if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
   if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
   if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
@@ -2024,23 +2277,22 @@ __global__ __launch_bounds__(NTHREADS) void tx_decide_kernel(TxArgs t) {
     H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
+  STAMP(11);
+  STAMP_FLUSH_AT(tile);
 }
+
+static inline size_t table_lds_bytes(uint32_t table_units);
 
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const ClassifyArgs &a = t.a;
   if (a.ntiles == 0) return hipSuccess;
   const dim3 g(a.ntiles), b(NTHREADS);
-  const bool in_lds = table_fits_lds(a.nbins, a.table_units);
-  const size_t core = lds_core_bytes(a.nbins);
-  const size_t with_table = classify_lds_bytes(a.nbins, a.table_units, in_lds, false);
-  const size_t scan_lds =
-      with_table + (t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0);
-  if (in_lds) hipLaunchKernelGGL(tx_scan_kernel<true>, g, b, scan_lds, stream, t);
-  else hipLaunchKernelGGL(tx_scan_kernel<false>, g, b, scan_lds, stream, t);
-  hipLaunchKernelGGL(tx_hits_kernel, g, b, core + TILE * 16, stream, t);
-  const size_t decide_lds = with_table + TILE * 4;   // + the tile's decisions
-  if (in_lds) hipLaunchKernelGGL(tx_decide_kernel<true>, g, b, decide_lds, stream, t);
-  else hipLaunchKernelGGL(tx_decide_kernel<false>, g, b, decide_lds, stream, t);
+  const size_t head = tx_lds_head(a.nbins);
+  const size_t bridge = t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0;
+  const size_t with_table = head + table_lds_bytes(a.table_units) + bridge;
+  const bool in_lds = table_fits_lds(a.nbins, a.table_units) && with_table <= 64u * 1024u;
+  if (in_lds) hipLaunchKernelGGL(tx_kernel<true>, g, b, with_table, stream, t);
+  else hipLaunchKernelGGL(tx_kernel<false>, g, b, head + bridge, stream, t);
   return hipGetLastError();
 }
 

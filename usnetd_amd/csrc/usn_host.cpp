@@ -285,15 +285,14 @@ struct Replica {
   size_t d_bridge_set_cap = 0;
   uint64_t bridge_version = 0;
   /* tx scratch */
-  uint4 *rec = nullptr;
-  uint64_t rec_frames = 0;
-  uint32_t *aux = nullptr;
+  uint64_t learned_frames = 0;
+  unsigned long long *aux = nullptr;   // TXA_GRANULES per tile, tagged with the epoch
   uint32_t aux_tiles = 0;
   unsigned long long *macset = nullptr, *ruleset = nullptr;
   uint32_t set_slots = 0;
   uint4 *learned = nullptr;
   uint32_t learned_cap = 0;
-  uint32_t *counters = nullptr;
+  uint32_t *counters = nullptr;   // TxArgs::counters
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   uint32_t epoch = 0;
@@ -868,7 +867,7 @@ void usn_ctx_destroy(usn_ctx *c) {
   for (Replica &R : c->reps) {
     (void)hipSetDevice(R.device);
     (void)hipDeviceSynchronize();
-    for (void *p : {(void *)R.d_table, (void *)R.d_bridge, (void *)R.d_bridge_set, (void *)R.rec,
+    for (void *p : {(void *)R.d_table, (void *)R.d_bridge, (void *)R.d_bridge_set,
                     (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
                     (void *)R.counters, (void *)R.listen})
       if (p) (void)hipFree(p);
@@ -1081,6 +1080,21 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   return USN_OK;
 }
 
+/* Test hook: the tx scratch state of the selected replica: counters[0..7]
+ * (learned, flags, sets used, timed-out epoch), epoch. */
+int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
+  if (!c || !out10 || c->reps.empty()) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  Replica &R = c->reps[c->sel];
+  std::memset(out10, 0, 10 * sizeof(uint32_t));
+  if (R.counters) {
+    HIPCHK(hipSetDevice(R.device));
+    HIPCHK(hipMemcpy(out10, R.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  out10[8] = R.epoch;
+  return USN_OK;
+}
+
 int usn_cache_clear(usn_ctx *c, uint16_t ep) {
   if (!c || ep >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1191,22 +1205,24 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
 /* device scratch of a tx batch of n frames on replica R; the epoch-tagged
  * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
 static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
-  if (n > T.rec_frames) {
-    if (T.rec) HIPCHK(hipFree(T.rec));
+  if (n > T.learned_frames) {
     if (T.learned) HIPCHK(hipFree(T.learned));
-    T.rec = nullptr; T.learned = nullptr;
-    HIPCHK(hipMalloc(&T.rec, n * sizeof(uint4)));
+    T.learned = nullptr;
     HIPCHK(hipMalloc(&T.learned, n * 4 * sizeof(uint4)));   // <= 2 items of 2 x uint4 per frame
-    T.rec_frames = n;
+    T.learned_frames = n;
     T.learned_cap = (uint32_t)(2 * n);
   }
-  if (ntiles > T.aux_tiles) {
+  if (ntiles > T.aux_tiles) {   // zeroed: no flag holds an epoch yet
     if (T.aux) HIPCHK(hipFree(T.aux));
     T.aux = nullptr;
-    HIPCHK(hipMalloc(&T.aux, (size_t)ntiles * 4 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&T.aux, (size_t)ntiles * usn::TXA_WORDS_BYTES));
+    HIPCHK(hipMemset(T.aux, 0, (size_t)ntiles * usn::TXA_WORDS_BYTES));
     T.aux_tiles = ntiles;
   }
-  if (!T.counters) HIPCHK(hipMalloc(&T.counters, 4 * sizeof(uint32_t)));
+  if (!T.counters) {
+    HIPCHK(hipMalloc(&T.counters, 8 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(T.counters, 0, 8 * sizeof(uint32_t)));
+  }
   const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
   bool clear = false;
   if (slots > T.set_slots) {
@@ -1222,6 +1238,8 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
   if (clear) {
     HIPCHK(hipMemset(T.macset, 0, (size_t)T.set_slots * 2 * 8));
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
+    HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
+    HIPCHK(hipMemset(T.counters + 3, 0, sizeof(uint32_t)));
     T.epoch = 1;
   }
   return USN_OK;
@@ -1337,7 +1355,6 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.a = m.b[0];
     st = tx_listen(R, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
-    t.rec = R.rec;
     t.aux = R.aux;
     t.macset = R.macset;
     t.ruleset = R.ruleset;
@@ -1350,7 +1367,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
-    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tx_scan zeroes t.counters
+    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
     c->tx.replica = rep;
@@ -1460,7 +1477,7 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
                       usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
                       const uint32_t *d_counters = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
-  const size_t need = sizeof(usn_summary) + tb + 16;
+  const size_t need = sizeof(usn_summary) + tb + 32;
   if (need > c->h_stage_cap) {
     if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
     c->h_stage = nullptr;
@@ -1473,12 +1490,12 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   HIPCHK(hipMemcpyAsync(p, r->summary, sizeof(usn_summary), hipMemcpyDeviceToHost, s));
   if (tb) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary), r->tiles, tb, hipMemcpyDeviceToHost, s));
   if (cnt)
-    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, 32, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   std::memcpy(&sum, p, sizeof sum);
   th.resize(ntiles);
   if (tb) std::memcpy(th.data(), p + sizeof(usn_summary), tb);
-  if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, 16);
+  if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, 32);
   return USN_OK;
 }
 
@@ -1568,11 +1585,14 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   Replica &R = c->reps[c->tx.replica];
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
-  uint32_t cnt[4];
+  uint32_t cnt[8];
   {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters);
     if (e) return e;
   }
+  // a tile wait of the kernel timed out (counters[3] = this epoch): the whole
+  // batch goes to the host stage
+  if (cnt[3] == R.epoch) cnt[1] |= 8u;
   clk.mark("state");
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);

@@ -87,15 +87,15 @@ struct MultiArgs {
 
 struct TxArgs {
   ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
-  uint4 *rec;                 /* n records r0 (the MACs are re-read from the frames) */
-  uint32_t *aux;              /* per tile x 4: [0] 1+last touching, [1] 1+last non-hit touching */
+  unsigned long long *aux;    /* per tile x TXA_GRANULES {epoch, value}: what crosses a tile boundary */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
   uint32_t macset_mask, ruleset_mask;
   uint32_t epoch;             /* 1..65535 */
   uint4 *learned;             /* items appended by tx_decide: {frame, kind 0 mac | 1 rule},
                                  {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
-  uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with items */
+  uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with
+                                 items, [3] epoch of a batch whose tile waits timed out */
   uint32_t learned_cap;
   const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
   uint32_t bridge_mask;
@@ -104,6 +104,8 @@ struct TxArgs {
   uint32_t next_dhcp_set;     /* the source's next_dhcp_endpoint is Some */
 };
 
+#define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
+constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
