@@ -973,11 +973,16 @@ __device__ __forceinline__ void stage_read_asm(const uint4 *st, uint32_t lane, u
   q[3] = make_uint4(0, 0, 0, 0);
 }
 
-/* LANE: this lane's 64-byte window of round r into registers */
+/* LANE: bytes 0..47 of this lane's window of round r into registers (parse
+ * reads 12..39; longer IPv4 headers' ports come from the frame).  At the
+ * 2048-byte stride a frame's read is one scattered HBM access whose cost
+ * grows with its bytes: 4M frames in 89 / 108 / 140 us at 32 / 48 / 64 bytes
+ * (tools/stride_floor.hip, profiles/r02f). */
 __device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
   const uint4 *w = reinterpret_cast<const uint4 *>(fp);
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) q[k] = ld_stream(w + k);
+  for (uint32_t k = 0; k < 3; ++k) q[k] = ld_stream(w + k);
+  q[3] = make_uint4(0, 0, 0, 0);
 }
 
 /* Which batch of a launch tile w belongs to: tile_base[] is increasing, so
@@ -1827,7 +1832,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
       S->flags = 0; S->first_break = 0xFFFFFFFFu;
     }
   }
-  /* all header loads of the tile first (64 B x 4 frames per lane in flight) */
+  /* all header loads of the tile first (48 B x 4 frames per lane in flight:
+     the MACs and up to byte 39 for parse; tools/stride_floor.hip, 4M frames
+     at a 64-byte stride: 61.6 us reading 48 B per frame, 73.3 us reading 64) */
   uint4 qq[ROUNDS][4];
   uint32_t ll[ROUNDS];
   const uint8_t *fps[ROUNDS];
@@ -1837,7 +1844,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint64_t i = base + (local < nt ? local : 0);
     fps[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
+    for (uint32_t k = 0; k < 3; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
+    qq[r][3] = make_uint4(0, 0, 0, 0);
     ll[r] = a.lens[i];
   }
   /* the bridge snapshot set in LDS when small */
