@@ -198,13 +198,15 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 }
 
 struct PhKeyH {        // a key's hashes for one table
-  uint32_t grp, h2;
+  uint32_t grp, h2, sbase;   // displacement index, slot hash, first slot of its shard
 };
 
 __device__ __forceinline__ PhKeyH ph_hash(const usn_ph_table &t, uint32_t x, uint32_t y,
                                           uint32_t z, uint32_t meta) {
   PhKeyH k;
-  k.grp = usn_mulhi32(usn_ph_h1(x, y, z, meta, t.seed), t.g);
+  const uint32_t h1 = usn_ph_h1(x, y, z, meta, t.seed);
+  k.grp = usn_ph_group(h1, t.shift, t.g);
+  k.sbase = usn_ph_shard(h1, t.shift) * t.m;
   k.h2 = usn_key_hash2(x, y, z, meta, t.seed);
   return k;
 }
@@ -258,8 +260,8 @@ __device__ __forceinline__ void ph_issue(const uint4 *T, const uint16_t *Dl, con
     d1 = D[a.ph[0].disp_off + (use1 ? k1.grp : 0u)];
     d2 = D[a.ph[1].disp_off + (use2 ? k2.grp : 0u)];
   }
-  const uint32_t si1 = a.ph[0].slot_off + (use1 ? usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u);
-  const uint32_t si2 = a.ph[1].slot_off + (use2 ? usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u);
+  const uint32_t si1 = a.ph[0].slot_off + (use1 ? k1.sbase + usn_ph_slot(k1.h2, d1, a.ph[0].m) : 0u);
+  const uint32_t si2 = a.ph[1].slot_off + (use2 ? k2.sbase + usn_ph_slot(k2.h2, d2, a.ph[1].m) : 0u);
   if (TM == TM_LDS) {
     asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=&v"(s1), "=&v"(s2)
@@ -323,8 +325,8 @@ __device__ __forceinline__ void asm_disp2(const uint16_t *D, const ClassifyArgs 
 __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a, bool use1,
                                           bool use2, const RoundKeys &k, uint32_t d1, uint32_t d2,
                                           v4u32 &s1, v4u32 &s2) {
-  const uint4 *p1 = T + a.ph[0].slot_off + (use1 ? usn_ph_slot(k.k1.h2, d1, a.ph[0].m) : 0u);
-  const uint4 *p2 = T + a.ph[1].slot_off + (use2 ? usn_ph_slot(k.k2.h2, d2, a.ph[1].m) : 0u);
+  const uint4 *p1 = T + a.ph[0].slot_off + (use1 ? k.k1.sbase + usn_ph_slot(k.k1.h2, d1, a.ph[0].m) : 0u);
+  const uint4 *p2 = T + a.ph[1].slot_off + (use2 ? k.k2.sbase + usn_ph_slot(k.k2.h2, d2, a.ph[1].m) : 0u);
   asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
 }
@@ -369,11 +371,11 @@ __device__ __forceinline__ uint32_t ph_probe1(const uint4 *T, const ClassifyArgs
                  : "v"(lds_addr(D + t.disp_off + k.grp)));
     v4u32 sv;
     asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(sv)
-                 : "v"(lds_addr(T + t.slot_off + usn_ph_slot(k.h2, d, t.m))));
+                 : "v"(lds_addr(T + t.slot_off + k.sbase + usn_ph_slot(k.h2, d, t.m))));
     return ph_hit(make_uint4(sv.x, sv.y, sv.z, sv.w), x, y, z, meta);
   }
   const uint32_t d = D[t.disp_off + k.grp];
-  return ph_hit(T[t.slot_off + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
+  return ph_hit(T[t.slot_off + k.sbase + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
 }
 
 /* N probes issued together: all N displacement reads, then all N slot
@@ -404,7 +406,7 @@ __device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
-    const uint32_t si = t.slot_off + (on[i] ? usn_ph_slot(k[i].h2, d[i], t.m) : 0u);
+    const uint32_t si = t.slot_off + (on[i] ? k[i].sbase + usn_ph_slot(k[i].h2, d[i], t.m) : 0u);
     if (IN_LDS) {
       const v4u32 v = ((lds_v4 *)T)[si];
       sl[i] = make_uint4(v.x, v.y, v.z, v.w);

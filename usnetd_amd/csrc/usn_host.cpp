@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -32,13 +33,16 @@ using usn::ClassifyArgs;
 
 /* perfect-hash image geometry: slot load and keys per displacement group.
  * 10 keys per u16 displacement keep c5's two arrays (65536 keys) at 13 KiB,
- * which the classify kernel stages in LDS at 4 workgroups per CU; 10-key
- * groups need the slot load at 0.75 to place within u16 displacements.
+ * which the classify kernel stages in LDS at 4 workgroups per CU.
  * A/B, c5, 8M frames per launch: group 8 / load 0.85 with the displacements
  * in global memory 174.2 us, the same in LDS (3 workgroups per CU) 161.3 us,
- * group 10 / load 0.75 in LDS 156.5 us (profiles/r02d). */
+ * group 10 / load 0.75 in LDS 156.5 us (profiles/r02d).  The slot load then
+ * went from 0.75 to 0.65: the kernel does not notice (c5 157.0 vs 158.1 us,
+ * c4 160.9 vs 162.5), and placement takes a third of the time (a group of s
+ * keys needs ~1/(1-fill)^s trials): 1.19M rules rebuilt in 83 instead of
+ * 155 ms (profiles/r02g). */
 #ifndef USN_PH_LOAD
-#define USN_PH_LOAD 0.75
+#define USN_PH_LOAD 0.65
 #endif
 #ifndef USN_PH_GROUP
 #define USN_PH_GROUP 10
@@ -411,12 +415,14 @@ struct PhKey {
   uint32_t h2, grp;
 };
 
-bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed,
+/* Place the keys of one shard: m slots, g groups (group = mulhi(h1 << shift,
+ * g); h1 of each key in k.grp on entry). */
+bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed, uint32_t shift,
               std::vector<uint4> &slots, std::vector<uint16_t> &disp) {
   const uint32_t n = (uint32_t)keys.size();
   for (PhKey &k : keys) {
     const uint32_t meta = k.e.w & USN_KEY_META_MASK;
-    k.grp = usn_mulhi32(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed), g);
+    k.grp = usn_mulhi32(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed) << shift, g);
     k.h2 = usn_key_hash2(k.e.x, k.e.y, k.e.z, meta, seed);
   }
   /* members of each group (counting sort), then groups by size, largest first */
@@ -435,18 +441,19 @@ bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed,
   for (uint32_t i = 0; i < g; ++i) order[bysz[maxsz - (start[i + 1] - start[i])]++] = i;
   slots.assign(m, make_uint4(0, 0, 0, 0));
   disp.assign(g, 0);
-  std::vector<uint8_t> used(m, 0);
-  uint32_t pos[64];
+  std::vector<uint64_t> used((m + 63) / 64, 0);   // a bit per slot: stays in L1/L2
+  uint32_t pos[64], h2[64];
   for (uint32_t gi : order) {
     const uint32_t a = start[gi], sz = start[gi + 1] - a;
     if (sz == 0) break;             // the rest are empty
     if (sz > 64) return false;
+    for (uint32_t j = 0; j < sz; ++j) h2[j] = keys[member[a + j]].h2;
     uint32_t d = 0;
     for (; d < 65536; ++d) {
       bool ok = true;
       for (uint32_t j = 0; j < sz && ok; ++j) {
-        const uint32_t p = usn_ph_slot(keys[member[a + j]].h2, d, m);
-        if (used[p]) { ok = false; break; }
+        const uint32_t p = usn_ph_slot(h2[j], d, m);
+        if ((used[p >> 6] >> (p & 63)) & 1u) { ok = false; break; }
         for (uint32_t q = 0; q < j; ++q)
           if (pos[q] == p) { ok = false; break; }
         pos[j] = p;
@@ -456,33 +463,85 @@ bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed,
     if (d == 65536) return false;
     disp[gi] = (uint16_t)d;
     for (uint32_t j = 0; j < sz; ++j) {
-      used[pos[j]] = 1;
+      used[pos[j] >> 6] |= 1ull << (pos[j] & 63);
       slots[pos[j]] = keys[member[a + j]].e;
     }
   }
   return true;
 }
 
-/* one table of the image: m, g, seed and its slots / displacements */
+/* up to this many keys per shard (one shard: c1-c5 never shard) */
+#ifndef USN_PH_SHARD_KEYS
+#define USN_PH_SHARD_KEYS 65536u
+#endif
+#ifndef USN_PH_THREADS
+#define USN_PH_THREADS 16u
+#endif
+
+/* run f(0..jobs) over up to `threads` threads */
+template <class F>
+void parallel_for(uint32_t jobs, uint32_t threads, F f) {
+  threads = std::max(1u, std::min(threads, jobs));
+  if (threads == 1) {
+    for (uint32_t j = 0; j < jobs; ++j) f(j);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      for (uint32_t j = t; j < jobs; j += threads) f(j);
+    });
+  for (std::thread &th : pool) th.join();
+}
+
+/* one table of the image: shards, m, g, seed and its slots / displacements
+ * (shard after shard) */
 bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
-              std::vector<uint16_t> &disp, double load0, uint32_t group) {
+              std::vector<uint16_t> &disp, double load0, uint32_t group, uint32_t threads) {
   const uint32_t n = (uint32_t)keys.size();
   t = usn_ph_table{};
   slots.clear();
   disp.clear();
   if (n == 0) return true;
+  uint32_t shift = 0;
+  while ((n >> shift) > USN_PH_SHARD_KEYS && shift < 16) ++shift;
+  const uint32_t S = 1u << shift;
   double load = load0;
+  std::vector<std::vector<PhKey>> part(S);
   for (uint32_t attempt = 0; attempt < 12; ++attempt) {
     if (attempt && attempt % 3 == 0) load *= 0.9;
-    const uint32_t m = std::max<uint32_t>(n + 1, (uint32_t)((double)n / load) + 1);
-    const uint32_t g = std::max<uint32_t>(1, (n + group - 1) / group);
     const uint32_t seed = 0x9E3779B9u * (attempt + 1);
-    if (ph_place(keys, m, g, seed, slots, disp)) {
-      t.m = m;
-      t.g = g;
-      t.seed = seed;
-      return true;
+    for (auto &v : part) v.clear();
+    if (S == 1) {
+      part[0] = keys;
+    } else {
+      for (const PhKey &k : keys) {
+        const uint32_t meta = k.e.w & USN_KEY_META_MASK;
+        part[usn_ph_shard(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed), shift)].push_back(k);
+      }
     }
+    uint32_t maxc = 0;
+    for (const auto &v : part) maxc = std::max(maxc, (uint32_t)v.size());
+    const uint32_t m = std::max<uint32_t>(maxc + 1, (uint32_t)((double)maxc / load) + 1);
+    const uint32_t g = std::max<uint32_t>(1, (maxc + group - 1) / group);
+    std::vector<std::vector<uint4>> ps(S);
+    std::vector<std::vector<uint16_t>> pd(S);
+    std::vector<uint8_t> ok(S, 0);
+    parallel_for(S, threads, [&](uint32_t sh) {
+      ok[sh] = ph_place(part[sh], m, g, seed, shift, ps[sh], pd[sh]) ? 1 : 0;
+    });
+    if (std::find(ok.begin(), ok.end(), 0) != ok.end()) continue;
+    slots.reserve((size_t)S * m);
+    disp.reserve((size_t)S * g);
+    for (uint32_t sh = 0; sh < S; ++sh) {
+      slots.insert(slots.end(), ps[sh].begin(), ps[sh].end());
+      disp.insert(disp.end(), pd[sh].begin(), pd[sh].end());
+    }
+    t.m = m;
+    t.g = g;
+    t.seed = seed;
+    t.shift = shift;
+    return true;
   }
   return false;
 }
@@ -509,14 +568,29 @@ int build_image(usn_ctx *c) {
   std::vector<uint4> slots[2];
   std::vector<uint16_t> disp[2];
   usn_ph_table t[2];
-  for (int i = 0; i < 2; ++i)
-    for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
-      if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp)) break;
-      if (grp <= 1) return USN_ENOMEM;
+  bool placed[2] = {false, false};
+  {
+    // the two tables side by side, each over its shards
+    const uint32_t hw = std::max(1u, std::min(USN_PH_THREADS, std::thread::hardware_concurrency()));
+    auto one = [&](int i, uint32_t threads) {
+      for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
+        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads)) { placed[i] = true; break; }
+        if (grp <= 1) break;
+      }
+    };
+    if (hw > 1 && !keys[0].empty() && !keys[1].empty()) {
+      std::thread other(one, 1, std::max(1u, hw / 2));
+      one(0, std::max(1u, hw - hw / 2));
+      other.join();
+    } else {
+      one(0, hw);
+      one(1, hw);
     }
+  }
+  if (!placed[0] || !placed[1]) return USN_ENOMEM;
   clk.mark("place");
-  const uint32_t u0 = t[0].m, u1 = t[1].m;
-  const uint32_t d0 = (t[0].g + 7) / 8, d1 = (t[1].g + 7) / 8;   // 8 u16 per 16-byte unit
+  const uint32_t u0 = (uint32_t)slots[0].size(), u1 = (uint32_t)slots[1].size();
+  const uint32_t d0 = ((uint32_t)disp[0].size() + 7) / 8, d1 = ((uint32_t)disp[1].size() + 7) / 8;   // 8 u16 per 16-byte unit
   c->img.assign((size_t)u0 + u1 + d0 + d1 + 1, make_uint4(0, 0, 0, 0));
   std::copy(slots[0].begin(), slots[0].end(), c->img.begin());
   std::copy(slots[1].begin(), slots[1].end(), c->img.begin() + u0);
@@ -540,9 +614,11 @@ int build_image(usn_ctx *c) {
 uint32_t image_probe(const usn_ctx *c, int table, uint32_t x, uint32_t y, uint32_t z, uint32_t meta) {
   const usn_ph_table &t = c->img_t[table];
   if (!t.m) return 0;
-  const uint32_t grp = usn_mulhi32(usn_ph_h1(x, y, z, meta, t.seed), t.g);
+  const uint32_t h1 = usn_ph_h1(x, y, z, meta, t.seed);
+  const uint32_t grp = usn_ph_group(h1, t.shift, t.g);
   const uint16_t d = reinterpret_cast<const uint16_t *>(c->img.data())[t.disp_off + grp];
-  const uint4 s = c->img[t.slot_off + usn_ph_slot(usn_key_hash2(x, y, z, meta, t.seed), d, t.m)];
+  const uint4 s = c->img[t.slot_off + usn_ph_shard(h1, t.shift) * t.m +
+                         usn_ph_slot(usn_key_hash2(x, y, z, meta, t.seed), d, t.m)];
   const bool hit = s.x == x && s.y == y && s.z == z && ((s.w ^ meta) & USN_KEY_META_MASK) == 0;
   return hit ? s.w : 0u;
 }
@@ -1066,7 +1142,8 @@ int64_t usn_debug_image_probe(usn_ctx *c, int table, uint32_t x, uint32_t y, uin
   return (int64_t)image_probe(c, table, x, y, z, meta);
 }
 
-/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask}. */
+/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask}
+ * (slots and groups of each table, all shards). */
 int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   if (!c || !out6) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1074,8 +1151,10 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
     const int s = build_image(c);
     if (s) return s;
   }
-  out6[0] = c->img_t[0].m; out6[1] = c->img_t[0].g;
-  out6[2] = c->img_t[1].m; out6[3] = c->img_t[1].g;
+  for (int i = 0; i < 2; ++i) {   // totals over the shards
+    out6[2 * i] = c->img_t[i].m << c->img_t[i].shift;
+    out6[2 * i + 1] = c->img_t[i].g << c->img_t[i].shift;
+  }
   out6[4] = (uint32_t)c->img.size(); out6[5] = c->probe_mask;
   return USN_OK;
 }

@@ -75,9 +75,12 @@ USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) 
  * The device image holds two tables: K1 = the rules key1 can hit (present
  * SRC or SRC|DPORT|SPORT), K2 = the rules key2 can hit (present 0 or DPORT);
  * rules of any other shape never match a frame and are not in the image.
- * Each table: m slots (16 B, the packed key above) and g 16-bit displacements.
- * A key's group is mulhi(h1, g); its slot is usn_ph_slot(h2, disp[group], m),
- * so a probe is one displacement read and ONE slot read, hit or miss. */
+ * Each table: 2^shift shards of m slots (16 B, the packed key above) and g
+ * 16-bit displacements each (one shard up to 64K keys).  A key's shard is the
+ * top `shift` bits of h1, its group within the shard mulhi(h1 << shift, g),
+ * its slot shard * m + usn_ph_slot(h2, disp[shard * g + group], m): a probe
+ * is one displacement read and ONE slot read, hit or miss.  Shards are
+ * placed independently (in parallel on the host). */
 USN_HD uint32_t usn_mulhi32(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
 }
@@ -104,15 +107,23 @@ USN_HD uint32_t usn_ph_h1(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uin
 USN_HD uint32_t usn_ph_slot(uint32_t h2, uint32_t d, uint32_t m) {
   return usn_mulhi32(usn_fmix32(h2 + d * 0x9E3779B9u), m);
 }
+USN_HD uint32_t usn_ph_shard(uint32_t h1, uint32_t shift) {
+  return shift ? h1 >> (32u - shift) : 0u;
+}
+/* index of the key's displacement within its table's displacements */
+USN_HD uint32_t usn_ph_group(uint32_t h1, uint32_t shift, uint32_t g) {
+  return usn_ph_shard(h1, shift) * g + usn_mulhi32(h1 << shift, g);
+}
 
 /* one table of the image, in 16-byte units / u16 units from the image base */
 typedef struct {
   uint32_t slot_off;   /* first slot (16-B units) */
-  uint32_t m;          /* slots */
+  uint32_t m;          /* slots per shard */
   uint32_t disp_off;   /* first displacement (u16 units) */
-  uint32_t g;          /* groups */
+  uint32_t g;          /* groups per shard */
   uint32_t seed;
-  uint32_t _pad[3];
+  uint32_t shift;      /* log2 of the shards */
+  uint32_t _pad[2];
 } usn_ph_table;
 
 /* 32-bit tag of a key in the tag array of a global-memory table (0 = empty) */
