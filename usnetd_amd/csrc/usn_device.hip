@@ -227,6 +227,9 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_BATCH2
 #define USN_BATCH2 1
 #endif
+#ifndef USN_SEQ_K2    /* key2's slot read only where key1 missed (get_endpoint's order) */
+#define USN_SEQ_K2 1
+#endif
 #define TM_GLOBAL 0
 #define TM_LDS 1
 #define TM_DISPLDS 2
@@ -329,6 +332,14 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
   const uint4 *p2 = T + a.ph[1].slot_off + (use2 ? k.k2.sbase + usn_ph_slot(k.k2.h2, d2, a.ph[1].m) : 0u);
   asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
+}
+
+/* one slot read of table t; a lane that does not need it reads the table's
+ * first slot, which every such lane of the wave shares: one L2 request */
+__device__ __forceinline__ void asm_slot1(const uint4 *T, const usn_ph_table &t, bool need,
+                                          const PhKeyH &k, uint32_t d, v4u32 &s) {
+  const uint4 *p = T + t.slot_off + (need ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(s) : "v"(p) : "memory");
 }
 
 /* TM_DISPLDS: both displacements from the LDS copy (indexed like the image) */
@@ -1099,7 +1110,46 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
   uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
   Parsed pr[ROUNDS];
-  if (BATCH2 && TM == TM_DISPLDS) {
+  if (BATCH2 && TM == TM_DISPLDS && USN_SEQ_K2) {
+    // displacements from LDS; key1's slot reads of both rounds first, then
+    // key2's only where key1 missed (get_endpoint reads key2 only then,
+    // endpoint.rs:317-327): a lane that needs no read shares the table's
+    // first line, so c5's half of frames that hit key1 cost no second L2
+    // request.  Round 1's header DMA flies under round 0's parse.
+    uint4 *sb = st;
+    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+    RoundKeys k0, k1;
+    uint32_t d01, d02, d11, d12;
+    v4u32 s01, s02, s11, s12;
+    stage_read_asm(sb, lane, q[0]);
+    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+    __builtin_amdgcn_sched_barrier(0);
+    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+    round_keys(a, pr[0], k0);
+    lds_disp2(Dl, a, use1, use2, k0, d01, d02);
+    const bool n01 = use1 && pr[0].status == 1u;
+    asm_slot1(T, a.ph[0], n01, k0.k1, d01, s01);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<1>();                                               // round 1 landed (1 younger load)
+    stage_read_asm(sb, lane, q[1]);
+    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+    round_keys(a, pr[1], k1);
+    lds_disp2(Dl, a, use1, use2, k1, d11, d12);
+    const bool n11 = use1 && pr[1].status == 1u;
+    asm_slot1(T, a.ph[0], n11, k1.k1, d11, s11);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s01) :: "memory");
+    const uint32_t w01 = n01 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u;
+    const bool n02 = use2 && pr[0].status == 1u && !w01;
+    asm_slot1(T, a.ph[1], n02, k0.k2, d02, s02);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s11) :: "memory");
+    const uint32_t w11 = n11 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u;
+    const bool n12 = use2 && pr[1].status == 1u && !w11;
+    asm_slot1(T, a.ph[1], n12, k1.k2, d12, s12);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s02) :: "memory");
+    dec[0] = decide_rx_w(a, pr[0], w01, n02 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s12) :: "memory");
+    dec[1] = decide_rx_w(a, pr[1], w11, n12 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+  } else if (BATCH2 && TM == TM_DISPLDS) {
     // displacements from LDS: one global round trip (the slots) per round,
     // round 1's header DMA in flight under round 0's parse and slot loads
     uint4 *sb = st;

@@ -1256,17 +1256,14 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   return USN_OK;
 }
 
-/* 512 threads per tile (two rounds per lane) when the rule image is in LDS
- * for both builds (c1/c2: 3 % faster), never when only the 256-thread build
- * can keep it in LDS (its stage is half as big), and for global images
- * above USN_T512_MIN_UNITS 16-byte units. */
-#ifndef USN_T512_MIN_UNITS
-#define USN_T512_MIN_UNITS 16384u
-#endif
+/* 512 threads per tile (two rounds per lane: both rounds' probes batched per
+ * wave, displacements in LDS) for every layout, except when only the
+ * 256-thread build can keep the image in LDS (its header stage is half as
+ * big).  A/B, c4 (4096 rules, displacements in LDS), 8M frames per launch:
+ * 161.8 us at 256 threads, 130.7 at 512 (profiles/r02h). */
 static bool use_t512(uint32_t nbins, uint32_t units) {
   if (usn_t512::table_fits_lds(nbins, units)) return true;
-  if (usn::table_fits_lds(nbins, units)) return false;
-  return units > USN_T512_MIN_UNITS;
+  return !usn::table_fits_lds(nbins, units);
 }
 
 static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
