@@ -60,6 +60,8 @@ def parse_args():
     ap.add_argument("--queues", type=int, default=0,
                     help="rx queues per rank (default: 8 rings' worth of launches on 2 streams)")
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--rings-per-launch", type=int, default=0,
+                    help="rx rings per usn_classify_multi launch (default: 8M frames' worth, <= 8)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: 64M frames per step for the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -73,11 +75,11 @@ class Run:
     """The rank's rx queues of one config, resident in HBM, and the launches
     of one poll round."""
 
-    def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong):
+    def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong, rings_per_launch=0):
         from usnetd_amd import shard, traffic
         self.L, self.ctx, self.name, self.n = L, ctx, name, n
         S = max(1, streams)
-        P = max(1, min(8, LAUNCH_FRAMES // n))           # rings per launch
+        P = rings_per_launch or max(1, min(8, LAUNCH_FRAMES // n))   # rings per launch
         if strong:
             total_q = max(world, STRONG_FRAMES // n)
             mine = shard.rank_queues(total_q, world, rank)
@@ -301,7 +303,8 @@ def main():
             device = local % ndev
     ctx = lib.Ctx(device)
     n = args.frames or DEFAULT_FRAMES[args.config]
-    run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong)
+    run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong,
+              args.rings_per_launch)
     res = measure(run, args, dist, world)
     out = {
         "metric": METRIC,

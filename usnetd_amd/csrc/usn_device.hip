@@ -227,6 +227,9 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_BATCH2
 #define USN_BATCH2 1
 #endif
+#ifndef USN_STAGE_ROWS   /* 64 < bins <= 1024: counting sort with byte rows in the stage */
+#define USN_STAGE_ROWS 1
+#endif
 #ifndef USN_SEQ_K2    /* key2's slot read only where key1 missed (get_endpoint's order) */
 #define USN_SEQ_K2 1
 #endif
@@ -852,6 +855,98 @@ __device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_
   return n_runs;
 }
 
+/* 64 < bins <= STAGE_BYTE_BINS in a 512-thread classify tile: a counting
+ * sort whose counters live in the header stage (free once every round is
+ * decided).  The 16 segments of 64 frames (segment r * 8 + wave) give each
+ * bin a 16-byte row of u8 counts; a frame's place is its bin's start plus the
+ * byte sum (v_sad_u8) of its row's earlier segments plus its rank in its
+ * segment.  One counting pass where tile_order_radix makes two (c5: 1005
+ * bins), and no [bin][segment] u16 counters in the dynamic LDS.  Same
+ * contract as tile_order. */
+#define STAGE_BYTE_BINS 1024u
+__device__ __forceinline__ uint32_t byte_sum(uint32_t v) { return __builtin_amdgcn_sad_u8(v, 0u, 0u); }
+__device__ uint32_t tile_order_bytes(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbins,
+                                     uint32_t nbits, uint32_t n_ep, const Lds &L, uint8_t *stage,
+                                     uint32_t tile, uint16_t *order_out, uint32_t *runs_out,
+                                     uint32_t cls[4]) {
+  static_assert(NSEG == 16, "a bin's row is 16 segment counts");
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint4 *rows = reinterpret_cast<uint4 *>(stage + TILE * 2 + TILE * 4);   // after order, keys
+  uint16_t *bstart = reinterpret_cast<uint16_t *>(rows + STAGE_BYTE_BINS);
+  uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
+  uint32_t *rdst = runs_out + (size_t)tile * TILE;
+  __syncthreads();   // every wave is done with the stage's headers
+  for (uint32_t b = tid; b < nbins; b += NTHREADS) rows[b] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  uint32_t rank[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    const uint32_t sg = r * (NTHREADS / 64) + wave;
+    const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
+    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+    if (local < nt && rank[r] == 0) cb[bins[r] * 16 + sg] = (uint8_t)__popcll(same);
+  }
+  __syncthreads();
+  // bin totals, starts and runs: thread t owns bins 2t and 2t + 1
+  uint32_t tot[2], packed = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 2; ++k) {
+    const uint32_t b = 2 * tid + k;
+    tot[k] = 0;
+    if (b < nbins) {
+      const uint4 w = rows[b];
+      tot[k] = byte_sum(w.x) + byte_sum(w.y) + byte_sum(w.z) + byte_sum(w.w);
+    }
+    packed += tot[k] | (tot[k] ? 0x10000u : 0u);
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan(packed, L.scratch, &total);
+#pragma unroll
+  for (uint32_t k = 0; k < 2; ++k) {
+    const uint32_t b = 2 * tid + k, c = tot[k];
+    if (b >= nbins) break;
+    const uint32_t start = run & 0xFFFFu;
+    bstart[b] = (uint16_t)start;
+    if (c) rdst[run >> 16] = (b << 16) | start;
+    run += c | (c ? 0x10000u : 0u);
+    cls[1] = b == n_ep ? c : cls[1];
+    cls[2] = b == n_ep + 1 ? c : cls[2];
+    cls[3] = b == n_ep + 2 ? c : cls[3];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local < nt) {
+      const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
+      const uint4 w = rows[b];
+      // bytes of the segments before sg: whole words, then the low bytes of one
+      const uint32_t q = sg >> 2, part = sg & 3u;
+      const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
+      const uint32_t p0 = q > 0 ? w.x : (w.x & mpart);
+      const uint32_t p1 = q > 1 ? w.y : q == 1 ? (w.y & mpart) : 0u;
+      const uint32_t p2 = q > 2 ? w.z : q == 2 ? (w.z & mpart) : 0u;
+      const uint32_t p3 = q == 3 ? (w.w & mpart) : 0u;
+      const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
+      L.order[bstart[b] + before + rank[r]] = (uint16_t)local;
+    }
+  }
+  __syncthreads();
+  uint16_t *dst = order_out + (size_t)tile * TILE;
+  const uint32_t p0 = tid * ROUNDS;
+  if (p0 + ROUNDS <= nt) {
+    if (ROUNDS == 2)
+      *reinterpret_cast<uint32_t *>(dst + p0) = *reinterpret_cast<const uint32_t *>(L.order + p0);
+    else
+      for (uint32_t k = 0; k < ROUNDS; ++k) dst[p0 + k] = L.order[p0 + k];
+  } else {
+    for (uint32_t k = 0; k < ROUNDS; ++k)
+      if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
+  }
+  return total >> 16;
+}
+
 /* --------------------------------------------------------------------------- */
 /* Carried-in decision cache for this batch, resolved by all threads of
  * workgroup 0: the state after the last cache-touching frame of the previous
@@ -1358,8 +1453,14 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
   const uint32_t n_runs = 0;
 #else
-  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
-                                     a.runs, cls);
+  // the stage's 24 KiB (512 threads): order 2 + radix keys 4 + rows 16 + starts 2
+  constexpr bool STAGE_ROWS = GLDS && NWAVES * GD * STAGE_ROUND_SLOTS * 16 >=
+                                          TILE * 6 + STAGE_BYTE_BINS * 18 && USN_STAGE_ROWS;
+  const uint32_t n_runs =
+      (STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS)
+          ? tile_order_bytes(bins, nt, a.nbins, a.nbits, a.n_ep, L,
+                             reinterpret_cast<uint8_t *>(s_stage), tile, a.order, a.runs, cls)
+          : tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order, a.runs, cls);
 #endif
   if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
   if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
