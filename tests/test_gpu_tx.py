@@ -232,3 +232,11 @@ def test_tx_runs_host_free(coracle_mod):
     V[3100:69000, 12:14] = 0x12                # 64+ tiles in a row without a touching frame
     info = _check(cfg, coracle_mod)
     assert info.n_host == 0
+
+
+def test_c4tx_more_tiles_than_resident(coracle_mod):
+    """4M frames (4096 tiles): more tiles than the GPU keeps resident at once,
+    so later tiles wait on tiles that were dispatched, not yet finished."""
+    from usnetd_amd import traffic
+    infos = _run(traffic.config("c4tx", n=1 << 22), coracle_mod, batches=2)
+    assert [i.n_host for i in infos] == [0, 0]

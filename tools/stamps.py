@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from usnetd_amd import lib, traffic  # noqa: E402
 
-NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided",
+NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided / probes issued",
          "all rounds decided", "stores+hostlist+lastreduce", "-", "-", "-",
          "tile_order+cls", "header"]
 # c4tx: the one-launch tx kernel (stamps indexed by tile)

@@ -46,6 +46,8 @@ using namespace ::usn;
 #define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
+#define GLDS_PARTS 3u                            /* 16-byte parts of a frame in the header stage */
+#define STAGE_ROUND_SLOTS (64u * GLDS_PARTS)     /* 16-byte slots per wave and round */
 #define MAX_NBITS 13   /* nbins <= USN_MAX_ENDPOINTS + 3 <= 8192 */
 #define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule images up to 32 KiB live in LDS */
 /* the LDS copy of the image, rounded up to whole 64-unit glds chunks */
@@ -875,8 +877,14 @@ __device__ uint32_t tile_order_bytes(const uint32_t bins[ROUNDS], uint32_t nt, u
   uint16_t *bstart = reinterpret_cast<uint16_t *>(rows + STAGE_BYTE_BINS);
   uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
   uint32_t *rdst = runs_out + (size_t)tile * TILE;
-  __syncthreads();   // every wave is done with the stage's headers
-  for (uint32_t b = tid; b < nbins; b += NTHREADS) rows[b] = make_uint4(0, 0, 0, 0);
+  {  // each wave zeroes the rows that lie in its own stage (it is done with
+     // its headers; no wave reads another's stage), then one barrier
+    constexpr uint32_t WSTAGE = STAGE_ROUND_SLOTS * 16;   // bytes of one wave's stage
+    const uint32_t r0 = TILE * 6, r1 = TILE * 6 + nbins * 16;
+    const uint32_t lo = max(r0, wave * WSTAGE), hi = min(r1, (wave + 1) * WSTAGE);
+    for (uint32_t o = lo + lane * 16; o < hi; o += 64 * 16)
+      *reinterpret_cast<uint4 *>(stage + o) = make_uint4(0, 0, 0, 0);
+  }
   __syncthreads();
   uint32_t rank[ROUNDS];
 #pragma unroll
@@ -1008,7 +1016,6 @@ __device__ uint32_t decide_info_rx(const uint4 *T, const uint16_t *Dl, const Cla
  * of frame f at slot 3f + j of a wave's 3 KiB round stage.  glds writes it
  * linearly, and the per-frame ds_read_b128s (a 12-dword stride) cover 16
  * distinct 4-bank groups per 16 lanes: no bank conflicts either way. */
-#define GLDS_PARTS 3u
 __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
   return GLDS_PARTS * f + j;
 }
@@ -1031,7 +1038,6 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #endif
 #define GD USN_GLDS_DEPTH
 #define NWAVES (NTHREADS / 64)
-#define STAGE_ROUND_SLOTS (64u * GLDS_PARTS)   /* 16-byte slots per wave and round */
 #define GLDS_NT 2                /* aux bits of the header glds: non-temporal */
 #ifndef USN_GLDS_ENABLE          /* A/B only: 0 = register loads for every layout */
 #define USN_GLDS_ENABLE 1
@@ -1130,6 +1136,11 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);   // this wave's stage
+  // 64 < bins <= 1024 at 512 threads: the sort's counters in the stage's 24 KiB
+  // (order 2 + radix keys 4 + byte rows 16 + starts 2; tile_order_bytes)
+  constexpr bool STAGE_ROWS = GLDS && GD == 1 && USN_STAGE_ROWS &&
+                              NWAVES * STAGE_ROUND_SLOTS * 16 >= TILE * 6 + STAGE_BYTE_BINS * 18;
+  const bool rows_sort = STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS;
   STAMP_DECL
   STAMP(0);
 
@@ -1173,7 +1184,8 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   STAMP(1);
   // ---- while they fly: zero the segment counters (the barrier also waits
   //      for every load: table and round 0 are in LDS / registers after it)
-  for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
+  if (!rows_sort)
+    for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
   if (tid < 8) s_misc[tid] = 0;
   __syncthreads();
   STAMP(2);
@@ -1240,6 +1252,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     const uint32_t w11 = n11 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u;
     const bool n12 = use2 && pr[1].status == 1u && !w11;
     asm_slot1(T, a.ph[1], n12, k1.k2, d12, s12);
+    STAMP(4);
     asm volatile("s_waitcnt vmcnt(1)" : "+v"(s02) :: "memory");
     dec[0] = decide_rx_w(a, pr[0], w01, n02 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(s12) :: "memory");
@@ -1453,11 +1466,8 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 #if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
   const uint32_t n_runs = 0;
 #else
-  // the stage's 24 KiB (512 threads): order 2 + radix keys 4 + rows 16 + starts 2
-  constexpr bool STAGE_ROWS = GLDS && NWAVES * GD * STAGE_ROUND_SLOTS * 16 >=
-                                          TILE * 6 + STAGE_BYTE_BINS * 18 && USN_STAGE_ROWS;
   const uint32_t n_runs =
-      (STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS)
+      rows_sort
           ? tile_order_bytes(bins, nt, a.nbins, a.nbits, a.n_ep, L,
                              reinterpret_cast<uint8_t *>(s_stage), tile, a.order, a.runs, cls)
           : tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order, a.runs, cls);
