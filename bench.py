@@ -67,7 +67,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the c2 line at N=1")
-    ap.add_argument("--launch-probe", type=int, default=60, help="per-launch event pairs")
+    ap.add_argument("--launch-probe", type=int, default=150, help="per-launch event pairs")
+    ap.add_argument("--ramp", type=int, default=40,
+                    help="untimed poll rounds between the probe and the timed steps (clock ramp)")
     return ap.parse_args()
 
 
@@ -230,9 +232,19 @@ def measure(run, args, dist, world):
     from usnetd_amd import shard
     for i in range(args.warmup):
         run.step(i)
+    # the per-launch probe (150 launches, ~25 ms of c5 work) runs before the
+    # timed steps: the GPU takes ~10 ms of work to reach its steady clocks, and
+    # with the probe after them K = 20 timed steps read 53.2 Gpkt/s against
+    # 58.1 at 100 steps (tools/steptime.py: 0.301 -> 0.292 -> 0.280 ms per
+    # step over the first three runs of 20 steps)
+    kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
+    # the GPU reaches its steady rate only after ~40 poll rounds on both
+    # streams (the single-stream probe does not get it there): untimed ramp
+    # rounds, reported in config.untimed_ramp_steps
+    for i in range(args.ramp):
+        run.step(args.warmup + i)
     wall, ev_ms = run.timed(args.steps, dist)
     elapsed = shard.max_over_ranks(wall, dist)
-    kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
     host_frames, flags, cls = run.finalize_all()
     frames = world * args.steps * run.frames_per_step()
     achieved = ALGO_BYTES * probe_frames / (kern_ms * 1e-3) / 1e9 if kern_ms else None
@@ -328,6 +340,7 @@ def main():
             "rotating_bytes_per_gpu": run.rotating_bytes,
             "parallelism": "replicas%d" % world,
             "event_ms_per_step": res["event_ms_per_step"],
+            "untimed_ramp_steps": args.ramp,
             "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],
             "host_stage_frames": res["host_stage_frames"],
             "summary_flags": res["summary_flags"],

@@ -36,7 +36,7 @@ def main():
             continue
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", name, "--frames", str(n),
                "--queues", str(q), "--streams", str(st), "--steps", str(steps), "--warmup",
-               str(max(4, steps // 8)), "--cpu-seconds", str(args.cpu_seconds), "--batches", "4"]
+               str(max(4, steps // 8)), "--cpu-seconds", str(args.cpu_seconds), "--no-extra"]
         print("==", " ".join(cmd[1:]), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         line = [x for x in r.stdout.splitlines() if x.startswith("{")]
