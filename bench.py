@@ -232,17 +232,17 @@ def measure(run, args, dist, world):
     from usnetd_amd import shard
     for i in range(args.warmup):
         run.step(i)
-    # the per-launch probe (150 launches, ~25 ms of c5 work) runs before the
-    # timed steps: the GPU takes ~10 ms of work to reach its steady clocks, and
-    # with the probe after them K = 20 timed steps read 53.2 Gpkt/s against
-    # 58.1 at 100 steps (tools/steptime.py: 0.301 -> 0.292 -> 0.280 ms per
-    # step over the first three runs of 20 steps)
-    kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
-    # the GPU reaches its steady rate only after ~40 poll rounds on both
-    # streams (the single-stream probe does not get it there): untimed ramp
-    # rounds, reported in config.untimed_ramp_steps
+    # The GPU reaches its steady rate only after ~40 poll rounds on both
+    # streams: untimed ramp rounds, the per-launch probe, ramp rounds again
+    # (config.untimed_ramp_steps counts both), then the timed steps.  With the probe after the timed
+    # steps and no ramp, K = 20 read 53.2 Gpkt/s against 58.1 at 100 steps
+    # (tools/steptime.py: 0.301 -> 0.292 -> 0.280 ms per step over the first
+    # three runs of 20 steps).
     for i in range(args.ramp):
         run.step(args.warmup + i)
+    kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
+    for i in range(args.ramp):      # again: the one-stream probe lets the rate drop
+        run.step(args.warmup + args.ramp + i)
     wall, ev_ms = run.timed(args.steps, dist)
     elapsed = shard.max_over_ranks(wall, dist)
     host_frames, flags, cls = run.finalize_all()
@@ -340,7 +340,7 @@ def main():
             "rotating_bytes_per_gpu": run.rotating_bytes,
             "parallelism": "replicas%d" % world,
             "event_ms_per_step": res["event_ms_per_step"],
-            "untimed_ramp_steps": args.ramp,
+            "untimed_ramp_steps": 2 * args.ramp,
             "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],
             "host_stage_frames": res["host_stage_frames"],
             "summary_flags": res["summary_flags"],
