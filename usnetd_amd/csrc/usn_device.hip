@@ -93,9 +93,6 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #ifndef USN_ABL_TXNOPROBE   /* A/B only: tx kernels without rule-table probes (wrong results) */
 #define USN_ABL_TXNOPROBE 0
 #endif
-#ifndef USN_ABL_NOHEAD   /* A/B only: tx_decide without the run-head recompute (wrong results) */
-#define USN_ABL_NOHEAD 0
-#endif
 
 #ifndef USN_LOAD_NT
 #define USN_LOAD_NT 0
@@ -1798,7 +1795,7 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
 #define TXG_LREC 1u    /* 4 granules: its record (flags of the scan; zeros if none) */
 #define TXG_INS 5u     /* bit 0/1: the tile inserted MACs / rules, bit 2: a set overflowed */
 #define TXG_HEAD 6u    /* 1 + tile-local index of the last non-hit touching frame, 0 none */
-#define TXG_HREC 7u    /* 4 granules: its record (flags after the hit pass; zeros if none) */
+#define TXG_HDEC 7u    /* the decision of TXG_HEAD's frame (out with the tile's decisions) */
 #define TXG_PINS 11u   /* INS of every tile up to and including this one */
 #define TXG_PHEAD 12u  /* 1 + batch index of the last non-hit touching frame up to this tile, 0 none */
 #define TXG_CIN 13u    /* tile 0: 6 granules, the carried-in cache {state, dst, info[4]} */
@@ -1925,21 +1922,6 @@ __device__ __forceinline__ void tx_load_cin(const TxArgs &t, uint32_t *cin) {
   uint32_t v[6];
   const bool ok = g_getn<6>(t.aux + TXG_CIN, t, v);
   for (int k = 0; k < 6; ++k) cin[k] = ok ? v[k] : 0u;
-}
-
-/* the decision of a non-hit touching tx frame (the run head before a tile) */
-template <bool LDS>
-__device__ uint32_t tx_nonhit_dec(const TxArgs &t, const uint4 *T, const uint4 &r0, const uint4 &r1,
-                                  uint32_t i, uint32_t ins) {
-  const uint32_t fl = r0.x, touch = tx_touch(r0), kind = fl & 0xFFu;
-  if (touch == 0u) return usn_mkdec(USN_CLS_DROP, USN_R_PARSE, 0xFFFFu);
-  if (fl & TXR_HOST)
-    return usn_mkdec(USN_CLS_DROP, (fl & TXR_WINDOW) ? USN_R_WINDOW : touch == 3u ? USN_R_FRAGMISS
-                                                                           : USN_R_NOMATCH, 0xFFFFu) |
-           USN_F_HOST;
-  if (kind == USN_INFO_ARP || kind == USN_INFO_EAPOL) return usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
-  if (touch == 2u) return usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
-  return decide_tx_ipv4<LDS>(t, T, r0, r1, i, ins);
 }
 
 /* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge */
@@ -2209,9 +2191,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
   for (uint32_t r = 0; r < ROUNDS; ++r) srec[r * NTHREADS + tid] = rec[r];   // flags after the hit pass
   __syncthreads();
   if (tid == 0) {   // INS last: its arrival also says the claims above have landed (R1)
-    const uint32_t hn = s_lastnh;
-    g_put4(aux + TXG_HREC, t.epoch, hn ? srec[hn - 1] : make_uint4(0, 0, 0, 0));
-    g_put(aux + TXG_HEAD, t.epoch, hn);
+    g_put(aux + TXG_HEAD, t.epoch, s_lastnh);
     g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
   }
   STAMP(4);
@@ -2253,20 +2233,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
   if (tid == 0) {
     if (s_ovf) atomicOr(t.counters + 1, 1u);
     if (s_ins) atomicOr(t.counters + 2, s_ins);
-    // the decision of the run head before the tile: recomputed from its record
-    const uint32_t hx = s_hidx;
-    uint32_t hd = 0;
-    uint32_t hv[4];
-    if (!hx) {   // no non-hit touching frame before the tile: the carried-in cache's
-      if (tile > 0) tx_load_cin(t, s_cin);
-      hd = s_cin[1];
-    } else if (!USN_ABL_NOHEAD &&   // (A/B only: NOHEAD measures the recompute)
-               g_getn<4>(t.aux + (size_t)((hx - 1) / TILE) * TXA_GRANULES + TXG_HREC, t, hv)) {
-      const uint4 h0 = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-      const uint4 h1 = (insall & 1u) ? frame_head(a, hx - 1) : make_uint4(0, 0, 0, 0);
-      hd = tx_nonhit_dec<LDS>(t, T, h0, h1, hx - 1, insall);
-    }
-    s_head = hd;
   }
   STAMP(5);
   // MACs (dmac test, the first learner's smac) only when some frame <= this tile learned one
@@ -2278,6 +2244,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     if ((insall & 1u) && local < nt) r1[r] = frame_head(a, base + local);
   }
   const uint32_t ins_d = insall;
+  const uint32_t my_nh = s_lastnh;   // 1 + this tile's last non-hit touching frame
   uint32_t dec[ROUNDS], v[ROUNDS], head[ROUNDS];
   // every decision but get_endpoint's first; then key1 and key2 of all the
   // rounds that need get_endpoint are probed together (two round trips for
@@ -2386,6 +2353,22 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     dec[r] = d;
     sdec[local] = d;
     v[r] = (touch && !(fl & TXR_HIT)) ? local + 1 : 0u;
+    if (local + 1 == my_nh) g_put(aux + TXG_HDEC, t.epoch, d);   // for the tiles after
+  }
+  if (tid == 0) {
+    // the decision of the run head before the tile: that tile's own, published
+    // with its decisions (round 1 recomputed it here from the head's record:
+    // up to four dependent probes in one lane)
+    const uint32_t hx = s_hidx;
+    uint32_t hd = 0;
+    if (!hx) {   // no non-hit touching frame before the tile: the carried-in cache's
+      if (tile > 0) tx_load_cin(t, s_cin);
+      hd = s_cin[1];
+    } else {
+      uint32_t hv[1];
+      if (g_getn<1>(t.aux + (size_t)((hx - 1) / TILE) * TXA_GRANULES + TXG_HDEC, t, hv)) hd = hv[0];
+    }
+    s_head = hd;
   }
   STAMP(6);
   tile_prefix_max(v, L, head);   // its barriers also publish sdec and s_head
