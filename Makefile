@@ -51,9 +51,11 @@ clean:
 
 # A/B experiment builds (tools/abl.py): build/abl/<variant>/libusn.so,
 # one variant per line of tools/abl_variants.txt: "<name> <extra hipcc flags>"
+# (ABL_ONLY="v1 v2": only those)
 abl: build/usn_host.o
 	@while read -r name flags; do \
 	  case "$$name" in ''|'#'*) continue;; esac; \
+	  case " $(ABL_ONLY) " in "  ") ;; *" $$name "*) ;; *) continue;; esac; \
 	  mkdir -p build/abl/$$name; echo "variant $$name: $$flags"; \
 	  $(HIPCC) $(HIPFLAGS) $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip & \
 	  $(HIPCC) $(HIPFLAGS) -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 $$flags -c -o build/abl/$$name/dev512.o $(CSRC)/usn_device.hip & \

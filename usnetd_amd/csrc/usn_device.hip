@@ -1107,8 +1107,16 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
   return bi;
 }
 
-/* One workgroup per 1024-frame tile of a launch (several batches = drained
- * rx rings may share one launch). */
+/* The 1024-frame tiles of a launch (several batches = drained rx rings may
+ * share one launch), one workgroup each.  USN_PERSIST=1 (A/B only): the grid
+ * is what the chip holds at once and each workgroup loops over tiles
+ * blockIdx.x, + gridDim.x, ..., copying the rule image (or its displacements)
+ * to LDS once instead of once per tile -- slower: c5 8M 185.5 vs 170.5 us, c4
+ * 175.8 vs 160.9 (profiles/r02ah; the workgroups then run their phases in
+ * step, the header streams of all of them at once). */
+#ifndef USN_PERSIST
+#define USN_PERSIST 0
+#endif
 template <int TM, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
@@ -1127,37 +1135,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // radix keys live in the header stage (carve)
   static_assert(!GLDS || NWAVES * GD * STAGE_ROUND_SLOTS * 16 >= STAGE_SORT_BYTES, "stage too small");
   const Lds L = carve(smem, m.b[0].nbins, GLDS ? s_stage : nullptr);
-  const uint32_t bi = batch_of(m, blockIdx.x);
-  const ClassifyArgs &a = m.b[bi];
-  const uint32_t tile = blockIdx.x - m.tile_base[bi];
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);   // this wave's stage
-  // 64 < bins <= 1024 at 512 threads: the sort's counters in the stage's 24 KiB
-  // (order 2 + radix keys 4 + byte rows 16 + starts 2; tile_order_bytes)
-  constexpr bool STAGE_ROWS = GLDS && GD == 1 && USN_STAGE_ROWS &&
-                              NWAVES * STAGE_ROUND_SLOTS * 16 >= TILE * 6 + STAGE_BYTE_BINS * 18;
-  const bool rows_sort = STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS;
-  STAMP_DECL
-  STAMP(0);
-
-  // ---- loads, oldest first: lengths, rule table (L2-resident), headers.
-  //      Unpredicated at a clamped index: a load under `local < nt` made the
-  //      compiler wait for each before issuing the next; lanes past nt are
-  //      masked at use.
-  uint32_t len[ROUNDS];
-  const uint8_t *fp[ROUNDS];
-  if (!GLDS && a.offsets) {   // uniform; GLDS launches have no offsets array
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r)
-      fp[r] = a.frames + a.offsets[base + min(r * NTHREADS + tid, nt - 1)];
-  } else {
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r)
-      fp[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
   const uint4 *T = m.b[0].table;
   const uint16_t *Dl = nullptr;
   if (TM != TM_GLOBAL) {   // image (or its displacements) -> LDS by glds, 64 units per instruction
@@ -1170,334 +1148,370 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     if (TM == TM_LDS) T = L.table;
     else Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)u0 * 8;
   }
-  uint4 q[ROUNDS][4];
-  if (GLDS) {
-#pragma unroll
-    for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
-      glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
-  } else {
-    lane_round(fp[0], q[0]);
-  }
-  STAMP(1);
-  // ---- while they fly: zero the segment counters (the barrier also waits
-  //      for every load: table and round 0 are in LDS / registers after it)
-  if (!rows_sort)
-    for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
-  if (tid < 8) s_misc[tid] = 0;
-  __syncthreads();
-  STAMP(2);
+  // (the first tile's barrier also waits for the image copy)
+  const uint32_t ntiles_launch = m.tile_base[m.count];
+  const uint32_t wstep = USN_PERSIST ? gridDim.x : ntiles_launch;
+  for (uint32_t w = blockIdx.x; w < ntiles_launch; w += wstep) {
+    if (w != blockIdx.x) __syncthreads();   // the previous tile is done with the stage and s_misc
+    const uint32_t bi = batch_of(m, w);
+    const ClassifyArgs &a = m.b[bi];
+    const uint32_t tile = w - m.tile_base[bi];
+    const uint64_t base = (uint64_t)tile * TILE;
+    const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
+    // 64 < bins <= 1024 at 512 threads: the sort's counters in the stage's 24 KiB
+    // (order 2 + radix keys 4 + byte rows 16 + starts 2; tile_order_bytes)
+    constexpr bool STAGE_ROWS = GLDS && GD == 1 && USN_STAGE_ROWS &&
+                                NWAVES * STAGE_ROUND_SLOTS * 16 >= TILE * 6 + STAGE_BYTE_BINS * 18;
+    const bool rows_sort = STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS;
+    STAMP_DECL
+    STAMP(0);
 
-  // ---- carried-in cache (block 0): stale check against the current table
-  if (tile == 0) {
-    resolve_carry(a, s_carry, L.scratch);
-    if (tid == 0) {
-      const uint32_t cst = s_carry[0], dst = s_carry[1];
-      uint32_t flags = 0;
-      if ((cst & USN_CS_VALID) &&
-          ((decide_info_rx<TM>(T, Dl, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
-        flags |= USN_S_STALE;
-      s_carry[6] = flags;
-      s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
-      usn_summary *S = a.summary;
-      S->cin_state = cst; S->cin_dst = dst;
-      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
-      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
-    }
-    __syncthreads();
-  }
-  const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
-  STAMP(3);
-
-  // ---- parse + decide, the next round's headers in flight meanwhile
-  uint32_t dec[ROUNDS], bins[ROUNDS];
-  uint32_t differs = 0;          // stale mode: bit r = touching frame whose info != carried
-  uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
-  uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
-  Parsed pr[ROUNDS];
-  if (BATCH2 && TM == TM_DISPLDS && USN_SEQ_K2) {
-    // displacements from LDS; key1's slot reads of both rounds first, then
-    // key2's only where key1 missed (get_endpoint reads key2 only then,
-    // endpoint.rs:317-327): a lane that needs no read shares the table's
-    // first line, so c5's half of frames that hit key1 cost no second L2
-    // request.  Round 1's header DMA flies under round 0's parse.
-    uint4 *sb = st;
-    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
-    RoundKeys k0, k1;
-    uint32_t d01, d02, d11, d12;
-    v4u32 s01, s02, s11, s12;
-    stage_read_asm(sb, lane, q[0]);
-    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
-    __builtin_amdgcn_sched_barrier(0);
-    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
-    round_keys(a, pr[0], k0);
-    lds_disp2(Dl, a, use1, use2, k0, d01, d02);
-    const bool n01 = use1 && pr[0].status == 1u;
-    asm_slot1(T, a.ph[0], n01, k0.k1, d01, s01);
-    __builtin_amdgcn_sched_barrier(0);
-    vm_wait<1>();                                               // round 1 landed (1 younger load)
-    stage_read_asm(sb, lane, q[1]);
-    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
-    round_keys(a, pr[1], k1);
-    lds_disp2(Dl, a, use1, use2, k1, d11, d12);
-    const bool n11 = use1 && pr[1].status == 1u;
-    asm_slot1(T, a.ph[0], n11, k1.k1, d11, s11);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s01) :: "memory");
-    const uint32_t w01 = n01 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u;
-    const bool n02 = use2 && pr[0].status == 1u && !w01;
-    asm_slot1(T, a.ph[1], n02, k0.k2, d02, s02);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s11) :: "memory");
-    const uint32_t w11 = n11 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u;
-    const bool n12 = use2 && pr[1].status == 1u && !w11;
-    asm_slot1(T, a.ph[1], n12, k1.k2, d12, s12);
-    STAMP(4);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(s02) :: "memory");
-    dec[0] = decide_rx_w(a, pr[0], w01, n02 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s12) :: "memory");
-    dec[1] = decide_rx_w(a, pr[1], w11, n12 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
-  } else if (BATCH2 && TM == TM_DISPLDS) {
-    // displacements from LDS: one global round trip (the slots) per round,
-    // round 1's header DMA in flight under round 0's parse and slot loads
-    uint4 *sb = st;
-    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
-    RoundKeys k0, k1;
-    uint32_t d01, d02, d11, d12;
-    v4u32 s01, s02, s11, s12;
-    stage_read_asm(sb, lane, q[0]);
-    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
-    __builtin_amdgcn_sched_barrier(0);
-    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
-    round_keys(a, pr[0], k0);
-    lds_disp2(Dl, a, use1, use2, k0, d01, d02);
-    asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
-    __builtin_amdgcn_sched_barrier(0);
-    vm_wait<2>();                                               // round 1 landed (2 younger loads)
-    stage_read_asm(sb, lane, q[1]);
-    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
-    round_keys(a, pr[1], k1);
-    lds_disp2(Dl, a, use1, use2, k1, d11, d12);
-    asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
-    asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
-    dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
-                         use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
-    dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
-                         use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
-  } else if (BATCH2) {
-    // round 0's headers are in the stage (the barrier above waited for them)
-    uint4 *sb = st;
-    const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
-    const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
-    RoundKeys k0, k1;
-    uint32_t d01, d02, d11, d12;
-    v4u32 s01, s02, s11, s12;
-    stage_read_asm(sb, lane, q[0]);
-    glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
-    __builtin_amdgcn_sched_barrier(0);
-    parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
-    round_keys(a, pr[0], k0);
-    asm_disp2(D, a, use1, use2, k0, d01, d02);
-    __builtin_amdgcn_sched_barrier(0);
-    vm_wait<2>();                                               // round 1 landed (2 younger loads)
-    stage_read_asm(sb, lane, q[1]);
-    parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
-    round_keys(a, pr[1], k1);
-    asm_disp2(D, a, use1, use2, k1, d11, d12);
-    vm_wait2<2>(d01, d02);
-    asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
-    vm_wait2<2>(d11, d12);
-    asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
-    asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
-    dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
-                         use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
-    dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
-                         use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
-  }
+    // ---- loads, oldest first: lengths, headers.
+    //      Unpredicated at a clamped index: a load under `local < nt` made the
+    //      compiler wait for each before issuing the next; lanes past nt are
+    //      masked at use.
+    uint32_t len[ROUNDS];
+    const uint8_t *fp[ROUNDS];
+    if (!GLDS && a.offsets) {   // uniform; GLDS launches have no offsets array
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS && !BATCH2; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    uint4 *sb = st + (r % GD) * STAGE_ROUND_SLOTS;
-    if (GLDS) {
-      // round r landed: only the rounds issued after it may still fly (GLDS_PARTS glds each)
-      constexpr uint32_t kAfterMax = GD - 1;
-      const uint32_t after = min(kAfterMax, ROUNDS - 1 - r);
-      if (r > 0) {
-        if (after >= 3) vm_wait<3 * GLDS_PARTS>();
-        else if (after == 2) vm_wait<2 * GLDS_PARTS>();
-        else if (after == 1) vm_wait<GLDS_PARTS>();
-        else vm_wait<0>();
-      }
-      stage_read(sb, lane, q[r]);
-      if (!LATE_DMA && r + GD < ROUNDS) {
-        lgkm_wait0();          // this round's reads are done before its buffer is refilled
-        glds_round(a, base, nt, r + GD, wave, lane, sb);
-      }
-    } else if (r + 1 < ROUNDS) {   // one round of headers in flight ahead of the one decided
-      __builtin_amdgcn_sched_barrier(0);
-      lane_round(fp[r + 1], q[r + 1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
-    dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
-                       (q[r][0].w ^ q[r][1].y ^ q[r][2].x ^ q[r][2].y ^ len[r]) & 0xFFFFu);
-    pr[r] = Parsed{};   // defined (a parse failure): the touch pass below reads it
-    continue;
-#endif
-    Parsed &p = pr[r];
-    parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
-    if (LATE_DMA) {
-      // global probes: the slot loads first, then the next round's header DMA,
-      // so the wait for the slots does not also wait for the DMA
-      uint32_t w1 = 0, w2 = 0;
-#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
-      w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
-#else
-      uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
-      rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
-      const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
-      v4u32 s1, s2;
-      ph_issue<TM, true>(T, Dl, a, use1, use2, x1, y1, z1, m1, x2, y2, z2, m2, s1, s2);
-#endif
-      if (r + GD < ROUNDS) {
-        __builtin_amdgcn_sched_barrier(0);
-        lgkm_wait0();
-        glds_round(a, base, nt, r + GD, wave, lane, sb);
-        __builtin_amdgcn_sched_barrier(0);
-#if !USN_ABL_NOPROBE
-        ph_slots_wait<GLDS_PARTS>(s1, s2);   // the next round's header DMAs may still fly
-#endif
-      } else {
-#if !USN_ABL_NOPROBE
-        ph_slots_wait<0>(s1, s2);
-#endif
-      }
-#if !USN_ABL_NOPROBE
-      w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
-      w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
-#endif
-      dec[r] = decide_rx_w(a, p, w1, w2);
+      for (uint32_t r = 0; r < ROUNDS; ++r)
+        fp[r] = a.frames + a.offsets[base + min(r * NTHREADS + tid, nt - 1)];
     } else {
-      dec[r] = decide_rx<TM>(T, Dl, a, p);
-    }
-    if (r == 0) STAMP(4);
-  }
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const Parsed &p = pr[r];
-    // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
-    uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
-                   : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
-    if (local >= nt) touch = 0;
-    if (touch) {
-      my_last = local + 1; my_touch = touch; my_dec = dec[r];
-      my_info[0] = p.i0; my_info[1] = p.src; my_info[2] = p.dst; my_info[3] = p.ports;
+      for (uint32_t r = 0; r < ROUNDS; ++r)
+        fp[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
     }
-    if (stale && touch && !(touch == 1 && p.i0 == s_carry[2] && p.src == s_carry[3] &&
-                            p.dst == s_carry[4] && p.ports == s_carry[5]))
-      differs |= 1u << r;        // later fragments also stop the device prefix
-  }
-  STAMP(5);
-
-  // ---- stale carried cache: frames before the first break take the cached
-  //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
-  if (stale) {
-    uint32_t fb = TILE;
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r)
-      if (differs & (1u << r)) fb = min(fb, r * NTHREADS + tid);
-    atomicMin(&s_carry[7], fb);
+    for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
+    uint4 q[ROUNDS][4];
+    if (GLDS) {
+#pragma unroll
+      for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
+        glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
+    } else {
+      lane_round(fp[0], q[0]);
+    }
+    STAMP(1);
+    // ---- while they fly: zero the segment counters (the barrier also waits
+    //      for every load: table and round 0 are in LDS / registers after it)
+    if (!rows_sort)
+      for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
+    if (tid < 8) s_misc[tid] = 0;
     __syncthreads();
-    const uint32_t first = s_carry[7];
+    STAMP(2);
+
+    // ---- carried-in cache (block 0): stale check against the current table
+    if (tile == 0) {
+      resolve_carry(a, s_carry, L.scratch);
+      if (tid == 0) {
+        const uint32_t cst = s_carry[0], dst = s_carry[1];
+        uint32_t flags = 0;
+        if ((cst & USN_CS_VALID) &&
+            ((decide_info_rx<TM>(T, Dl, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
+          flags |= USN_S_STALE;
+        s_carry[6] = flags;
+        s_carry[7] = TILE;   // first break in tile 0 (min over frames), TILE = none
+        usn_summary *S = a.summary;
+        S->cin_state = cst; S->cin_dst = dst;
+        for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
+        S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      }
+      __syncthreads();
+    }
+    const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
+    STAMP(3);
+
+    // ---- parse + decide, the next round's headers in flight meanwhile
+    uint32_t dec[ROUNDS], bins[ROUNDS];
+    uint32_t differs = 0;          // stale mode: bit r = touching frame whose info != carried
+    uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
+    uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
+    Parsed pr[ROUNDS];
+    if (BATCH2 && TM == TM_DISPLDS && USN_SEQ_K2) {
+      // displacements from LDS; key1's slot reads of both rounds first, then
+      // key2's only where key1 missed (get_endpoint reads key2 only then,
+      // endpoint.rs:317-327): a lane that needs no read shares the table's
+      // first line, so c5's half of frames that hit key1 cost no second L2
+      // request.  Round 1's header DMA flies under round 0's parse.
+      uint4 *sb = st;
+      const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+      RoundKeys k0, k1;
+      uint32_t d01, d02, d11, d12;
+      v4u32 s01, s02, s11, s12;
+      stage_read_asm(sb, lane, q[0]);
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      __builtin_amdgcn_sched_barrier(0);
+      parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+      round_keys(a, pr[0], k0);
+      lds_disp2(Dl, a, use1, use2, k0, d01, d02);
+      const bool n01 = use1 && pr[0].status == 1u;
+      asm_slot1(T, a.ph[0], n01, k0.k1, d01, s01);
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<1>();                                               // round 1 landed (1 younger load)
+      stage_read_asm(sb, lane, q[1]);
+      parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+      round_keys(a, pr[1], k1);
+      lds_disp2(Dl, a, use1, use2, k1, d11, d12);
+      const bool n11 = use1 && pr[1].status == 1u;
+      asm_slot1(T, a.ph[0], n11, k1.k1, d11, s11);
+      asm volatile("s_waitcnt vmcnt(1)" : "+v"(s01) :: "memory");
+      const uint32_t w01 = n01 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u;
+      const bool n02 = use2 && pr[0].status == 1u && !w01;
+      asm_slot1(T, a.ph[1], n02, k0.k2, d02, s02);
+      asm volatile("s_waitcnt vmcnt(1)" : "+v"(s11) :: "memory");
+      const uint32_t w11 = n11 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u;
+      const bool n12 = use2 && pr[1].status == 1u && !w11;
+      asm_slot1(T, a.ph[1], n12, k1.k2, d12, s12);
+      STAMP(4);
+      asm volatile("s_waitcnt vmcnt(1)" : "+v"(s02) :: "memory");
+      dec[0] = decide_rx_w(a, pr[0], w01, n02 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(s12) :: "memory");
+      dec[1] = decide_rx_w(a, pr[1], w11, n12 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+    } else if (BATCH2 && TM == TM_DISPLDS) {
+      // displacements from LDS: one global round trip (the slots) per round,
+      // round 1's header DMA in flight under round 0's parse and slot loads
+      uint4 *sb = st;
+      const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+      RoundKeys k0, k1;
+      uint32_t d01, d02, d11, d12;
+      v4u32 s01, s02, s11, s12;
+      stage_read_asm(sb, lane, q[0]);
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      __builtin_amdgcn_sched_barrier(0);
+      parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+      round_keys(a, pr[0], k0);
+      lds_disp2(Dl, a, use1, use2, k0, d01, d02);
+      asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<2>();                                               // round 1 landed (2 younger loads)
+      stage_read_asm(sb, lane, q[1]);
+      parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+      round_keys(a, pr[1], k1);
+      lds_disp2(Dl, a, use1, use2, k1, d11, d12);
+      asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
+      asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
+      dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
+                           use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
+      dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
+                           use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+    } else if (BATCH2) {
+      // round 0's headers are in the stage (the barrier above waited for them)
+      uint4 *sb = st;
+      const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+      const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
+      RoundKeys k0, k1;
+      uint32_t d01, d02, d11, d12;
+      v4u32 s01, s02, s11, s12;
+      stage_read_asm(sb, lane, q[0]);
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      __builtin_amdgcn_sched_barrier(0);
+      parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+      round_keys(a, pr[0], k0);
+      asm_disp2(D, a, use1, use2, k0, d01, d02);
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<2>();                                               // round 1 landed (2 younger loads)
+      stage_read_asm(sb, lane, q[1]);
+      parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+      round_keys(a, pr[1], k1);
+      asm_disp2(D, a, use1, use2, k1, d11, d12);
+      vm_wait2<2>(d01, d02);
+      asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
+      vm_wait2<2>(d11, d12);
+      asm_slot2(T, a, use1, use2, k1, d11, d12, s11, s12);
+      asm volatile("s_waitcnt vmcnt(2)" : "+v"(s01), "+v"(s02) :: "memory");
+      dec[0] = decide_rx_w(a, pr[0], use1 ? ph_hitv(s01, k0.x1, k0.y1, k0.z1, k0.m1) : 0u,
+                           use2 ? ph_hitv(s02, k0.x2, k0.y2, k0.z2, k0.m2) : 0u);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(s11), "+v"(s12) :: "memory");
+      dec[1] = decide_rx_w(a, pr[1], use1 ? ph_hitv(s11, k1.x1, k1.y1, k1.z1, k1.m1) : 0u,
+                           use2 ? ph_hitv(s12, k1.x2, k1.y2, k1.z2, k1.m2) : 0u);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS && !BATCH2; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      uint4 *sb = st + (r % GD) * STAGE_ROUND_SLOTS;
+      if (GLDS) {
+        // round r landed: only the rounds issued after it may still fly (GLDS_PARTS glds each)
+        constexpr uint32_t kAfterMax = GD - 1;
+        const uint32_t after = min(kAfterMax, ROUNDS - 1 - r);
+        if (r > 0) {
+          if (after >= 3) vm_wait<3 * GLDS_PARTS>();
+          else if (after == 2) vm_wait<2 * GLDS_PARTS>();
+          else if (after == 1) vm_wait<GLDS_PARTS>();
+          else vm_wait<0>();
+        }
+        stage_read(sb, lane, q[r]);
+        if (!LATE_DMA && r + GD < ROUNDS) {
+          lgkm_wait0();          // this round's reads are done before its buffer is refilled
+          glds_round(a, base, nt, r + GD, wave, lane, sb);
+        }
+      } else if (r + 1 < ROUNDS) {   // one round of headers in flight ahead of the one decided
+        __builtin_amdgcn_sched_barrier(0);
+        lane_round(fp[r + 1], q[r + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
+      dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
+                         (q[r][0].w ^ q[r][1].y ^ q[r][2].x ^ q[r][2].y ^ len[r]) & 0xFFFFu);
+      pr[r] = Parsed{};   // defined (a parse failure): the touch pass below reads it
+      continue;
+#endif
+      Parsed &p = pr[r];
+      parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
+      if (LATE_DMA) {
+        // global probes: the slot loads first, then the next round's header DMA,
+        // so the wait for the slots does not also wait for the DMA
+        uint32_t w1 = 0, w2 = 0;
+#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
+        w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
+#else
+        uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+        rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
+        const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
+        v4u32 s1, s2;
+        ph_issue<TM, true>(T, Dl, a, use1, use2, x1, y1, z1, m1, x2, y2, z2, m2, s1, s2);
+#endif
+        if (r + GD < ROUNDS) {
+          __builtin_amdgcn_sched_barrier(0);
+          lgkm_wait0();
+          glds_round(a, base, nt, r + GD, wave, lane, sb);
+          __builtin_amdgcn_sched_barrier(0);
+#if !USN_ABL_NOPROBE
+          ph_slots_wait<GLDS_PARTS>(s1, s2);   // the next round's header DMAs may still fly
+#endif
+        } else {
+#if !USN_ABL_NOPROBE
+          ph_slots_wait<0>(s1, s2);
+#endif
+        }
+#if !USN_ABL_NOPROBE
+        w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
+        w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
+#endif
+        dec[r] = decide_rx_w(a, p, w1, w2);
+      } else {
+        dec[r] = decide_rx<TM>(T, Dl, a, p);
+      }
+      if (r == 0) STAMP(4);
+    }
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) {
       const uint32_t local = r * NTHREADS + tid;
-      const bool touching_same = local < nt && local < first &&
-                                 USN_DEC_REASON(dec[r]) != USN_R_PARSE;
-      if (touching_same)
-        dec[r] = (s_carry[1] & USN_PARITY_MASK) | USN_F_CACHE |
-                 (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_DHCP));
-      if (local + 1 == my_last && touching_same) my_dec = dec[r];
+      const Parsed &p = pr[r];
+      // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
+      uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
+                     : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
+      if (local >= nt) touch = 0;
+      if (touch) {
+        my_last = local + 1; my_touch = touch; my_dec = dec[r];
+        my_info[0] = p.i0; my_info[1] = p.src; my_info[2] = p.dst; my_info[3] = p.ports;
+      }
+      if (stale && touch && !(touch == 1 && p.i0 == s_carry[2] && p.src == s_carry[3] &&
+                              p.dst == s_carry[4] && p.ports == s_carry[5]))
+        differs |= 1u << r;        // later fragments also stop the device prefix
+    }
+    STAMP(5);
+
+    // ---- stale carried cache: frames before the first break take the cached
+    //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
+    if (stale) {
+      uint32_t fb = TILE;
+#pragma unroll
+      for (uint32_t r = 0; r < ROUNDS; ++r)
+        if (differs & (1u << r)) fb = min(fb, r * NTHREADS + tid);
+      atomicMin(&s_carry[7], fb);
+      __syncthreads();
+      const uint32_t first = s_carry[7];
+#pragma unroll
+      for (uint32_t r = 0; r < ROUNDS; ++r) {
+        const uint32_t local = r * NTHREADS + tid;
+        const bool touching_same = local < nt && local < first &&
+                                   USN_DEC_REASON(dec[r]) != USN_R_PARSE;
+        if (touching_same)
+          dec[r] = (s_carry[1] & USN_PARITY_MASK) | USN_F_CACHE |
+                   (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_DHCP));
+        if (local + 1 == my_last && touching_same) my_dec = dec[r];
+      }
+      if (tid == 0) {
+        uint32_t f = s_carry[6];
+        if (first >= nt && a.n > TILE) f |= USN_S_STALE_EXTENDS;
+        a.summary->first_break = first;
+        s_carry[6] = f;
+      }
+    }
+    if (tile == 0 && tid == 0) {
+      a.summary->flags = s_carry[6];
+      if (!(s_carry[6] & USN_S_STALE)) a.summary->first_break = 0xFFFFFFFFu;
+    }
+
+    // ---- decisions out (coalesced), host list, last touching frame
+    uint32_t *hl = a.host_list + (size_t)tile * TILE;
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      const bool v = local < nt;
+      if (v) a.decisions[base + local] = dec[r];
+      bins[r] = dec_bin(dec[r], a.n_ep);
+      const bool host = v && (dec[r] & USN_F_HOST);
+      if (__ballot(host)) {                                // rare: unordered append (host sorts)
+        if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
+      }
+    }
+    {
+      // the wave's last touching frame: highest lane of the latest round with one
+      const uint64_t rounds_with = __ballot(my_last != 0);
+      if (rounds_with) {
+        const uint32_t r_last = (my_last - 1) / NTHREADS;
+        const uint32_t rmax = __builtin_amdgcn_readfirstlane(
+            __reduce_max_rounds(r_last, my_last != 0));
+        const uint64_t in_r = __ballot(my_last != 0 && r_last == rmax);
+        const uint32_t hi = 63 - (uint32_t)__builtin_clzll(in_r);
+        if (lane == 0) atomicMax(&s_misc[0], rmax * NTHREADS + wave * 64 + hi + 1);
+      }
+    }
+
+    STAMP(6);
+    // ---- stable per-endpoint order of the tile
+    uint32_t cls[4] = {0, 0, 0, 0};
+#if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
+    const uint32_t n_runs = 0;
+#else
+    const uint32_t n_runs =
+        rows_sort
+            ? tile_order_bytes(bins, nt, a.nbins, a.nbits, a.n_ep, L,
+                               reinterpret_cast<uint8_t *>(s_stage), tile, a.order, a.runs, cls)
+            : tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order, a.runs, cls);
+#endif
+    if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
+    if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
+    if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
+    __syncthreads();
+    STAMP(10);
+
+    // ---- tile header
+    usn_tile_hdr *H = a.tiles + tile;
+    const uint32_t lastp = s_misc[0];
+    if (lastp && my_last == lastp) {
+      H->last_state = USN_TS_HAS | (my_touch == 1u ? USN_TS_RETAINED : 0u) |
+                      (my_touch == 3u ? USN_TS_UNKNOWN : 0u);
+      H->last_dst = my_dec & USN_PARITY_MASK;
+      for (int k = 0; k < 4; ++k) H->last_info[k] = my_info[k];
+      H->last_idx = (uint32_t)(base + lastp - 1);
     }
     if (tid == 0) {
-      uint32_t f = s_carry[6];
-      if (first >= nt && a.n > TILE) f |= USN_S_STALE_EXTENDS;
-      a.summary->first_break = first;
-      s_carry[6] = f;
+      H->n_frames = (uint16_t)nt;
+      H->n_runs = (uint16_t)n_runs;
+      H->n_host = (uint16_t)s_misc[1];
+      H->bin_nic = (uint16_t)a.n_ep;
+      H->class_count[0] = (uint16_t)s_misc[5];                       // DROP bin
+      H->class_count[2] = (uint16_t)s_misc[3];                       // NIC bin
+      H->class_count[3] = (uint16_t)s_misc[4];                       // FLOOD bin
+      H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
+      if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
     }
+    STAMP(11);
+    STAMP_FLUSH_AT(w);
   }
-  if (tile == 0 && tid == 0) {
-    a.summary->flags = s_carry[6];
-    if (!(s_carry[6] & USN_S_STALE)) a.summary->first_break = 0xFFFFFFFFu;
-  }
-
-  // ---- decisions out (coalesced), host list, last touching frame
-  uint32_t *hl = a.host_list + (size_t)tile * TILE;
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const bool v = local < nt;
-    if (v) a.decisions[base + local] = dec[r];
-    bins[r] = dec_bin(dec[r], a.n_ep);
-    const bool host = v && (dec[r] & USN_F_HOST);
-    if (__ballot(host)) {                                // rare: unordered append (host sorts)
-      if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
-    }
-  }
-  {
-    // the wave's last touching frame: highest lane of the latest round with one
-    const uint64_t rounds_with = __ballot(my_last != 0);
-    if (rounds_with) {
-      const uint32_t r_last = (my_last - 1) / NTHREADS;
-      const uint32_t rmax = __builtin_amdgcn_readfirstlane(
-          __reduce_max_rounds(r_last, my_last != 0));
-      const uint64_t in_r = __ballot(my_last != 0 && r_last == rmax);
-      const uint32_t hi = 63 - (uint32_t)__builtin_clzll(in_r);
-      if (lane == 0) atomicMax(&s_misc[0], rmax * NTHREADS + wave * 64 + hi + 1);
-    }
-  }
-
-  STAMP(6);
-  // ---- stable per-endpoint order of the tile
-  uint32_t cls[4] = {0, 0, 0, 0};
-#if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
-  const uint32_t n_runs = 0;
-#else
-  const uint32_t n_runs =
-      rows_sort
-          ? tile_order_bytes(bins, nt, a.nbins, a.nbits, a.n_ep, L,
-                             reinterpret_cast<uint8_t *>(s_stage), tile, a.order, a.runs, cls)
-          : tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order, a.runs, cls);
-#endif
-  if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
-  if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
-  if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
-  __syncthreads();
-  STAMP(10);
-
-  // ---- tile header
-  usn_tile_hdr *H = a.tiles + tile;
-  const uint32_t lastp = s_misc[0];
-  if (lastp && my_last == lastp) {
-    H->last_state = USN_TS_HAS | (my_touch == 1u ? USN_TS_RETAINED : 0u) |
-                    (my_touch == 3u ? USN_TS_UNKNOWN : 0u);
-    H->last_dst = my_dec & USN_PARITY_MASK;
-    for (int k = 0; k < 4; ++k) H->last_info[k] = my_info[k];
-    H->last_idx = (uint32_t)(base + lastp - 1);
-  }
-  if (tid == 0) {
-    H->n_frames = (uint16_t)nt;
-    H->n_runs = (uint16_t)n_runs;
-    H->n_host = (uint16_t)s_misc[1];
-    H->bin_nic = (uint16_t)a.n_ep;
-    H->class_count[0] = (uint16_t)s_misc[5];                       // DROP bin
-    H->class_count[2] = (uint16_t)s_misc[3];                       // NIC bin
-    H->class_count[3] = (uint16_t)s_misc[4];                       // FLOOD bin
-    H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
-    if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
-  }
-  STAMP(11);
-  STAMP_FLUSH();
 }
 
 
@@ -2500,6 +2514,28 @@ static bool glds_layout(const MultiArgs &m) {
   return true;
 }
 
+/* USN_PERSIST: workgroups of kernel `fn` the device holds at once (its CUs x
+ * the occupancy at `lds` bytes of dynamic LDS), cached per device and kernel */
+template <typename K>
+static uint32_t resident_grid(K fn, size_t lds) {
+  struct Entry { int dev; const void *fn; size_t lds; uint32_t blocks; };
+  thread_local Entry cache[16];
+  thread_local int used = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  for (int k = 0; k < used; ++k)
+    if (cache[k].dev == dev && cache[k].fn == reinterpret_cast<const void *>(fn) && cache[k].lds == lds)
+      return cache[k].blocks;
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHREADS, lds) != hipSuccess)
+    return 0;
+  const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 0) * (uint32_t)(per_cu > 0 ? per_cu : 0);
+  cache[used % 16] = Entry{dev, reinterpret_cast<const void *>(fn), lds, blocks};
+  if (used < 16) ++used;
+  return blocks;
+}
+
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
@@ -2509,8 +2545,17 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const size_t lds = lds_core_bytes(a.nbins, !glds) +
                      (tm == TM_LDS ? table_lds_bytes(a.table_units)
                       : tm == TM_DISPLDS ? table_lds_bytes(a.table_units - a.disp_unit) : 0);
-  const dim3 g(tiles), b(NTHREADS);
-#define USN_LAUNCH(T_, G_) hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), g, b, lds, stream, m)
+  const dim3 b(NTHREADS);
+  // a grid of at most what the chip holds (0 = the query failed: one per tile)
+#define USN_LAUNCH(T_, G_)                                                              \
+  do {                                                                                  \
+    uint32_t grid = tiles;                                                              \
+    if (USN_PERSIST) {                                                                  \
+      const uint32_t res = resident_grid(classify_rx_kernel<T_, G_>, lds);              \
+      if (res) grid = min(grid, res);                                                   \
+    }                                                                                   \
+    hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(grid), b, lds, stream, m);    \
+  } while (0)
   if (tm == TM_LDS) { if (glds) USN_LAUNCH(TM_LDS, true); else USN_LAUNCH(TM_LDS, false); }
   else if (tm == TM_DISPLDS) { if (glds) USN_LAUNCH(TM_DISPLDS, true); else USN_LAUNCH(TM_DISPLDS, false); }
   else { if (glds) USN_LAUNCH(TM_GLOBAL, true); else USN_LAUNCH(TM_GLOBAL, false); }
