@@ -18,8 +18,8 @@ NAMES = ["start", "loads issued", "table+zero barrier", "carry", "round0 decided
          "all rounds decided", "stores+hostlist+lastreduce", "-", "-", "-",
          "tile_order+cls", "header"]
 # c4tx: the one-launch tx kernel (stamps indexed by tile)
-TX_NAMES = ["start", "header loads + bridge", "parse, flags, probes", "LAST out, walk back",
-            "hits, claims, INS out", "look-back", "decisions", "fill, host list", "-", "-",
+TX_NAMES = ["start", "header loads + bridge", "parse, flags, probes", "LAST out",
+            "hits, HEAD/INS out, walk back", "look-back", "decisions", "fill, host list", "-", "-",
             "tile_order+cls", "header"]
 TX_STEPS = [1, 2, 3, 4, 5, 6, 7, 10, 11]
 
@@ -27,7 +27,7 @@ TX_STEPS = [1, 2, 3, 4, 5, 6, 7, 10, 11]
 def main():
     cfgname = sys.argv[1] if len(sys.argv) > 1 else "c2"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
-    path = os.path.join(ROOT, "build", "abl", "stamps", "libusn.so")
+    path = os.path.join(ROOT, "build", "abl", os.environ.get("STAMPS_BUILD", "stamps"), "libusn.so")
     ctx = lib.Ctx(0, libpath=path)
     # tx: one ring replayed (steady state: its answer rules are learned by the first pass)
     cfgs = [traffic.config(cfgname, n=n, seed=6 if cfgname == "c4tx" else 17 * k + 2)
@@ -68,6 +68,11 @@ def main():
     tot = st[:, 11] - st[:, 0]
     print("  %-28s median %6.2f  p90 %6.2f  max %6.2f us" % ("TOTAL per block", us(np.median(tot)),
                                                         us(np.percentile(tot, 90)), us(tot.max())))
+    # workgroups in flight: the stamped part of every block over the span.  Below
+    # what the chip holds, the rest is dispatch, prologue and the stamp flush.
+    span = st[:, 11].max() - t0
+    print("  workgroups in flight (stamped part): mean %.1f; mean block %.2f us, %.1f blocks per slot"
+          % (tot.sum() / span, us(tot.mean()), ntiles / max(1.0, tot.sum() / span)))
 
 
 if __name__ == "__main__":

@@ -66,11 +66,16 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 /* stamps live in registers until the end: a global store per stamp would
  * queue behind the header loads and time the memory queue instead */
+#ifndef USN_STAMP_MIN   /* 1: only the first and last stamp (registers as in the product) */
+#define USN_STAMP_MIN 0
+#endif
 #define STAMP(k)                                                                 \
   do {                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    stamp_t[(k)] = wall_clock64();                                               \
-    __builtin_amdgcn_sched_barrier(0);                                           \
+    if (!USN_STAMP_MIN || (k) == 0 || (k) == 11) {                               \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+      stamp_t[(k)] = wall_clock64();                                             \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+    }                                                                            \
   } while (0)
 #define STAMP_DECL unsigned long long stamp_t[12] = {0};
 #define STAMP_FLUSH_AT(slot)                                                     \
@@ -391,30 +396,31 @@ __device__ __forceinline__ uint32_t ph_probe1(const uint4 *T, const ClassifyArgs
   return ph_hit(T[t.slot_off + k.sbase + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
 }
 
-/* N probes issued together: all N displacement reads, then all N slot
- * reads -- two round trips for the lot instead of two per key.  Keys
- * [0, N1) go to table K1, the rest to K2; use[i] false (or an empty table)
- * gives w[i] = 0 with a harmless read of the table's first entries.  IN_LDS:
- * the image is the LDS copy. */
-template <bool IN_LDS, int N, int N1>
-__device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs &a,
-                                              const uint32_t (&x)[N], const uint32_t (&y)[N],
-                                              const uint32_t (&z)[N], const uint32_t (&m)[N],
-                                              const bool (&use)[N], uint32_t (&w)[N]) {
+/* One key's displacement read of table `tb` (0 = K1, 1 = K2): its hash,
+ * whether it is probed at all (use, and the table non-empty), and the read
+ * (a key not probed reads the table's first displacement). */
+template <bool IN_LDS>
+__device__ __forceinline__ void ph_disp_issue(const uint4 *T, const ClassifyArgs &a, int tb, uint32_t x,
+                                              uint32_t y, uint32_t z, uint32_t m, bool use, PhKeyH &k,
+                                              uint32_t &d, bool &on) {
   typedef __attribute__((address_space(3))) const uint16_t lds_u16;
-  typedef __attribute__((address_space(3))) const v4u32 lds_v4;
   const uint16_t *D = reinterpret_cast<const uint16_t *>(T);
-  PhKeyH k[N];
-  uint32_t d[N];
-  bool on[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
-    on[i] = use[i] && ((a.probe_mask >> (i < N1 ? 0 : 1)) & 1u);
-    k[i] = ph_hash(t, x[i], y[i], z[i], m[i]);
-    const uint32_t di = t.disp_off + (on[i] ? k[i].grp : 0u);
-    d[i] = IN_LDS ? (uint32_t)((lds_u16 *)D)[di] : (uint32_t)D[di];
-  }
+  const usn_ph_table &t = a.ph[tb];
+  on = use && ((a.probe_mask >> tb) & 1u);
+  k = ph_hash(t, x, y, z, m);
+  const uint32_t di = t.disp_off + (on ? k.grp : 0u);
+  d = IN_LDS ? (uint32_t)((lds_u16 *)D)[di] : (uint32_t)D[di];
+}
+
+/* The slot reads of N keys whose displacements were read (ph_disp_issue;
+ * keys [0, N1) in K1, the rest in K2), then the hits. */
+template <bool IN_LDS, int N, int N1>
+__device__ __forceinline__ void ph_slots_hit(const uint4 *T, const ClassifyArgs &a,
+                                             const uint32_t (&x)[N], const uint32_t (&y)[N],
+                                             const uint32_t (&z)[N], const uint32_t (&m)[N],
+                                             const PhKeyH (&k)[N], const uint32_t (&d)[N],
+                                             const bool (&on)[N], uint32_t (&w)[N]) {
+  typedef __attribute__((address_space(3))) const v4u32 lds_v4;
   uint4 sl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -429,6 +435,25 @@ __device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) w[i] = on[i] ? ph_hit(sl[i], x[i], y[i], z[i], m[i]) : 0u;
+}
+
+/* N probes issued together: all N displacement reads, then all N slot
+ * reads -- two round trips for the lot instead of two per key.  Keys
+ * [0, N1) go to table K1, the rest to K2; use[i] false (or an empty table)
+ * gives w[i] = 0 with a harmless read of the table's first entries.  IN_LDS:
+ * the image is the LDS copy. */
+template <bool IN_LDS, int N, int N1>
+__device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs &a,
+                                              const uint32_t (&x)[N], const uint32_t (&y)[N],
+                                              const uint32_t (&z)[N], const uint32_t (&m)[N],
+                                              const bool (&use)[N], uint32_t (&w)[N]) {
+  PhKeyH k[N];
+  uint32_t d[N];
+  bool on[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    ph_disp_issue<IN_LDS>(T, a, i < N1 ? 0 : 1, x[i], y[i], z[i], m[i], use[i], k[i], d[i], on[i]);
+  ph_slots_hit<IN_LDS, N, N1>(T, a, x, y, z, m, k, d, on, w);
 }
 
 /* find_forward for a NIC source (incoming == true), cache handled outside:
@@ -1108,7 +1133,8 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 }
 
 /* The 1024-frame tiles of a launch (several batches = drained rx rings may
- * share one launch), one workgroup each.  USN_PERSIST=1 (A/B only): the grid
+ * share one launch), one workgroup each.  USN_PERSIST=k > 1 (A/B only): k
+ * tiles per workgroup, strided by the grid.  USN_PERSIST=1 (A/B only): the grid
  * is what the chip holds at once and each workgroup loops over tiles
  * blockIdx.x, + gridDim.x, ..., copying the rule image (or its displacements)
  * to LDS once instead of once per tile -- slower: c5 8M 185.5 vs 170.5 us, c4
@@ -1117,8 +1143,16 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 #ifndef USN_PERSIST
 #define USN_PERSIST 0
 #endif
+#ifndef USN_PERSIST_CAP
+#define USN_PERSIST_CAP 1
+#endif
+#if USN_PERSIST && USN_PERSIST_CAP   /* the loop must not cost occupancy: 8 waves per SIMD (<= 64 VGPRs) */
+#define USN_RX_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#else
+#define USN_RX_ATTR
+#endif
 template <int TM, bool GLDS>
-__global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
+__global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
   constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
@@ -1149,10 +1183,20 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     else Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)u0 * 8;
   }
   // (the first tile's barrier also waits for the image copy)
+  // (one pass when USN_PERSIST is 0: no loop for hipcc to keep values live
+  // across, 46 VGPRs instead of 115 at 512 threads)
   const uint32_t ntiles_launch = m.tile_base[m.count];
-  const uint32_t wstep = USN_PERSIST ? gridDim.x : ntiles_launch;
-  for (uint32_t w = blockIdx.x; w < ntiles_launch; w += wstep) {
-    if (w != blockIdx.x) __syncthreads();   // the previous tile is done with the stage and s_misc
+  for (uint32_t w = blockIdx.x;; w += gridDim.x) {
+    if (USN_PERSIST && w != blockIdx.x) __syncthreads();   // the previous tile is done with the stage and s_misc
+#if USN_PERSIST
+    // per-lane values recomputed for every tile (kept live across the loop
+    // they cost VGPRs: the lane, its stage and LDS addresses)
+    uint32_t tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const uint32_t lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);
+#endif
     const uint32_t bi = batch_of(m, w);
     const ClassifyArgs &a = m.b[bi];
     const uint32_t tile = w - m.tile_base[bi];
@@ -1511,6 +1555,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     }
     STAMP(11);
     STAMP_FLUSH_AT(w);
+    if (!USN_PERSIST || w + gridDim.x >= ntiles_launch) break;
   }
 }
 
@@ -1588,6 +1633,21 @@ __device__ __forceinline__ bool bridge_has(const unsigned long long *set, uint32
   uint32_t h = usn_mac_hash(mac) & mask;
   for (uint32_t it = 0; it <= mask; ++it) {
     const unsigned long long v = set[h];
+    if (!(v >> 63)) return false;
+    if ((v & 0xFFFFFFFFFFFFull) == mac) return true;
+    h = (h + 1) & mask;
+  }
+  return false;
+}
+
+/* the same on the LDS copy, read as LDS (a generic pointer's flat loads
+ * would also wait for every global load in flight) */
+__device__ __forceinline__ bool bridge_has_lds(const unsigned long long *set, uint32_t mask, uint64_t mac) {
+  typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
+  const lds_u64 *S = (const lds_u64 *)set;
+  uint32_t h = usn_mac_hash(mac) & mask;
+  for (uint32_t it = 0; it <= mask; ++it) {
+    const unsigned long long v = S[h];
     if (!(v >> 63)) return false;
     if ((v & 0xFFFFFFFFFFFFull) == mac) return true;
     h = (h + 1) & mask;
@@ -1715,6 +1775,21 @@ __device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t
 }
 
 #define TX_BRIDGE_LDS_SLOTS 2048u   /* bridge sets up to 16 KiB are staged in LDS */
+#define TX_LISTEN_LDS 64u           /* listening triples of the source staged in LDS */
+
+/* (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport; L:
+ * the source's {ip, proto | has_ports << 8 | port << 16} pairs (global or LDS) */
+template <typename P>
+__device__ __forceinline__ bool tx_listening(P L, uint32_t n, const Parsed &p) {
+  bool listening = false;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t ld = L[2 * k], lw = L[2 * k + 1];
+    const uint32_t lhas = (lw >> 8) & 1u;
+    listening |= ld == p.src && (lw & 0xFFu) == p.proto && lhas == p.has_ports &&
+                 (!lhas || (lw >> 16) == p.sport);
+  }
+  return listening;
+}
 
 /* Decision of a non-hit, non-host, cache-retaining tx frame i (IPv4, not
  * loopback): endpoint.rs:254-295 against the snapshot plus everything learned
@@ -1943,8 +2018,12 @@ __host__ __device__ inline size_t tx_lds_head(uint32_t nbins) {
   return lds_core_bytes(nbins) + (size_t)TILE * 16 + (size_t)TILE * 4;
 }
 
+#ifndef USN_TX_PIPE   /* phase 1: probes of a round issued as it is parsed; LDS-only barrier */
+#define USN_TX_PIPE 1
+#endif
 template <bool LDS>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void tx_kernel(TxArgs t) {
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(NTHREADS / 64)))
+void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames all resident)
   extern __shared__ __align__(16) uint8_t smem[];
   const ClassifyArgs &a = t.a;
   const Lds L = carve(smem, a.nbins);
@@ -1953,14 +2032,15 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
   uint4 *stab = reinterpret_cast<uint4 *>(sdec + TILE);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   __shared__ uint32_t s_last, s_lastnh, s_ins, s_ovf, s_insall, s_hidx, s_before, s_head;
-  __shared__ uint32_t s_early, s_early_all, s_slow;
+  __shared__ uint32_t s_early, s_early_all, s_slow, s_dlearn;
   __shared__ uint32_t s_cin[6];   // the carried-in cache {state, dst, info[4]} (tile 0's)
   __shared__ uint4 s_brec;
   __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
+  __shared__ uint32_t s_listen[2 * TX_LISTEN_LDS];
   if (tid == 0) {
     s_last = 0; s_lastnh = 0; s_ins = 0; s_ovf = 0; s_insall = 0; s_hidx = 0; s_before = 0;
-    s_early = 0; s_early_all = 0; s_slow = 0;
+    s_early = 0; s_early_all = 0; s_slow = 0; s_dlearn = 0;
   }
   if (tid < 8) s_misc[tid] = 0;
   for (uint32_t k = tid; k < NSEG * cnt_rows(a.nbins); k += NTHREADS) L.cnt[k] = 0;
@@ -1991,30 +2071,71 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
       S->flags = 0; S->first_break = 0xFFFFFFFFu;
     }
   }
+  /* the bridge snapshot set goes to LDS when small; its loads go out first
+     (USN_TX_PIPE), so that its LDS copy and the barrier after it wait for
+     them and not for the header loads */
+  const unsigned long long *BS = t.bridge_set;
+  const bool bridge_lds = t.bridge_mask < TX_BRIDGE_LDS_SLOTS;
+  unsigned long long *bs = reinterpret_cast<unsigned long long *>(stab + (LDS ? table_lds_units(a.table_units) : 0));
+  constexpr uint32_t BRIDGE_PER_THREAD = TX_BRIDGE_LDS_SLOTS / NTHREADS;
+  unsigned long long bv[USN_TX_PIPE ? BRIDGE_PER_THREAD : 1];
+  if (USN_TX_PIPE && bridge_lds) {
+#pragma unroll
+    for (uint32_t j = 0; j < BRIDGE_PER_THREAD; ++j) {
+      const uint32_t k = tid + j * NTHREADS;
+      bv[j] = k <= t.bridge_mask ? t.bridge_set[k] : 0ull;
+    }
+  }
+  // the source's listening triples (read by every frame): to LDS with the bridge
+  const bool listen_lds = t.n_listen <= TX_LISTEN_LDS;
+  const uint32_t lv = listen_lds && tid < 2 * t.n_listen ? t.listen[tid] : 0u;
   /* all header loads of the tile first (48 B x 4 frames per lane in flight:
      the MACs and up to byte 39 for parse; tools/stride_floor.hip, 4M frames
-     at a 64-byte stride: 61.6 us reading 48 B per frame, 73.3 us reading 64) */
+     at a 64-byte stride: 61.6 us reading 48 B per frame, 73.3 us reading 64).
+     Every round's frame address first: an offsets[] read feeding a round's
+     loads made hipcc wait for all earlier loads before each round's. */
   uint4 qq[ROUNDS][4];
   uint32_t ll[ROUNDS];
   const uint8_t *fps[ROUNDS];
+#pragma unroll   // lengths before the headers: round 0's parse then waits for round 0 only
+  for (uint32_t r = 0; r < ROUNDS; ++r) ll[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
+  if (a.offsets) {
+    uint64_t off[ROUNDS];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) off[r] = a.offsets[base + min(r * NTHREADS + tid, nt - 1)];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) fps[r] = a.frames + off[r];
+  } else {
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) fps[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
+  }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const uint64_t i = base + (local < nt ? local : 0);
-    fps[r] = a.offsets ? a.frames + a.offsets[i] : a.frames + i * a.stride;
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
     qq[r][3] = make_uint4(0, 0, 0, 0);
-    ll[r] = a.lens[i];
   }
-  /* the bridge snapshot set in LDS when small */
-  const unsigned long long *BS = t.bridge_set;
-  if (t.bridge_mask < TX_BRIDGE_LDS_SLOTS) {
-    unsigned long long *bs = reinterpret_cast<unsigned long long *>(stab + (LDS ? table_lds_units(a.table_units) : 0));
-    for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
+  if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
+  if (bridge_lds) {
+    if (USN_TX_PIPE) {
+#pragma unroll
+      for (uint32_t j = 0; j < BRIDGE_PER_THREAD; ++j) {
+        const uint32_t k = tid + j * NTHREADS;
+        if (k <= t.bridge_mask) bs[k] = bv[j];
+      }
+    } else {
+      for (uint32_t k = tid; k <= t.bridge_mask; k += NTHREADS) bs[k] = t.bridge_set[k];
+    }
     BS = bs;
   }
-  __syncthreads();
+  if (USN_TX_PIPE) {
+    // LDS only: the header loads stay in flight; each round below waits for its own
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  } else {
+    __syncthreads();
+  }
   STAMP(1);
   // parse and flag every round; the answer-key probes of all rounds are then
   // issued together (two round trips for the tile's four rounds)
@@ -2026,6 +2147,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
   constexpr int R3 = 3 * ROUNDS;
   bool need[R3];
   uint32_t ax[R3], ay[R3], az[R3], am[R3];
+  PhKeyH pk[R3];      // USN_TX_PIPE: each round's displacement reads go out when it is parsed
+  uint32_t pd[R3];
+  bool pon[R3];
 #pragma unroll
   for (int k = 0; k < R3; ++k) { need[k] = false; ax[k] = 0; ay[k] = 0; az[k] = 0; am[k] = 0; }
 #pragma unroll
@@ -2050,8 +2174,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t py = __shfl_up(r0.y, 1, 64), pz = __shfl_up(r0.z, 1, 64), pw = __shfl_up(r0.w, 1, 64);
     const bool repeat = lane > 0 && touch == 1u && pi0 == i0 && py == r0.y && pz == r0.z && pw == r0.w;
     if (touch == 1u || touch == 2u) {
-      const bool s_in = bridge_has(BS, t.bridge_mask, smac);
-      const bool d_in = bridge_has(BS, t.bridge_mask, dmac);
+      const bool s_in = bridge_lds ? bridge_has_lds(BS, t.bridge_mask, smac)
+                                   : bridge_has(BS, t.bridge_mask, smac);
+      const bool d_in = bridge_lds ? bridge_has_lds(BS, t.bridge_mask, dmac)
+                                   : bridge_has(BS, t.bridge_mask, dmac);
       if (s_in) f |= TXR_SMAC_IN;
       if (d_in) f |= TXR_DMAC_IN;
       if (!(smac & 1u) && !s_in) f |= TXR_LEARNMAC;           // is_unicast && not contained
@@ -2060,13 +2186,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     if (p.status == 5u) f |= TXR_WINDOW;                      // ports past the window
     if (touch == 1u) {
       // (W.dst, proto, W.dport) in S.listening?  W.dst = src, W.dport = sport
-      bool listening = false;
-      for (uint32_t k = 0; k < t.n_listen; ++k) {
-        const uint32_t ld = t.listen[2 * k], lw = t.listen[2 * k + 1];
-        const uint32_t lhas = (lw >> 8) & 1u;
-        listening |= ld == p.src && (lw & 0xFFu) == p.proto && lhas == p.has_ports &&
-                     (!lhas || (lw >> 16) == p.sport);
-      }
+      typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+      const bool listening = listen_lds ? tx_listening((const lds_u32 *)s_listen, t.n_listen, p)
+                                        : tx_listening(t.listen, t.n_listen, p);
       const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
                             p.dport == 67u && (p.dst & 0xFFu) == 255u;
       if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
@@ -2087,12 +2209,20 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
       key1_of(r0, ax[ROUNDS + r], ay[ROUNDS + r], az[ROUNDS + r], am[ROUNDS + r]);
       key2_of(r0, ax[2 * ROUNDS + r], ay[2 * ROUNDS + r], az[2 * ROUNDS + r], am[2 * ROUNDS + r]);
     }
+    if (USN_TX_PIPE) {   // under the later rounds' header loads
+#pragma unroll
+      for (uint32_t j = 0; j < 3; ++j) {
+        const uint32_t i = j * ROUNDS + r;
+        ph_disp_issue<LDS>(T, a, j < 2 ? 0 : 1, ax[i], ay[i], az[i], am[i], need[i], pk[i], pd[i], pon[i]);
+      }
+    }
   }
   uint32_t w1e[ROUNDS], w2e[ROUNDS];   // key1 / key2 results, valid where need[R + r]
   bool pre[ROUNDS];
   {
     uint32_t w[R3];
-    ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
+    if (USN_TX_PIPE) ph_slots_hit<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, pk, pd, pon, w);
+    else ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) {
       if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
@@ -2123,57 +2253,26 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     g_put4(aux + TXG_LREC, t.epoch, lt ? srec[lt - 1] : make_uint4(0, 0, 0, 0));
     g_put(aux + TXG_LAST, t.epoch, lt);
     g_put(aux + TXG_EARLY, t.epoch, s_early);
-    // the last touching frame before the tile (a tile without one is skipped)
-    uint32_t before = 0;
-    uint4 brec = make_uint4(0, 0, 0, 0);
-    for (int u = (int)tile - 1; u >= 0; --u) {
-      uint32_t v[5];   // LAST, LREC
-      if (!g_getn<5>(t.aux + (size_t)u * TXA_GRANULES + TXG_LAST, t, v)) break;
-      const uint32_t lu = min(v[0], (uint32_t)TILE);
-      if (lu) {
-        before = (uint32_t)u * TILE + lu;
-        brec = make_uint4(v[1], v[2], v[3], v[4]);
-        break;
-      }
-    }
-    s_before = before;
-    s_brec = brec;
-    if (tile > 0 && before == 0) tx_load_cin(t, s_cin);   // the first touching frame's cache
   }
-  __syncthreads();
   STAMP(3);
   // ---- cache hits (endpoint.rs:186-191); what a frame really learns is
-  //      claimed in the epoch-tagged sets with its index (first occurrence wins)
-  const uint32_t before = s_before;
-  const uint4 brec = s_brec;
+  //      claimed in the epoch-tagged sets with its index (first occurrence wins).
+  //      Only the tile's first touching frame compares with a frame before the
+  //      tile: it is done after the others, once the tiles before have
+  //      published (the walk back), and HEAD / INS go out before that walk
+  //      whenever that frame cannot change them (a later frame is a non-hit,
+  //      and it has nothing to claim): the tiles after then do not wait on the
+  //      tiles before this one through it.
   uint32_t last_nh = 0, ins = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
+  int deferred = -1;   // the round of this lane's first touching frame (touch 1, prev 0)
+  auto hit_claim = [&](uint32_t r, bool hit) {
     const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) continue;
     const uint64_t i = base + local;
     uint32_t fl = rec[r].x;
-    const uint32_t touch = tx_touch(rec[r]);
-    if (!touch) continue;
-    bool hit = false;
-    if (touch == 1u) {
-      const uint32_t k1 = prev[r] ? (uint32_t)(base + prev[r]) : before;   // 1 + index, 0 = none
-      const uint32_t info0 = fl & TXR_I0_MASK;
-      if (k1) {
-        const uint4 pr = prev[r] ? srec[prev[r] - 1] : brec;
-        const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == rec[r].y &&
-                          pr.z == rec[r].z && pr.w == rec[r].w;
-        if (same && (pr.x & TXR_HOST)) fl |= TXR_HOST;       // its cache effect is the host's
-        else hit = same;
-      } else {
-        hit = (s_cin[0] & USN_CS_VALID) && s_cin[2] == info0 && s_cin[3] == rec[r].y &&
-              s_cin[4] == rec[r].z && s_cin[5] == rec[r].w;
-      }
-    }
     if (hit) fl |= TXR_HIT;
     rec[r].x = fl;
     if (!hit) last_nh = local + 1;
-    if (hit || (fl & TXR_HOST)) continue;
+    if (hit || (fl & TXR_HOST)) return;
     if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
       if (fl & TXR_LEARNMAC) {
         const uint64_t m = rec_smac(frame_head(a, i));
@@ -2196,15 +2295,84 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
         ins |= 2u;
       }
     }
+  };
+  // (a frame equal to a host-decided one takes the host's cache effect)
+  auto same_as = [&](uint32_t r, const uint4 &pr, bool &hit) {
+    const uint32_t info0 = rec[r].x & TXR_I0_MASK;
+    const bool same = tx_touch(pr) == 1u && (pr.x & TXR_I0_MASK) == info0 && pr.y == rec[r].y &&
+                      pr.z == rec[r].z && pr.w == rec[r].w;
+    if (same && (pr.x & TXR_HOST)) rec[r].x |= TXR_HOST;
+    else hit = same;
+  };
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint32_t touch = tx_touch(rec[r]);
+    if (!touch) continue;
+    bool hit = false;
+    if (touch == 1u) {
+      if (!prev[r]) { deferred = (int)r; continue; }
+      same_as(r, srec[prev[r] - 1], hit);
+    }
+    hit_claim(r, hit);
   }
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r)
+    if ((int)r == deferred && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE))) atomicOr(&s_dlearn, 1u);
   if (last_nh) atomicMax(&s_lastnh, last_nh);
   if (ins) atomicOr(&s_ins, ins);
   vm_drain();                  // this wave's claims (atomics, sc1 stores) have landed
   __syncthreads();             // (and every frame has read srec)
+  // HEAD and INS now unless the first touching frame can change them
+  const bool early_pub = s_lastnh != 0 && s_dlearn == 0;
+  if (tid == 0) {
+    if (early_pub) {   // INS last: its arrival also says the claims above have landed (R1)
+      g_put(aux + TXG_HEAD, t.epoch, s_lastnh);
+      g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
+    }
+    // the last touching frame before the tile (a tile without one is skipped)
+    uint32_t before = 0;
+    uint4 brec = make_uint4(0, 0, 0, 0);
+    for (int u = (int)tile - 1; u >= 0; --u) {
+      uint32_t v[5];   // LAST, LREC
+      if (!g_getn<5>(t.aux + (size_t)u * TXA_GRANULES + TXG_LAST, t, v)) break;
+      const uint32_t lu = min(v[0], (uint32_t)TILE);
+      if (lu) {
+        before = (uint32_t)u * TILE + lu;
+        brec = make_uint4(v[1], v[2], v[3], v[4]);
+        break;
+      }
+    }
+    s_before = before;
+    s_brec = brec;
+    if (tile > 0 && before == 0) tx_load_cin(t, s_cin);   // the first touching frame's cache
+  }
+  __syncthreads();
+  if (deferred >= 0) {   // the tile's first touching frame
+    last_nh = 0;
+    ins = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      if ((int)r != deferred) continue;
+      bool hit = false;
+      if (s_before) {
+        same_as(r, s_brec, hit);
+      } else {
+        const uint32_t info0 = rec[r].x & TXR_I0_MASK;
+        hit = (s_cin[0] & USN_CS_VALID) && s_cin[2] == info0 && s_cin[3] == rec[r].y &&
+              s_cin[4] == rec[r].z && s_cin[5] == rec[r].w;
+      }
+      hit_claim(r, hit);
+    }
+    if (last_nh) atomicMax(&s_lastnh, last_nh);
+    if (ins) atomicOr(&s_ins, ins);
+    vm_drain();
+  }
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) srec[r * NTHREADS + tid] = rec[r];   // flags after the hit pass
   __syncthreads();
-  if (tid == 0) {   // INS last: its arrival also says the claims above have landed (R1)
+  if (tid == 0 && !early_pub) {   // INS last: its arrival also says the claims above have landed (R1)
     g_put(aux + TXG_HEAD, t.epoch, s_lastnh);
     g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
   }
@@ -2550,9 +2718,11 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
 #define USN_LAUNCH(T_, G_)                                                              \
   do {                                                                                  \
     uint32_t grid = tiles;                                                              \
-    if (USN_PERSIST) {                                                                  \
+    if (USN_PERSIST == 1) {                                                             \
       const uint32_t res = resident_grid(classify_rx_kernel<T_, G_>, lds);              \
       if (res) grid = min(grid, res);                                                   \
+    } else if (USN_PERSIST > 1) {                                                       \
+      grid = (tiles + USN_PERSIST - 1) / USN_PERSIST;                                   \
     }                                                                                   \
     hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(grid), b, lds, stream, m);    \
   } while (0)

@@ -306,6 +306,8 @@ struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
   uint32_t sel = 0;      // selected replica (usn_replica_select)
   int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
+  int tx512 = 1;   // USN_TX_T512 env (A/B): the tx kernel at 512 threads per tile (c4tx 1M:
+                   // 51.2 vs 53.2 us at 256; two rounds per lane, 64 VGPRs, 4 workgroups per CU)
   double ph_load = USN_PH_LOAD;   // perfect-hash image geometry (env knobs)
   uint32_t ph_group = USN_PH_GROUP;
   std::mutex mu;
@@ -910,6 +912,7 @@ int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
   c->reps.swap(reps);
   c->device = hip_devices[0];
   if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
+  if (const char *e = std::getenv("USN_TX_T512")) c->tx512 = std::atoi(e) ? 1 : 0;
   c->ph_load = ph_load_knob();
   c->ph_group = ph_group_knob();
   *out = c;
@@ -1443,7 +1446,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
-    HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
+    if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
+    else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
     c->tx.pending = true;
     c->tx.src = tb.src_endpoint;
     c->tx.replica = rep;

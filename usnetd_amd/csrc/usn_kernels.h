@@ -122,6 +122,7 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
+hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }
 
