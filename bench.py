@@ -68,7 +68,7 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the c2 line at N=1")
     ap.add_argument("--launch-probe", type=int, default=150, help="per-launch event pairs")
-    ap.add_argument("--ramp", type=int, default=40,
+    ap.add_argument("--ramp", type=int, default=200,
                     help="untimed poll rounds between the probe and the timed steps (clock ramp)")
     return ap.parse_args()
 
@@ -232,12 +232,14 @@ def measure(run, args, dist, world):
     from usnetd_amd import shard
     for i in range(args.warmup):
         run.step(i)
-    # The GPU reaches its steady rate only after ~40 poll rounds on both
+    # The GPU reaches its steady rate only after many poll rounds on both
     # streams: untimed ramp rounds, the per-launch probe, ramp rounds again
     # (config.untimed_ramp_steps counts both), then the timed steps.  With the probe after the timed
     # steps and no ramp, K = 20 read 53.2 Gpkt/s against 58.1 at 100 steps
     # (tools/steptime.py: 0.301 -> 0.292 -> 0.280 ms per step over the first
-    # three runs of 20 steps).
+    # three runs of 20 steps); K = 20 after 2 x 40 / 100 / 200 ramp rounds:
+    # 58.7-58.8 / 59.1-60.0 / 59.6-59.8 Gpkt/s against 60.5 at 400 steps
+    # (profiles/r02aq; 200 rounds cost ~0.1 s).
     for i in range(args.ramp):
         run.step(args.warmup + i)
     kern_ms, probe_frames = run.launch_probe(args.launch_probe) if args.launch_probe else (None, 0)
