@@ -341,12 +341,24 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
 }
 
+#ifndef USN_SLOT_POLK   /* A/B only: cache-policy bits of the slot reads: 1 sc0, 2 nt, 3 sc1 */
+#define USN_SLOT_POLK 0
+#endif
+#if USN_SLOT_POLK == 1
+#define USN_SLOT_POL " sc0"
+#elif USN_SLOT_POLK == 2
+#define USN_SLOT_POL " nt"
+#elif USN_SLOT_POLK == 3
+#define USN_SLOT_POL " sc1"
+#else
+#define USN_SLOT_POL ""
+#endif
 /* one slot read of table t; a lane that does not need it reads the table's
  * first slot, which every such lane of the wave shares: one L2 request */
 __device__ __forceinline__ void asm_slot1(const uint4 *T, const usn_ph_table &t, bool need,
                                           const PhKeyH &k, uint32_t d, v4u32 &s) {
   const uint4 *p = T + t.slot_off + (need ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(s) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off" USN_SLOT_POL : "=&v"(s) : "v"(p) : "memory");
 }
 
 /* TM_DISPLDS: both displacements from the LDS copy (indexed like the image) */
