@@ -106,6 +106,9 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
 #ifndef USN_ABL_NOPROBE   /* A/B only: no rule-table probes (wrong results) */
 #define USN_ABL_NOPROBE 0
 #endif
+#ifndef USN_ABL_NODISPCOPY   /* A/B only: one 1 KiB chunk of the image copied to LDS (wrong results) */
+#define USN_ABL_NODISPCOPY 0
+#endif
 #ifndef USN_ABL_LOADONLY   /* A/B only: loads and stores, no parse/probe/decide */
 #define USN_ABL_LOADONLY 0
 #endif
@@ -1186,7 +1189,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   const uint16_t *Dl = nullptr;
   if (TM != TM_GLOBAL) {   // image (or its displacements) -> LDS by glds, 64 units per instruction
     const uint32_t u0 = TM == TM_LDS ? 0u : m.b[0].disp_unit;
-    const uint32_t units = m.b[0].table_units - u0;
+    const uint32_t units = USN_ABL_NODISPCOPY ? min(64u, m.b[0].table_units - u0) : m.b[0].table_units - u0;
     for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
       const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
