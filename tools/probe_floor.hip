@@ -8,6 +8,8 @@
 //   3  stream + one probe per frame (no dependent second read)
 //   10+c probes only, inline-asm loads with cache policy c (0 none, 1 sc0,
 //        2 nt, 3 sc1, 4 sc0 sc1, 5 dword instead of dwordx4)
+//   glds stream (the classify kernel's LDS-DMA header stage), alone and with
+//        the probes keyed by the staged bytes
 // If mode 1 alone takes about as long as the gap between mode 2 and mode 0,
 // the probes are bound by their own request rate, not by latency.
 //
@@ -59,6 +61,67 @@ __global__ __launch_bounds__(256) void probe(const v4u *frames, const v4u *t1, c
     w ^= s2.x ^ s2.z;
   }
   out[i] = w;
+}
+
+/* The classify kernel's header stream: each wave moves its 64 frames' first
+ * 48 bytes into LDS by three 1 KiB LDS-DMA instructions (lane u of
+ * instruction k: part (64k+u) % 3 of frame (64k+u) / 3), then each lane reads
+ * its frame from LDS.  PROBES: then the two-table probe of mode 2 keyed by
+ * the frame's bytes. */
+typedef __attribute__((address_space(3))) void lds_void_t;
+template <bool PROBES>
+__global__ __launch_bounds__(256) void glds_stream(const uint8_t *frames, const v4u *t1, const v4u *t2,
+                                                   uint32_t m1, uint32_t m2, uint32_t n, uint32_t *out) {
+  __shared__ v4u st[4][192];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t f0 = blockIdx.x * 256 + wave * 64;
+  if (f0 >= n) return;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {
+    const uint32_t u = 64 * k + lane, f = u / 3, part = u - 3 * f;
+    __builtin_amdgcn_global_load_lds(frames + (size_t)(f0 + f) * 64 + part * 16,
+                                     (lds_void_t *)(&st[wave][64 * k]), 16, 0, 2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const v4u a = st[wave][3 * lane], b = st[wave][3 * lane + 1], c = st[wave][3 * lane + 2];
+  uint32_t x = a.x ^ a.w ^ b.y ^ b.z ^ c.x ^ c.y;
+  if (PROBES) {
+    const uint32_t key = mix(x ^ ((f0 + lane) * 0x9e3779b9u));
+    const v4u s1 = t1[mix(key) % m1];
+    x = s1.x ^ s1.w;
+    if ((s1.y % 100u) < 55u) {
+      const v4u s2 = t2[mix(key ^ 0x5bd1e995u) % m2];
+      x ^= s2.x ^ s2.z;
+    }
+  }
+  out[f0 + lane] = x;
+}
+
+template <bool PROBES>
+static void run_glds(const uint8_t *f, const v4u *t1, const v4u *t2, uint32_t m, uint32_t n, uint32_t *out,
+                     int launches) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const dim3 g((n + 255) / 256), b(256);
+  for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(glds_stream<PROBES>, g, b, 0, 0, f, t1, t2, m, m, n, out);
+  CK(hipDeviceSynchronize());
+  std::vector<float> ms;
+  for (int k = 0; k < launches; ++k) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(glds_stream<PROBES>, g, b, 0, 0, f, t1, t2, m, m, n, out);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float t;
+    CK(hipEventElapsedTime(&t, e0, e1));
+    ms.push_back(t);
+  }
+  std::sort(ms.begin(), ms.end());
+  const double us = ms[ms.size() / 2] * 1e3;
+  printf("{\"mode\": \"glds stream%s\", \"frames\": %u, \"table_slots\": %u, \"us_median\": %.2f}\n",
+         PROBES ? "+probes" : "", n, m, us);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
 }
 
 template <int C>
@@ -228,6 +291,8 @@ int main(int argc, char **argv) {
     run_pol<4>(t1, t2, m, n, out, launches);
     run_pol<5>(t1, t2, m, n, out, launches);
   }
+  run_glds<false>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
+  run_glds<true>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
   run_batched<1>(t1, t2, m, n, out, launches);
   run_batched<2>(t1, t2, m, n, out, launches);
   run_batched<4>(t1, t2, m, n, out, launches);
