@@ -76,13 +76,14 @@ def rand_want(rng):
     return w
 
 
-def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True):
-    """Returns a fixture-shaped dict {endpoints, bridge, steps} without expectations."""
+def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, n_rules=None):
+    """Returns a fixture-shaped dict {endpoints, bridge, steps} without expectations.
+    n_rules: how many initial rules (default 3..11)."""
     rng = random.Random(seed)
     endpoints = [[0, 0, -1], [1, 1, 0], [2, 2, 0], [3, 2, 0], [4, 3, 0], [5, 0, -1], [6, 2, 5]]
     live = {1, 2, 3, 4, 6}
     steps = []
-    for _ in range(rng.randrange(3, 12)):
+    for _ in range(n_rules if n_rules is not None else rng.randrange(3, 12)):
         owner = rng.choice(sorted(live))
         steps.append({"op": "add_match", "want": rand_want(rng), "owner": owner, "sticky": False})
     idents = [1, 2, 3]

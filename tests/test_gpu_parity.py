@@ -5,6 +5,8 @@ per-tile order must be the stable sort of the decisions by endpoint bin and
 its expansion must equal the oracle's per-endpoint ordered frame lists.
 PARITY UNPINNED beyond the hand-derived fixtures (see DESIGN.md "Oracle").
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -45,6 +47,43 @@ def test_random_streams_gpu(seed, tx_frac, coracle_mod):
     stream = randtraffic.make_stream(100 + seed, n_events=700, tx_frac=tx_frac)
     want = randtraffic.run_stream(stream, katrun.COracleBackend())
     got = randtraffic.run_stream(stream, _gpu())
+    assert len(want) == len(got)
+    for i, (x, y) in enumerate(zip(want, got)):
+        if isinstance(x, tuple):
+            assert x == y, (i, x, y)
+        else:
+            assert (x & katrun.PARITY_MASK) == (y & katrun.PARITY_MASK), (i, hex(x), hex(y))
+
+
+def _filler(n):
+    """n rules no frame of randtraffic hits (dst 10.77.0.0/16): they push the
+    image past LDS, so the rx kernel takes the projection table U."""
+    out = []
+    for i in range(n):
+        conn = i % 2 == 0
+        out.append({"op": "add_match", "owner": 2, "sticky": False,
+                    "want": {"dst": "10.77.%d.%d" % (i >> 8, i & 255), "proto": 17, "dport": 1000 + i % 7,
+                             "src": "10.1.1.1" if conn else None, "sport": 5000 + i % 13 if conn else None}})
+    return out
+
+
+@pytest.mark.parametrize("tx_frac", [0.0, 0.5])
+@pytest.mark.parametrize("seed", range(6))
+def test_random_streams_projection_gpu(seed, tx_frac, coracle_mod):
+    """Random streams over a table too large for LDS: 3000 filler rules plus
+    40 random ones of every Want shape from small pools (several K1 rules per
+    projection: the overflow table X).  The rx kernel reads U (+ X) with
+    displacements in LDS; bit-exact against the oracle.  (NIC-owned rules:
+    tests/test_table_image.py, through usn_table_build.)"""
+    stream = randtraffic.make_stream(300 + seed, n_events=900, tx_frac=tx_frac, n_rules=40)
+    stream["steps"] = _filler(3000) + stream["steps"]
+    want = randtraffic.run_stream(stream, katrun.COracleBackend())
+    gb = _gpu()
+    got = randtraffic.run_stream(stream, gb)
+    info = (ctypes.c_uint32 * 8)()
+    gb.ctx.L.usn_debug_image_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert gb.ctx.L.usn_debug_image_info(gb.ctx.h, info) == 0
+    assert info[5] & 4 and info[4] * 16 > 40000   # U built; the image is past LDS
     assert len(want) == len(got)
     for i, (x, y) in enumerate(zip(want, got)):
         if isinstance(x, tuple):

@@ -40,9 +40,15 @@ def _packed(w):
 
 
 def _info(L, h):
-    out = (C.c_uint32 * 6)()
+    out = (C.c_uint32 * 8)()
     assert L.usn_debug_image_info(h, out) == 0
-    return list(out)
+    return list(out)[:6]
+
+
+def _uinfo(L, h):
+    out = (C.c_uint32 * 8)()
+    assert L.usn_debug_image_info(h, out) == 0
+    return list(out)[6:]
 
 
 def test_image_finds_every_rule_c5():
@@ -56,9 +62,11 @@ def test_image_finds_every_rule_c5():
         assert L.usn_add_match(h, C.byref(want), owner, int(sticky)) == 1
         ws.append((want, owner))
     m0, g0, m1, g1, units, pmask = _info(L, h)
-    assert pmask == 3
+    assert pmask == 7                             # K1, K2, and U built
     assert m0 >= 32768 and m1 >= 32768 and m0 < 32768 / 0.6 and m1 < 32768 / 0.6
-    assert units * 16 < 1.7 * 2 ** 20            # the c5 image is L2-resident (4 MiB per XCD)
+    mu, mx = _uinfo(L, h)
+    assert (mu + mx) * 16 < 1.7 * 2 ** 20        # what rx reads is L2-resident (4 MiB per XCD)
+    assert mu >= 32768 + 30000 and mx < 4000     # c5: ~5 % of connected rules share a projection
     for want, owner in ws:
         t, x, y, z, meta = _packed(want)
         got = L.usn_debug_image_probe(h, t, x, y, z, meta)
@@ -156,4 +164,74 @@ def test_image_bulk_sizes(n):
         assert got, i
         # duplicates keep the first owner (HashMap::entry().or_insert)
         assert (got >> 16) in range(1, 9)
+    L.usn_ctx_destroy(h)
+
+
+def _rx_probe(L, h, dst, src, proto, has, dport, sport):
+    out = (C.c_uint32 * 4)()
+    r = L.usn_debug_image_probe_rx(h, dst, src, proto, has, dport, sport, out)
+    return r, list(out)
+
+
+HAS_PORTS = (6, 17, 33, 132, 136)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_projection_image_equals_k1_k2(seed):
+    """The projection table U (+ its overflow X) that the rx kernel reads
+    answers get_endpoint's two lookups (endpoint.rs:317-327) exactly as the
+    K1 / K2 tables do: every key1 / key2 of small address, port and protocol
+    pools, against rules of every Want shape (several K1 rules per projection,
+    K1 without K2 and the reverse, NIC-owned rules, shapes no frame matches)."""
+    import random
+    rng = random.Random(seed)
+    L, h = _ctx()
+    L.usn_debug_image_probe_rx.argtypes = [C.c_void_p] + [C.c_uint32] * 6 + [C.c_void_p]
+    L.usn_debug_image_probe_rx.restype = C.c_int
+    assert L.usn_endpoint_add(h, 0, 0, -1) == 0      # NIC
+    assert L.usn_endpoint_add(h, 1, 1, 0) == 0       # host ring
+    for e in range(2, 9):
+        assert L.usn_endpoint_add(h, e, 2, 0) == 0
+    assert L.usn_endpoint_add(h, 9, 0, -1) == 0      # a second NIC
+    ips_s = ("10.0.0.1", "10.0.0.2", "0.0.0.0", "255.255.255.255")
+    ips = [lib.ip2int(s) for s in ips_s]
+    ports = [0, 22, 80, 443, 3333, 65535]
+    protos = [6, 17, 1, 132, 50, 33, 136, 0]
+    # usn_table_build: NIC owners are allowed there (AddMatch from a NIC panics, main.rs:287-289)
+    nr = rng.choice([40, 400, 1500])
+    rules = np.zeros(nr, lib.RULE_DTYPE)
+    for i in range(nr):
+        present = rng.choice([0, 1, 2, 7, 7, 7, 3, 5, 4])
+        rules[i] = (rng.choice(ips), rng.choice(ips) if present & 2 else 0,
+                    rng.choice(ports) if present & 1 else 0, rng.choice(ports) if present & 4 else 0,
+                    rng.choice(protos), present, rng.choice(range(10)))
+    assert L.usn_table_build(h, rules.ctypes.data, nr) > 10
+    n = nic = 0
+    for dst in ips:
+        for src in ips:
+            for proto in protos:
+                combos = [(0, 0, 0)] + ([(1, d, s) for d in ports for s in ports] if proto in HAS_PORTS else [])
+                for has, dport, sport in combos:
+                    r, out = _rx_probe(L, h, dst, src, proto, has, dport, sport)
+                    assert r == 1
+                    assert out[:2] == out[2:], (dst, src, proto, has, dport, sport, out)
+                    n += (out[2] != 0) + (out[3] != 0)
+                    nic += (out[2] == 0x11FFE) + (out[3] == 0x11FFE)
+    assert n > 10 and nic > 0
+    _, _, _, _, _, pmask = _info(L, h)
+    assert pmask & 4
+    L.usn_ctx_destroy(h)
+
+
+def test_projection_image_off(monkeypatch):
+    """USN_NO_PROJ (A/B): no U is built; the K1 / K2 path answers alone."""
+    monkeypatch.setenv("USN_NO_PROJ", "1")
+    L, h = _ctx()
+    L.usn_debug_image_probe_rx.argtypes = [C.c_void_p] + [C.c_uint32] * 6 + [C.c_void_p]
+    assert L.usn_endpoint_add(h, 0, 0, -1) == 0
+    assert L.usn_endpoint_add(h, 2, 2, 0) == 0
+    w = lib.make_want("10.0.0.1", 6, 80)
+    assert L.usn_add_match(h, C.byref(w), 2, 0) == 1
+    r, out = _rx_probe(L, h, lib.ip2int("10.0.0.1"), 5, 6, 1, 80, 1234)
+    assert r == 0 and out[3] == 0x10002 and out[0] == 0
     L.usn_ctx_destroy(h)

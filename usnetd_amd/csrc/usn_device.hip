@@ -471,6 +471,62 @@ __device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs
   ph_slots_hit<IN_LDS, N, N1>(T, a, x, y, z, m, k, d, on, w);
 }
 
+/* ---- get_endpoint through the projection table U (usn_internal.h) ---------
+ * Both lookups of a frame from ONE U slot: U's displacement from the LDS
+ * copy (Dl), its slot from L2.  X (the projection's further K1 rules) only
+ * when the slot says MORE and its inline K1 rule is not the frame's key1. */
+__device__ __forceinline__ uint32_t u_key_e(const Parsed &p) {
+  return usn_u_e(p.proto, p.has_ports, p.dport);
+}
+
+/* w1/w2 as a K1/K2 probe would return them, and whether key1 needs X */
+__device__ __forceinline__ void u_decode(const v4u32 &s, const Parsed &p, uint32_t E, uint32_t &w1,
+                                         uint32_t &w2, bool &need_x) {
+  const bool hit = s.x == p.dst && (s.w & USN_U_EMASK) == E;
+  const uint32_t o1 = (s.z >> 16) & 0x1FFFu;
+  const bool in1 = hit && o1 != USN_U_NONE && s.y == p.src && (s.z & 0xFFFFu) == p.sport;
+  w1 = in1 ? usn_u_meta(o1) : 0u;
+  w2 = hit ? usn_u_meta(s.w >> 19) : 0u;
+  need_x = hit && !in1 && (s.z & USN_U_MORE) != 0u;
+}
+
+/* one displacement read from the LDS copy (a lane that skips reads the table's first) */
+__device__ __forceinline__ uint32_t lds_disp1(const uint16_t *Dl, const usn_ph_table &t, bool need,
+                                              const PhKeyH &k) {
+  uint32_t d;
+  asm volatile("ds_read_u16 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
+               : "v"(lds_addr(Dl + t.disp_off + (need ? k.grp : 0u))) : "memory");
+  return d;
+}
+
+/* key1 in X for the lanes with `need` (all of this wave's loads are done) */
+__device__ __forceinline__ uint32_t x_probe(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                            const Parsed &p, bool need) {
+  uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+  rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
+  const usn_ph_table &t = a.ph[3];
+  const PhKeyH k = ph_hash(t, x1, y1, z1, m1);
+  const uint32_t d = lds_disp1(Dl, t, need, k);
+  v4u32 s;
+  asm_slot1(T, t, need, k, d, s);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s) :: "memory");
+  return need ? ph_hitv(s, x1, y1, z1, m1) : 0u;
+}
+
+/* both lookups, synchronous (tile 0's carried-cache check, the generic rounds) */
+__device__ __forceinline__ void u_probe_sync(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                             const Parsed &p, uint32_t &w1, uint32_t &w2) {
+  const uint32_t E = u_key_e(p);
+  const PhKeyH k = ph_hash(a.ph[2], p.dst, 0u, E, 0u);
+  const uint32_t d = lds_disp1(Dl, a.ph[2], true, k);
+  v4u32 s;
+  asm_slot1(T, a.ph[2], true, k, d, s);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s) :: "memory");
+  bool nx;
+  u_decode(s, p, E, w1, w2, nx);
+  if (nx) w1 = x_probe(T, Dl, a, p, true);
+}
+
 /* find_forward for a NIC source (incoming == true), cache handled outside:
  * ARP/EAPOL -> FLOOD, loopback -> DROP, else get_endpoint (endpoint.rs:307-338:
  * key1 = with src, key2 = without, only on a key1 miss; a hit on a NIC-owned
@@ -497,10 +553,14 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const uint16_t *Dl
 #if USN_ABL_NOPROBE   /* ablation build only: no table probes */
   w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
 #else
-  uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
-  rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
-  ph_probe2<TM>(T, Dl, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
-                y2, z2, m2, w1, w2);
+  if (TM == TM_DISPLDS && (a.probe_mask & 4u)) {   // Dl holds U's and X's displacements
+    u_probe_sync(T, Dl, a, p, w1, w2);
+  } else {
+    uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
+    rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
+    ph_probe2<TM>(T, Dl, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
+                  y2, z2, m2, w1, w2);
+  }
 #endif
   return decide_rx_w(a, p, w1, w2);
 }
@@ -1188,8 +1248,11 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   const uint4 *T = m.b[0].table;
   const uint16_t *Dl = nullptr;
   if (TM != TM_GLOBAL) {   // image (or its displacements) -> LDS by glds, 64 units per instruction
-    const uint32_t u0 = TM == TM_LDS ? 0u : m.b[0].disp_unit;
-    const uint32_t units = USN_ABL_NODISPCOPY ? min(64u, m.b[0].table_units - u0) : m.b[0].table_units - u0;
+    // TM_DISPLDS with U built: U's and X's displacements, else K1's and K2's
+    const bool um = TM == TM_DISPLDS && (m.b[0].probe_mask & 4u);
+    const uint32_t u0 = TM == TM_LDS ? 0u : um ? m.b[0].u_disp_unit : m.b[0].disp_unit;
+    const uint32_t uend = um ? m.b[0].u_end_unit : m.b[0].table_units;
+    const uint32_t units = USN_ABL_NODISPCOPY ? min(64u, uend - u0) : uend - u0;
     for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
       const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
@@ -1286,7 +1349,51 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     uint32_t my_last = 0;          // 1 + tile-local index of this lane's last touching frame
     uint32_t my_touch = 0, my_dec = 0, my_info[4] = {0, 0, 0, 0};
     Parsed pr[ROUNDS];
-    if (BATCH2 && TM == TM_DISPLDS && USN_SEQ_K2) {
+    if (BATCH2 && TM == TM_DISPLDS && (a.probe_mask & 4u)) {
+      // U: one slot read per frame answers key1 AND key2 (they share the
+      // projection); both rounds' reads fly together, round 1's header DMA
+      // under round 0's parse.  X only where a projection holds several K1
+      // rules and the inline one is not the frame's key1 (rare: one wave-
+      // uniform branch, after every load of the wave has landed).
+      uint4 *sb = st;
+      uint32_t du0, du1;
+      v4u32 su0, su1;
+      stage_read_asm(sb, lane, q[0]);
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      __builtin_amdgcn_sched_barrier(0);
+      parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
+      const uint32_t e0 = u_key_e(pr[0]);
+      const PhKeyH ku0 = ph_hash(a.ph[2], pr[0].dst, 0u, e0, 0u);
+      const bool n0 = pr[0].status == 1u;
+      du0 = lds_disp1(Dl, a.ph[2], n0, ku0);
+      asm_slot1(T, a.ph[2], n0, ku0, du0, su0);
+      __builtin_amdgcn_sched_barrier(0);
+      vm_wait<1>();                                               // round 1 landed (1 younger load)
+      stage_read_asm(sb, lane, q[1]);
+      parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
+      const uint32_t e1 = u_key_e(pr[1]);
+      const PhKeyH ku1 = ph_hash(a.ph[2], pr[1].dst, 0u, e1, 0u);
+      const bool n1 = pr[1].status == 1u;
+      du1 = lds_disp1(Dl, a.ph[2], n1, ku1);
+      asm_slot1(T, a.ph[2], n1, ku1, du1, su1);
+      uint32_t w01, w02, w11, w12;
+      bool x0, x1;
+      asm volatile("s_waitcnt vmcnt(1)" : "+v"(su0) :: "memory");
+      u_decode(su0, pr[0], e0, w01, w02, x0);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(su1) :: "memory");
+      u_decode(su1, pr[1], e1, w11, w12, x1);
+      x0 = x0 && n0;
+      x1 = x1 && n1;
+      STAMP(4);
+      if (__ballot(x0 || x1)) {
+        const uint32_t wx0 = x_probe(T, Dl, a, pr[0], x0);
+        const uint32_t wx1 = x_probe(T, Dl, a, pr[1], x1);
+        if (x0) w01 = wx0;
+        if (x1) w11 = wx1;
+      }
+      dec[0] = decide_rx_w(a, pr[0], w01, w02);
+      dec[1] = decide_rx_w(a, pr[1], w11, w12);
+    } else if (BATCH2 && TM == TM_DISPLDS && USN_SEQ_K2) {
       // displacements from LDS; key1's slot reads of both rounds first, then
       // key2's only where key1 missed (get_endpoint reads key2 only then,
       // endpoint.rs:317-327): a lane that needs no read shares the table's
@@ -1417,7 +1524,19 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
 #endif
       Parsed &p = pr[r];
       parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
-      if (LATE_DMA) {
+      if (LATE_DMA && !USN_ABL_NOPROBE && TM == TM_DISPLDS && (a.probe_mask & 4u)) {
+        // U (rare here: the 512-thread build batches both rounds above);
+        // synchronous, then the next round's header DMA
+        uint32_t w1 = 0, w2 = 0;
+        u_probe_sync(T, Dl, a, p, w1, w2);
+        if (r + GD < ROUNDS) {
+          __builtin_amdgcn_sched_barrier(0);
+          lgkm_wait0();
+          glds_round(a, base, nt, r + GD, wave, lane, sb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        dec[r] = decide_rx_w(a, p, w1, w2);
+      } else if (LATE_DMA) {
         // global probes: the slot loads first, then the next round's header DMA,
         // so the wait for the slots does not also wait for the DMA
         uint32_t w1 = 0, w2 = 0;
@@ -2671,9 +2790,14 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
 #ifndef USN_DISP_LDS_MAX
 #define USN_DISP_LDS_MAX (26u * 1024u)
 #endif
+/* units of the displacements TM_DISPLDS copies to LDS: U's and X's when U is
+ * built (one slot read per frame), else K1's and K2's */
+static uint32_t disp_lds_units(const ClassifyArgs &a) {
+  return (a.probe_mask & 4u) ? a.u_end_unit - a.u_disp_unit : a.table_units - a.disp_unit;
+}
 static int table_mode(const ClassifyArgs &a) {
   if (table_fits_lds(a.nbins, a.table_units)) return TM_LDS;
-  const size_t disp = (size_t)(a.table_units - a.disp_unit) * 16;
+  const size_t disp = (size_t)disp_lds_units(a) * 16;
   return disp <= USN_DISP_LDS_MAX ? TM_DISPLDS : TM_GLOBAL;
 }
 
@@ -2727,7 +2851,7 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
   const size_t lds = lds_core_bytes(a.nbins, !glds) +
                      (tm == TM_LDS ? table_lds_bytes(a.table_units)
-                      : tm == TM_DISPLDS ? table_lds_bytes(a.table_units - a.disp_unit) : 0);
+                      : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
   const dim3 b(NTHREADS);
   // a grid of at most what the chip holds (0 = the query failed: one per tile)
 #define USN_LAUNCH(T_, G_)                                                              \

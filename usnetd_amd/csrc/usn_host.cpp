@@ -324,8 +324,11 @@ struct usn_ctx {
   bool table_dirty = true;
   uint64_t table_version = 0;
   std::vector<uint4> img;          // the whole image in 16-byte units
-  usn_ph_table img_t[2] = {};
+  usn_ph_table img_t[4] = {};  // K1, K2, U, X (usn_internal.h)
+  uint32_t img_base = 0;       // units of the K1/K2 part; U and X follow
+  uint32_t img_udisp = 0;      // first unit of U's and X's displacements
   uint32_t probe_mask = 0;   // tables holding rules (ClassifyArgs::probe_mask)
+  bool proj = std::getenv("USN_NO_PROJ") == nullptr;   // A/B: build U and X
   bool bridge_dirty = true;
   uint64_t bridge_version = 0;
   std::vector<unsigned long long> bridge_set;
@@ -413,19 +416,19 @@ uint32_t ph_group_knob() {
 }
 
 struct PhKey {
-  uint4 e;         // x, y, z, meta | NICOWNER | owner << 16
+  uint4 e;         // the slot: K1/K2 x, y, z, meta | NICOWNER | owner << 16; U: usn_internal.h
+  uint4 k;         // the hashed key (x, y, z, meta): K1/K2 the packed key, U (dst, 0, E, 0)
   uint32_t h2, grp;
 };
 
 /* Place the keys of one shard: m slots, g groups (group = mulhi(h1 << shift,
  * g); h1 of each key in k.grp on entry). */
 bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed, uint32_t shift,
-              std::vector<uint4> &slots, std::vector<uint16_t> &disp) {
+              const uint4 &empty, std::vector<uint4> &slots, std::vector<uint16_t> &disp) {
   const uint32_t n = (uint32_t)keys.size();
   for (PhKey &k : keys) {
-    const uint32_t meta = k.e.w & USN_KEY_META_MASK;
-    k.grp = usn_mulhi32(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed) << shift, g);
-    k.h2 = usn_key_hash2(k.e.x, k.e.y, k.e.z, meta, seed);
+    k.grp = usn_mulhi32(usn_ph_h1(k.k.x, k.k.y, k.k.z, k.k.w, seed) << shift, g);
+    k.h2 = usn_key_hash2(k.k.x, k.k.y, k.k.z, k.k.w, seed);
   }
   /* members of each group (counting sort), then groups by size, largest first */
   std::vector<uint32_t> start(g + 1, 0), member(n);
@@ -441,7 +444,7 @@ bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed, u
   for (uint32_t i = 0; i < g; ++i) bysz[maxsz - (start[i + 1] - start[i]) + 1]++;
   for (uint32_t s = 0; s <= maxsz; ++s) bysz[s + 1] += bysz[s];
   for (uint32_t i = 0; i < g; ++i) order[bysz[maxsz - (start[i + 1] - start[i])]++] = i;
-  slots.assign(m, make_uint4(0, 0, 0, 0));
+  slots.assign(m, empty);
   disp.assign(g, 0);
   std::vector<uint64_t> used((m + 63) / 64, 0);   // a bit per slot: stays in L1/L2
   uint32_t pos[64], h2[64];
@@ -499,7 +502,8 @@ void parallel_for(uint32_t jobs, uint32_t threads, F f) {
 /* one table of the image: shards, m, g, seed and its slots / displacements
  * (shard after shard) */
 bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
-              std::vector<uint16_t> &disp, double load0, uint32_t group, uint32_t threads) {
+              std::vector<uint16_t> &disp, double load0, uint32_t group, uint32_t threads,
+              const uint4 &empty = make_uint4(0, 0, 0, 0)) {
   const uint32_t n = (uint32_t)keys.size();
   t = usn_ph_table{};
   slots.clear();
@@ -517,10 +521,8 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
     if (S == 1) {
       part[0] = keys;
     } else {
-      for (const PhKey &k : keys) {
-        const uint32_t meta = k.e.w & USN_KEY_META_MASK;
-        part[usn_ph_shard(usn_ph_h1(k.e.x, k.e.y, k.e.z, meta, seed), shift)].push_back(k);
-      }
+      for (const PhKey &k : keys)
+        part[usn_ph_shard(usn_ph_h1(k.k.x, k.k.y, k.k.z, k.k.w, seed), shift)].push_back(k);
     }
     uint32_t maxc = 0;
     for (const auto &v : part) maxc = std::max(maxc, (uint32_t)v.size());
@@ -530,7 +532,7 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
     std::vector<std::vector<uint16_t>> pd(S);
     std::vector<uint8_t> ok(S, 0);
     parallel_for(S, threads, [&](uint32_t sh) {
-      ok[sh] = ph_place(part[sh], m, g, seed, shift, ps[sh], pd[sh]) ? 1 : 0;
+      ok[sh] = ph_place(part[sh], m, g, seed, shift, empty, ps[sh], pd[sh]) ? 1 : 0;
     });
     if (std::find(ok.begin(), ok.end(), 0) != ok.end()) continue;
     slots.reserve((size_t)S * m);
@@ -548,11 +550,65 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
   return false;
 }
 
-/* The host image of the registry: [K1 slots][K2 slots][K1 disp][K2 disp],
- * each part starting on a 16-byte unit. */
+/* U and X keys (usn_internal.h) from the K1 / K2 keys: one U slot per
+ * projection with the K2 owner and one K1 rule inline; the projection's
+ * further K1 rules go to X.  Rules no frame can hit (ports on a protocol that
+ * has none, pkt.rs protocol_has_ports) are left out. */
+#ifndef USN_U_MAX_KEYS   /* above: U's displacements would not fit LDS, U is not built */
+#define USN_U_MAX_KEYS 131072u
+#endif
+void proj_keys(const std::vector<PhKey> *keys, std::vector<PhKey> &ukeys, std::vector<PhKey> &xkeys) {
+  struct Ent { uint32_t dst, e, o1, o2, src, sport; bool more; };
+  std::vector<Ent> ents;
+  std::unordered_map<uint64_t, uint32_t> at;
+  at.reserve(keys[0].size() + keys[1].size());
+  auto code = [](const uint4 &e) {
+    return (e.w & USN_SLOT_NICOWNER) ? USN_U_NIC : (e.w >> 16);
+  };
+  for (int t = 1; t >= 0; --t)   // K2 first: a projection's slot exists before its K1 rules look for it
+    for (const PhKey &k : keys[t]) {
+      const uint32_t proto = k.e.w & 0xFFu, present = (k.e.w >> 8) & 7u;
+      const uint32_t has = (present & USN_WANT_DPORT) ? 1u : 0u;
+      if (has && usn_u_pidx(proto) == 7u) continue;   // never matched
+      const uint32_t E = usn_u_e(proto, has, k.e.z & 0xFFFFu);
+      const uint64_t pk = (uint64_t)k.e.x << 32 | E;
+      auto it = at.find(pk);
+      uint32_t i;
+      if (it == at.end()) {
+        i = (uint32_t)ents.size();
+        at.emplace(pk, i);
+        ents.push_back(Ent{k.e.x, E, USN_U_NONE, USN_U_NONE, 0u, 0u, false});
+      } else {
+        i = it->second;
+      }
+      Ent &en = ents[i];
+      if (t == 1) {
+        en.o2 = code(k.e);
+      } else if (en.o1 == USN_U_NONE) {
+        en.o1 = code(k.e);
+        en.src = k.e.y;
+        en.sport = has ? (k.e.z >> 16) : 0u;
+      } else {
+        en.more = true;
+        xkeys.push_back(k);
+      }
+    }
+  ukeys.resize(ents.size());
+  for (size_t i = 0; i < ents.size(); ++i) {
+    const Ent &en = ents[i];
+    PhKey &u = ukeys[i];
+    u.e = make_uint4(en.dst, en.src, en.sport | en.o1 << 16 | (en.more ? USN_U_MORE : 0u), en.e | en.o2 << 19);
+    u.k = make_uint4(en.dst, 0u, en.e, 0u);
+    u.h2 = u.grp = 0;
+  }
+}
+
+/* The host image of the registry: [K1 slots][K2 slots][K1 disp][K2 disp][pad]
+ * (table_units), then, when built, [U slots][X slots][U disp][X disp][pad];
+ * each part starts on a 16-byte unit. */
 int build_image(usn_ctx *c) {
   StageClock clk("build_image");
-  std::vector<PhKey> keys[2];
+  std::vector<PhKey> keys[4];
   for (const auto &kv : c->rules) {
     const WantKey &k = kv.first;
     const int t = image_table(k);
@@ -563,37 +619,56 @@ int build_image(usn_ctx *c) {
     pk.e = make_uint4(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
                       usn_key_meta(k.proto, k.present) | (nic ? USN_SLOT_NICOWNER : 0u) |
                           ((uint32_t)owner << 16));
+    pk.k = make_uint4(pk.e.x, pk.e.y, pk.e.z, pk.e.w & USN_KEY_META_MASK);
     pk.h2 = pk.grp = 0;
     keys[t].push_back(pk);
   }
+  const bool proj = c->proj && (keys[0].size() + keys[1].size()) > 0 &&
+                    keys[0].size() + keys[1].size() <= USN_U_MAX_KEYS;
+  if (proj) proj_keys(keys, keys[2], keys[3]);
   clk.mark("keys");
-  std::vector<uint4> slots[2];
-  std::vector<uint16_t> disp[2];
-  usn_ph_table t[2];
-  bool placed[2] = {false, false};
+  std::vector<uint4> slots[4];
+  std::vector<uint16_t> disp[4];
+  usn_ph_table t[4] = {};
+  bool placed[4] = {false, false, !proj, !proj};
   {
-    // the two tables side by side, each over its shards
+    // the tables side by side, each over its shards
     const uint32_t hw = std::max(1u, std::min(USN_PH_THREADS, std::thread::hardware_concurrency()));
-    auto one = [&](int i, uint32_t threads) {
+    const uint32_t nt = proj ? 4u : 2u;
+    auto one = [&](uint32_t i, uint32_t threads) {
+      const uint4 empty = i == 2 ? make_uint4(0, 0, 0, USN_U_EMPTY_W) : make_uint4(0, 0, 0, 0);
       for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
-        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads)) { placed[i] = true; break; }
+        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads, empty)) {
+          placed[i] = true;
+          break;
+        }
         if (grp <= 1) break;
       }
     };
-    if (hw > 1 && !keys[0].empty() && !keys[1].empty()) {
-      std::thread other(one, 1, std::max(1u, hw / 2));
-      one(0, std::max(1u, hw - hw / 2));
-      other.join();
+    uint32_t busy = 0;
+    for (uint32_t i = 0; i < nt; ++i) busy += keys[i].empty() ? 0u : 1u;
+    if (hw > 1 && busy > 1) {
+      const uint32_t per = std::max(1u, hw / busy);
+      std::vector<std::thread> pool;
+      for (uint32_t i = 1; i < nt; ++i) pool.emplace_back(one, i, per);
+      one(0, per);
+      for (std::thread &th : pool) th.join();
     } else {
-      one(0, hw);
-      one(1, hw);
+      for (uint32_t i = 0; i < nt; ++i) one(i, hw);
     }
   }
-  if (!placed[0] || !placed[1]) return USN_ENOMEM;
+  if (!placed[0] || !placed[1] || !placed[2] || !placed[3]) return USN_ENOMEM;
   clk.mark("place");
+  // 8 u16 displacements per 16-byte unit
+  auto units = [](size_t n16) { return (uint32_t)((n16 + 7) / 8); };
   const uint32_t u0 = (uint32_t)slots[0].size(), u1 = (uint32_t)slots[1].size();
-  const uint32_t d0 = ((uint32_t)disp[0].size() + 7) / 8, d1 = ((uint32_t)disp[1].size() + 7) / 8;   // 8 u16 per 16-byte unit
-  c->img.assign((size_t)u0 + u1 + d0 + d1 + 1, make_uint4(0, 0, 0, 0));
+  const uint32_t d0 = units(disp[0].size()), d1 = units(disp[1].size());
+  const uint32_t base = u0 + u1 + d0 + d1 + 1;
+  // X's displacements take at least one unit: a lane that skips X still reads one inside the LDS copy
+  const uint32_t u2 = (uint32_t)slots[2].size(), u3 = (uint32_t)slots[3].size();
+  const uint32_t d2 = units(disp[2].size()), d3 = std::max(1u, units(disp[3].size()));
+  const uint32_t total = proj ? base + u2 + u3 + d2 + d3 + 1 : base;
+  c->img.assign(total, make_uint4(0, 0, 0, 0));
   std::copy(slots[0].begin(), slots[0].end(), c->img.begin());
   std::copy(slots[1].begin(), slots[1].end(), c->img.begin() + u0);
   uint16_t *dp = reinterpret_cast<uint16_t *>(c->img.data() + u0 + u1);
@@ -603,9 +678,21 @@ int build_image(usn_ctx *c) {
   t[1].slot_off = u0;
   t[0].disp_off = (u0 + u1) * 8;
   t[1].disp_off = (u0 + u1 + d0) * 8;
-  c->img_t[0] = t[0];
-  c->img_t[1] = t[1];
-  c->probe_mask = (keys[0].empty() ? 0u : 1u) | (keys[1].empty() ? 0u : 2u);
+  if (proj) {
+    std::copy(slots[2].begin(), slots[2].end(), c->img.begin() + base);
+    std::copy(slots[3].begin(), slots[3].end(), c->img.begin() + base + u2);
+    uint16_t *up = reinterpret_cast<uint16_t *>(c->img.data() + base + u2 + u3);
+    std::copy(disp[2].begin(), disp[2].end(), up);
+    std::copy(disp[3].begin(), disp[3].end(), up + (size_t)d2 * 8);
+    t[2].slot_off = base;
+    t[3].slot_off = base + u2;
+    t[2].disp_off = (base + u2 + u3) * 8;
+    t[3].disp_off = (base + u2 + u3 + d2) * 8;
+  }
+  for (int i = 0; i < 4; ++i) c->img_t[i] = t[i];
+  c->img_base = base;
+  c->img_udisp = proj ? base + u2 + u3 : base;
+  c->probe_mask = (keys[0].empty() ? 0u : 1u) | (keys[1].empty() ? 0u : 2u) | (proj ? 4u : 0u);
   c->table_dirty = false;
   ++c->table_version;
   clk.mark("image");
@@ -623,6 +710,28 @@ uint32_t image_probe(const usn_ctx *c, int table, uint32_t x, uint32_t y, uint32
                          usn_ph_slot(usn_key_hash2(x, y, z, meta, t.seed), d, t.m)];
   const bool hit = s.x == x && s.y == y && s.z == z && ((s.w ^ meta) & USN_KEY_META_MASK) == 0;
   return hit ? s.w : 0u;
+}
+
+/* get_endpoint's two lookups for a parsed IPv4 frame through U (and X) as the
+ * device computes them: w[0] = key1's slot meta word, w[1] = key2's (0 = miss) */
+void image_probe_u(const usn_ctx *c, uint32_t dst, uint32_t src, uint32_t proto, uint32_t has,
+                   uint32_t dport, uint32_t sport, uint32_t w[2]) {
+  w[0] = w[1] = 0;
+  const usn_ph_table &t = c->img_t[2];
+  if (!(c->probe_mask & 4u) || !t.m) return;
+  const uint32_t E = usn_u_e(proto, has, dport);
+  const uint32_t h1 = usn_ph_h1(dst, 0u, E, 0u, t.seed);
+  const uint16_t d = reinterpret_cast<const uint16_t *>(c->img.data())[t.disp_off + usn_ph_group(h1, t.shift, t.g)];
+  const uint4 s = c->img[t.slot_off + usn_ph_shard(h1, t.shift) * t.m +
+                         usn_ph_slot(usn_key_hash2(dst, 0u, E, 0u, t.seed), d, t.m)];
+  if (s.x != dst || (s.w & USN_U_EMASK) != E) return;
+  const uint32_t o1 = (s.z >> 16) & 0x1FFFu, sp = has ? sport : 0u;
+  const bool in1 = o1 != USN_U_NONE && s.y == src && (s.z & 0xFFFFu) == sp;
+  w[0] = in1 ? usn_u_meta(o1) : 0u;
+  if (!in1 && (s.z & USN_U_MORE))
+    w[0] = image_probe(c, 3, dst, src, has ? (dport | sport << 16) : 0u,
+                       usn_key_meta(proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT) : USN_WANT_SRC));
+  w[1] = usn_u_meta(s.w >> 19);
 }
 
 /* the replica's device table at the current image version; no batch still
@@ -1145,8 +1254,33 @@ int64_t usn_debug_image_probe(usn_ctx *c, int table, uint32_t x, uint32_t y, uin
   return (int64_t)image_probe(c, table, x, y, z, meta);
 }
 
-/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask}
- * (slots and groups of each table, all shards). */
+/* Test hook: get_endpoint's lookups for one parsed IPv4 frame, through U / X
+ * (out[0], out[1]) and through K1 / K2 (out[2], out[3]), each normalised to
+ * 0 (miss), 0x10000 | owner, or 0x11FFE (a NIC owns the rule).  Returns 1
+ * when U is built, 0 when not. */
+int usn_debug_image_probe_rx(usn_ctx *c, uint32_t dst, uint32_t src, uint32_t proto, uint32_t has,
+                             uint32_t dport, uint32_t sport, uint32_t *out4) {
+  if (!c || !out4) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->table_dirty) {
+    const int s = build_image(c);
+    if (s) return s;
+  }
+  auto norm = [](uint32_t w) {
+    return w == 0 ? 0u : 0x10000u | ((w & USN_SLOT_NICOWNER) ? USN_U_NIC : (w >> 16));
+  };
+  uint32_t wu[2];
+  image_probe_u(c, dst, src, proto, has, dport, sport, wu);
+  const uint32_t w1 = image_probe(c, 0, dst, src, has ? (dport | sport << 16) : 0u,
+                                  usn_key_meta(proto, has ? (USN_WANT_DPORT | USN_WANT_SRC | USN_WANT_SPORT)
+                                                          : USN_WANT_SRC));
+  const uint32_t w2 = image_probe(c, 1, dst, 0u, has ? dport : 0u, usn_key_meta(proto, has ? USN_WANT_DPORT : 0u));
+  out4[0] = norm(wu[0]); out4[1] = norm(wu[1]); out4[2] = norm(w1); out4[3] = norm(w2);
+  return (c->probe_mask & 4u) ? 1 : 0;
+}
+
+/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask, mU, mX}
+ * (slots and groups of each table, all shards; slots of U and X). */
 int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   if (!c || !out6) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1159,6 +1293,8 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
     out6[2 * i + 1] = c->img_t[i].g << c->img_t[i].shift;
   }
   out6[4] = (uint32_t)c->img.size(); out6[5] = c->probe_mask;
+  out6[6] = c->img_t[2].m << c->img_t[2].shift;
+  out6[7] = c->img_t[3].m << c->img_t[3].shift;
   return USN_OK;
 }
 
@@ -1240,10 +1376,11 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   a.summary = r->summary;
   a.host_list = r->host_list;
   a.table = R.d_table;
-  a.table_units = (uint32_t)c->img.size();
-  a.disp_unit = c->img_t[1].slot_off + c->img_t[1].m;
-  a.ph[0] = c->img_t[0];
-  a.ph[1] = c->img_t[1];
+  a.table_units = c->img_base;
+  a.disp_unit = c->img_t[1].slot_off + (c->img_t[1].m << c->img_t[1].shift);
+  for (int i = 0; i < 4; ++i) a.ph[i] = c->img_t[i];
+  a.u_disp_unit = c->img_udisp;
+  a.u_end_unit = (uint32_t)c->img.size();
   a.bridge = R.d_bridge;
   a.n_bridge = (uint32_t)c->bridge.size();
   const Ep &S = c->eps[b->src_endpoint];

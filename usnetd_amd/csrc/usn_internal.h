@@ -126,6 +126,42 @@ typedef struct {
   uint32_t _pad[2];
 } usn_ph_table;
 
+/* ---- projection table U and its overflow table X (rx, displacements in LDS)
+ * key1 and key2 of a frame (pkt.rs:96-113) share their projection (dst,
+ * proto, has_ports, dport): key2 IS the projection, key1 adds (src, sport).
+ * U holds one slot per projection that some matchable K1 or K2 rule has:
+ *   x = dst
+ *   y = src of one K1 rule of the projection (inline)
+ *   z = that rule's sport | o1 << 16 | USN_U_MORE
+ *   w = E | o2 << 19                       (o2: the K2 rule of the projection)
+ * E = has_ports ? pidx(proto) << 16 | dport : 5 << 16 | proto (19 bits; a
+ * frame has ports only for the five protocols of protocol_has_ports).
+ * o1 / o2: the owner id, USN_U_NIC (owned by a NIC: get_endpoint returns
+ * None) or USN_U_NONE.  USN_U_MORE: further K1 rules share the projection;
+ * they are in table X (K1's slot format).  A frame reads ONE U slot for both
+ * of get_endpoint's lookups (endpoint.rs:317-327), and X only when MORE is
+ * set and the inline rule is not its key1.  Empty U slots are USN_U_EMPTY_W
+ * in w (E = 0x7FFFF never occurs).  Hashed as the key (dst, 0, E, 0). */
+#define USN_U_NONE 0x1FFFu
+#define USN_U_NIC 0x1FFEu
+#define USN_U_MORE (1u << 29)
+#define USN_U_EMASK 0x7FFFFu
+#define USN_U_EMPTY_W 0xFFFFFFFFu
+/* 0..4 for TCP, UDP, DCCP, SCTP, UDPLite (pkt.rs protocol_has_ports), 7 else */
+USN_HD uint32_t usn_u_pidx(uint32_t proto) {
+  return proto == 6u ? 0u : proto == 17u ? 1u : proto == 33u ? 2u : proto == 132u ? 3u
+         : proto == 136u ? 4u : 7u;
+}
+USN_HD uint32_t usn_u_e(uint32_t proto, uint32_t has_ports, uint32_t dport) {
+  return has_ports ? (usn_u_pidx(proto) << 16 | (dport & 0xFFFFu)) : (5u << 16 | (proto & 0xFFu));
+}
+/* an owner code as the slot meta word a K1/K2 probe returns (0 = no rule) */
+USN_HD uint32_t usn_u_meta(uint32_t o) {
+  return o == USN_U_NONE ? 0u
+         : o == USN_U_NIC ? (USN_SLOT_VALID | USN_SLOT_NICOWNER)
+                          : (USN_SLOT_VALID | (o << 16));
+}
+
 /* 32-bit tag of a key in the tag array of a global-memory table (0 = empty) */
 USN_HD uint32_t usn_key_tag(uint32_t h) { return h | 1u; }
 

@@ -33,9 +33,11 @@ struct ClassifyArgs {
   uint32_t *host_list;      /* per tile USN_TILE slots */
   /* rule image (usn_internal.h): K1 / K2 perfect-hash tables in one buffer */
   const uint4 *table;
-  uint32_t table_units;     /* 16-byte units of the whole image */
-  uint32_t disp_unit;       /* first unit of the displacement arrays (the rest of the image) */
-  usn_ph_table ph[2];       /* K1 (key1 shapes), K2 (key2 shapes) */
+  uint32_t table_units;     /* 16-byte units of the K1/K2 image (U and X follow it) */
+  uint32_t disp_unit;       /* first unit of the K1/K2 displacement arrays (up to table_units) */
+  usn_ph_table ph[4];       /* K1 (key1 shapes), K2 (key2 shapes), U (projections), X (U overflow) */
+  uint32_t u_disp_unit;     /* first unit of U's then X's displacements (probe_mask bit 2) */
+  uint32_t u_end_unit;      /* end of the image */
   /* inner L2 bridge (tx): MACs in the low 48 bits */
   const uint64_t *bridge;
   uint32_t n_bridge;
@@ -46,7 +48,7 @@ struct ClassifyArgs {
   uint32_t nbins;           /* endpoints + 3 */
   uint32_t nbits;           /* bits to tell bins apart (ceil log2 nbins) */
   uint32_t n_ep;            /* endpoints (bin of NIC) */
-  uint32_t probe_mask;      /* bit0: K1 holds rules; bit1: K2 holds rules */
+  uint32_t probe_mask;      /* bit0: K1 holds rules; bit1: K2 holds rules; bit2: U and X built */
   uint32_t next_dhcp_set;   /* the source's next_dhcp_endpoint is Some: DHCP answers need the host */
   /* carried 1-entry decision cache */
   uint32_t carry_mode;
@@ -65,6 +67,7 @@ struct MultiArgs {
   uint32_t tile_base[USN_MAX_MULTI + 1];
   uint32_t count;
 };
+static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 
 /* ---- tx direction (a non-NIC source sends): four launches ---------------- */
 /* per-frame record, two planes of n uint4 written by tx_scan:
