@@ -61,7 +61,7 @@ def _filler(n):
     out = []
     for i in range(n):
         conn = i % 2 == 0
-        out.append({"op": "add_match", "owner": 2, "sticky": False,
+        out.append({"op": "add_match", "owner": 1, "sticky": False,   # endpoint 1 is never removed
                     "want": {"dst": "10.77.%d.%d" % (i >> 8, i & 255), "proto": 17, "dport": 1000 + i % 7,
                              "src": "10.1.1.1" if conn else None, "sport": 5000 + i % 13 if conn else None}})
     return out
