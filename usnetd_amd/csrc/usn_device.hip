@@ -2147,11 +2147,19 @@ __device__ __forceinline__ void tx_load_cin(const TxArgs &t, uint32_t *cin) {
   for (int k = 0; k < 6; ++k) cin[k] = ok ? v[k] : 0u;
 }
 
-/* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge */
+/* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge.
+ * The header loads' per-wave redistribution scratch (3 KiB per wave: 64
+ * frames x 48 bytes) aliases the records and decisions, which are written
+ * only after every wave has parsed (a barrier in between). */
+#define TX_SCRATCH_BYTES ((size_t)NWAVES * 64 * 48)
 __host__ __device__ inline size_t tx_lds_head(uint32_t nbins) {
-  return lds_core_bytes(nbins) + (size_t)TILE * 16 + (size_t)TILE * 4;
+  const size_t recs = (size_t)TILE * 16 + (size_t)TILE * 4;
+  return lds_core_bytes(nbins) + (recs > TX_SCRATCH_BYTES ? recs : TX_SCRATCH_BYTES);
 }
 
+#ifndef USN_TX_COAL   /* coalesced header loads at a fixed stride (0: each lane its own frame) */
+#define USN_TX_COAL 1
+#endif
 #ifndef USN_TX_PIPE   /* phase 1: probes of a round issued as it is parsed; LDS-only barrier */
 #define USN_TX_PIPE 1
 #endif
@@ -2163,8 +2171,9 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   const Lds L = carve(smem, a.nbins);
   uint4 *srec = reinterpret_cast<uint4 *>(smem + lds_core_bytes(a.nbins));   // the tile's records
   uint32_t *sdec = reinterpret_cast<uint32_t *>(srec + TILE);               // its decisions
-  uint4 *stab = reinterpret_cast<uint4 *>(sdec + TILE);
+  uint4 *stab = reinterpret_cast<uint4 *>(smem + tx_lds_head(a.nbins));
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   __shared__ uint32_t s_last, s_lastnh, s_ins, s_ovf, s_insall, s_hidx, s_before, s_head;
   __shared__ uint32_t s_early, s_early_all, s_slow, s_dlearn;
   __shared__ uint32_t s_cin[6];   // the carried-in cache {state, dst, info[4]} (tile 0's)
@@ -2229,6 +2238,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
      Every round's frame address first: an offsets[] read feeding a round's
      loads made hipcc wait for all earlier loads before each round's. */
   uint4 qq[ROUNDS][4];
+  uint4 cc[ROUNDS][3];
   uint32_t ll[ROUNDS];
   const uint8_t *fps[ROUNDS];
 #pragma unroll   // lengths before the headers: round 0's parse then waits for round 0 only
@@ -2243,10 +2253,24 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) fps[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
   }
+  /* fixed stride (16-byte aligned): coalesced loads.  Lane u of instruction k
+     reads part u % 3 of frame u / 3 (u = 64k + lane) of its wave's 64 frames
+     of the round, so an instruction reads 1 KiB runs instead of 16 bytes at
+     every frame start (tools/probe_floor, 8M x 64 B: 86 vs 145 us); the parse
+     loop moves each part to its frame's lane through the wave's LDS scratch.
+     Otherwise lane L reads its own frame.  One load instruction either way. */
+  const bool coal = USN_TX_COAL && !a.offsets && (a.stride & 15u) == 0 &&
+                    (reinterpret_cast<uintptr_t>(a.frames) & 15u) == 0;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
 #pragma unroll
-    for (uint32_t k = 0; k < 3; ++k) qq[r][k] = ld_stream(reinterpret_cast<const uint4 *>(fps[r]) + k);
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t u = 64u * k + lane, f = (u * 0xAAABu) >> 17, part = u - 3u * f;
+      const uint64_t fi = base + min(r * NTHREADS + wave * 64u + f, nt - 1);
+      const uint8_t *pc = a.frames + fi * a.stride + part * 16u;
+      const uint8_t *pl = fps[r] + 16u * k;
+      cc[r][k] = ld_stream(reinterpret_cast<const uint4 *>(coal ? pc : pl));
+    }
     qq[r][3] = make_uint4(0, 0, 0, 0);
   }
   if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
@@ -2289,6 +2313,20 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
+    if (coal) {   // the wave's parts to their frames' lanes (in order per wave: no barrier)
+      typedef __attribute__((address_space(3))) v4u32 lds_v4;
+      lds_v4 *ws = (lds_v4 *)srec + wave * 192u;
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k) ws[64u * k + lane] = v4u32{cc[r][k].x, cc[r][k].y, cc[r][k].z, cc[r][k].w};
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k) {
+        const v4u32 v = ws[3u * lane + k];
+        qq[r][k] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k) qq[r][k] = cc[r][k];
+    }
     const uint4 *q = qq[r];
     Parsed p;
     parse(q, local < nt ? ll[r] : 0u, fps[r], a.window, p);
@@ -2367,6 +2405,10 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   }
 
   STAMP(2);
+  // every wave is done with its header scratch before the records overwrite it
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   // ---- the tile's records in LDS; each frame's previous touching frame
   uint32_t vt[ROUNDS], prev[ROUNDS];
 #pragma unroll
