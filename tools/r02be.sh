@@ -10,6 +10,7 @@ step() { name=$1; to=$2; shift 2; echo "-- $name $(date +%T)"; timeout -k 10 $to
 step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 5
+step abl_c5 300 python tools/abl.py --config c5 --frames 8388608 --batches 2 --rounds 5 --launches 40 base xseq base@USN_NO_PROJ=1
 rm -rf $O/prof
 step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --ramp 40
 step trace_summary 60 python3 tools/trace_summary.py $O/prof/run_kernel_trace.csv

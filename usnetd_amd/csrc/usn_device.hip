@@ -237,6 +237,9 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_STAGE_ROWS   /* 64 < bins <= 1024: counting sort with byte rows in the stage */
 #define USN_STAGE_ROWS 1
 #endif
+#ifndef USN_X_BATCH   /* U path: both rounds' X probes in flight together */
+#define USN_X_BATCH 1
+#endif
 #ifndef USN_SEQ_K2    /* key2's slot read only where key1 missed (get_endpoint's order) */
 #define USN_SEQ_K2 1
 #endif
@@ -511,6 +514,24 @@ __device__ __forceinline__ uint32_t x_probe(const uint4 *T, const uint16_t *Dl, 
   asm_slot1(T, t, need, k, d, s);
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(s) :: "memory");
   return need ? ph_hitv(s, x1, y1, z1, m1) : 0u;
+}
+
+/* key1 of both rounds' frames in X, the two slot reads in flight together */
+__device__ __forceinline__ void x_probe2(const uint4 *T, const uint16_t *Dl, const ClassifyArgs &a,
+                                         const Parsed &p0, bool need0, const Parsed &p1, bool need1,
+                                         uint32_t &w0, uint32_t &w1) {
+  const usn_ph_table &t = a.ph[3];
+  uint32_t x0, y0, z0, m0, x1, y1, z1, m1, xx, yy, zz, mm;
+  rx_keys(p0, x0, y0, z0, m0, xx, yy, zz, mm);
+  rx_keys(p1, x1, y1, z1, m1, xx, yy, zz, mm);
+  const PhKeyH k0 = ph_hash(t, x0, y0, z0, m0), k1 = ph_hash(t, x1, y1, z1, m1);
+  const uint32_t d0 = lds_disp1(Dl, t, need0, k0), d1 = lds_disp1(Dl, t, need1, k1);
+  v4u32 s0, s1;
+  asm_slot1(T, t, need0, k0, d0, s0);
+  asm_slot1(T, t, need1, k1, d1, s1);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s0), "+v"(s1) :: "memory");
+  w0 = need0 ? ph_hitv(s0, x0, y0, z0, m0) : 0u;
+  w1 = need1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
 }
 
 /* both lookups, synchronous (tile 0's carried-cache check, the generic rounds) */
@@ -1386,8 +1407,13 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       x1 = x1 && n1;
       STAMP(4);
       if (__ballot(x0 || x1)) {
-        const uint32_t wx0 = x_probe(T, Dl, a, pr[0], x0);
-        const uint32_t wx1 = x_probe(T, Dl, a, pr[1], x1);
+        uint32_t wx0, wx1;
+        if (USN_X_BATCH) {
+          x_probe2(T, Dl, a, pr[0], x0, pr[1], x1, wx0, wx1);
+        } else {   // A/B: one round after the other
+          wx0 = x_probe(T, Dl, a, pr[0], x0);
+          wx1 = x_probe(T, Dl, a, pr[1], x1);
+        }
         if (x0) w01 = wx0;
         if (x1) w11 = wx1;
       }
