@@ -69,22 +69,30 @@ __global__ __launch_bounds__(256) void probe(const v4u *frames, const v4u *t1, c
  * its frame from LDS.  PROBES: then the two-table probe of mode 2 keyed by
  * the frame's bytes. */
 typedef __attribute__((address_space(3))) void lds_void_t;
-template <bool PROBES>
+template <bool PROBES, int PARTS = 3>
 __global__ __launch_bounds__(256) void glds_stream(const uint8_t *frames, const v4u *t1, const v4u *t2,
                                                    uint32_t m1, uint32_t m2, uint32_t n, uint32_t *out) {
+  // PARTS 3: bytes 0..47 of each frame; PARTS 2: bytes 12..43 (what the rx parse reads)
+  constexpr uint32_t OFF = PARTS == 2 ? 12u : 0u;
   __shared__ v4u st[4][192];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t f0 = blockIdx.x * 256 + wave * 64;
   if (f0 >= n) return;
 #pragma unroll
-  for (uint32_t k = 0; k < 3; ++k) {
-    const uint32_t u = 64 * k + lane, f = u / 3, part = u - 3 * f;
-    __builtin_amdgcn_global_load_lds(frames + (size_t)(f0 + f) * 64 + part * 16,
+  for (uint32_t k = 0; k < PARTS; ++k) {
+    const uint32_t u = 64 * k + lane, f = u / PARTS, part = u - PARTS * f;
+    __builtin_amdgcn_global_load_lds(frames + (size_t)(f0 + f) * 64 + OFF + part * 16,
                                      (lds_void_t *)(&st[wave][64 * k]), 16, 0, 2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const v4u a = st[wave][3 * lane], b = st[wave][3 * lane + 1], c = st[wave][3 * lane + 2];
-  uint32_t x = a.x ^ a.w ^ b.y ^ b.z ^ c.x ^ c.y;
+  uint32_t x;
+  if (PARTS == 3) {
+    const v4u a = st[wave][3 * lane], b = st[wave][3 * lane + 1], c = st[wave][3 * lane + 2];
+    x = a.x ^ a.w ^ b.y ^ b.z ^ c.x ^ c.y;
+  } else {
+    const v4u a = st[wave][2 * lane], b = st[wave][2 * lane + 1];
+    x = a.x ^ a.w ^ b.y ^ b.z;
+  }
   if (PROBES) {
     const uint32_t key = mix(x ^ ((f0 + lane) * 0x9e3779b9u));
     const v4u s1 = t1[mix(key) % m1];
@@ -97,19 +105,19 @@ __global__ __launch_bounds__(256) void glds_stream(const uint8_t *frames, const 
   out[f0 + lane] = x;
 }
 
-template <bool PROBES>
+template <bool PROBES, int PARTS = 3>
 static void run_glds(const uint8_t *f, const v4u *t1, const v4u *t2, uint32_t m, uint32_t n, uint32_t *out,
                      int launches) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const dim3 g((n + 255) / 256), b(256);
-  for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(glds_stream<PROBES>, g, b, 0, 0, f, t1, t2, m, m, n, out);
+  for (int k = 0; k < 3; ++k) hipLaunchKernelGGL((glds_stream<PROBES, PARTS>), g, b, 0, 0, f, t1, t2, m, m, n, out);
   CK(hipDeviceSynchronize());
   std::vector<float> ms;
   for (int k = 0; k < launches; ++k) {
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(glds_stream<PROBES>, g, b, 0, 0, f, t1, t2, m, m, n, out);
+    hipLaunchKernelGGL((glds_stream<PROBES, PARTS>), g, b, 0, 0, f, t1, t2, m, m, n, out);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float t;
@@ -118,8 +126,8 @@ static void run_glds(const uint8_t *f, const v4u *t1, const v4u *t2, uint32_t m,
   }
   std::sort(ms.begin(), ms.end());
   const double us = ms[ms.size() / 2] * 1e3;
-  printf("{\"mode\": \"glds stream%s\", \"frames\": %u, \"table_slots\": %u, \"us_median\": %.2f}\n",
-         PROBES ? "+probes" : "", n, m, us);
+  printf("{\"mode\": \"glds stream%s %d parts\", \"frames\": %u, \"table_slots\": %u, \"us_median\": %.2f}\n",
+         PROBES ? "+probes" : "", PARTS, n, m, us);
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
 }
@@ -293,6 +301,10 @@ int main(int argc, char **argv) {
   }
   run_glds<false>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
   run_glds<true>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
+  run_glds<false, 2>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
+  run_glds<true, 2>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
+  run_glds<false>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
+  run_glds<false, 2>(reinterpret_cast<const uint8_t *>(f), t1, t2, m, n, out, launches);
   run_batched<1>(t1, t2, m, n, out, launches);
   run_batched<2>(t1, t2, m, n, out, launches);
   run_batched<4>(t1, t2, m, n, out, launches);

@@ -1,0 +1,15 @@
+# r02bg: 32-byte header stage (bytes 12..43, two LDS-DMA parts per frame): parity, A/B c5 / c4 / c2, bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02bg
+mkdir -p $O
+export TMPDIR=/tmp
+fatal() { [ $1 -ge 124 ] || [ $1 -eq 134 ] || [ $1 -eq 139 ]; }
+step() { name=$1; to=$2; shift 2; echo "-- $name $(date +%T)"; timeout -k 10 $to "$@" > $O/$name.log 2>&1; rc=$?; echo "== $name rc=$rc"; grep -v "^\s\|^ Kernel\|^VGPU\|^W20\|^E20\|tx state\|\"batch\"" $O/$name.log | tail -${TAILN:-4} | cut -c1-400; fatal $rc && exit $rc; return 0; }
+step pytest_par 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_volume.py tests/test_gpu_window.py -m gpu -x -q --timeout 300 --timeout-method thread
+for c in c5 c4; do
+  step abl_$c 300 python tools/abl.py --config $c --frames 8388608 --batches 2 --rounds 5 --launches 40 base stage48
+done
+step abl_c2 300 python tools/abl.py --config c2 --frames 1048576 --batches 8 --multi 8 --rounds 5 --launches 40 base stage48
+step bench 600 python bench.py --steps 20 --warmup 5
+exit 0

@@ -46,8 +46,13 @@ using namespace ::usn;
 #define NTHREADS USN_NTHREADS   /* 256, 512 or 1024 threads per 1024-frame tile */
 #define ROUNDS (TILE / NTHREADS)
 #define NSEG (TILE / 64)
-#define GLDS_PARTS 3u                            /* 16-byte parts of a frame in the header stage */
-#define STAGE_ROUND_SLOTS (64u * GLDS_PARTS)     /* 16-byte slots per wave and round */
+#ifndef USN_STAGE32   /* header stage: bytes 12..43 of a frame (2 parts), else 0..47 (3) */
+#define USN_STAGE32 1
+#endif
+#define GLDS_PARTS (USN_STAGE32 ? 2u : 3u)       /* 16-byte LDS-DMA parts per frame and round */
+#define GLDS_OFF (USN_STAGE32 ? 12u : 0u)        /* first byte of a frame in the stage */
+#define STAGE_ROUND_SLOTS (64u * 3u)             /* 16-byte slots per wave and round (the sort
+                                                    also counts in the stage: 24 KiB at 512 threads) */
 #define MAX_NBITS 13   /* nbins <= USN_MAX_ENDPOINTS + 3 <= 8192 */
 #define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule images up to 32 KiB live in LDS */
 /* the LDS copy of the image, rounded up to whole 64-unit glds chunks */
@@ -1129,11 +1134,14 @@ __device__ uint32_t decide_info_rx(const uint4 *T, const uint16_t *Dl, const Cla
   return decide_rx<TM>(T, Dl, a, p);
 }
 
-/* The stage holds bytes 0..47 of each frame (parse reads 12..39; the port
- * words of longer IPv4 headers come from the frame itself): 16-byte part j
- * of frame f at slot 3f + j of a wave's 3 KiB round stage.  glds writes it
- * linearly, and the per-frame ds_read_b128s (a 12-dword stride) cover 16
- * distinct 4-bank groups per 16 lanes: no bank conflicts either way. */
+/* The stage holds bytes 12..43 of each frame (USN_STAGE32; else 0..47): the
+ * parse reads 12..39, and the port words of longer IPv4 headers come from
+ * the frame itself.  16-byte part j of frame f at slot GLDS_PARTS f + j of a
+ * wave's round stage.  glds writes it linearly, and the per-frame
+ * ds_read_b128s (an 8- or 12-dword stride) cover distinct 4-bank groups per
+ * 16 lanes: no bank conflicts either way.  Two parts instead of three: one
+ * DMA instruction less per wave and round, the same HBM lines
+ * (tools/probe_floor: stream + probes 134.7 vs 141.3 us per 8M frames). */
 __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
   return GLDS_PARTS * f + j;
 }
@@ -1178,13 +1186,27 @@ __device__ __forceinline__ void glds_round(const ClassifyArgs &a, uint64_t base,
     const uint32_t f = u / GLDS_PARTS, p = u - GLDS_PARTS * f;
     uint32_t local = r * NTHREADS + wave * 64 + f;
     local = local < nt ? local : nt - 1;          // tail tile: re-read the last frame
-    const uint8_t *src = a.frames + (base + local) * a.stride + p * 16;
+    const uint8_t *src = a.frames + (base + local) * a.stride + GLDS_OFF + p * 16;
     __builtin_amdgcn_global_load_lds(src, (lds_void_t *)(st + 64 * k), 16, 0, GLDS_NT);
   }
 }
 
-/* this lane's frame (parts 0..2: bytes 0..47; parse reads bytes 12..39) */
+/* the staged bytes 12..43 as the 64-byte window words parse() reads
+ * (bytes 0..11 and 44.. read as zero; nothing on the rx path uses them) */
+__device__ __forceinline__ void stage32_words(const v4u32 &a0, const v4u32 &a1, uint4 (&q)[4]) {
+  q[0] = make_uint4(0, 0, 0, a0.x);
+  q[1] = make_uint4(a0.y, a0.z, a0.w, a1.x);
+  q[2] = make_uint4(a1.y, a1.z, a1.w, 0);
+  q[3] = make_uint4(0, 0, 0, 0);
+}
+
+/* this lane's frame (parse reads bytes 12..39) */
 __device__ __forceinline__ void stage_read(const uint4 *st, uint32_t lane, uint4 (&q)[4]) {
+  if (USN_STAGE32) {
+    const uint4 b0 = st[stage_slot(lane, 0)], b1 = st[stage_slot(lane, 1)];
+    stage32_words(v4u32{b0.x, b0.y, b0.z, b0.w}, v4u32{b1.x, b1.y, b1.z, b1.w}, q);
+    return;
+  }
 #pragma unroll
   for (uint32_t j = 0; j < 3; ++j) q[j] = st[stage_slot(lane, j)];
   q[3] = make_uint4(0, 0, 0, 0);
@@ -1193,6 +1215,14 @@ __device__ __forceinline__ void stage_read(const uint4 *st, uint32_t lane, uint4
 /* the same by inline asm: no vmcnt wait of hipcc's (which would also wait
  * for asm probe loads in flight); the caller has waited for the DMA */
 __device__ __forceinline__ void stage_read_asm(const uint4 *st, uint32_t lane, uint4 (&q)[4]) {
+  if (USN_STAGE32) {
+    v4u32 a0, a1;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(a0), "=&v"(a1)
+                 : "v"(lds_addr(st + stage_slot(lane, 0))), "v"(lds_addr(st + stage_slot(lane, 1))));
+    stage32_words(a0, a1, q);
+    return;
+  }
   v4u32 a0, a1, a2;
   asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %5\n\t"
                "s_waitcnt lgkmcnt(0)"
