@@ -80,7 +80,7 @@ def test_random_streams_projection_gpu(seed, tx_frac, coracle_mod):
     want = randtraffic.run_stream(stream, katrun.COracleBackend())
     gb = _gpu()
     got = randtraffic.run_stream(stream, gb)
-    info = (ctypes.c_uint32 * 8)()
+    info = (ctypes.c_uint32 * 10)()
     gb.ctx.L.usn_debug_image_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     assert gb.ctx.L.usn_debug_image_info(gb.ctx.h, info) == 0
     assert info[5] & 4 and info[4] * 16 > 40000   # U built; the image is past LDS

@@ -40,15 +40,15 @@ def _packed(w):
 
 
 def _info(L, h):
-    out = (C.c_uint32 * 8)()
+    out = (C.c_uint32 * 10)()
     assert L.usn_debug_image_info(h, out) == 0
     return list(out)[:6]
 
 
 def _uinfo(L, h):
-    out = (C.c_uint32 * 8)()
+    out = (C.c_uint32 * 10)()
     assert L.usn_debug_image_info(h, out) == 0
-    return list(out)[6:]
+    return list(out)[6:8]
 
 
 def test_image_finds_every_rule_c5():

@@ -1240,6 +1240,8 @@ __device__ __forceinline__ void stage_read_asm(const uint4 *st, uint32_t lane, u
  * 2048-byte stride a frame's read is one scattered HBM access whose cost
  * grows with its bytes: 4M frames in 89 / 108 / 140 us at 32 / 48 / 64 bytes
  * (tools/stride_floor.hip, profiles/r02f). */
+/* (Bytes 12..43 in two dword-aligned 16-byte loads instead, as the 32-byte
+ * stage's DMA does: slower here, c3 1M frames 34.7 vs 33.4 us, profiles/r02bh.) */
 __device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
   const uint4 *w = reinterpret_cast<const uint4 *>(fp);
 #pragma unroll

@@ -1279,8 +1279,8 @@ int usn_debug_image_probe_rx(usn_ctx *c, uint32_t dst, uint32_t src, uint32_t pr
   return (c->probe_mask & 4u) ? 1 : 0;
 }
 
-/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask, mU, mX}
- * (slots and groups of each table, all shards; slots of U and X). */
+/* Test hook: the image's geometry {m0, g0, m1, g1, units, probe_mask, mU, mX,
+ * gU, gX} (slots and groups of each table, all shards). */
 int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   if (!c || !out6) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1295,6 +1295,8 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   out6[4] = (uint32_t)c->img.size(); out6[5] = c->probe_mask;
   out6[6] = c->img_t[2].m << c->img_t[2].shift;
   out6[7] = c->img_t[3].m << c->img_t[3].shift;
+  out6[8] = c->img_t[2].g << c->img_t[2].shift;
+  out6[9] = c->img_t[3].g << c->img_t[3].shift;
   return USN_OK;
 }
 
