@@ -1,0 +1,12 @@
+# r02bj: U and X placed in 16K-key shards (parallel rebuild): parity, c5 A/B vs no U, bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02bj
+mkdir -p $O
+export TMPDIR=/tmp
+fatal() { [ $1 -ge 124 ] || [ $1 -eq 134 ] || [ $1 -eq 139 ]; }
+step() { name=$1; to=$2; shift 2; echo "-- $name $(date +%T)"; timeout -k 10 $to "$@" > $O/$name.log 2>&1; rc=$?; echo "== $name rc=$rc"; grep -v "^\s\|^ Kernel\|^VGPU\|^W20\|^E20\|tx state\|\"batch\"" $O/$name.log | tail -${TAILN:-4} | cut -c1-400; fatal $rc && exit $rc; return 0; }
+step pytest_par 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_volume.py -m gpu -x -q --timeout 300 --timeout-method thread
+step abl_c5 300 python tools/abl.py --config c5 --frames 8388608 --batches 2 --rounds 5 --launches 40 base base@USN_NO_PROJ=1
+step bench 600 python bench.py --steps 20 --warmup 5
+exit 0

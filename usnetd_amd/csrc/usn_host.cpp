@@ -503,14 +503,14 @@ void parallel_for(uint32_t jobs, uint32_t threads, F f) {
  * (shard after shard) */
 bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
               std::vector<uint16_t> &disp, double load0, uint32_t group, uint32_t threads,
-              const uint4 &empty = make_uint4(0, 0, 0, 0)) {
+              const uint4 &empty = make_uint4(0, 0, 0, 0), uint32_t shard_keys = USN_PH_SHARD_KEYS) {
   const uint32_t n = (uint32_t)keys.size();
   t = usn_ph_table{};
   slots.clear();
   disp.clear();
   if (n == 0) return true;
   uint32_t shift = 0;
-  while ((n >> shift) > USN_PH_SHARD_KEYS && shift < 16) ++shift;
+  while ((n >> shift) > shard_keys && shift < 16) ++shift;
   const uint32_t S = 1u << shift;
   double load = load0;
   std::vector<std::vector<PhKey>> part(S);
@@ -560,8 +560,10 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
 void proj_keys(const std::vector<PhKey> *keys, std::vector<PhKey> &ukeys, std::vector<PhKey> &xkeys) {
   struct Ent { uint32_t dst, e, o1, o2, src, sport; bool more; };
   std::vector<Ent> ents;
-  std::unordered_map<uint64_t, uint32_t> at;
-  at.reserve(keys[0].size() + keys[1].size());
+  ents.reserve(keys[0].size() + keys[1].size());
+  // projection -> entry: flat open addressing (E < 2^19, so ~0 is never a key)
+  const uint32_t cap = next_pow2(2 * (uint32_t)(keys[0].size() + keys[1].size()) + 16);
+  std::vector<std::pair<uint64_t, uint32_t>> at(cap, {~0ull, 0u});
   auto code = [](const uint4 &e) {
     return (e.w & USN_SLOT_NICOWNER) ? USN_U_NIC : (e.w >> 16);
   };
@@ -572,14 +574,15 @@ void proj_keys(const std::vector<PhKey> *keys, std::vector<PhKey> &ukeys, std::v
       if (has && usn_u_pidx(proto) == 7u) continue;   // never matched
       const uint32_t E = usn_u_e(proto, has, k.e.z & 0xFFFFu);
       const uint64_t pk = (uint64_t)k.e.x << 32 | E;
-      auto it = at.find(pk);
+      uint32_t h = usn_key_hash(k.e.x, 0u, E, 0u) & (cap - 1);
+      while (at[h].first != ~0ull && at[h].first != pk) h = (h + 1) & (cap - 1);
       uint32_t i;
-      if (it == at.end()) {
+      if (at[h].first == ~0ull) {
         i = (uint32_t)ents.size();
-        at.emplace(pk, i);
+        at[h] = {pk, i};
         ents.push_back(Ent{k.e.x, E, USN_U_NONE, USN_U_NONE, 0u, 0u, false});
       } else {
-        i = it->second;
+        i = at[h].second;
       }
       Ent &en = ents[i];
       if (t == 1) {
@@ -637,8 +640,11 @@ int build_image(usn_ctx *c) {
     const uint32_t nt = proj ? 4u : 2u;
     auto one = [&](uint32_t i, uint32_t threads) {
       const uint4 empty = i == 2 ? make_uint4(0, 0, 0, USN_U_EMPTY_W) : make_uint4(0, 0, 0, 0);
+      // U and X in shards of up to 16K keys: placed in parallel (an AddMatch
+      // rebuilds the image before the next batch)
+      const uint32_t shard_keys = i >= 2 ? 16384u : USN_PH_SHARD_KEYS;
       for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
-        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads, empty)) {
+        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads, empty, shard_keys)) {
           placed[i] = true;
           break;
         }
