@@ -235,3 +235,19 @@ def test_projection_image_off(monkeypatch):
     r, out = _rx_probe(L, h, lib.ip2int("10.0.0.1"), 5, 6, 1, 80, 1234)
     assert r == 0 and out[3] == 0x10002 and out[0] == 0
     L.usn_ctx_destroy(h)
+
+
+def test_projection_image_only_unmatchable_rules():
+    """Rules no frame can hit (ports on a protocol without ports) leave U
+    unbuilt: the K1 / K2 path answers (a miss), never an empty U table."""
+    L, h = _ctx()
+    L.usn_debug_image_probe_rx.argtypes = [C.c_void_p] + [C.c_uint32] * 6 + [C.c_void_p]
+    assert L.usn_endpoint_add(h, 0, 0, -1) == 0
+    assert L.usn_endpoint_add(h, 2, 2, 0) == 0
+    w = lib.make_want("0.0.0.0", 50, 0)          # ESP has no ports: never matched
+    assert L.usn_add_match(h, C.byref(w), 2, 0) == 1
+    r, out = _rx_probe(L, h, 0, 0, 6, 1, 0, 0)
+    assert r == 0 and out == [0, 0, 0, 0]
+    _, _, _, _, _, pmask = _info(L, h)
+    assert pmask & 4 == 0
+    L.usn_ctx_destroy(h)

@@ -626,9 +626,13 @@ int build_image(usn_ctx *c) {
     pk.h2 = pk.grp = 0;
     keys[t].push_back(pk);
   }
-  const bool proj = c->proj && (keys[0].size() + keys[1].size()) > 0 &&
-                    keys[0].size() + keys[1].size() <= USN_U_MAX_KEYS;
+  bool proj = c->proj && (keys[0].size() + keys[1].size()) > 0 &&
+              keys[0].size() + keys[1].size() <= USN_U_MAX_KEYS;
   if (proj) proj_keys(keys, keys[2], keys[3]);
+  if (keys[2].empty()) {   // no rule a frame can hit: nothing for U to answer
+    proj = false;
+    keys[3].clear();
+  }
   clk.mark("keys");
   std::vector<uint4> slots[4];
   std::vector<uint16_t> disp[4];
