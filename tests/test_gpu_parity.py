@@ -108,7 +108,9 @@ def _oracle_lists(d, n_ep):
     # ragged last tiles; c5's 1005 bins take the radix order in both builds
     ("c3", 5003, None), ("c4", 70001, None), ("c5", 100003, "0"), ("c5", 100003, "1"),
     # 4093 pipes + NIC + host ring: the whole 12-bit endpoint id space (4098 bins, 3 radix passes)
-    ("c5-4093", 300007, None)])
+    ("c5-4093", 300007, None),
+    # connected rules on listening ports: most frames also probe the overflow table X
+    ("c5x", 1 << 20, None)])
 def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     from usnetd_amd import lib, traffic
     if t512 is not None:   # USN_T512 (read at context creation): force one build

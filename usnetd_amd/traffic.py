@@ -8,6 +8,7 @@
       (512 listening + 512 connected), 2048 B stride (netmap slots)
   c4  IPv4 70 % / IPv6 10 % / ARP 10 % / 802.1Q 10 %, 4096 rules
   c5  64 B, 65536 rules (16 IPs x 2048 listening ports + 32768 connected)
+  c5x c5 with the connected rules on 64 of the listening ports (overflow-heavy)
 
 Frames are generated directly into their HBM layout (fixed stride); every
 frame start has 64 readable bytes.  Data is synthetic (no captures).  A
@@ -126,7 +127,8 @@ def c2(n=1 << 20, seed=2):
     return Config("c2", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(16), rules)
 
 
-def _listen_conn_rules(rng, n_listen, n_conn, n_ips, n_ep, protos=(TCP, UDP), icmp=True):
+def _listen_conn_rules(rng, n_listen, n_conn, n_ips, n_ep, protos=(TCP, UDP), icmp=True,
+                       conn_ports=(40000, 50000)):
     ips = LOCAL - np.arange(n_ips, dtype=np.int64)
     rules, listen, conn = [], [], []
     seen = set()
@@ -148,7 +150,7 @@ def _listen_conn_rules(rng, n_listen, n_conn, n_ips, n_ep, protos=(TCP, UDP), ic
     while len(conn) < n_conn:
         ip = int(ips[rng.integers(0, n_ips)])
         proto = protos[int(rng.integers(0, len(protos)))]
-        port = int(rng.integers(40000, 50000))
+        port = int(rng.integers(*conn_ports))
         rsrc = (10 << 24) | int(rng.integers(0, 1 << 20))
         rsport = int(rng.integers(1024, 65536))
         key = (ip, proto, port, rsrc, rsport)
@@ -227,6 +229,20 @@ def c5(n=1 << 23, seed=5, n_ep=1000):
     return Config("c5", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(n_ep), rules)
 
 
+def c5x(n=1 << 23, seed=5, n_ep=1000):
+    """c5 with the connected rules on the listening ports 1000..1063 (a server's
+    accepted connections): ~16 connected rules share each of those projections
+    with a listening rule, so most frames of the projection table's path also
+    read its overflow table X (its worst case, not a BASELINE config)."""
+    rng = np.random.default_rng(seed)
+    ips, rules, listen, conn = _listen_conn_rules(np.random.default_rng(5), 16 * 2048, 32768, 16, n_ep,
+                                                  icmp=False, conn_ports=(1000, 1064))
+    dst, src, proto, sport, dport = _ipv4_mix(rng, n, ips, listen, conn, p_icmp=0.0)
+    lens = np.full(n, 64, np.uint16)
+    H = build_ipv4(n, dst, src, proto, sport, dport, lens)
+    return Config("c5x", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(n_ep), rules)
+
+
 def c4tx(n=1 << 18, seed=6, host_at=None):
     """c4's mix SENT by the host endpoint (tx: find_forward with incoming ==
     false, endpoint.rs:194-256), the "ADD_MACS learned-MAC path" of
@@ -287,7 +303,7 @@ def c1fixed(n=1 << 16, seed=1):
     return c1(n=n, variant="fixed", seed=seed)
 
 
-CONFIGS = {"c1": c1, "c1fixed": c1fixed, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4tx": c4tx}
+CONFIGS = {"c1": c1, "c1fixed": c1fixed, "c2": c2, "c3": c3, "c4": c4, "c5": c5, "c4tx": c4tx, "c5x": c5x}
 
 
 def config(name, n=None, seed=None, **kw):
