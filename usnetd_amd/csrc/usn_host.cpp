@@ -124,6 +124,10 @@ class RuleMap {
   using const_iterator = iterator;
 
   size_t size() const { return n_; }
+  /* slot i of the flat array (0 <= i < slots()), or nullptr when it holds no
+   * entry: lets a scan of the map be split over threads */
+  size_t slots() const { return slot_.size(); }
+  const value_type *at_slot(size_t i) const { return slot_[i].state == FULL ? &slot_[i] : nullptr; }
   iterator begin() const { return iterator(self(), 0); }
   iterator end() const { return iterator(self(), slot_.size()); }
   void clear() { for (value_type &v : slot_) v.state = EMPTY; n_ = used_ = 0; }
@@ -416,23 +420,25 @@ uint32_t ph_group_knob() {
 }
 
 struct PhKey {
+  PhKey() {}       // no value-initialisation: vectors of 10^6 keys are resized, then filled
   uint4 e;         // the slot: K1/K2 x, y, z, meta | NICOWNER | owner << 16; U: usn_internal.h
   uint4 k;         // the hashed key (x, y, z, meta): K1/K2 the packed key, U (dst, 0, E, 0)
   uint32_t h2, grp;
 };
 
-/* Place the keys of one shard: m slots, g groups (group = mulhi(h1 << shift,
- * g); h1 of each key in k.grp on entry). */
-bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed, uint32_t shift,
-              const uint4 &empty, std::vector<uint4> &slots, std::vector<uint16_t> &disp) {
-  const uint32_t n = (uint32_t)keys.size();
-  for (PhKey &k : keys) {
+/* Place the n keys of one shard into its m slots and g displacements
+ * (group = mulhi(h1 << shift, g)); the outputs are this shard's part of the
+ * table's arrays. */
+bool ph_place(PhKey *keys, uint32_t n, uint32_t m, uint32_t g, uint32_t seed, uint32_t shift,
+              const uint4 &empty, uint4 *slots, uint16_t *disp) {
+  for (uint32_t i = 0; i < n; ++i) {
+    PhKey &k = keys[i];
     k.grp = usn_mulhi32(usn_ph_h1(k.k.x, k.k.y, k.k.z, k.k.w, seed) << shift, g);
     k.h2 = usn_key_hash2(k.k.x, k.k.y, k.k.z, k.k.w, seed);
   }
   /* members of each group (counting sort), then groups by size, largest first */
   std::vector<uint32_t> start(g + 1, 0), member(n);
-  for (const PhKey &k : keys) start[k.grp + 1]++;
+  for (uint32_t i = 0; i < n; ++i) start[keys[i].grp + 1]++;
   uint32_t maxsz = 0;
   for (uint32_t i = 0; i < g; ++i) maxsz = std::max(maxsz, start[i + 1]);
   for (uint32_t i = 0; i < g; ++i) start[i + 1] += start[i];
@@ -444,8 +450,8 @@ bool ph_place(std::vector<PhKey> &keys, uint32_t m, uint32_t g, uint32_t seed, u
   for (uint32_t i = 0; i < g; ++i) bysz[maxsz - (start[i + 1] - start[i]) + 1]++;
   for (uint32_t s = 0; s <= maxsz; ++s) bysz[s + 1] += bysz[s];
   for (uint32_t i = 0; i < g; ++i) order[bysz[maxsz - (start[i + 1] - start[i])]++] = i;
-  slots.assign(m, empty);
-  disp.assign(g, 0);
+  std::fill(slots, slots + m, empty);
+  std::fill(disp, disp + g, (uint16_t)0);
   std::vector<uint64_t> used((m + 63) / 64, 0);   // a bit per slot: stays in L1/L2
   uint32_t pos[64], h2[64];
   for (uint32_t gi : order) {
@@ -500,7 +506,9 @@ void parallel_for(uint32_t jobs, uint32_t threads, F f) {
 }
 
 /* one table of the image: shards, m, g, seed and its slots / displacements
- * (shard after shard) */
+ * (shard after shard).  The keys are partitioned by shard in parallel (shard
+ * ids, per-chunk counts, scatter) and every shard is placed straight into
+ * its part of `slots` / `disp`. */
 bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slots,
               std::vector<uint16_t> &disp, double load0, uint32_t group, uint32_t threads,
               const uint4 &empty = make_uint4(0, 0, 0, 0), uint32_t shard_keys = USN_PH_SHARD_KEYS) {
@@ -513,40 +521,70 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
   while ((n >> shift) > shard_keys && shift < 16) ++shift;
   const uint32_t S = 1u << shift;
   double load = load0;
-  std::vector<std::vector<PhKey>> part(S);
+  std::vector<PhKey> part;   // the keys, shard after shard (S > 1)
+  std::vector<uint32_t> off(S + 1, 0);
+  StageClock clk("ph_build");
   for (uint32_t attempt = 0; attempt < 12; ++attempt) {
     if (attempt && attempt % 3 == 0) load *= 0.9;
     const uint32_t seed = 0x9E3779B9u * (attempt + 1);
-    for (auto &v : part) v.clear();
+    PhKey *base = keys.data();
     if (S == 1) {
-      part[0] = keys;
+      off[0] = 0;
+      off[1] = n;
     } else {
-      for (const PhKey &k : keys)
-        part[usn_ph_shard(usn_ph_h1(k.k.x, k.k.y, k.k.z, k.k.w, seed), shift)].push_back(k);
+      const uint32_t C = std::max(1u, std::min(threads, n / 4096 + 1));   // chunks
+      std::vector<uint16_t> sid(n);
+      std::vector<uint32_t> cnt((size_t)C * S, 0);
+      parallel_for(C, threads, [&](uint32_t ch) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * ch / C), hi = (uint32_t)((uint64_t)n * (ch + 1) / C);
+        uint32_t *c = cnt.data() + (size_t)ch * S;
+        for (uint32_t i = lo; i < hi; ++i) {
+          const PhKey &k = keys[i];
+          sid[i] = (uint16_t)usn_ph_shard(usn_ph_h1(k.k.x, k.k.y, k.k.z, k.k.w, seed), shift);
+          c[sid[i]]++;
+        }
+      });
+      // chunk-major offsets within each shard keep the keys' order (deterministic)
+      uint32_t run = 0;
+      for (uint32_t sh = 0; sh < S; ++sh) {
+        off[sh] = run;
+        for (uint32_t ch = 0; ch < C; ++ch) {
+          const uint32_t v = cnt[(size_t)ch * S + sh];
+          cnt[(size_t)ch * S + sh] = run;
+          run += v;
+        }
+      }
+      off[S] = run;
+      part.resize(n);
+      parallel_for(C, threads, [&](uint32_t ch) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * ch / C), hi = (uint32_t)((uint64_t)n * (ch + 1) / C);
+        uint32_t *c = cnt.data() + (size_t)ch * S;
+        for (uint32_t i = lo; i < hi; ++i) part[c[sid[i]]++] = keys[i];
+      });
+      base = part.data();
     }
+    clk.mark("partition");
     uint32_t maxc = 0;
-    for (const auto &v : part) maxc = std::max(maxc, (uint32_t)v.size());
+    for (uint32_t sh = 0; sh < S; ++sh) maxc = std::max(maxc, off[sh + 1] - off[sh]);
     const uint32_t m = std::max<uint32_t>(maxc + 1, (uint32_t)((double)maxc / load) + 1);
     const uint32_t g = std::max<uint32_t>(1, (maxc + group - 1) / group);
-    std::vector<std::vector<uint4>> ps(S);
-    std::vector<std::vector<uint16_t>> pd(S);
+    slots.resize((size_t)S * m);
+    disp.resize((size_t)S * g);
     std::vector<uint8_t> ok(S, 0);
     parallel_for(S, threads, [&](uint32_t sh) {
-      ok[sh] = ph_place(part[sh], m, g, seed, shift, empty, ps[sh], pd[sh]) ? 1 : 0;
+      ok[sh] = ph_place(base + off[sh], off[sh + 1] - off[sh], m, g, seed, shift, empty,
+                        slots.data() + (size_t)sh * m, disp.data() + (size_t)sh * g) ? 1 : 0;
     });
+    clk.mark("place");
     if (std::find(ok.begin(), ok.end(), 0) != ok.end()) continue;
-    slots.reserve((size_t)S * m);
-    disp.reserve((size_t)S * g);
-    for (uint32_t sh = 0; sh < S; ++sh) {
-      slots.insert(slots.end(), ps[sh].begin(), ps[sh].end());
-      disp.insert(disp.end(), pd[sh].begin(), pd[sh].end());
-    }
     t.m = m;
     t.g = g;
     t.seed = seed;
     t.shift = shift;
     return true;
   }
+  slots.clear();
+  disp.clear();
   return false;
 }
 
@@ -612,19 +650,52 @@ void proj_keys(const std::vector<PhKey> *keys, std::vector<PhKey> &ukeys, std::v
 int build_image(usn_ctx *c) {
   StageClock clk("build_image");
   std::vector<PhKey> keys[4];
-  for (const auto &kv : c->rules) {
-    const WantKey &k = kv.first;
-    const int t = image_table(k);
-    if (t < 0) continue;
-    const uint16_t owner = kv.second.owner;
-    const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
-    PhKey pk;
-    pk.e = make_uint4(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
-                      usn_key_meta(k.proto, k.present) | (nic ? USN_SLOT_NICOWNER : 0u) |
-                          ((uint32_t)owner << 16));
-    pk.k = make_uint4(pk.e.x, pk.e.y, pk.e.z, pk.e.w & USN_KEY_META_MASK);
-    pk.h2 = pk.grp = 0;
-    keys[t].push_back(pk);
+  const uint32_t hw = std::max(1u, std::min(USN_PH_THREADS, std::thread::hardware_concurrency()));
+  {
+    // the registry scanned in chunks over threads: count per chunk and table,
+    // then each chunk writes its keys at its offsets (the serial order)
+    const size_t NS = c->rules.slots();
+    const uint32_t C = (uint32_t)std::max<size_t>(1, std::min<size_t>(hw, NS / 65536 + 1));
+    std::vector<uint32_t> cnt((size_t)C * 2, 0);
+    auto chunk = [&](uint32_t ch, size_t &lo, size_t &hi) { lo = NS * ch / C; hi = NS * (ch + 1) / C; };
+    parallel_for(C, hw, [&](uint32_t ch) {
+      size_t lo, hi;
+      chunk(ch, lo, hi);
+      for (size_t i = lo; i < hi; ++i)
+        if (const auto *kv = c->rules.at_slot(i)) {
+          const int t = image_table(kv->first);
+          if (t >= 0) cnt[(size_t)ch * 2 + t]++;
+        }
+    });
+    uint32_t tot[2] = {0, 0};
+    for (uint32_t ch = 0; ch < C; ++ch)
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t v = cnt[(size_t)ch * 2 + t];
+        cnt[(size_t)ch * 2 + t] = tot[t];
+        tot[t] += v;
+      }
+    keys[0].resize(tot[0]);
+    keys[1].resize(tot[1]);
+    parallel_for(C, hw, [&](uint32_t ch) {
+      size_t lo, hi;
+      chunk(ch, lo, hi);
+      uint32_t at[2] = {cnt[(size_t)ch * 2], cnt[(size_t)ch * 2 + 1]};
+      for (size_t i = lo; i < hi; ++i) {
+        const auto *kv = c->rules.at_slot(i);
+        if (!kv) continue;
+        const WantKey &k = kv->first;
+        const int t = image_table(k);
+        if (t < 0) continue;
+        const uint16_t owner = kv->second.owner;
+        const bool nic = c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
+        PhKey &pk = keys[t][at[t]++];
+        pk.e = make_uint4(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
+                          usn_key_meta(k.proto, k.present) | (nic ? USN_SLOT_NICOWNER : 0u) |
+                              ((uint32_t)owner << 16));
+        pk.k = make_uint4(pk.e.x, pk.e.y, pk.e.z, pk.e.w & USN_KEY_META_MASK);
+        pk.h2 = pk.grp = 0;
+      }
+    });
   }
   bool proj = c->proj && (keys[0].size() + keys[1].size()) > 0 &&
               keys[0].size() + keys[1].size() <= USN_U_MAX_KEYS;
@@ -640,14 +711,18 @@ int build_image(usn_ctx *c) {
   bool placed[4] = {false, false, !proj, !proj};
   {
     // the tables side by side, each over its shards
-    const uint32_t hw = std::max(1u, std::min(USN_PH_THREADS, std::thread::hardware_concurrency()));
     const uint32_t nt = proj ? 4u : 2u;
+    // beyond U's range the K1/K2 displacements never go to LDS (TM_GLOBAL): half
+    // the keys per displacement there places twice as fast (1.19 M rules: 102
+    // -> 49 ms of placement on 8 threads) for twice the (L2-resident) bytes
+    const bool global_only = keys[0].size() + keys[1].size() > USN_U_MAX_KEYS;
     auto one = [&](uint32_t i, uint32_t threads) {
       const uint4 empty = i == 2 ? make_uint4(0, 0, 0, USN_U_EMPTY_W) : make_uint4(0, 0, 0, 0);
       // U and X in shards of up to 16K keys: placed in parallel (an AddMatch
       // rebuilds the image before the next batch)
       const uint32_t shard_keys = i >= 2 ? 16384u : USN_PH_SHARD_KEYS;
-      for (uint32_t grp = c->ph_group;; grp /= 2) {   // large groups may not place: smaller ones do
+      const uint32_t grp0 = (global_only && i < 2) ? std::min(c->ph_group, 5u) : c->ph_group;
+      for (uint32_t grp = grp0;; grp /= 2) {   // large groups may not place: smaller ones do
         if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads, empty, shard_keys)) {
           placed[i] = true;
           break;
