@@ -236,12 +236,15 @@ def test_offsets_layout(coracle_mod):
     ctx.close()
 
 
-def test_classify_multi_matches_separate(coracle_mod):
+@pytest.mark.parametrize("name", ["c2", "c5"])
+def test_classify_multi_matches_separate(name, coracle_mod):
     """One launch over the drained rings of several NICs (usn_classify_multi)
-    gives each source exactly its sequential decisions and carried cache."""
+    gives each source exactly its sequential decisions and carried cache
+    (c2: the image in LDS; c5: the projection table, whose tile-0 check of
+    each carried cache runs through U too)."""
     import ctypes as C
     from usnetd_amd import lib, traffic
-    cfgs = [traffic.config("c2", n=n, seed=40 + k) for k, n in enumerate([5000, 1024, 20000])]
+    cfgs = [traffic.config(name, n=n, seed=40 + k) for k, n in enumerate([5000, 1024, 20000])]
     ctx = lib.Ctx(0)
     traffic.install_ctx(ctx, cfgs[0])
     nics = [0] + traffic.extra_nics(cfgs[0], 2, ctx)
