@@ -14,8 +14,9 @@ when the timed region starts.  At N=1 the line also carries configs[1] ("c2":
 One step = one poll round: every rx queue the rank owns is drained once (one
 batch per queue, the reference's Endpoint::forward drain of each readable
 ring, /root/reference/src/main.rs:1029-1046), classified on the device with
-usn_classify_multi (up to 8 rings per launch, 2 HIP streams).  c5: 2 queues of
-8M frames per rank = 16M frames per step; c2: 16 queues of 1M.
+usn_classify_multi (up to 16M frames per launch).  c5: 2 queues of 8M frames
+per rank = 16M frames per step, both in one launch on one stream; c2: 16
+queues of 1M, 8 per launch on 2 HIP streams.
 
 Multi-GPU: one process per GPU (torchrun), "replicas only": each rank owns a
 disjoint block of the node's rx queues (usnetd_amd.shard.rank_queues) and a
@@ -42,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 ALGO_BYTES = 64 + 2 + 4 + 2   # header window + length + decision + order index per frame
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-LAUNCH_FRAMES = 1 << 23       # frames per launch the rings are grouped to (8 x 1M, or 1 x 8M)
+LAUNCH_FRAMES = 1 << 24       # frames per launch the rings are grouped to (8 x 1M, or 2 x 8M)
 ROTATE_BYTES = 1 << 30        # distinct batch bytes per rank, > the 256 MiB Infinity Cache
 STRONG_FRAMES = 1 << 26       # --strong: 64M frames per step for the whole job
 METRIC = "Mpkts/s device-resident L4 classify @64B frames; HBM GB/s vs roofline"
@@ -58,8 +59,9 @@ def parse_args():
     ap.add_argument("--config", default="c5")
     ap.add_argument("--frames", type=int, default=0, help="frames per batch (default: config's)")
     ap.add_argument("--queues", type=int, default=0,
-                    help="rx queues per rank (default: 8 rings' worth of launches on 2 streams)")
-    ap.add_argument("--streams", type=int, default=2)
+                    help="rx queues per rank (default: one launch's rings per stream)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="streams (default: 1 when one launch covers a poll round's 16M frames, else 2)")
     ap.add_argument("--rings-per-launch", type=int, default=0,
                     help="rx rings per usn_classify_multi launch (default: 8M frames' worth, <= 8)")
     ap.add_argument("--strong", action="store_true",
@@ -80,8 +82,13 @@ class Run:
     def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong, rings_per_launch=0):
         from usnetd_amd import shard, traffic
         self.L, self.ctx, self.name, self.n = L, ctx, name, n
-        S = max(1, streams)
         P = rings_per_launch or max(1, min(8, LAUNCH_FRAMES // n))   # rings per launch
+        # c4/c5 (8M-frame rings): both rings of a poll round in ONE launch on one
+        # stream, as the daemon's usn_classify_multi does (A/B, profiles/r02cg:
+        # 64.9-65.6 Gpkt/s against 64.8-65.9 for one ring per launch on two
+        # streams, with no dependence on how two streams' launches overlap;
+        # two 2-ring launches on two streams: 61.1-62.0)
+        S = max(1, streams) if streams else (1 if P * n >= LAUNCH_FRAMES else 2)
         if strong:
             total_q = max(world, STRONG_FRAMES // n)
             mine = shard.rank_queues(total_q, world, rank)
