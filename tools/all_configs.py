@@ -20,7 +20,7 @@ RUNS = [
     ("c2", 1 << 20, 16, 2, 400),
     ("c3", 1 << 18, 16, 2, 400),     # IMIX at 2048 B stride: 512 MiB per rotation of 16 rings
     ("c4", 1 << 20, 16, 2, 200),
-    ("c5", 1 << 23, 2, 2, 40),       # 8M frames (512 MiB) per batch, 2 rings
+    ("c5", 1 << 23, 2, 1, 40),       # 8M frames (512 MiB) per batch, 2 rings in one launch (bench default)
 ]
 
 
