@@ -1164,7 +1164,9 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #endif
 #define GD USN_GLDS_DEPTH
 #define NWAVES (NTHREADS / 64)
-#define GLDS_NT 2                /* aux bits of the header glds: non-temporal */
+#ifndef GLDS_NT                  /* aux bits of the header glds: non-temporal */
+#define GLDS_NT 2
+#endif
 #ifndef USN_GLDS_ENABLE          /* A/B only: 0 = register loads for every layout */
 #define USN_GLDS_ENABLE 1
 #endif
