@@ -25,7 +25,12 @@ barrier and the max-over-ranks time).  --strong fixes the whole job's frames
 per step at 64M (c5) and splits the queues over the ranks; the default is
 weak scaling (fixed queues per rank).
 
-Usage: python bench.py [--gpus N --steps K --warmup W] (torchrun for N > 1)
+Usage: python bench.py [--gpus N --steps K --warmup W]
+For N > 1 under torch.distributed.run (WORLD_SIZE set) each process is one
+rank and WORLD_SIZE must equal N.  Without a launcher, `--gpus N` starts N
+rank processes itself (before anything touches the GPU: launch_ranks) and
+prints rank 0's line; "n_gpus" is the number of ranks that joined the process
+group, checked against N.
 """
 from __future__ import annotations
 
@@ -51,7 +56,7 @@ DEFAULT_FRAMES = {"c1": 1 << 20, "c1fixed": 1 << 20, "c2": 1 << 20, "c3": 1 << 1
                   "c5": 1 << 23}
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
@@ -72,7 +77,43 @@ def parse_args():
     ap.add_argument("--launch-probe", type=int, default=150, help="per-launch event pairs")
     ap.add_argument("--ramp", type=int, default=200,
                     help="untimed poll rounds between the probe and the timed steps (clock ramp)")
-    return ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher self-test: ranks join the process group and report, no GPU")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n, port, base_env=None):
+    """The environment of each of the n rank processes launch_ranks starts
+    (torch.distributed.run's variables, rendezvous on 127.0.0.1)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env if base_env is not None else os.environ)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (this process never touches the GPU) and exit with the worst exit
+    status.  Rank 0 prints the JSON line."""
+    import subprocess
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e)
+             for e in rank_envs(n, port)]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 class Run:
@@ -305,11 +346,19 @@ def workload(run, strong):
                run.S, "; strong scaling: 64M frames per step in all" if strong else ""))
 
 
-def main():
-    args = parse_args()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d: refusing to report a different GPU count"
+                 % (args.gpus, world))
+    if args.launch_check:
+        return launch_check(rank, world)
     from usnetd_amd import lib
     L = lib.load()            # the HIP runtime is loaded here, before torch (if any)
     dist = None
@@ -323,6 +372,7 @@ def main():
         if ndev > 0:                       # more ranks than GPUs (a rehearsal): round-robin
             device = local % ndev
     ctx = lib.Ctx(device)
+    joined = joined_ranks(dist, rank, device)   # every rank is in the group, on its device
     n = args.frames or DEFAULT_FRAMES[args.config]
     run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong,
               args.rings_per_launch)
@@ -331,7 +381,7 @@ def main():
         "metric": METRIC,
         "value": res["value"],
         "unit": "Mpkts/s",
-        "n_gpus": world,
+        "n_gpus": len(joined),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": res["ms_per_step"],
@@ -348,6 +398,7 @@ def main():
             "batches_per_launch": run.P,
             "rotating_bytes_per_gpu": run.rotating_bytes,
             "parallelism": "replicas%d" % world,
+            "rank_devices": [d for _, d in joined],
             "event_ms_per_step": res["event_ms_per_step"],
             "untimed_ramp_steps": 2 * args.ramp,
             "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],
@@ -379,6 +430,33 @@ def main():
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:
+        dist.destroy_process_group()
+
+
+def joined_ranks(dist, rank, device):
+    """(rank, HIP device) of every rank in the process group, checked: each
+    rank 0..WORLD_SIZE-1 exactly once (so n_gpus counts ranks that ran)."""
+    from usnetd_amd import shard
+    got = shard.gather_objects((rank, device), dist)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if sorted(r for r, _ in got) != list(range(world)):
+        raise SystemExit("bench.py: ranks %s joined, expected 0..%d" % (got, world - 1))
+    return got
+
+
+def launch_check(rank, world):
+    """--launch-check: the ranks rendezvous over gloo and rank 0 prints who
+    joined (CPU test of launch_ranks; no GPU call)."""
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    joined = joined_ranks(dist, rank, -1)
+    if rank == 0:
+        print(json.dumps({"n_gpus": len(joined), "ranks": [r for r, _ in joined],
+                          "pid": os.getpid()}), flush=True)
+    if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -91,3 +91,21 @@ def test_two_ranks_classify_their_queues(tmp_path):
     assert all(v["bad"] == 0 for v in merged.values()), merged
     assert all(v["hits"] > 0.85 * n for v in merged.values())
     assert d["max_t"] == float(world)
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (both on
+    the box's one GPU: the round-robin rehearsal placement) and reports
+    n_gpus 2 from the ranks that joined, with each rank's device."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                          "--no-extra", "--launch-probe", "4", "--ramp", "2"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and len(line["config"]["rank_devices"]) == 2
+    assert line["value"] > 0

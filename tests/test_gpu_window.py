@@ -129,6 +129,49 @@ def test_window64_ports_past_window(src, coracle_mod):
     ctx.close()
 
 
+@pytest.mark.parametrize("window", [66, 67, 70, 78])
+@pytest.mark.parametrize("src", [0, 1], ids=["rx", "tx"])
+def test_window_not_multiple_of_4(window, src, coracle_mod):
+    """Windows of 66/67/70/78 bytes at stride 80 (usn_batch.window is any
+    value >= 64): every byte of a frame past its window is poisoned in HBM, so
+    a read past the window changes a decision.  IHL 12 frames have their
+    ports at 62..65 (inside a 66-byte window: decided on the device from the
+    reloaded bytes 60..65), IHL >= 13 past it (resolved from the frame
+    reader); bit-exact against the oracle on the whole frames."""
+    from usnetd_amd import lib
+    n = 3000
+    full, lens, ihl = _frames(n, 31 + window + src)
+    eps, rules = _setup()
+    ctx = lib.Ctx(0)
+    o = coracle_mod.Oracle()
+    _install(ctx, o, eps, rules)
+    want = o.forward_batch(src, full.reshape(-1), lens, stride=FULL)
+    dev = np.ascontiguousarray(full[:, :80]).copy()
+    dev[:, window:] = 0xA5                      # poison: never readable
+    b = lib.DeviceBatch(ctx, dev.reshape(-1), lens, src, stride=80, window=window)
+    assert b.desc.window == window
+    r = lib.DeviceResult(ctx, n)
+    s = ctx.stream()
+    ctx.classify(b, r, s)
+    ctx.sync(s)
+    pre = r.decisions()
+    flagged = ((pre >> 20) & 0xF) == lib.R_WINDOW
+    if src == 0:
+        # exactly the TCP/UDP frames whose ports end past the window (18 + hl > window)
+        past = (18 + 4 * ihl > window) & (full[:, 23] != 1)
+        assert np.array_equal(flagged, past)
+        assert not (flagged & (ihl == 12)).any()        # ports at 62..65 lie inside
+    ctx.set_frame_reader(lambda s_, i: full[i, :int(lens[i])].tobytes())
+    ctx.finalize(b, r, s)
+    got = r.decisions()
+    mism = np.nonzero((got & katrun.PARITY_MASK) != (want & katrun.PARITY_MASK))[0]
+    assert mism.size == 0, "first mismatches %s: got %s want %s" % (
+        mism[:5], [hex(x) for x in got[mism[:5]]], [hex(x) for x in want[mism[:5]]])
+    if src == 1:
+        assert ctx.rule_count() == o.rule_count()
+    ctx.close()
+
+
 def test_window64_without_reader_is_refused(coracle_mod):
     """No frame reader: usn_finalize returns USN_EINVAL and changes nothing."""
     from usnetd_amd import lib
@@ -148,7 +191,17 @@ def test_window64_without_reader_is_refused(coracle_mod):
         with pytest.raises(lib.UsnError, match="EINVAL"):
             ctx.finalize(b, r, s)
         if src == 1:
-            assert ctx.rule_count() == nrules   # nothing learned was applied
+            # nothing learned was applied, and the batch is still pending:
+            # registry calls are busy until a finalize with a reader succeeds
+            with pytest.raises(lib.UsnError, match="EBUSY"):
+                ctx.rule_count()
+            want = o.forward_batch(1, full.reshape(-1), lens, stride=FULL)
+            ctx.set_frame_reader(lambda s_, i: full[i, :int(lens[i])].tobytes())
+            ctx.finalize(b, r, s)
+            got = r.decisions()
+            assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK)
+            assert ctx.rule_count() == o.rule_count()
+            ctx.set_frame_reader(None)
     ctx.close()
 
 

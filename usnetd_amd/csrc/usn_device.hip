@@ -169,13 +169,16 @@ __device__ __forceinline__ void parse(const uint4 q[4], uint32_t len, const uint
   // reload goes to its own registers (defaults are constants, so nothing
   // waits on this round's headers before the branch) and is waited for in
   // the branch: a wait after the join would be vmcnt(0) on every path and
-  // drain the next round's prefetch.
+  // drain the next round's prefetch.  The reload reads bytes 12+hl .. 17+hl
+  // (a dword, then the dport halfword), never past the ports' last byte, so
+  // `18 + hl <= window` is exactly what it needs for any window (a second
+  // dword would end at 19+hl: 1-2 bytes past a window of 66 or 67).
   uint32_t ra = 0, rb = 0;
   const bool beyond = has && 18u + hl > window;                      // ports at 14+hl..17+hl
   const bool reload = has && ihl != 5u && !beyond;
   if (reload) {
     ra = *reinterpret_cast<const uint32_t *>(frame + 12 + hl);
-    rb = *reinterpret_cast<const uint32_t *>(frame + 16 + hl);
+    rb = *reinterpret_cast<const uint16_t *>(frame + 16 + hl);
     __builtin_amdgcn_s_waitcnt(0);
   }
   const uint32_t a = reload ? ra : w8, b = reload ? rb : w9;

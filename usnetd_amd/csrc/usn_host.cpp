@@ -385,6 +385,10 @@ struct Chain {
   const usn_summary *summary = nullptr;
   uint32_t state = 0, dst = 0;      // explicit state when !device_chain
   uint32_t info[4] = {0, 0, 0, 0};
+  /* recorded on the stream of the source's last batch, one per replica
+   * (created on that replica's device): chain_to_host waits for it before it
+   * reads that batch's summary and tile headers */
+  hipEvent_t done[USN_MAX_REPLICAS] = {};
 };
 
 struct ParsedH {   // host-side extract_pkt_info result
@@ -474,6 +478,10 @@ struct usn_ctx {
   /* host frame reader: frames whose ports lie past the batch window */
   usn_frame_reader reader = nullptr;
   void *reader_user = nullptr;
+  /* the replica each classified result (keyed by its decisions array) was
+   * classified on: usn_finalize acts on the batch's own replica, not on the
+   * replica of the source's latest batch */
+  std::unordered_map<const void *, uint32_t> batch_rep;
 };
 
 namespace {
@@ -1263,6 +1271,12 @@ void usn_ctx_destroy(usn_ctx *c) {
                     (void *)R.counters, (void *)R.listen})
       if (p) (void)hipFree(p);
   }
+  for (Chain &ch : c->chains)
+    for (uint32_t k = 0; k < USN_MAX_REPLICAS; ++k)
+      if (ch.done[k]) {
+        (void)hipSetDevice(c->reps[k].device);
+        (void)hipEventDestroy(ch.done[k]);
+      }
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
   if (c->h_items) (void)hipHostFree(c->h_items);
@@ -1690,6 +1704,8 @@ static int tx_listen(Replica &T, const Ep &S, uint32_t &n_listen) {
  * as the kernel's resolve_carry would. */
 static int chain_to_host(usn_ctx *c, Chain &ch) {
   HIPCHK(hipSetDevice(c->reps[ch.replica].device));
+  // that batch may still be in flight on its (non-blocking) stream
+  if (ch.done[ch.replica]) HIPCHK(hipEventSynchronize(ch.done[ch.replica]));
   usn_summary ps;
   HIPCHK(hipMemcpy(&ps, ch.summary, sizeof ps, hipMemcpyDeviceToHost));
   uint32_t st = 0, dst = 0, info[4] = {0, 0, 0, 0};
@@ -1806,6 +1822,9 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     ch.tiles = r[k].tiles;
     ch.ntiles = m.b[k].ntiles;
     ch.summary = r[k].summary;
+    if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
+    c->batch_rep[r[k].decisions] = rep;
   }
   return USN_OK;
 }
@@ -1818,6 +1837,10 @@ int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
 namespace {
 
 uint32_t batch_window(const usn_batch *b) { return b->window ? b->window : USN_WINDOW; }
+
+/* internal: finalize_tx refused before any side effect for want of a frame
+ * reader (usn_finalize returns USN_EINVAL and keeps the batch pending) */
+constexpr int USN_EAGAIN_READER = -1000;
 
 /* extract_pkt_info would read the L4 ports (pkt.rs:177-186, bytes 14+hl ..
  * 17+hl) past the first `have` bytes of this frame: the kernel's status 5 */
@@ -2032,7 +2055,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   HostView hv{c, b, r, s, {}, {}, false, false};
   st = hv.fetch_dec();
   if (st) return st;
-  if (!c->reader && needs_reader(hv.dec, hosts)) return USN_EINVAL;   // before any side effect
+  if (!c->reader && needs_reader(hv.dec, hosts)) return USN_EAGAIN_READER;   // before any side effect
   clk.mark("decisions");
   uint64_t h = n;
   if (cnt[1]) h = 0;
@@ -2230,15 +2253,20 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   if (c->reps.empty()) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
   const bool txb = c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions;
-  const uint32_t rep = txb ? c->tx.replica : c->chains[b->src_endpoint].replica;
+  const auto br = c->batch_rep.find(r->decisions);
+  const uint32_t rep = txb ? c->tx.replica
+                     : br != c->batch_rep.end() ? br->second : c->chains[b->src_endpoint].replica;
   HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
   if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
     if (c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions) {
       const int st = finalize_tx(c, b, r, s, info);
-      c->tx.pending = false;
-      return st;
+      // refused before any side effect (a frame needs the frame reader and
+      // none is set): the batch stays pending, so a call after
+      // usn_set_frame_reader applies what it learned
+      if (st != USN_EAGAIN_READER) c->tx.pending = false;
+      return st == USN_EAGAIN_READER ? USN_EINVAL : st;
     }
     if (c->tx.pending) return USN_EBUSY;
     /* an already finalized tx batch: its results are final */
