@@ -56,6 +56,13 @@ DEFAULT_FRAMES = {"c1": 1 << 20, "c1fixed": 1 << 20, "c2": 1 << 20, "c3": 1 << 1
                   "c5": 1 << 23}
 
 
+def launch_frames(name):
+    """Frames per classify launch of a config in the bench's launch shape
+    (Run: up to 8 rings of the config's batch size, at most 16M frames)."""
+    n = DEFAULT_FRAMES[name]
+    return n * max(1, min(8, LAUNCH_FRAMES // n))
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
