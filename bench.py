@@ -46,7 +46,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ALGO_BYTES = 64 + 2 + 4 + 2   # header window + length + decision + order index per frame
+ALGO_BYTES = 64 + 2 + 4 + 4   # header window + length + decision + per-endpoint list entry per frame
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 LAUNCH_FRAMES = 1 << 24       # frames per launch the rings are grouped to (8 x 1M, or 2 x 8M)
 ROTATE_BYTES = 1 << 30        # distinct batch bytes per rank, > the 256 MiB Infinity Cache
@@ -312,12 +312,13 @@ def measure(run, args, dist, world):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": None,
-        "kernel": "classify_rx_kernel",
+        "kernel": "classify_rx_kernel + per-endpoint scatter (scan_agg, scan_off, scatter_kernel)",
         "kernel_us_median": round(kern_ms * 1e3, 3) if kern_ms else None,
         "frames_per_launch": probe_frames,
         "algo_bytes_per_frame": ALGO_BYTES,
-        "achieved_basis": "algorithmic bytes of one launch / its median duration (HIP events on "
-                          "its stream, launches serialised on one stream)",
+        "achieved_basis": "algorithmic bytes of one usn_classify_multi call (its four kernels) / "
+                          "its median duration (HIP events on its stream, calls serialised on one "
+                          "stream)",
         # the timed region (launches overlapping on the streams): per GPU,
         # algorithmic bytes of all its frames / the timed region's wall time
         "achieved_steady_state": round(ALGO_BYTES * args.steps * run.frames_per_step() / elapsed

@@ -33,10 +33,10 @@
 extern "C" {
 #endif
 
-#define USN_ABI_VERSION 2
+#define USN_ABI_VERSION 3
 #define USN_WINDOW 64     /* default readable header bytes at every frame start (usn_batch.window) */
 #define USN_WINDOW_MAX 80 /* the most extract_pkt_info ever reads: L4 ports of IHL 15 end at byte 78 */
-#define USN_TILE 1024     /* frames per tile of the per-endpoint order output */
+#define USN_TILE 1024     /* frames per tile (one classify workgroup; tile headers) */
 #define USN_MAX_ENDPOINTS 4095 /* endpoint ids 0..4094 (0xFFFF = none); netmap pipe ids are 12 bits
                                   (/root/reference/src/devices.rs:36-37) */
 
@@ -124,10 +124,9 @@ typedef struct {
  * so no device-wide atomics and no per-batch memset are needed). */
 typedef struct {
   uint16_t n_frames;       /* frames in this tile */
-  uint16_t n_runs;         /* entries of runs[] used by this tile */
+  uint16_t _r0;
   uint16_t n_host;         /* frames of this tile listed for the ordered host stage */
-  uint16_t bin_nic;        /* bins of order/runs: endpoint ids 0..bin_nic-1, then bin_nic = NIC
-                              (Target::Nic, the source's NIC), bin_nic+1 = FLOOD, +2 = DROP */
+  uint16_t bin_nic;        /* = usn_summary.n_ep: the bin of Target::Nic (see usn_result.index) */
   uint16_t class_count[4]; /* frames per decision class (before host fix-ups) */
   uint32_t last_state;     /* internal: 1-entry cache state after this tile */
   uint32_t last_dst;
@@ -144,21 +143,42 @@ typedef struct {
   uint32_t n_tiles;
   uint32_t cin_state, cin_dst, cin_info[4];   /* carried-in cache as resolved on device */
   uint32_t cout_state, cout_dst, cout_info[4];/* carried-out override (finalize) */
-} usn_summary;             /* 64 bytes */
+  uint32_t n_ep;           /* endpoint bins of usn_result.index: bins 0..n_ep-1 are endpoint ids,
+                              n_ep = NIC, n_ep+1 = FLOOD, n_ep+2 = DROP */
+  uint32_t n_bins;         /* n_ep + 3: usn_result.bin_off has n_bins + 1 entries */
+  uint32_t _pad[2];
+} usn_summary;             /* 80 bytes */
 #define USN_S_STALE 1u         /* carried cache entry disagrees with the current table */
 #define USN_S_STALE_EXTENDS 2u /* stale prefix may continue past tile 0 */
 #define USN_S_COUT 8u          /* cout_* is authoritative (set by finalize) */
 
-/* Result buffers (device), carved by usn_result_bind from one allocation. */
+/* Result buffers (device), carved by usn_result_bind from one allocation.
+ *
+ * The per-endpoint output (SURVEY §2 scatter_by_endpoint; the reference
+ * writes each frame straight into its target's ring, endpoint.rs:61-74, and
+ * copies FLOOD frames to every other endpoint, :340-363): `index` holds the
+ * batch's frame indices grouped by bin and in frame order within each bin,
+ * bin b's frames at index[bin_off[b] .. bin_off[b+1]).  Bins are the
+ * endpoint ids 0..n_ep-1, then NIC (Target::Nic, the source's NIC), FLOOD
+ * (mirror_to_all: every endpoint but the source) and DROP; n_ep and n_bins
+ * are in the summary.  An endpoint receives its own list merged in frame
+ * order with the FLOOD list.  Both are final after usn_classify (stream
+ * order), and again after usn_finalize where the host stage patched
+ * decisions. */
 typedef struct {
   uint32_t *decisions;     /* n decision words */
-  uint16_t *order;         /* n: per tile, tile-local frame indices stably sorted by bin */
-  uint32_t *runs;          /* per tile USN_TILE slots: (bin << 16) | start, n_runs used */
+  uint32_t *index;         /* n: frame indices grouped by bin, stable */
+  uint32_t *bin_off;       /* USN_MAX_BINS + 1: bin b = index[bin_off[b] .. bin_off[b+1]) */
   usn_tile_hdr *tiles;     /* ceil(n / USN_TILE) */
   usn_summary *summary;    /* 1 */
   uint32_t *host_list;     /* per tile USN_TILE slots: frames for the ordered host stage */
+  void *scratch;           /* device scratch of the per-endpoint scatter (per-tile bin counts
+                              and list offsets) */
   uint64_t n;
+  uint32_t max_bins;       /* bins the scratch holds (a batch with more endpoints: USN_ERANGE) */
+  uint32_t _pad;
 } usn_result;
+#define USN_MAX_BINS (USN_MAX_ENDPOINTS + 3)
 
 /* Per-batch outcome of the ordered host stage. */
 typedef struct {
@@ -248,11 +268,18 @@ int usn_bridge_set(usn_ctx *ctx, const uint8_t (*macs)[6], uint32_t n);
 int usn_frag_clear(usn_ctx *ctx);
 
 /* ---- the hot path ------------------------------------------------------------ */
+/* Bytes of a result for n frames, sized for any endpoint count (USN_MAX_BINS:
+ * about 24 bytes of scatter scratch per frame); usn_result_bytes_ep sizes it
+ * for endpoint ids < max_endpoints (max id + 1; c5's 1002 endpoints: 6 bytes
+ * per frame).  usn_result_bind carves a buffer of `bytes` and sets max_bins
+ * from what the scratch holds. */
 size_t usn_result_bytes(uint64_t n);
+size_t usn_result_bytes_ep(uint64_t n, uint32_t max_endpoints);
 int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
 
 /* Classify one batch on `hip_stream` (hipStream_t; NULL = default stream).
- * Asynchronous: writes decisions, per-tile order/runs and the summary.
+ * Asynchronous: writes decisions, the per-endpoint lists (index, bin_off),
+ * tile headers and the summary.
  * Consecutive batches of one source may be enqueued back to back; the 1-entry
  * decision cache is carried on the device from the previous batch's result,
  * which must stay allocated until this call's work has been enqueued.
@@ -269,7 +296,7 @@ int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t
 
 /* Ordered host stage for one classified batch (synchronises the stream).
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
- * frame order and patches decisions/order on the device.  Must be called
+ * frame order and patches decisions and the per-endpoint lists on the device.  Must be called
  * before the next usn_classify of the same source whenever the summary has
  * n_host > 0 or flags != 0; calling it always is allowed. */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(L, n)]
     assert not missing, missing
     assert set(declared()) <= set(lib.EXPORTED)
-    assert L.usn_abi_version() == 2
+    assert L.usn_abi_version() == 3
 
 
 def test_device_code_is_gfx950():
@@ -45,7 +45,12 @@ def test_result_layout():
     base = (ctypes.addressof(buf) + 255) & ~255
     r = lib.Result()
     assert L.usn_result_bind(base, nbytes, n, ctypes.byref(r)) == 0
-    ptrs = [r.decisions, r.order, r.runs, r.tiles, r.summary, r.host_list]
+    ptrs = [r.decisions, r.index, r.bin_off, r.tiles, r.summary, r.host_list, r.scratch]
     assert ptrs == sorted(ptrs) and all(p % 256 == 0 for p in ptrs)
-    assert r.order - r.decisions >= 4 * n
-    assert L.usn_result_bind(base, nbytes - 1, n, ctypes.byref(r)) == -34
+    assert r.index - r.decisions >= 4 * n and r.bin_off - r.index >= 4 * n
+    assert r.max_bins == lib.USN_MAX_BINS            # usn_result_bytes: any endpoint count
+    # sized for endpoint ids < 1002 (c5): a smaller scratch, max_bins 1005
+    small = L.usn_result_bytes_ep(n, 1002)
+    assert small < nbytes
+    assert L.usn_result_bind(base, small, n, ctypes.byref(r)) == 0 and 1005 <= r.max_bins < 1016
+    assert L.usn_result_bind(base, L.usn_result_bytes_ep(n, 0) - 1, n, ctypes.byref(r)) == -34

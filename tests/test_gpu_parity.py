@@ -105,9 +105,9 @@ def _oracle_lists(d, n_ep):
 @pytest.mark.parametrize("name,n,t512", [
     ("c1", 50000, None), ("c2", 1 << 20, None), ("c3", 1 << 17, None), ("c4", 1 << 18, None),
     ("c5", 1 << 20, None),
-    # ragged last tiles; c5's 1005 bins take the radix order in both builds
+    # ragged last tiles; both classify builds for c5
     ("c3", 5003, None), ("c4", 70001, None), ("c5", 100003, "0"), ("c5", 100003, "1"),
-    # 4093 pipes + NIC + host ring: the whole 12-bit endpoint id space (4098 bins, 3 radix passes)
+    # 4093 pipes + NIC + host ring: the whole 12-bit endpoint id space (4098 bins)
     ("c5-4093", 300007, None),
     # connected rules on listening ports: most frames also probe the overflow table X
     ("c5x", 1 << 20, None)])
@@ -134,7 +134,8 @@ def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     assert mism.size == 0, "first mismatches %s: got %s want %s" % (
         mism[:5], [hex(x) for x in got[mism[:5]]], [hex(x) for x in want[mism[:5]]])
     n_ep = max(e[0] for e in cfg.endpoints) + 1
-    lists = lib.per_endpoint_lists(r.order(), r.runs(), r.tiles(), cfg.n)
+    assert int(r.summary()["n_ep"]) == n_ep
+    lists = r.lists(cfg.n)
     ref = _oracle_lists(want, n_ep)
     assert sorted(lists) == sorted(ref)
     for k in ref:

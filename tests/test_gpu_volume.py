@@ -5,7 +5,7 @@ batch).
 Each config streams rotating batches of fresh random traffic (one seed per
 batch, the config's fixed rule table) from several rx queues through the C
 ABI, back to back with the device-carried 1-entry cache, and compares every
-decision (bits [23:0]) and every tile's per-endpoint order with the
+decision (bits [23:0]) and the per-endpoint lists with the
 sequential C oracle.  PARITY UNPINNED beyond the hand-derived fixtures (see
 DESIGN.md "Oracle").
 """
@@ -25,39 +25,17 @@ def coracle_mod():
 
 
 def check_order_vec(r, d, n_ep):
-    """The per-tile order/runs equal the stable sort of each tile's frames by
-    endpoint bin (endpoints, NIC, FLOOD, DROP) -- vectorised for 8M frames."""
+    """The device-wide per-endpoint lists (usn_result.index / bin_off) equal
+    the stable sort of the batch's frames by endpoint bin (endpoints, NIC,
+    FLOOD, DROP) -- vectorised for 8M frames."""
     from usnetd_amd import lib
-    T = lib.USN_TILE
     n = d.shape[0]
-    cls = (d >> 16) & 0xF
-    ep = (d & 0xFFFF).astype(np.int64)
-    bins = np.where(cls == 1, ep, np.where(cls == 2, n_ep, np.where(cls == 3, n_ep + 1, n_ep + 2)))
-    tile = np.arange(n, dtype=np.int64) // T
-    key = tile * (1 << 16) + bins
-    pos = np.argsort(key, kind="stable")
-    want_local = (pos - tile * T).astype(np.uint16)          # tile-major: pos is within its tile
-    order = r.order()
-    ntiles = (n + T - 1) // T
-    got = np.concatenate([order[t * T:t * T + min(T, n - t * T)] for t in range(ntiles)]) \
-        if n % T else order[:n]
-    assert np.array_equal(got, want_local), "per-tile order differs from the stable bin sort"
-    # runs: (bin << 16 | start) where the sorted bin changes inside each tile
-    skey = key[pos]
-    head = np.ones(n, bool)
-    head[1:] = skey[1:] != skey[:-1]
-    hidx = np.nonzero(head)[0]
-    tiles = r.tiles()
-    runs = r.runs()
-    nr = tiles["n_runs"].astype(np.int64)
-    ht = tile[hidx]
-    assert np.array_equal(np.bincount(ht, minlength=ntiles), nr)
-    start = hidx - ht * T
-    want_runs = ((skey[hidx] & 0xFFFF) << 16) | start
-    first = np.concatenate([[0], np.cumsum(nr)[:-1]])
-    got_runs = runs.reshape(-1, T) if runs.size % T == 0 else None
-    k = np.arange(hidx.size) - np.repeat(first, nr)
-    assert np.array_equal(got_runs[ht, k].astype(np.int64), want_runs)
+    bins = lib.dec_bin(d, n_ep)
+    want = np.argsort(bins, kind="stable").astype(np.uint32)
+    off = r.bin_off()
+    assert off.size == n_ep + 4 and off[0] == 0 and off[-1] == n
+    assert np.array_equal(np.diff(off.astype(np.int64)), np.bincount(bins, minlength=n_ep + 3))
+    assert np.array_equal(r.index(n), want), "index differs from the stable bin sort"
 
 
 VOLUME = {          # config: (frames per batch, batches, rx queues)

@@ -1,53 +1,74 @@
 #!/usr/bin/env python3
-"""HBM traffic per classify launch from two rocprofv3 PMC passes (FETCH_SIZE
+"""HBM traffic per classify call from two rocprofv3 PMC passes (FETCH_SIZE
 and WRITE_SIZE collected in separate runs, MI355X_MICROARCH.md §HBM):
   bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024
-FETCH_SIZE is doubled because on gfx950 it reports half of the bytes of a
-16-byte-per-lane streaming read; our frame loads are 16 B per lane, and the
-known read volume of a launch (64 B window + 2 B length per frame) checks the
-factor (printed as fetch_vs_algorithmic).
+FETCH_SIZE is doubled because on gfx950 it tallies the 128-byte requests of
+coalesced streaming reads at 64 B; the known read volume of a call (64 B
+window + 2 B length per frame) checks the factor (fetch_vs_algorithmic).
+
+One usn_classify_multi call = classify_rx_kernel + the per-endpoint scatter
+(scan_agg_kernel, scan_off_kernel, scatter_kernel): the counters of every
+dispatch of these kernels are summed per kernel name and divided by the
+number of classify dispatches covering `frames` frames (every call of the
+run has that shape).
 usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json>"""
 import csv
 import glob
 import json
 import os
-import statistics
 import sys
+from collections import defaultdict
+
+KERNELS = ("classify_rx_kernel", "scan_agg_kernel", "scan_off_kernel", "scatter_kernel")
 
 
-def per_dispatch(d, counter, frames):
-    """Counter values of the classify dispatches covering `frames` frames
-    (1024-frame tiles: grid = frames / 4 threads for 256-thread workgroups,
-    frames / 2 for the 512-thread build)."""
-    vals = []
+def per_kernel(d, counter, frames):
+    """{kernel: summed counter}, and the number of classify dispatches
+    covering `frames` frames (1024-frame tiles of 512 or 256 threads)."""
+    tot = defaultdict(float)
+    calls = 0
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if ("classify_rx_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter
-                    and int(r["Grid_Size"]) in (frames // 4, frames // 2)):
-                vals.append(float(r["Counter_Value"]))
-    return vals
+            if r["Counter_Name"] != counter:
+                continue
+            k = next((k for k in KERNELS if k in r.get("Kernel_Name", "")), None)
+            if k is None:
+                continue
+            tot[k] += float(r["Counter_Value"])
+            if k == "classify_rx_kernel" and int(r["Grid_Size"]) in (frames // 4, frames // 2):
+                calls += 1
+    return tot, calls
 
 
-fd, wd, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-fetch = per_dispatch(fd, "FETCH_SIZE", frames)
-write = per_dispatch(wd, "WRITE_SIZE", frames)
-f_kb = statistics.median(fetch)
-w_kb = statistics.median(write)
-read_algo = frames * (64 + 2)
-write_algo = frames * (4 + 2)
-res = {
-    "frames_per_launch": frames,
-    "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
-    "dispatches": [len(fetch), len(write)],
-    "hbm_read_bytes_per_launch": int(2 * f_kb * 1024),
-    "hbm_write_bytes_per_launch": int(w_kb * 1024),
-    "hbm_bytes_per_launch": int((2 * f_kb + w_kb) * 1024),
-    "algorithmic_bytes_per_launch": frames * 72,
-    "fetch_vs_algorithmic": round(2 * f_kb * 1024 / read_algo, 4),
-    "write_vs_algorithmic": round(w_kb * 1024 / write_algo, 4),
-    "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane loads), WRITE_SIZE x1",
-}
-os.makedirs(os.path.dirname(out), exist_ok=True)
-with open(out, "w") as fh:
-    json.dump(res, fh, indent=1)
-print(json.dumps(res))
+def main():
+    fd, wd, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    fetch, nf = per_kernel(fd, "FETCH_SIZE", frames)
+    write, nw = per_kernel(wd, "WRITE_SIZE", frames)
+    if not nf or not nw:
+        sys.exit("no classify dispatch of %d frames in %s / %s" % (frames, fd, wd))
+    rd = {k: 2 * v * 1024 / nf for k, v in fetch.items()}
+    wr = {k: v * 1024 / nw for k, v in write.items()}
+    read_algo = frames * (64 + 2)
+    write_algo = frames * (4 + 4)
+    res = {
+        "frames_per_launch": frames,
+        "calls": [nf, nw],
+        "hbm_read_bytes_per_launch": int(sum(rd.values())),
+        "hbm_write_bytes_per_launch": int(sum(wr.values())),
+        "hbm_bytes_per_launch": int(sum(rd.values()) + sum(wr.values())),
+        "algorithmic_bytes_per_launch": frames * 74,
+        "per_kernel_read_bytes": {k: int(v) for k, v in rd.items()},
+        "per_kernel_write_bytes": {k: int(v) for k, v in wr.items()},
+        "fetch_vs_algorithmic": round(sum(rd.values()) / read_algo, 4),
+        "write_vs_algorithmic": round(sum(wr.values()) / write_algo, 4),
+        "traffic_vs_algorithmic": round((sum(rd.values()) + sum(wr.values())) / (frames * 74), 4),
+        "correction": "FETCH_SIZE x2 (gfx950, 128-B requests tallied at 64 B), WRITE_SIZE x1",
+    }
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -242,9 +242,6 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_BATCH2
 #define USN_BATCH2 1
 #endif
-#ifndef USN_STAGE_ROWS   /* 64 < bins <= 1024: counting sort with byte rows in the stage */
-#define USN_STAGE_ROWS 1
-#endif
 #ifndef USN_X_BATCH   /* U path: both rounds' X probes in flight together */
 #define USN_X_BATCH 1
 #endif
@@ -638,50 +635,29 @@ __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
 /* --------------------------------------------------------------------------- */
 /* LDS layout of a block                                                        */
 struct Lds {
-  uint16_t *cnt;      // [rows][NSEG]: per-segment counts, then segment prefixes
-  uint16_t *bstart;   // [nbins]: tile totals, then bin starts (64 < nbins <= RADIX_MIN)
+  uint32_t *hist;     // [nbw / 2]: the tile's frames per bin, u16 pairs (tile_hist)
   uint32_t *scratch;  // [16]
-  uint32_t *keys;     // [TILE] (bin << 16 | index) between radix passes (> RADIX_MIN)
-  uint16_t *order;    // [TILE]
+  uint16_t *order;    // [TILE] u16 scratch row (the tx kernel's prefix max)
   uint4 *table;       // staged rule table (optional)
 };
 
-/* Up to USN_RADIX_MIN_BINS bins the tile is counted per (bin, segment); with
- * more it is sorted by 6-bit digits of the bin (tile_order_radix, one counter
- * row per digit value).  A/B (c4: 261 bins, c5: 1005): the direct form costs
- * in proportion to the bins, the radix passes a constant; they meet near 450. */
-#define USN_RADIX_MIN_BINS 512u
-__host__ __device__ inline bool radix_bins(uint32_t nbins) { return nbins > USN_RADIX_MIN_BINS; }
-__host__ __device__ inline uint32_t cnt_rows(uint32_t nbins) { return radix_bins(nbins) ? 64 : nbins; }
-__host__ __device__ inline size_t cnt_bytes(uint32_t nbins) {
-  const size_t b = (size_t)NSEG * cnt_rows(nbins) * 2 + (nbins > 64 && !radix_bins(nbins) ? nbins * 2 : 0);
-  return (b + 15) & ~(size_t)15;
-}
+/* bins of a per-tile count row, rounded up to 8 (16-byte rows) */
+__host__ __device__ inline uint32_t bin_words(uint32_t nbins) { return (nbins + 7u) & ~7u; }
+__host__ __device__ inline size_t hist_bytes(uint32_t nbins) { return (size_t)bin_words(nbins) * 2; }
 
-/* cnt | bstart | scratch[16] | keys[TILE] (radix) | order[TILE] | table.
- * A kernel with a header stage (the GLDS classify) passes it as `stage`: the
- * order row and the radix keys then live there (the stage is free once every
- * round is decided; the sort starts after a barrier), which leaves the
- * dynamic LDS to the counters and the image. */
-__host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) {
-  return cnt_bytes(nbins) + 16 * 4 + (radix_bins(nbins) ? (size_t)TILE * 4 : 0);
-}
+/* hist | scratch[16] | order[TILE] | table.  A kernel with a header stage
+ * (the GLDS classify) passes it as `stage`: its (unused) order row is then
+ * the stage's, which leaves the dynamic LDS to the histogram and the image. */
+__host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) { return hist_bytes(nbins) + 16 * 4; }
 __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_stage = true) {
-  return own_stage ? lds_head_bytes(nbins) + TILE * 2 : cnt_bytes(nbins) + 16 * 4;
+  return own_stage ? lds_head_bytes(nbins) + TILE * 2 : lds_head_bytes(nbins);
 }
-#define STAGE_SORT_BYTES (TILE * 2 + TILE * 4)   /* order row + radix keys in a stage */
 __device__ __forceinline__ Lds carve(uint8_t *smem, uint32_t nbins, uint4 *stage = nullptr) {
   Lds L;
-  L.cnt = reinterpret_cast<uint16_t *>(smem);
-  L.bstart = L.cnt + (size_t)NSEG * cnt_rows(nbins);
-  L.scratch = reinterpret_cast<uint32_t *>(smem + cnt_bytes(nbins));
-  if (stage) {
-    L.order = reinterpret_cast<uint16_t *>(stage);
-    L.keys = radix_bins(nbins) ? reinterpret_cast<uint32_t *>(L.order + TILE) : nullptr;
-  } else {
-    L.keys = radix_bins(nbins) ? L.scratch + 16 : nullptr;
-    L.order = reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
-  }
+  L.hist = reinterpret_cast<uint32_t *>(smem);
+  L.scratch = reinterpret_cast<uint32_t *>(smem + hist_bytes(nbins));
+  L.order = stage ? reinterpret_cast<uint16_t *>(stage)
+                  : reinterpret_cast<uint16_t *>(smem + lds_head_bytes(nbins));
   L.table = reinterpret_cast<uint4 *>(smem + lds_core_bytes(nbins, stage == nullptr));
   return L;
 }
@@ -747,338 +723,42 @@ __device__ __forceinline__ uint64_t match_bin(uint32_t b, uint64_t valid, uint32
   return same;
 }
 
-/* Stable sort of a tile with more than 64 bins: LSD radix passes over 6-bit
- * digits of the bin.  Each pass is the <=64-bin counting sort of tile_order
- * (bit-sliced ballots, one wave scans the 64 digit rows) and moves the keys
- * (bin << 16 | tile-local index) to their sorted slots in L.keys.  The direct
- * form's [bin][segment] counters grow with the endpoints (16 K counters, 32
- * KiB to zero and scan per tile at 1000 endpoints); these stay 64 x 16.
- * Leaves the order row in L.order, writes the runs, returns their number;
- * cls[1..3] get this thread's NIC / FLOOD / DROP frames.  L.cnt is zero on
- * entry and on return. */
-__device__ uint32_t tile_order_radix(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbits,
-                                     uint32_t n_ep, const Lds &L, uint32_t *rdst, uint32_t cls[4]) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t key[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) key[r] = (bins[r] << 16) | (r * NTHREADS + tid);
-  for (uint32_t shift = 0; shift < nbits; shift += 6) {
-    uint32_t dg[ROUNDS], rank[ROUNDS];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      const uint32_t s = r * (NTHREADS / 64) + wave;       // 64-slot segment, slot order
-      dg[r] = (key[r] >> (16 + shift)) & 63u;
-      const uint64_t same = match_bin(dg[r], __ballot(local < nt), 6);
-      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-      if (local < nt && rank[r] == 0) L.cnt[dg[r] * NSEG + s] = (uint16_t)__popcll(same);
-    }
-    __syncthreads();
-    if (wave == 0) {   // lane d: segment prefixes of digit d plus the digit's start
-      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + lane * NSEG);
-      const uint4 r0 = row[0], r1 = row[1];
-      uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-      uint32_t acc = 0;
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 8; ++k2) {
-        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
-        w[k2] = acc | ((acc + lo) << 16);
-        acc += lo + hi;
-      }
-      const uint32_t start = wave_incl_scan(acc, lane) - acc;
-      const uint32_t st2 = start | (start << 16);
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 8; ++k2) w[k2] += st2;
-      row[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      row[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      const uint32_t s = r * (NTHREADS / 64) + wave;
-      if (local < nt) L.keys[L.cnt[dg[r] * NSEG + s] + rank[r]] = key[r];
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < 64 * NSEG; i += NTHREADS) L.cnt[i] = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) key[r] = L.keys[r * NTHREADS + tid];   // slots >= nt unused
-    __syncthreads();
-  }
-  // sorted keys in L.keys[0, nt): the order row, and a run wherever the bin changes
-  const uint32_t p0 = tid * ROUNDS;
-  uint32_t kb[ROUNDS], starts = 0;
-  uint32_t prev = (p0 > 0 && p0 <= nt) ? (L.keys[p0 - 1] >> 16) : 0xFFFFFFFFu;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) {
-    const uint32_t p = p0 + k;
-    kb[k] = 0xFFFFFFFFu;
-    if (p < nt) {
-      const uint32_t kv = L.keys[p];
-      kb[k] = kv >> 16;
-      L.order[p] = (uint16_t)(kv & 0xFFFFu);
-      starts += kb[k] != prev ? 1u : 0u;
-      prev = kb[k];
-      cls[1] += kb[k] == n_ep ? 1u : 0u;
-      cls[2] += kb[k] == n_ep + 1 ? 1u : 0u;
-      cls[3] += kb[k] == n_ep + 2 ? 1u : 0u;
-    }
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan(starts, L.scratch, &total);
-  prev = (p0 > 0 && p0 <= nt) ? (L.keys[p0 - 1] >> 16) : 0xFFFFFFFFu;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) {
-    const uint32_t p = p0 + k;
-    if (p < nt && kb[k] != prev) rdst[run++] = (kb[k] << 16) | p;
-    if (p < nt) prev = kb[k];
-  }
-  return total;
-}
-
-/* Stable counting sort of the tile by bin, written out as the tile's order
- * (tile-local indices) and bin runs.  bins[r] belongs to tile-local frame
- * r*256 + tid (valid when < nt).  L.cnt must be zero on entry.  Returns the
- * number of runs; cls[1..3] receive this thread's share of the NIC, FLOOD and
- * DROP bin totals. */
-__device__ uint32_t tile_order(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbins,
-                               uint32_t nbits, uint32_t n_ep, const Lds &L, uint32_t tile,
-                               uint16_t *order_out, uint32_t *runs_out, uint32_t cls[4]) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t *rdst = runs_out + (size_t)tile * TILE;
-  uint32_t n_runs;
-  if (nbins <= USN_RADIX_MIN_BINS) {
-    uint32_t rank[ROUNDS];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      const uint32_t s = r * (NTHREADS / 64) + wave;         // 64-frame segment, index order
-      const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
-      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-      if (local < nt && rank[r] == 0) L.cnt[bins[r] * NSEG + s] = (uint16_t)__popcll(same);
-    }
-    __syncthreads();
-    if (nbins <= 64) {
-    // one wave does all of it, lane b for bin b: column scan of the bin's 16
-    // segment counts, a wave scan of (present << 16 | total) for the bin
-    // starts and run indices, and the start folded into the row, so the
-    // scatter below reads one word per frame.  Two barriers fewer than the
-    // block-wide form.
-    if (wave == 0) {
-      const uint32_t b = lane;
-      uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
-      if (b < nbins) {
-        const uint4 r0 = row[0], r1 = row[1];
-        w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
-        w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
-      }
-      uint32_t acc = 0;
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 8; ++k2) {
-        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
-        w[k2] = acc | ((acc + lo) << 16);
-        acc += lo + hi;
-      }
-      const uint32_t packed = acc | (acc ? 0x10000u : 0u);
-      const uint32_t inc = wave_incl_scan(packed, lane);
-      const uint32_t run = inc - packed;
-      const uint32_t start = run & 0xFFFFu;
-      if (b < nbins) {
-        const uint32_t st2 = start | (start << 16);
-#pragma unroll
-        for (uint32_t k2 = 0; k2 < 8; ++k2) w[k2] += st2;
-        row[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        row[1] = make_uint4(w[4], w[5], w[6], w[7]);
-        if (acc) rdst[run >> 16] = (b << 16) | start;
-      }
-      cls[1] = b == n_ep ? acc : 0u;
-      cls[2] = b == n_ep + 1 ? acc : 0u;
-      cls[3] = b == n_ep + 2 ? acc : 0u;
-      if (lane == 63) L.scratch[15] = inc >> 16;
-    }
-    __syncthreads();
-    n_runs = L.scratch[15];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local < nt) {
-        const uint32_t s = r * (NTHREADS / 64) + wave;
-        L.order[L.cnt[bins[r] * NSEG + s] + rank[r]] = (uint16_t)local;
-      }
-    }
-    } else {
-    // each thread owns a contiguous chunk of bins: column scan over the 16
-    // segments (cnt[s][b] := frames of bin b in earlier segments), then one
-    // block scan of (present << 16 | total) gives bin starts and run indices
-    const uint32_t per = (nbins + NTHREADS - 1) / NTHREADS;
-    const uint32_t b0 = tid * per;
-    uint32_t packed = 0;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = b0 + k;
-      if (b >= nbins) break;
-      // the 16 u16 counts of bin b are 32 contiguous bytes: two 16-byte LDS
-      // reads, an exclusive prefix in registers, two 16-byte writes
-      uint4 *row = reinterpret_cast<uint4 *>(L.cnt + b * NSEG);
-      uint32_t w[8];
-      const uint4 r0 = row[0], r1 = row[1];
-      w[0] = r0.x; w[1] = r0.y; w[2] = r0.z; w[3] = r0.w;
-      w[4] = r1.x; w[5] = r1.y; w[6] = r1.z; w[7] = r1.w;
-      uint32_t acc = 0;
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < 8; ++k2) {
-        const uint32_t lo = w[k2] & 0xFFFFu, hi = w[k2] >> 16;
-        w[k2] = acc | ((acc + lo) << 16);
-        acc += lo + hi;
-      }
-      row[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      row[1] = make_uint4(w[4], w[5], w[6], w[7]);
-      L.bstart[b] = (uint16_t)acc;
-      packed += acc | (acc ? 0x10000u : 0u);
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(packed, L.scratch, &total);
-    n_runs = total >> 16;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = b0 + k;
-      if (b >= nbins) break;
-      const uint32_t c = L.bstart[b];
-      const uint32_t start = run & 0xFFFFu;
-      L.bstart[b] = (uint16_t)start;
-      if (c) rdst[run >> 16] = (b << 16) | start;
-      run += c | (c ? 0x10000u : 0u);
-      // NIC, FLOOD, DROP totals (selects: a runtime index would put cls in scratch)
-      cls[1] = b == n_ep ? c : cls[1];
-      cls[2] = b == n_ep + 1 ? c : cls[2];
-      cls[3] = b == n_ep + 2 ? c : cls[3];
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local < nt) {
-        const uint32_t s = r * (NTHREADS / 64) + wave;
-        const uint32_t b = bins[r];
-        L.order[L.bstart[b] + L.cnt[b * NSEG + s] + rank[r]] = (uint16_t)local;
-      }
-    }
-    }
-  } else {
-    n_runs = tile_order_radix(bins, nt, nbits, n_ep, L, rdst, cls);
-  }
-  __syncthreads();
-  uint16_t *dst = order_out + (size_t)tile * TILE;
-  const uint32_t p0 = tid * ROUNDS;
-  if (p0 + ROUNDS <= nt) {
-    if (ROUNDS == 4)
-      *reinterpret_cast<uint2 *>(dst + p0) = *reinterpret_cast<const uint2 *>(L.order + p0);
-    else if (ROUNDS == 2)
-      *reinterpret_cast<uint32_t *>(dst + p0) = *reinterpret_cast<const uint32_t *>(L.order + p0);
-    else
-      dst[p0] = L.order[p0];
-  } else {
-    for (uint32_t k = 0; k < ROUNDS; ++k)
-      if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
-  }
-  return n_runs;
-}
-
-/* 64 < bins <= STAGE_BYTE_BINS in a 512-thread classify tile: a counting
- * sort whose counters live in the header stage (free once every round is
- * decided).  The 16 segments of 64 frames (segment r * 8 + wave) give each
- * bin a 16-byte row of u8 counts; a frame's place is its bin's start plus the
- * byte sum (v_sad_u8) of its row's earlier segments plus its rank in its
- * segment.  One counting pass where tile_order_radix makes two (c5: 1005
- * bins), and no [bin][segment] u16 counters in the dynamic LDS.  Same
- * contract as tile_order. */
-#define STAGE_BYTE_BINS 1024u
-__device__ __forceinline__ uint32_t byte_sum(uint32_t v) { return __builtin_amdgcn_sad_u8(v, 0u, 0u); }
-__device__ uint32_t tile_order_bytes(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbins,
-                                     uint32_t nbits, uint32_t n_ep, const Lds &L, uint8_t *stage,
-                                     uint32_t tile, uint16_t *order_out, uint32_t *runs_out,
-                                     uint32_t cls[4]) {
-  static_assert(NSEG == 16, "a bin's row is 16 segment counts");
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint4 *rows = reinterpret_cast<uint4 *>(stage + TILE * 2 + TILE * 4);   // after order, keys
-  uint16_t *bstart = reinterpret_cast<uint16_t *>(rows + STAGE_BYTE_BINS);
-  uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
-  uint32_t *rdst = runs_out + (size_t)tile * TILE;
-  {  // each wave zeroes the rows that lie in its own stage (it is done with
-     // its headers; no wave reads another's stage), then one barrier
-    constexpr uint32_t WSTAGE = STAGE_ROUND_SLOTS * 16;   // bytes of one wave's stage
-    const uint32_t r0 = TILE * 6, r1 = TILE * 6 + nbins * 16;
-    const uint32_t lo = max(r0, wave * WSTAGE), hi = min(r1, (wave + 1) * WSTAGE);
-    for (uint32_t o = lo + lane * 16; o < hi; o += 64 * 16)
-      *reinterpret_cast<uint4 *>(stage + o) = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  uint32_t rank[ROUNDS];
+/* The tile's frames per bin (the scatter's input, scan_agg / scan_off /
+ * scatter below) into the LDS histogram: u16 counts in pairs per u32 word,
+ * zeroed by the caller before a barrier.  With few bins (nbits <= 6) one LDS
+ * add per distinct bin of a wave (bit-sliced match: c2's 19 bins would put
+ * ~50 lanes of a wave on a handful of words), else one per frame (c5: ~1000
+ * bins, lanes rarely collide).  Replaces round 2's per-tile stable sort: the
+ * ranks are computed by the scatter kernel, outside this latency-bound
+ * kernel. */
+__device__ __forceinline__ void tile_hist(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbits,
+                                          uint32_t *hist) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
-    const uint32_t sg = r * (NTHREADS / 64) + wave;
-    const uint64_t same = match_bin(bins[r], __ballot(local < nt), nbits);
-    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-    if (local < nt && rank[r] == 0) cb[bins[r] * 16 + sg] = (uint8_t)__popcll(same);
-  }
-  __syncthreads();
-  // bin totals, starts and runs: thread t owns bins 2t and 2t + 1
-  uint32_t tot[2], packed = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 2; ++k) {
-    const uint32_t b = 2 * tid + k;
-    tot[k] = 0;
-    if (b < nbins) {
-      const uint4 w = rows[b];
-      tot[k] = byte_sum(w.x) + byte_sum(w.y) + byte_sum(w.z) + byte_sum(w.w);
-    }
-    packed += tot[k] | (tot[k] ? 0x10000u : 0u);
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan(packed, L.scratch, &total);
-#pragma unroll
-  for (uint32_t k = 0; k < 2; ++k) {
-    const uint32_t b = 2 * tid + k, c = tot[k];
-    if (b >= nbins) break;
-    const uint32_t start = run & 0xFFFFu;
-    bstart[b] = (uint16_t)start;
-    if (c) rdst[run >> 16] = (b << 16) | start;
-    run += c | (c ? 0x10000u : 0u);
-    cls[1] = b == n_ep ? c : cls[1];
-    cls[2] = b == n_ep + 1 ? c : cls[2];
-    cls[3] = b == n_ep + 2 ? c : cls[3];
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local < nt) {
-      const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
-      const uint4 w = rows[b];
-      // bytes of the segments before sg: whole words, then the low bytes of one
-      const uint32_t q = sg >> 2, part = sg & 3u;
-      const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
-      const uint32_t p0 = q > 0 ? w.x : (w.x & mpart);
-      const uint32_t p1 = q > 1 ? w.y : q == 1 ? (w.y & mpart) : 0u;
-      const uint32_t p2 = q > 2 ? w.z : q == 2 ? (w.z & mpart) : 0u;
-      const uint32_t p3 = q == 3 ? (w.w & mpart) : 0u;
-      const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
-      L.order[bstart[b] + before + rank[r]] = (uint16_t)local;
+    const bool v = local < nt;
+    const uint32_t b = bins[r];
+    if (nbits <= 6) {
+      const uint64_t same = match_bin(b, __ballot(v), nbits);
+      if (v && (same & lanemask_lt(lane)) == 0)
+        atomicAdd(&hist[b >> 1], (uint32_t)__popcll(same) << (16u * (b & 1u)));
+    } else if (v) {
+      atomicAdd(&hist[b >> 1], 1u << (16u * (b & 1u)));
     }
   }
-  __syncthreads();
-  uint16_t *dst = order_out + (size_t)tile * TILE;
-  const uint32_t p0 = tid * ROUNDS;
-  if (p0 + ROUNDS <= nt) {
-    if (ROUNDS == 2)
-      *reinterpret_cast<uint32_t *>(dst + p0) = *reinterpret_cast<const uint32_t *>(L.order + p0);
-    else
-      for (uint32_t k = 0; k < ROUNDS; ++k) dst[p0 + k] = L.order[p0 + k];
-  } else {
-    for (uint32_t k = 0; k < ROUNDS; ++k)
-      if (p0 + k < nt) dst[p0 + k] = L.order[p0 + k];
-  }
-  return total >> 16;
+}
+__device__ __forceinline__ uint32_t hist_get(const uint32_t *hist, uint32_t b) {
+  return (hist[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
+}
+/* after a barrier: the histogram as the tile's count row (16-byte stores) */
+__device__ __forceinline__ void hist_out(const uint32_t *hist, uint32_t nbw, uint16_t *row) {
+  const uint4 *h = reinterpret_cast<const uint4 *>(hist);
+  uint4 *w = reinterpret_cast<uint4 *>(row);
+  for (uint32_t i = threadIdx.x; i < nbw / 8; i += NTHREADS) w[i] = h[i];
+}
+__device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw) {
+  for (uint32_t i = threadIdx.x; i < nbw / 2; i += NTHREADS) hist[i] = 0;
 }
 
 /* --------------------------------------------------------------------------- */
@@ -1300,7 +980,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // bins and table are shared by the batches.  GLDS: the order row and the
   // radix keys live in the header stage (carve)
-  static_assert(!GLDS || NWAVES * GD * STAGE_ROUND_SLOTS * 16 >= STAGE_SORT_BYTES, "stage too small");
   const Lds L = carve(smem, m.b[0].nbins, GLDS ? s_stage : nullptr);
   uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);   // this wave's stage
   const uint4 *T = m.b[0].table;
@@ -1338,11 +1017,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     const uint32_t tile = w - m.tile_base[bi];
     const uint64_t base = (uint64_t)tile * TILE;
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-    // 64 < bins <= 1024 at 512 threads: the sort's counters in the stage's 24 KiB
-    // (order 2 + radix keys 4 + byte rows 16 + starts 2; tile_order_bytes)
-    constexpr bool STAGE_ROWS = GLDS && GD == 1 && USN_STAGE_ROWS &&
-                                NWAVES * STAGE_ROUND_SLOTS * 16 >= TILE * 6 + STAGE_BYTE_BINS * 18;
-    const bool rows_sort = STAGE_ROWS && a.nbins > 64 && a.nbins <= STAGE_BYTE_BINS;
     STAMP_DECL
     STAMP(0);
 
@@ -1372,10 +1046,9 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       lane_round(fp[0], q[0]);
     }
     STAMP(1);
-    // ---- while they fly: zero the segment counters (the barrier also waits
+    // ---- while they fly: zero the bin histogram (the barrier also waits
     //      for every load: table and round 0 are in LDS / registers after it)
-    if (!rows_sort)
-      for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
+    hist_zero(L.hist, a.nbw);
     if (tid < 8) s_misc[tid] = 0;
     __syncthreads();
     STAMP(2);
@@ -1395,6 +1068,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
         S->cin_state = cst; S->cin_dst = dst;
         for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
         S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+        S->n_ep = a.n_ep; S->n_bins = a.nbins;
       }
       __syncthreads();
     }
@@ -1712,22 +1386,13 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     }
 
     STAMP(6);
-    // ---- stable per-endpoint order of the tile
-    uint32_t cls[4] = {0, 0, 0, 0};
-#if USN_ABL_NOSORT || USN_ABL_LOADONLY   /* ablation builds only */
-    const uint32_t n_runs = 0;
-#else
-    const uint32_t n_runs =
-        rows_sort
-            ? tile_order_bytes(bins, nt, a.nbins, a.nbits, a.n_ep, L,
-                               reinterpret_cast<uint8_t *>(s_stage), tile, a.order, a.runs, cls)
-            : tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order, a.runs, cls);
+    // ---- the tile's frames per bin: LDS histogram, then its count row
+#if !USN_ABL_LOADONLY
+    tile_hist(bins, nt, a.nbits, L.hist);
 #endif
-    if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
-    if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
-    if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
     __syncthreads();
     STAMP(10);
+    hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
 
     // ---- tile header
     usn_tile_hdr *H = a.tiles + tile;
@@ -1740,14 +1405,16 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       H->last_idx = (uint32_t)(base + lastp - 1);
     }
     if (tid == 0) {
+      const uint32_t nic = hist_get(L.hist, a.n_ep), fl = hist_get(L.hist, a.n_ep + 1),
+                     dr = hist_get(L.hist, a.n_ep + 2);
       H->n_frames = (uint16_t)nt;
-      H->n_runs = (uint16_t)n_runs;
+      H->_r0 = 0;
       H->n_host = (uint16_t)s_misc[1];
       H->bin_nic = (uint16_t)a.n_ep;
-      H->class_count[0] = (uint16_t)s_misc[5];                       // DROP bin
-      H->class_count[2] = (uint16_t)s_misc[3];                       // NIC bin
-      H->class_count[3] = (uint16_t)s_misc[4];                       // FLOOD bin
-      H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
+      H->class_count[0] = (uint16_t)dr;                              // DROP bin
+      H->class_count[2] = (uint16_t)nic;                             // NIC bin
+      H->class_count[3] = (uint16_t)fl;                              // FLOOD bin
+      H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
       if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
     }
     STAMP(11);
@@ -1757,17 +1424,16 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
 }
 
 
-/* Rebuild order / runs / class counts of tiles from patched decisions. */
-__global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32_t t0) {
+/* Recount the bin rows and class counts of tiles from patched decisions
+ * (usn_finalize; the scatter then runs again over the whole batch). */
+__global__ __launch_bounds__(NTHREADS) void recount_kernel(ClassifyArgs a, uint32_t t0) {
   extern __shared__ __align__(16) uint8_t smem[];
   const Lds L = carve(smem, a.nbins);
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = t0 + blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  __shared__ uint32_t s_cls[4];
-  if (tid < 4) s_cls[tid] = 0;
-  for (uint32_t i = tid; i < NSEG * cnt_rows(a.nbins); i += NTHREADS) L.cnt[i] = 0;
+  hist_zero(L.hist, a.nbw);
   uint32_t bins[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -1776,19 +1442,17 @@ __global__ __launch_bounds__(NTHREADS) void resort_kernel(ClassifyArgs a, uint32
     bins[r] = dec_bin(local < nt ? d : 0u, a.n_ep);
   }
   __syncthreads();
-  uint32_t cls[4] = {0, 0, 0, 0};
-  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
-                                     a.runs, cls);
-  for (int c = 1; c < 4; ++c)
-    if (cls[c]) atomicAdd(&s_cls[c], cls[c]);
+  tile_hist(bins, nt, a.nbits, L.hist);
   __syncthreads();
+  hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
   if (tid == 0) {
     usn_tile_hdr *H = a.tiles + tile;
-    H->n_runs = (uint16_t)n_runs;
-    H->class_count[0] = (uint16_t)s_cls[3];
-    H->class_count[2] = (uint16_t)s_cls[1];
-    H->class_count[3] = (uint16_t)s_cls[2];
-    H->class_count[1] = (uint16_t)(nt - s_cls[1] - s_cls[2] - s_cls[3]);
+    const uint32_t nic = hist_get(L.hist, a.n_ep), fl = hist_get(L.hist, a.n_ep + 1),
+                   dr = hist_get(L.hist, a.n_ep + 2);
+    H->class_count[0] = (uint16_t)dr;
+    H->class_count[2] = (uint16_t)nic;
+    H->class_count[3] = (uint16_t)fl;
+    H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
   }
 }
 
@@ -2249,7 +1913,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     s_early = 0; s_early_all = 0; s_slow = 0; s_dlearn = 0;
   }
   if (tid < 8) s_misc[tid] = 0;
-  for (uint32_t k = tid; k < NSEG * cnt_rows(a.nbins); k += NTHREADS) L.cnt[k] = 0;
+  hist_zero(L.hist, a.nbw);
   __syncthreads();
   const uint32_t tile = blockIdx.x;
   STAMP_DECL
@@ -2274,6 +1938,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
       for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
       S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      S->n_ep = a.n_ep; S->n_bins = a.nbins;
       S->flags = 0; S->first_break = 0xFFFFFFFFu;
     }
   }
@@ -2823,16 +2488,11 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     for (uint32_t d = 32; d >= 1; d >>= 1) lm = max(lm, (uint32_t)__shfl_xor(lm, d, 64));
     if (lane == 0 && lm) atomicMax(&s_misc[0], lm);
   }
+  tile_hist(bins, nt, a.nbits, L.hist);
   __syncthreads();
   STAMP(7);
-  uint32_t cls[4] = {0, 0, 0, 0};
-  const uint32_t n_runs = tile_order(bins, nt, a.nbins, a.nbits, a.n_ep, L, tile, a.order,
-                                     a.runs, cls);
+  hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
   STAMP(10);
-  if (cls[1]) atomicAdd(&s_misc[3], cls[1]);
-  if (cls[2]) atomicAdd(&s_misc[4], cls[2]);
-  if (cls[3]) atomicAdd(&s_misc[5], cls[3]);
-  __syncthreads();
   usn_tile_hdr *H = a.tiles + tile;
   const uint32_t lastp = s_misc[0];
   if (lastp && my_last == lastp) {
@@ -2844,14 +2504,16 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     H->last_idx = (uint32_t)(base + lastp - 1);
   }
   if (tid == 0) {
+    const uint32_t nic = hist_get(L.hist, a.n_ep), fl = hist_get(L.hist, a.n_ep + 1),
+                   dr = hist_get(L.hist, a.n_ep + 2);
     H->n_frames = (uint16_t)nt;
-    H->n_runs = (uint16_t)n_runs;
+    H->_r0 = 0;
     H->n_host = (uint16_t)s_misc[1];
     H->bin_nic = (uint16_t)a.n_ep;
-    H->class_count[0] = (uint16_t)s_misc[5];
-    H->class_count[2] = (uint16_t)s_misc[3];
-    H->class_count[3] = (uint16_t)s_misc[4];
-    H->class_count[1] = (uint16_t)(nt - s_misc[3] - s_misc[4] - s_misc[5]);
+    H->class_count[0] = (uint16_t)dr;
+    H->class_count[2] = (uint16_t)nic;
+    H->class_count[3] = (uint16_t)fl;
+    H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
   }
   STAMP(11);
@@ -2977,12 +2639,232 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream) {
+hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream) {
   if (t1 <= t0) return hipSuccess;
   const size_t lds = lds_core_bytes(a.nbins);
-  hipLaunchKernelGGL(resort_kernel, dim3(t1 - t0), dim3(NTHREADS), lds, stream, a, t0);
+  hipLaunchKernelGGL(recount_kernel, dim3(t1 - t0), dim3(NTHREADS), lds, stream, a, t0);
   return hipGetLastError();
 }
+
+#if USN_NTHREADS == 512
+/* ===========================================================================
+ * Per-endpoint lists: the device-wide stable scatter (usn_kernels.h).
+ * The classify / tx kernel leaves each tile's decisions and its count row
+ * cnt[tile][bin] (u16).  Three launches turn them into `index` (the batch's
+ * frame indices grouped by bin, frame order inside a bin) and bin_off:
+ *   scan_agg  (chunk, bin block): the chunk's frames per bin          agg
+ *   scan_off  (chunk, bin block): each bin's base (bins before it, all
+ *             chunks) + the chunks before this one, then per tile of the
+ *             chunk the list position of its first frame of the bin     off
+ *   scatter   (tile): rank of each frame among the tile's frames of its bin,
+ *             index[off[tile][bin] + rank] = frame
+ * Algorithmic bytes per frame: 4 (index).  The reference writes each frame
+ * straight into its target's ring (endpoint.rs:61-74) and copies FLOOD frames
+ * to every other endpoint (:340-363): an endpoint's frames are its list merged
+ * in frame order with the FLOOD list.
+ * =========================================================================== */
+__device__ __forceinline__ uint32_t base_of(const uint32_t *base, uint32_t count, uint32_t w) {
+  uint32_t bi = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < USN_MAX_MULTI; ++k) bi += (k < count && w >= base[k]) ? 1u : 0u;
+  return bi;
+}
+
+#define SCAN_THREADS 256
+static_assert(USN_SCAN_BINS_PER_BLOCK == 2 * SCAN_THREADS, "two bins per scan thread");
+
+/* frames of bins 2w, 2w+1 over tiles [t0, t1): 8 row loads in flight */
+__device__ __forceinline__ void col_sum(const uint32_t *col, uint32_t stride, uint32_t t0, uint32_t t1,
+                                        uint32_t &lo, uint32_t &hi) {
+  uint32_t t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = col[(size_t)(t + k) * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { lo += v[k] & 0xFFFFu; hi += v[k] >> 16; }
+  }
+  for (; t < t1; ++t) {
+    const uint32_t v = col[(size_t)t * stride];
+    lo += v & 0xFFFFu; hi += v >> 16;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_agg_kernel(ScatterArgs s) {
+  __shared__ uint32_t red[SCAN_THREADS / 64];
+  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
+  const uint32_t bi = base_of(s.chunk_base, s.count, g);
+  const ScatterBatch &B = s.b[bi];
+  const uint32_t c = g - s.chunk_base[bi];
+  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
+  const uint32_t w = bb * SCAN_THREADS + tid;          // bins 2w, 2w + 1
+  uint32_t lo = 0, hi = 0;
+  if (2 * w < s.nbw) {
+    col_sum(reinterpret_cast<const uint32_t *>(B.cnt) + w, s.nbw / 2, t0, t1, lo, hi);
+    *reinterpret_cast<uint2 *>(B.agg + (size_t)c * s.nbw + 2 * w) = make_uint2(lo, hi);
+  }
+  uint32_t sum = lo + hi;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_THREADS / 64; ++k) t += red[k];
+    B.blk[(size_t)c * s.nblk + bb] = t;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_off_kernel(ScatterArgs s) {
+  __shared__ uint32_t red[2 * (SCAN_THREADS / 64)];
+  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  const uint32_t bi = base_of(s.chunk_base, s.count, g);
+  const ScatterBatch &B = s.b[bi];
+  const uint32_t c = g - s.chunk_base[bi];
+  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
+  const uint32_t w = bb * SCAN_THREADS + tid;
+  const bool on = 2 * w < s.nbw;
+  // this bin pair over every chunk: its total, and the chunks before c
+  uint32_t tlo = 0, thi = 0, elo = 0, ehi = 0;
+  if (on) {
+    const uint32_t *col = B.agg + 2 * w;
+    for (uint32_t k = 0; k < B.nchunks; ++k) {
+      const uint2 v = *reinterpret_cast<const uint2 *>(col + (size_t)k * s.nbw);
+      tlo += v.x; thi += v.y;
+      if (k < c) { elo += v.x; ehi += v.y; }
+    }
+  }
+  // frames of the bin blocks before bb (every chunk)
+  uint32_t before = 0;
+  for (uint32_t k = tid; k < B.nchunks * bb; k += SCAN_THREADS)
+    before += B.blk[(size_t)(k / bb) * s.nblk + (k % bb)];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) before += __shfl_xor(before, d, 64);
+  // + the bins of this block before 2w
+  const uint32_t v = tlo + thi;
+  const uint32_t inc = wave_incl_scan(v, lane);
+  if (lane == 63) red[wave] = inc;
+  if (lane == 0) red[SCAN_THREADS / 64 + wave] = before;
+  __syncthreads();
+  uint32_t pre = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN_THREADS / 64; ++k) pre += red[SCAN_THREADS / 64 + k] + (k < wave ? red[k] : 0u);
+  const uint32_t base_lo = pre + inc - v, base_hi = base_lo + tlo;
+  if (c == 0) {   // bin offsets (pad bins past nbins are empty: bin_off[nbins] = n)
+    if (2 * w <= s.nbins) B.bin_off[2 * w] = base_lo;
+    if (2 * w + 1 <= s.nbins) B.bin_off[2 * w + 1] = base_hi;
+    if (bb == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+  }
+  if (!on) return;
+  uint32_t slo = base_lo + elo, shi = base_hi + ehi;
+  const uint32_t stride = s.nbw / 2;
+  const uint32_t *col = reinterpret_cast<const uint32_t *>(B.cnt) + w;
+  uint2 *out = reinterpret_cast<uint2 *>(B.off + 2 * w);
+  uint32_t t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    uint32_t cv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cv[k] = col[(size_t)(t + k) * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      out[(size_t)(t + k) * stride] = make_uint2(slo, shi);
+      slo += cv[k] & 0xFFFFu; shi += cv[k] >> 16;
+    }
+  }
+  for (; t < t1; ++t) {
+    const uint32_t cv = col[(size_t)t * stride];
+    out[(size_t)t * stride] = make_uint2(slo, shi);
+    slo += cv & 0xFFFFu; shi += cv >> 16;
+  }
+}
+
+/* one tile per workgroup of 512 threads (two frames per lane).  Blocks are
+ * dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them so that an
+ * XCD takes a contiguous run of tiles, whose list entries of a bin are
+ * adjacent: its L2 assembles each bin's lines before writing them back
+ * (cdna_hip_programming.md T1 swizzle, bijective). */
+#ifndef USN_SCATTER_XCD
+#define USN_SCATTER_XCD 1
+#endif
+__global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint32_t *offrow = reinterpret_cast<uint32_t *>(smem);            // [nbw]
+  uint4 *rows = reinterpret_cast<uint4 *>(smem + (size_t)s.nbw * 4);  // [nbins]: u8 per segment
+  uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nwg = s.tile_base[s.count];
+  uint32_t w = blockIdx.x;
+  if (USN_SCATTER_XCD) {
+    const uint32_t q = nwg / 8, r = nwg % 8, x = w % 8;
+    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+  }
+  const uint32_t bi = base_of(s.tile_base, s.count, w);
+  const ScatterBatch &B = s.b[bi];
+  const uint32_t tile = w - s.tile_base[bi];
+  const uint64_t base = (uint64_t)tile * TILE;
+  const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
+  uint32_t d[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(B.off + (size_t)tile * s.nbw);
+    for (uint32_t i = tid; i < s.nbw / 4; i += NTHREADS) reinterpret_cast<uint4 *>(offrow)[i] = src[i];
+    for (uint32_t i = tid; i < s.nbins; i += NTHREADS) rows[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  uint32_t bins[ROUNDS], rank[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    const bool v = local < nt;
+    bins[r] = dec_bin(d[r], s.n_ep);
+    const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
+    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+    if (v && rank[r] == 0) cb[bins[r] * 16 + r * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) continue;
+    const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
+    const uint4 wv = rows[b];
+    // frames of bin b in the segments before sg: whole words, then the low bytes of one
+    const uint32_t q = sg >> 2, part = sg & 3u;
+    const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
+    const uint32_t p0 = q > 0 ? wv.x : (wv.x & mpart);
+    const uint32_t p1 = q > 1 ? wv.y : q == 1 ? (wv.y & mpart) : 0u;
+    const uint32_t p2 = q > 2 ? wv.z : q == 2 ? (wv.z & mpart) : 0u;
+    const uint32_t p3 = q == 3 ? (wv.w & mpart) : 0u;
+    const uint32_t before = __builtin_amdgcn_sad_u8(p0, 0u, 0u) + __builtin_amdgcn_sad_u8(p1, 0u, 0u) +
+                            __builtin_amdgcn_sad_u8(p2, 0u, 0u) + __builtin_amdgcn_sad_u8(p3, 0u, 0u);
+    B.index[offrow[b] + before + rank[r]] = (uint32_t)(base + local);
+  }
+}
+static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
+
+hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
+  const uint32_t chunks = s.chunk_base[s.count], tiles = s.tile_base[s.count];
+  if (tiles == 0) return hipSuccess;
+  const dim3 sg(chunks, s.nblk);
+  hipLaunchKernelGGL(scan_agg_kernel, sg, dim3(SCAN_THREADS), 0, stream, s);
+  hipLaunchKernelGGL(scan_off_kernel, sg, dim3(SCAN_THREADS), 0, stream, s);
+  const size_t lds = (size_t)s.nbw * 4 + (size_t)s.nbins * 16;
+  if (lds > 64u * 1024u) {
+    static thread_local bool raised = false;
+    if (!raised) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&scatter_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL(scatter_kernel, dim3(tiles), dim3(NTHREADS), lds, stream, s);
+  return hipGetLastError();
+}
+#endif  // USN_NTHREADS == 512
 
 }  // namespace USN_NS
 

@@ -1175,6 +1175,47 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 }  // namespace
 
 /* ========================================================================== */
+namespace usn {
+/* scratch of the per-endpoint scatter for one batch of n frames and nbins
+ * bins: cnt[ntiles][nbw] u16 | off[ntiles][nbw] u32 | agg[nchunks][nbw] u32 |
+ * blk[nchunks][nblk] u32, with chunks of tc tiles (at most
+ * USN_SCAN_MAX_CHUNKS chunks) */
+struct ScatterGeom {
+  uint32_t nbw, ntiles, tc, nchunks, nblk;
+  size_t cnt, off, agg, blk, total;
+};
+static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
+  ScatterGeom g;
+  g.nbw = (nbins + 7u) & ~7u;
+  g.ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
+  g.tc = std::max<uint32_t>(1, (g.ntiles + USN_SCAN_MAX_CHUNKS - 1) / USN_SCAN_MAX_CHUNKS);
+  g.nchunks = (g.ntiles + g.tc - 1) / g.tc;
+  g.nblk = (g.nbw + USN_SCAN_BINS_PER_BLOCK - 1) / USN_SCAN_BINS_PER_BLOCK;
+  size_t o = 0;
+  auto a256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw * 2);
+  g.off = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
+  g.agg = o; o = a256(o + (size_t)g.nchunks * g.nbw * 4);
+  g.blk = o; o = a256(o + (size_t)g.nchunks * g.nblk * 4);
+  g.total = o;
+  return g;
+}
+size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins) { return scatter_geom(n, nbins).total; }
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt) {
+  const ScatterGeom g = scatter_geom(n, nbins);
+  uint8_t *p = static_cast<uint8_t *>(scratch);
+  *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
+  sb.cnt = *cnt;
+  sb.off = reinterpret_cast<uint32_t *>(p + g.off);
+  sb.agg = reinterpret_cast<uint32_t *>(p + g.agg);
+  sb.blk = reinterpret_cast<uint32_t *>(p + g.blk);
+  sb.n = (uint32_t)n;
+  sb.ntiles = g.ntiles;
+  sb.tc = g.tc;
+  sb.nchunks = g.nchunks;
+}
+}  // namespace usn
+
 extern "C" {
 
 int usn_abi_version(void) { return USN_ABI_VERSION; }
@@ -1543,37 +1584,52 @@ int usn_cache_clear(usn_ctx *c, uint16_t ep) {
 /* ---- result layout ------------------------------------------------------- */
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+
 struct Layout {
-  size_t dec, order, runs, tiles, summary, host, total;
+  size_t dec, index, bin_off, tiles, summary, host, scratch, total;
 };
-static Layout layout_for(uint64_t n) {
+static Layout layout_for(uint64_t n, uint32_t nbins) {
   const uint64_t nt = (n + USN_TILE - 1) / USN_TILE;
   Layout L;
   size_t off = 0;
   L.dec = off; off = align256(off + n * 4);
-  L.order = off; off = align256(off + nt * USN_TILE * 2);
-  L.runs = off; off = align256(off + nt * USN_TILE * 4);
+  L.index = off; off = align256(off + n * 4);
+  L.bin_off = off; off = align256(off + (size_t)(USN_MAX_BINS + 1) * 4);
   L.tiles = off; off = align256(off + nt * sizeof(usn_tile_hdr));
   L.summary = off; off = align256(off + sizeof(usn_summary));
   L.host = off; off = align256(off + nt * USN_TILE * 4);
+  L.scratch = off; off = align256(off + usn::scatter_scratch_bytes(n, nbins));
   L.total = off;
   return L;
 }
 
-size_t usn_result_bytes(uint64_t n) { return layout_for(n).total; }
+size_t usn_result_bytes(uint64_t n) { return layout_for(n, USN_MAX_BINS).total; }
+size_t usn_result_bytes_ep(uint64_t n, uint32_t max_endpoints) {
+  if (max_endpoints > USN_MAX_ENDPOINTS) max_endpoints = USN_MAX_ENDPOINTS;
+  return layout_for(n, max_endpoints + 3).total;
+}
 
 int usn_result_bind(void *mem, size_t bytes, uint64_t n, usn_result *out) {
   if (!mem || !out || n == 0) return USN_EINVAL;
-  const Layout L = layout_for(n);
+  const Layout L = layout_for(n, 3);   // the fixed part and the smallest scratch
   if (bytes < L.total) return USN_ERANGE;
+  // the most bins the scratch holds
+  uint32_t lo = 3, hi = USN_MAX_BINS;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (L.scratch + usn::scatter_scratch_bytes(n, mid) <= bytes) lo = mid; else hi = mid - 1;
+  }
   uint8_t *b = static_cast<uint8_t *>(mem);
   out->decisions = reinterpret_cast<uint32_t *>(b + L.dec);
-  out->order = reinterpret_cast<uint16_t *>(b + L.order);
-  out->runs = reinterpret_cast<uint32_t *>(b + L.runs);
+  out->index = reinterpret_cast<uint32_t *>(b + L.index);
+  out->bin_off = reinterpret_cast<uint32_t *>(b + L.bin_off);
   out->tiles = reinterpret_cast<usn_tile_hdr *>(b + L.tiles);
   out->summary = reinterpret_cast<usn_summary *>(b + L.summary);
   out->host_list = reinterpret_cast<uint32_t *>(b + L.host);
+  out->scratch = b + L.scratch;
   out->n = n;
+  out->max_bins = lo;
+  out->_pad = 0;
   return USN_OK;
 }
 
@@ -1589,8 +1645,6 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   a.ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
   a.window = b->window ? b->window : USN_WINDOW;
   a.decisions = r->decisions;
-  a.order = r->order;
-  a.runs = r->runs;
   a.tiles = r->tiles;
   a.summary = r->summary;
   a.host_list = r->host_list;
@@ -1612,6 +1666,35 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   a.nbits = 1;
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   a.probe_mask = c->probe_mask;
+  usn::ScatterBatch sb;
+  usn::scatter_carve(r->scratch, b->n, a.nbins, sb, &a.cnt);
+  a.nbw = (a.nbins + 7u) & ~7u;
+  return USN_OK;
+}
+
+/* the per-endpoint scatter of `count` classified batches (after their
+ * classify / tx launch, or after finalize recounted patched tiles) */
+static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint32_t count,
+                          hipStream_t s) {
+  usn::ScatterArgs x;
+  std::memset(&x, 0, sizeof x);
+  x.count = count;
+  x.nbins = as[0].nbins;
+  x.nbw = as[0].nbw;
+  x.nblk = (x.nbw + USN_SCAN_BINS_PER_BLOCK - 1) / USN_SCAN_BINS_PER_BLOCK;
+  x.n_ep = as[0].n_ep;
+  x.nbits = as[0].nbits;
+  for (uint32_t k = 0; k < count; ++k) {
+    usn::ScatterBatch &sb = x.b[k];
+    uint16_t *cnt;
+    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, sb, &cnt);
+    sb.decisions = r[k].decisions;
+    sb.index = r[k].index;
+    sb.bin_off = r[k].bin_off;
+    x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
+    x.tile_base[k + 1] = x.tile_base[k] + sb.ntiles;
+  }
+  HIPCHK(usn_t512::launch_scatter(x, s));
   return USN_OK;
 }
 
@@ -1634,6 +1717,7 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
   if (((uintptr_t)b->frames & 15) != 0) return USN_EINVAL;
   if (b->n > 0xFFFFFFFFull) return USN_ERANGE;
   if (b->src_endpoint >= USN_MAX_ENDPOINTS || !c->eps[b->src_endpoint].used) return USN_EINVAL;
+  if (!r->scratch || !r->index || !r->bin_off || r->max_bins < c->n_ep + 3) return USN_ERANGE;
   return USN_OK;
 }
 
@@ -1815,6 +1899,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   } else {
     HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
+  { int st = launch_scatter(m.b, r, count, (hipStream_t)stream); if (st) return st; }
   for (uint32_t k = 0; k < count; ++k) {
     Chain &ch = c->chains[b[k].src_endpoint];
     ch.device_chain = true;
@@ -2234,7 +2319,9 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     HIPCHK(hipMemcpy(r->decisions + h, out.data(), out.size() * 4, hipMemcpyHostToDevice));
     ClassifyArgs a;
     fill_args(c, R, b, r, a);
-    HIPCHK(usn::launch_resort(a, (uint32_t)(h / USN_TILE), ntiles, s));
+    HIPCHK(usn::launch_recount(a, (uint32_t)(h / USN_TILE), ntiles, s));
+    st = launch_scatter(&a, r, 1, s);
+    if (st) return st;
     usn_summary o = sum;
     o.flags |= USN_S_COUT;
     o.cout_state = cs.valid ? USN_CS_VALID : 0u;
@@ -2383,15 +2470,21 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   }
   st = advance(b->n);
   if (st) return st;
-  /* patched tiles: rebuild their order / runs / counts */
+  /* patched tiles: recount their bin rows, then the lists again */
   ClassifyArgs a;
   fill_args(c, c->reps[rep], b, r, a);
+  bool any = false;
   for (uint32_t t = 0; t < ntiles;) {
     if (!dirty[t]) { ++t; continue; }
     uint32_t e = t;
     while (e < ntiles && dirty[e]) ++e;
-    HIPCHK(usn::launch_resort(a, t, e, s));
+    HIPCHK(usn::launch_recount(a, t, e, s));
+    any = true;
     t = e;
+  }
+  if (any) {
+    st = launch_scatter(&a, r, 1, s);
+    if (st) return st;
   }
   /* carried-out cache: authoritative from now on */
   usn_summary out = sum;

@@ -26,8 +26,8 @@ struct ClassifyArgs {
   uint32_t window;          /* readable bytes at every frame start (usn_batch.window) */
   /* outputs */
   uint32_t *decisions;
-  uint16_t *order;
-  uint32_t *runs;
+  uint16_t *cnt;            /* [ntiles][nbw] frames per bin of each tile (the scatter's input) */
+  uint32_t nbw;             /* row length of cnt: nbins rounded up to 8 */
   usn_tile_hdr *tiles;
   usn_summary *summary;
   uint32_t *host_list;      /* per tile USN_TILE slots */
@@ -116,8 +116,42 @@ size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_ld
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
-/* Rebuild order/runs/counts of tiles [t0, t1) from the (patched) decisions. */
-hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
+/* Recount the bin rows and class counts of tiles [t0, t1) from the (patched)
+ * decisions (the scatter then runs again). */
+hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
+
+/* ---- per-endpoint lists: the device-wide stable scatter ------------------
+ * After the classify (or tx) kernel has written each tile's decisions and its
+ * row of per-bin frame counts (cnt[tile][bin], u16), three launches:
+ *   scan_agg   per chunk of `tc` tiles and bin: the chunk's total (agg)
+ *   scan_off   per (tile, bin): where its first frame goes in `index`
+ *              (bin base + earlier chunks + earlier tiles of the chunk), and
+ *              the bin offsets
+ *   scatter    per tile: each frame's rank among the tile's frames of its bin
+ *              (bit-sliced ballots + per-segment byte counts), index[off + rank]
+ * Stable: bins in order, frames in frame order inside a bin. */
+#define USN_SCAN_MAX_CHUNKS 256u
+#define USN_SCAN_BINS_PER_BLOCK 512u   /* scan kernels: 256 threads x 2 bins */
+struct ScatterBatch {
+  const uint32_t *decisions;
+  const uint16_t *cnt;      /* [ntiles][nbw] */
+  uint32_t *off;            /* [ntiles][nbw] */
+  uint32_t *agg;            /* [nchunks][nbw] */
+  uint32_t *blk;            /* [nchunks][nblk] */
+  uint32_t *index;          /* [n] */
+  uint32_t *bin_off;        /* [nbins + 1] */
+  uint32_t n, ntiles, tc, nchunks;
+};
+struct ScatterArgs {
+  ScatterBatch b[USN_MAX_MULTI];
+  uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan grid: chunks of batch i from chunk_base[i] */
+  uint32_t tile_base[USN_MAX_MULTI + 1];    /* scatter grid */
+  uint32_t count;
+  uint32_t nbins, nbw, nblk, n_ep, nbits;
+};
+/* scratch bytes of one batch (cnt | off | agg | blk) and its carve */
+size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt);
 
 }  // namespace usn
 
@@ -125,6 +159,7 @@ hipError_t launch_resort(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStr
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
+hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream);
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }

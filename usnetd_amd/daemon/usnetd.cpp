@@ -196,13 +196,16 @@ class Daemon {
 
   /* data path buffers, one set per device replica (USNETD_HIP_DEVICES) */
   static const uint32_t HDR = 128;        // header window stride on the device
+  /* per source in h_out: the summary, bin_off[USN_MAX_BINS + 1], then index[n] */
+  static const size_t OUT_BINS = 128;
+  static const size_t OUT_HEAD = OUT_BINS + (size_t)(USN_MAX_BINS + 1) * 4;
   uint32_t max_batch_ = 4096;             // frames per source per round
   struct RepBuf {
     void *stream = nullptr;
     uint8_t *h_hdr = nullptr, *d_hdr = nullptr;   // headers of the round (pinned / device)
     uint16_t *h_lens = nullptr, *d_lens = nullptr;
     uint32_t cap = 0;                             // frames
-    uint8_t *h_out = nullptr;                     // pinned: tile headers, order, runs per source
+    uint8_t *h_out = nullptr;                     // pinned: summary, bin offsets, lists per source
     size_t out_cap = 0;
   };
   std::vector<RepBuf> reps_;
@@ -805,7 +808,7 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
     DevP dev;
     uint32_t start, n;     // arena frames [start, start + n)
     uint32_t dstart;       // first window in its replica's device buffer
-    size_t out_off;        // tile headers / order / runs in the replica's h_out
+    size_t out_off;        // summary / bin offsets / index in the replica's h_out
     usn_batch b;
     usn_result res;
   };
@@ -839,9 +842,8 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
     const uint32_t r = s.dev->rep;
     s.dstart = total[r];
     total[r] += s.n;
-    const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
     s.out_off = outb[r];
-    outb[r] += (size_t)nt * (sizeof(usn_tile_hdr) + USN_TILE * 2 + USN_TILE * 4);
+    outb[r] += OUT_HEAD + (size_t)s.n * 4;
   }
   for (uint32_t r = 0; r < R; ++r) {
     RepBuf &B = reps_[r];
@@ -956,15 +958,12 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
       st = usn_finalize(ctx_, &s.b, &s.res, B.stream, &info);
       if (st != USN_OK) break;
       for (int c = 0; c < 4; ++c) class_count_[c] += info.class_count[c];
-      /* the per-tile order output: tile headers, order rows, runs */
-      const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
+      /* the per-endpoint lists: summary (n_ep), bin offsets, index */
       uint8_t *o = B.h_out + s.out_off;
       select(s.dev->rep);
-      usn_memcpy_d2h(ctx_, o, s.res.tiles, nt * sizeof(usn_tile_hdr), B.stream);
-      usn_memcpy_d2h(ctx_, o + nt * sizeof(usn_tile_hdr), s.res.order, (size_t)nt * USN_TILE * 2,
-                     B.stream);
-      usn_memcpy_d2h(ctx_, o + nt * (sizeof(usn_tile_hdr) + USN_TILE * 2), s.res.runs,
-                     (size_t)nt * USN_TILE * 4, B.stream);
+      usn_memcpy_d2h(ctx_, o, s.res.summary, sizeof(usn_summary), B.stream);
+      usn_memcpy_d2h(ctx_, o + OUT_BINS, s.res.bin_off, (size_t)(USN_MAX_BINS + 1) * 4, B.stream);
+      usn_memcpy_d2h(ctx_, o + OUT_HEAD, s.res.index, (size_t)s.n * 4, B.stream);
     }
     k = e;
   }
@@ -976,36 +975,32 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
   for (uint32_t r = 0; r < R; ++r)
     if (total[r]) { select(r); usn_stream_sync(ctx_, reps_[r].stream); }
   /* 5. deliver, source by source, each target's frames in frame order with
-   *    one sendmmsg stream per target: the per-endpoint runs of the order
-   *    output, FLOOD (mirror_to_all, endpoint.rs:340-363: every endpoint but
-   *    the source) and Target::Nic merged in by frame index */
+   *    one sendmmsg stream per target: its list of the device-wide scatter
+   *    (usn_result.index, grouped by bin), with FLOOD (mirror_to_all,
+   *    endpoint.rs:340-363: every endpoint but the source) and Target::Nic
+   *    merged in by frame index */
   std::vector<DevP> unaddressable;
   std::vector<std::vector<uint32_t>> per(USN_MAX_ENDPOINTS);
   std::vector<uint32_t> nic, flood, merged, tmp;
   std::vector<uint16_t> touched;
   for (const Src &s : srcs) {
-    const uint32_t nt = (s.n + USN_TILE - 1) / USN_TILE;
     const uint8_t *o = reps_[s.dev->rep].h_out + s.out_off;
-    const usn_tile_hdr *th = reinterpret_cast<const usn_tile_hdr *>(o);
-    const uint16_t *order = reinterpret_cast<const uint16_t *>(o + nt * sizeof(usn_tile_hdr));
-    const uint32_t *runs =
-        reinterpret_cast<const uint32_t *>(o + nt * (sizeof(usn_tile_hdr) + USN_TILE * 2));
+    const usn_summary *sum = reinterpret_cast<const usn_summary *>(o);
+    const uint32_t *bin_off = reinterpret_cast<const uint32_t *>(o + OUT_BINS);
+    const uint32_t *index = reinterpret_cast<const uint32_t *>(o + OUT_HEAD);
+    const uint32_t bn = sum->n_ep;
+    auto list = [&](uint32_t bin, std::vector<uint32_t> &dst) {
+      for (uint32_t p = bin_off[bin]; p < bin_off[bin + 1]; ++p) dst.push_back(s.start + index[p]);
+    };
     nic.clear();
     flood.clear();
     touched.clear();
-    for (uint32_t t = 0; t < nt; ++t) {
-      const uint32_t nf = th[t].n_frames, nr = th[t].n_runs, bn = th[t].bin_nic;
-      for (uint32_t q = 0; q < nr; ++q) {
-        const uint32_t bin = runs[(size_t)t * USN_TILE + q] >> 16;
-        const uint32_t a = runs[(size_t)t * USN_TILE + q] & 0xFFFFu;
-        const uint32_t z = q + 1 < nr ? (runs[(size_t)t * USN_TILE + q + 1] & 0xFFFFu) : nf;
-        std::vector<uint32_t> *dst = bin < bn ? &per[bin] : bin == bn ? &nic : bin == bn + 1 ? &flood
-                                                                                          : nullptr;
-        if (!dst) continue;   // DROP
-        if (bin < bn && dst->empty()) touched.push_back((uint16_t)bin);
-        for (uint32_t p = a; p < z; ++p)
-          dst->push_back(s.start + t * USN_TILE + order[(size_t)t * USN_TILE + p]);
-      }
+    list(bn, nic);
+    list(bn + 1, flood);
+    for (uint32_t bin = 0; bin < bn; ++bin) {
+      if (bin_off[bin] == bin_off[bin + 1]) continue;
+      touched.push_back((uint16_t)bin);
+      list(bin, per[bin]);
     }
     const uint32_t nic_id = (uint32_t)s.dev->for_nic;   // Target::Nic of a sending endpoint
     for (const DevP &t : devices_) {

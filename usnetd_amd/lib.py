@@ -18,6 +18,7 @@ USN_TILE = 1024
 USN_WINDOW = 64
 USN_WINDOW_MAX = 80
 USN_MAX_ENDPOINTS = 4095
+USN_MAX_BINS = USN_MAX_ENDPOINTS + 3
 R_WINDOW = 7
 PARITY_MASK = 0x00FFFFFF
 EP_NIC, EP_HOST, EP_PIPE, EP_UDS = 0, 1, 2, 3
@@ -52,9 +53,10 @@ FRAME_READER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint16, C.c_uint64, C.POINTE
 
 
 class Result(C.Structure):
-    _fields_ = [("decisions", C.c_void_p), ("order", C.c_void_p), ("runs", C.c_void_p),
+    _fields_ = [("decisions", C.c_void_p), ("index", C.c_void_p), ("bin_off", C.c_void_p),
                 ("tiles", C.c_void_p), ("summary", C.c_void_p), ("host_list", C.c_void_p),
-                ("n", C.c_uint64)]
+                ("scratch", C.c_void_p), ("n", C.c_uint64), ("max_bins", C.c_uint32),
+                ("_pad", C.c_uint32)]
 
 
 class FinalizeInfo(C.Structure):
@@ -62,18 +64,19 @@ class FinalizeInfo(C.Structure):
                 ("flags", C.c_uint32), ("class_count", C.c_uint32 * 4)]
 
 
-TILE_HDR_DTYPE = np.dtype([("n_frames", "<u2"), ("n_runs", "<u2"), ("n_host", "<u2"),
+TILE_HDR_DTYPE = np.dtype([("n_frames", "<u2"), ("_r0", "<u2"), ("n_host", "<u2"),
                            ("bin_nic", "<u2"), ("class_count", "<u2", (4,)), ("last_state", "<u4"),
                            ("last_dst", "<u4"), ("last_idx", "<u4"), ("last_info", "<u4", (4,)),
                            ("_pad", "<u4")])
 SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames", "<u4"),
                           ("n_tiles", "<u4"), ("cin_state", "<u4"), ("cin_dst", "<u4"),
                           ("cin_info", "<u4", (4,)), ("cout_state", "<u4"), ("cout_dst", "<u4"),
-                          ("cout_info", "<u4", (4,))])
+                          ("cout_info", "<u4", (4,)), ("n_ep", "<u4"), ("n_bins", "<u4"),
+                          ("_pad", "<u4", (2,))])
 RULE_DTYPE = np.dtype([("dst_addr", "<u4"), ("src_addr", "<u4"), ("dst_port", "<u2"),
                        ("src_port", "<u2"), ("protocol", "u1"), ("present", "u1"),
                        ("endpoint", "<u2")])
-assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 64 and RULE_DTYPE.itemsize == 16
+assert TILE_HDR_DTYPE.itemsize == 48 and SUMMARY_DTYPE.itemsize == 80 and RULE_DTYPE.itemsize == 16
 
 _libs: dict = {}
 
@@ -102,7 +105,7 @@ def load(path: str | None = None):
         "usn_bridge_add": ([P, C.c_char_p], I), "usn_bridge_count": ([P], I),
         "usn_bridge_set": ([P, P, U32], I), "usn_table_build": ([P, P, U32], I),
         "usn_frag_clear": ([P], I), "usn_cache_clear": ([P, U16], I),
-        "usn_result_bytes": ([U64], SZ),
+        "usn_result_bytes": ([U64], SZ), "usn_result_bytes_ep": ([U64, U32], SZ),
         "usn_result_bind": ([P, SZ, U64, C.POINTER(Result)], I),
         "usn_classify": ([P, C.POINTER(Batch), C.POINTER(Result), P], I),
         "usn_finalize": ([P, C.POINTER(Batch), C.POINTER(Result), P, C.POINTER(FinalizeInfo)], I),
@@ -123,7 +126,7 @@ def load(path: str | None = None):
         "usn_replica_device": ([P, U32], I),
     }
     optional = {"usn_set_frame_reader", "usn_ctx_create_group", "usn_ctx_replicas",
-                "usn_replica_select", "usn_replica_device"}   # A/B builds of older ABI versions lack these
+                "usn_replica_select", "usn_replica_device", "usn_result_bytes_ep"}   # A/B builds of older ABI versions lack these
     for name, (args, res) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -137,7 +140,7 @@ def load(path: str | None = None):
 EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_create",
             "usn_ctx_destroy", "usn_endpoint_add", "usn_endpoint_remove", "usn_add_match",
             "usn_remove_match", "usn_rule_count", "usn_rules_get", "usn_lookup", "usn_bridge_add",
-            "usn_bridge_count", "usn_frag_clear", "usn_cache_clear", "usn_result_bytes",
+            "usn_bridge_count", "usn_frag_clear", "usn_cache_clear", "usn_result_bytes", "usn_result_bytes_ep",
             "usn_result_bind", "usn_classify", "usn_finalize", "usn_dev_alloc", "usn_dev_free",
             "usn_host_alloc_pinned", "usn_host_free_pinned", "usn_memcpy_h2d", "usn_memcpy_d2h",
             "usn_memset_d", "usn_stream_create", "usn_stream_destroy", "usn_stream_sync",
@@ -412,10 +415,17 @@ class DeviceBatch:
 
 
 class DeviceResult:
-    def __init__(self, ctx: Ctx, n: int):
+    """One usn_result: decisions, the per-endpoint lists (index, bin_off),
+    tile headers, summary.  max_endpoints sizes the scatter scratch for
+    endpoint ids below it (default: any id, USN_MAX_ENDPOINTS)."""
+
+    def __init__(self, ctx: Ctx, n: int, max_endpoints: int | None = None):
         self.ctx = ctx
         self.n = int(n)
-        nbytes = ctx.L.usn_result_bytes(self.n)
+        if max_endpoints is None:
+            nbytes = ctx.L.usn_result_bytes(self.n)
+        else:
+            nbytes = ctx.L.usn_result_bytes_ep(self.n, int(max_endpoints))
         self.buf = ctx.alloc(nbytes)
         self.desc = Result()
         check(ctx.L.usn_result_bind(self.buf.ptr, nbytes, self.n, C.byref(self.desc)),
@@ -428,11 +438,19 @@ class DeviceResult:
     def decisions(self, n=None) -> np.ndarray:
         return self.buf.download(np.uint32, n or self.n, self._off(self.desc.decisions))
 
-    def order(self) -> np.ndarray:
-        return self.buf.download(np.uint16, self.ntiles * USN_TILE, self._off(self.desc.order))
+    def index(self, n=None) -> np.ndarray:
+        return self.buf.download(np.uint32, n or self.n, self._off(self.desc.index))
 
-    def runs(self) -> np.ndarray:
-        return self.buf.download(np.uint32, self.ntiles * USN_TILE, self._off(self.desc.runs))
+    def bin_off(self, nbins=None) -> np.ndarray:
+        nb = int(self.summary()["n_bins"]) if nbins is None else nbins
+        return self.buf.download(np.uint32, nb + 1, self._off(self.desc.bin_off))
+
+    def lists(self, n=None) -> dict:
+        """{bin: frame indices in frame order} of the device-wide scatter
+        (bins: endpoint ids, then n_ep = NIC, n_ep + 1 = FLOOD, n_ep + 2 = DROP)."""
+        off = self.bin_off()
+        idx = self.index(n)
+        return {b: idx[off[b]:off[b + 1]] for b in range(off.size - 1) if off[b + 1] > off[b]}
 
     def tiles(self) -> np.ndarray:
         raw = self.buf.download(np.uint8, self.ntiles * TILE_HDR_DTYPE.itemsize,
@@ -447,17 +465,20 @@ class DeviceResult:
         self.buf.free()
 
 
-def per_endpoint_lists(order: np.ndarray, runs: np.ndarray, tiles: np.ndarray, n: int):
-    """Expand the per-tile (order, runs) output into {bin: global frame indices}."""
-    out: dict[int, list] = {}
-    for t in range(tiles.shape[0]):
-        nr = int(tiles[t]["n_runs"])
-        nf = int(tiles[t]["n_frames"])
-        r = runs[t * USN_TILE:t * USN_TILE + nr]
-        starts = (r & 0xFFFF).astype(np.int64)
-        bins = (r >> 16).astype(np.int64)
-        ends = np.append(starts[1:], nf)
-        o = order[t * USN_TILE:t * USN_TILE + nf].astype(np.int64) + t * USN_TILE
-        for b, s, e in zip(bins, starts, ends):
-            out.setdefault(int(b), []).append(o[s:e])
-    return {b: np.concatenate(v) for b, v in out.items()}
+def dec_bin(dec: np.ndarray, n_ep: int) -> np.ndarray:
+    """bin of each decision word: its endpoint id (class EP), else NIC / FLOOD / DROP after the
+    endpoints (usn_classify.h, usn_result.index)."""
+    cls = (dec >> 16) & 0xF
+    ep = dec & 0xFFFF
+    other = n_ep + ((cls + 2) & 3)
+    return np.where(cls == CLS_EP, ep, other).astype(np.int64)
+
+
+def expected_lists(dec: np.ndarray, n_ep: int) -> dict:
+    """{bin: frame indices} a stable scatter of these decisions must produce."""
+    bins = dec_bin(np.asarray(dec, np.uint32), n_ep)
+    order = np.argsort(bins, kind="stable")
+    sb = bins[order]
+    cuts = np.flatnonzero(np.diff(sb)) + 1
+    return {int(sb[g[0]]): order[g].astype(np.uint32) for g in np.split(np.arange(sb.size), cuts)
+            if g.size}
