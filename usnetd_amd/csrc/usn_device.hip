@@ -242,6 +242,16 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_BATCH2
 #define USN_BATCH2 1
 #endif
+/* tests/test_isa_waits.py builds perturbed variants to show its check fails:
+ * 1 = an extra load between a slot read and its wait, 2 = a stale count */
+#ifndef USN_ISA_PERTURB
+#define USN_ISA_PERTURB 0
+#endif
+#if USN_ISA_PERTURB == 2
+#define USN_U_WAIT0 "2"
+#else
+#define USN_U_WAIT0 "1"   /* round 0's U slot read: round 1's is the one younger load */
+#endif
 #ifndef USN_X_BATCH   /* U path: both rounds' X probes in flight together */
 #define USN_X_BATCH 1
 #endif
@@ -748,6 +758,7 @@ __device__ __forceinline__ void tile_hist(const uint32_t bins[ROUNDS], uint32_t 
     }
   }
 }
+__device__ __forceinline__ uint32_t byte_sum(uint32_t v) { return __builtin_amdgcn_sad_u8(v, 0u, 0u); }
 __device__ __forceinline__ uint32_t hist_get(const uint32_t *hist, uint32_t b) {
   return (hist[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
 }
@@ -1108,12 +1119,19 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       const bool n1 = pr[1].status == 1u;
       du1 = lds_disp1(Dl, a.ph[2], n1, ku1);
       asm_slot1(T, a.ph[2], n1, ku1, du1, su1);
+#if USN_ISA_PERTURB == 1   /* tests/test_isa_waits.py only: a load between issue and wait */
+      uint32_t perturb;
+      asm volatile("global_load_dword %0, %1, off" : "=v"(perturb) : "v"(a.lens + tid) : "memory");
+#endif
       uint32_t w01, w02, w11, w12;
       bool x0, x1;
-      asm volatile("s_waitcnt vmcnt(1)" : "+v"(su0) :: "memory");
+      asm volatile("s_waitcnt vmcnt(" USN_U_WAIT0 ")" : "+v"(su0) :: "memory");
       u_decode(su0, pr[0], e0, w01, w02, x0);
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(su1) :: "memory");
       u_decode(su1, pr[1], e1, w11, w12, x1);
+#if USN_ISA_PERTURB == 1
+      if (perturb == 0xFFFFFFFFu) w01 = 0;
+#endif
       x0 = x0 && n0;
       x1 = x1 && n1;
       STAMP(4);
@@ -2652,12 +2670,13 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
  * The classify / tx kernel leaves each tile's decisions and its count row
  * cnt[tile][bin] (u16).  Three launches turn them into `index` (the batch's
  * frame indices grouped by bin, frame order inside a bin) and bin_off:
- *   scan_agg  (chunk, bin block): the chunk's frames per bin          agg
- *   scan_off  (chunk, bin block): each bin's base (bins before it, all
- *             chunks) + the chunks before this one, then per tile of the
- *             chunk the list position of its first frame of the bin     off
- *   scatter   (tile): rank of each frame among the tile's frames of its bin,
- *             index[off[tile][bin] + rank] = frame
+ *   scan_agg     (chunk, bin block): the chunk's frames per bin           agg
+ *   scan_chunks  (bin pair, one wave): agg := its exclusive scan over the
+ *                chunks; tot = the bin's frames
+ *   scatter      (chunk, its tiles in order): running[bin] = bin base (block
+ *                scan of tot) + agg; per tile each frame's rank among the
+ *                tile's frames of its bin, index[running + rank] = frame,
+ *                running += the tile's count
  * Algorithmic bytes per frame: 4 (index).  The reference writes each frame
  * straight into its target's ring (endpoint.rs:61-74) and copies FLOOD frames
  * to every other endpoint (:340-363): an endpoint's frames are its list merged
@@ -2672,11 +2691,21 @@ __device__ __forceinline__ uint32_t base_of(const uint32_t *base, uint32_t count
 
 #define SCAN_THREADS 256
 static_assert(USN_SCAN_BINS_PER_BLOCK == 2 * SCAN_THREADS, "two bins per scan thread");
+static_assert(USN_SCAN_MAX_CHUNKS <= 64 * 16, "scan_chunks: 16 chunks per lane");
 
-/* frames of bins 2w, 2w+1 over tiles [t0, t1): 8 row loads in flight */
-__device__ __forceinline__ void col_sum(const uint32_t *col, uint32_t stride, uint32_t t0, uint32_t t1,
-                                        uint32_t &lo, uint32_t &hi) {
-  uint32_t t = t0;
+/* (chunk, bin block): frames of bins 2w, 2w+1 over the chunk's tiles, 8 row
+ * loads in flight */
+__global__ __launch_bounds__(SCAN_THREADS) void scan_agg_kernel(ScatterArgs s) {
+  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
+  const uint32_t bi = base_of(s.chunk_base, s.count, g);
+  const ScatterBatch &B = s.b[bi];
+  const uint32_t c = g - s.chunk_base[bi];
+  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
+  const uint32_t w = bb * SCAN_THREADS + tid;          // bins 2w, 2w + 1
+  if (2 * w >= s.nbw) return;
+  const uint32_t *col = reinterpret_cast<const uint32_t *>(B.cnt) + w;
+  const uint32_t stride = s.nbw / 2;
+  uint32_t lo = 0, hi = 0, t = t0;
   for (; t + 8 <= t1; t += 8) {
     uint32_t v[8];
 #pragma unroll
@@ -2688,169 +2717,149 @@ __device__ __forceinline__ void col_sum(const uint32_t *col, uint32_t stride, ui
     const uint32_t v = col[(size_t)t * stride];
     lo += v & 0xFFFFu; hi += v >> 16;
   }
+  *reinterpret_cast<uint2 *>(B.agg + (size_t)c * s.nbw + 2 * w) = make_uint2(lo, hi);
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void scan_agg_kernel(ScatterArgs s) {
-  __shared__ uint32_t red[SCAN_THREADS / 64];
-  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
-  const uint32_t bi = base_of(s.chunk_base, s.count, g);
-  const ScatterBatch &B = s.b[bi];
-  const uint32_t c = g - s.chunk_base[bi];
-  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
-  const uint32_t w = bb * SCAN_THREADS + tid;          // bins 2w, 2w + 1
+/* (bin pair, batch): one wave, lane L owns chunks 16L .. 16L+15: agg of the
+ * bin pair over the chunks -> its exclusive scan in place, and the totals */
+__global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ScatterBatch &B = s.b[blockIdx.y];
+  const uint32_t p = blockIdx.x * (SCAN_THREADS / 64) + wave;   // bins 2p, 2p + 1
+  if (2 * p >= s.nbw) return;
+  uint2 *col = reinterpret_cast<uint2 *>(B.agg + 2 * p);
+  const uint32_t stride = s.nbw / 2;                           // uint2 per agg row
+  uint2 v[16];
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t c = lane * 16 + k;
+    v[k] = c < B.nchunks ? col[(size_t)c * stride] : make_uint2(0, 0);
+  }
   uint32_t lo = 0, hi = 0;
-  if (2 * w < s.nbw) {
-    col_sum(reinterpret_cast<const uint32_t *>(B.cnt) + w, s.nbw / 2, t0, t1, lo, hi);
-    *reinterpret_cast<uint2 *>(B.agg + (size_t)c * s.nbw + 2 * w) = make_uint2(lo, hi);
-  }
-  uint32_t sum = lo + hi;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-  if ((tid & 63) == 0) red[tid >> 6] = sum;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t t = 0;
+  for (uint32_t k = 0; k < 16; ++k) { lo += v[k].x; hi += v[k].y; }
+  const uint32_t ilo = wave_incl_scan(lo, lane), ihi = wave_incl_scan(hi, lane);
+  uint32_t elo = ilo - lo, ehi = ihi - hi;
 #pragma unroll
-    for (int k = 0; k < SCAN_THREADS / 64; ++k) t += red[k];
-    B.blk[(size_t)c * s.nblk + bb] = t;
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t c = lane * 16 + k;
+    if (c < B.nchunks) col[(size_t)c * stride] = make_uint2(elo, ehi);
+    elo += v[k].x; ehi += v[k].y;
   }
+  if (lane == 63) *reinterpret_cast<uint2 *>(B.tot + 2 * p) = make_uint2(ilo, ihi);
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void scan_off_kernel(ScatterArgs s) {
-  __shared__ uint32_t red[2 * (SCAN_THREADS / 64)];
-  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
-  const uint32_t lane = tid & 63, wave = tid >> 6;
-  const uint32_t bi = base_of(s.chunk_base, s.count, g);
-  const ScatterBatch &B = s.b[bi];
-  const uint32_t c = g - s.chunk_base[bi];
-  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
-  const uint32_t w = bb * SCAN_THREADS + tid;
-  const bool on = 2 * w < s.nbw;
-  // this bin pair over every chunk: its total, and the chunks before c
-  uint32_t tlo = 0, thi = 0, elo = 0, ehi = 0;
-  if (on) {
-    const uint32_t *col = B.agg + 2 * w;
-    for (uint32_t k = 0; k < B.nchunks; ++k) {
-      const uint2 v = *reinterpret_cast<const uint2 *>(col + (size_t)k * s.nbw);
-      tlo += v.x; thi += v.y;
-      if (k < c) { elo += v.x; ehi += v.y; }
-    }
-  }
-  // frames of the bin blocks before bb (every chunk)
-  uint32_t before = 0;
-  for (uint32_t k = tid; k < B.nchunks * bb; k += SCAN_THREADS)
-    before += B.blk[(size_t)(k / bb) * s.nblk + (k % bb)];
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) before += __shfl_xor(before, d, 64);
-  // + the bins of this block before 2w
-  const uint32_t v = tlo + thi;
-  const uint32_t inc = wave_incl_scan(v, lane);
-  if (lane == 63) red[wave] = inc;
-  if (lane == 0) red[SCAN_THREADS / 64 + wave] = before;
-  __syncthreads();
-  uint32_t pre = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < SCAN_THREADS / 64; ++k) pre += red[SCAN_THREADS / 64 + k] + (k < wave ? red[k] : 0u);
-  const uint32_t base_lo = pre + inc - v, base_hi = base_lo + tlo;
-  if (c == 0) {   // bin offsets (pad bins past nbins are empty: bin_off[nbins] = n)
-    if (2 * w <= s.nbins) B.bin_off[2 * w] = base_lo;
-    if (2 * w + 1 <= s.nbins) B.bin_off[2 * w + 1] = base_hi;
-    if (bb == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
-  }
-  if (!on) return;
-  uint32_t slo = base_lo + elo, shi = base_hi + ehi;
-  const uint32_t stride = s.nbw / 2;
-  const uint32_t *col = reinterpret_cast<const uint32_t *>(B.cnt) + w;
-  uint2 *out = reinterpret_cast<uint2 *>(B.off + 2 * w);
-  uint32_t t = t0;
-  for (; t + 8 <= t1; t += 8) {
-    uint32_t cv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cv[k] = col[(size_t)(t + k) * stride];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      out[(size_t)(t + k) * stride] = make_uint2(slo, shi);
-      slo += cv[k] & 0xFFFFu; shi += cv[k] >> 16;
-    }
-  }
-  for (; t < t1; ++t) {
-    const uint32_t cv = col[(size_t)t * stride];
-    out[(size_t)t * stride] = make_uint2(slo, shi);
-    slo += cv & 0xFFFFu; shi += cv >> 16;
-  }
-}
-
-/* one tile per workgroup of 512 threads (two frames per lane).  Blocks are
- * dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them so that an
- * XCD takes a contiguous run of tiles, whose list entries of a bin are
- * adjacent: its L2 assembles each bin's lines before writing them back
- * (cdna_hip_programming.md T1 swizzle, bijective). */
+/* (chunk): its tiles in order, one workgroup of 512 threads (two frames per
+ * lane).  Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD
+ * remaps them so that an XCD takes a contiguous run of chunks, whose list
+ * entries of a bin are adjacent: its L2 assembles each bin's lines before
+ * writing them back (cdna_hip_programming.md T1 swizzle, bijective). */
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   extern __shared__ __align__(16) uint8_t smem[];
-  uint32_t *offrow = reinterpret_cast<uint32_t *>(smem);            // [nbw]
+  __shared__ uint32_t s_scan[16];
+  uint32_t *run = reinterpret_cast<uint32_t *>(smem);               // [nbw]
   uint4 *rows = reinterpret_cast<uint4 *>(smem + (size_t)s.nbw * 4);  // [nbins]: u8 per segment
   uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nwg = s.tile_base[s.count];
-  uint32_t w = blockIdx.x;
+  const uint32_t nwg = s.chunk_base[s.count];
+  uint32_t g = blockIdx.x;
   if (USN_SCATTER_XCD) {
-    const uint32_t q = nwg / 8, r = nwg % 8, x = w % 8;
-    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+    const uint32_t q = nwg / 8, r = nwg % 8, x = g % 8;
+    g = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + g / 8;
   }
-  const uint32_t bi = base_of(s.tile_base, s.count, w);
+  const uint32_t bi = base_of(s.chunk_base, s.count, g);
   const ScatterBatch &B = s.b[bi];
-  const uint32_t tile = w - s.tile_base[bi];
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
+  const uint32_t c = g - s.chunk_base[bi];
+  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
+  // the first tile's decisions fly while the bases are formed
   uint32_t d[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
   {
-    const uint4 *src = reinterpret_cast<const uint4 *>(B.off + (size_t)tile * s.nbw);
-    for (uint32_t i = tid; i < s.nbw / 4; i += NTHREADS) reinterpret_cast<uint4 *>(offrow)[i] = src[i];
-    for (uint32_t i = tid; i < s.nbins; i += NTHREADS) rows[i] = make_uint4(0, 0, 0, 0);
+    const uint64_t base = (uint64_t)t0 * TILE;
+    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
+  }
+  // running[b] = base[b] (frames of the bins before b) + this chunk's offset in b
+  {
+    const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;   // bins per thread, contiguous
+    const uint32_t b0 = tid * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; ++k)
+      if (b0 + k < s.nbw) sum += B.tot[b0 + k];
+    uint32_t total;
+    uint32_t pre = block_excl_scan(sum, s_scan, &total);
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = b0 + k;
+      if (b >= s.nbw) break;
+      run[b] = pre + B.agg[(size_t)c * s.nbw + b];
+      if (c == 0 && b <= s.nbins) B.bin_off[b] = pre;   // pad bins past nbins are empty
+      pre += B.tot[b];
+    }
+    if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  uint32_t bins[ROUNDS], rank[ROUNDS];
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint64_t base = (uint64_t)t * TILE;
+    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
+    uint32_t bins[ROUNDS], rank[ROUNDS];
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    const bool v = local < nt;
-    bins[r] = dec_bin(d[r], s.n_ep);
-    const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
-    rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-    if (v && rank[r] == 0) cb[bins[r] * 16 + r * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
-  }
-  __syncthreads();
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      const bool v = local < nt;
+      bins[r] = dec_bin(d[r], s.n_ep);
+      const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
+      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
+      if (v && rank[r] == 0) cb[bins[r] * 16 + r * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
+    }
+    if (t + 1 < t1) {   // the next tile's decisions fly under this one
+      const uint64_t nb = base + TILE;
+      const uint32_t nn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - nb);
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) {
-    const uint32_t local = r * NTHREADS + tid;
-    if (local >= nt) continue;
-    const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
-    const uint4 wv = rows[b];
-    // frames of bin b in the segments before sg: whole words, then the low bytes of one
-    const uint32_t q = sg >> 2, part = sg & 3u;
-    const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
-    const uint32_t p0 = q > 0 ? wv.x : (wv.x & mpart);
-    const uint32_t p1 = q > 1 ? wv.y : q == 1 ? (wv.y & mpart) : 0u;
-    const uint32_t p2 = q > 2 ? wv.z : q == 2 ? (wv.z & mpart) : 0u;
-    const uint32_t p3 = q == 3 ? (wv.w & mpart) : 0u;
-    const uint32_t before = __builtin_amdgcn_sad_u8(p0, 0u, 0u) + __builtin_amdgcn_sad_u8(p1, 0u, 0u) +
-                            __builtin_amdgcn_sad_u8(p2, 0u, 0u) + __builtin_amdgcn_sad_u8(p3, 0u, 0u);
-    B.index[offrow[b] + before + rank[r]] = (uint32_t)(base + local);
+      for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[nb + min(r * NTHREADS + tid, nn - 1)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      const uint32_t local = r * NTHREADS + tid;
+      if (local >= nt) continue;
+      const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
+      const uint4 wv = rows[b];
+      // frames of bin b in the segments before sg: whole words, then the low bytes of one
+      const uint32_t q = sg >> 2, part = sg & 3u;
+      const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
+      const uint32_t p0 = q > 0 ? wv.x : (wv.x & mpart);
+      const uint32_t p1 = q > 1 ? wv.y : q == 1 ? (wv.y & mpart) : 0u;
+      const uint32_t p2 = q > 2 ? wv.z : q == 2 ? (wv.z & mpart) : 0u;
+      const uint32_t p3 = q == 3 ? (wv.w & mpart) : 0u;
+      const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
+      B.index[run[b] + before + rank[r]] = (uint32_t)(base + local);
+    }
+    __syncthreads();
+    // running += the tile's frames per bin; rows cleared for the next tile
+    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) {
+      const uint4 wv = rows[b];
+      const uint32_t n = byte_sum(wv.x) + byte_sum(wv.y) + byte_sum(wv.z) + byte_sum(wv.w);
+      if (n) {
+        run[b] += n;
+        rows[b] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    __syncthreads();
   }
 }
 static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
 
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
-  const uint32_t chunks = s.chunk_base[s.count], tiles = s.tile_base[s.count];
-  if (tiles == 0) return hipSuccess;
-  const dim3 sg(chunks, s.nblk);
-  hipLaunchKernelGGL(scan_agg_kernel, sg, dim3(SCAN_THREADS), 0, stream, s);
-  hipLaunchKernelGGL(scan_off_kernel, sg, dim3(SCAN_THREADS), 0, stream, s);
+  const uint32_t chunks = s.chunk_base[s.count];
+  if (chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_agg_kernel, dim3(chunks, s.nblk), dim3(SCAN_THREADS), 0, stream, s);
+  const uint32_t pairs = s.nbw / 2;
+  hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
+                     dim3(SCAN_THREADS), 0, stream, s);
   const size_t lds = (size_t)s.nbw * 4 + (size_t)s.nbins * 16;
   if (lds > 64u * 1024u) {
     static thread_local bool raised = false;
@@ -2861,7 +2870,7 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
       raised = true;
     }
   }
-  hipLaunchKernelGGL(scatter_kernel, dim3(tiles), dim3(NTHREADS), lds, stream, s);
+  hipLaunchKernelGGL(scatter_kernel, dim3(chunks), dim3(NTHREADS), lds, stream, s);
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512

@@ -123,35 +123,38 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
 /* ---- per-endpoint lists: the device-wide stable scatter ------------------
  * After the classify (or tx) kernel has written each tile's decisions and its
  * row of per-bin frame counts (cnt[tile][bin], u16), three launches:
- *   scan_agg   per chunk of `tc` tiles and bin: the chunk's total (agg)
- *   scan_off   per (tile, bin): where its first frame goes in `index`
- *              (bin base + earlier chunks + earlier tiles of the chunk), and
- *              the bin offsets
- *   scatter    per tile: each frame's rank among the tile's frames of its bin
- *              (bit-sliced ballots + per-segment byte counts), index[off + rank]
+ *   scan_agg     (chunk of tc tiles, bin block): the chunk's frames per bin
+ *   scan_chunks  (bin pair, one wave): exclusive scan of agg over the chunks
+ *                (in place) and the bin's total
+ *   scatter      (chunk, persistent over its tiles): the bin bases (a block
+ *                scan of the totals), then per tile each frame's rank among
+ *                the tile's frames of its bin (bit-sliced ballots + per-segment
+ *                byte counts) and index[running[bin] + rank] = frame
  * Stable: bins in order, frames in frame order inside a bin. */
-#define USN_SCAN_MAX_CHUNKS 256u
-#define USN_SCAN_BINS_PER_BLOCK 512u   /* scan kernels: 256 threads x 2 bins */
+#define USN_SCAN_MAX_CHUNKS 1024u      /* chunks per batch (one wave scans them: 16 per lane) */
+#define USN_SCAN_LAUNCH_CHUNKS 1024u   /* scatter workgroups a launch aims at (4 per CU) */
+#define USN_SCAN_BINS_PER_BLOCK 512u   /* scan_agg: 256 threads x 2 bins */
 struct ScatterBatch {
   const uint32_t *decisions;
   const uint16_t *cnt;      /* [ntiles][nbw] */
-  uint32_t *off;            /* [ntiles][nbw] */
-  uint32_t *agg;            /* [nchunks][nbw] */
-  uint32_t *blk;            /* [nchunks][nblk] */
+  uint32_t *agg;            /* [nchunks][nbw]: chunk totals, then their exclusive scan */
+  uint32_t *tot;            /* [nbw]: frames per bin */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
   uint32_t n, ntiles, tc, nchunks;
 };
 struct ScatterArgs {
   ScatterBatch b[USN_MAX_MULTI];
-  uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan grid: chunks of batch i from chunk_base[i] */
-  uint32_t tile_base[USN_MAX_MULTI + 1];    /* scatter grid */
+  uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan_agg / scatter grid: chunks of batch i */
   uint32_t count;
   uint32_t nbins, nbw, nblk, n_ep, nbits;
 };
-/* scratch bytes of one batch (cnt | off | agg | blk) and its carve */
+/* scratch bytes of one batch (cnt | agg | tot) and its carve; tc = tiles per
+ * chunk, chosen per launch (scatter_tc) */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt);
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
+                   uint16_t **cnt);
+uint32_t scatter_tc(uint32_t ntiles, uint32_t launch_tiles);
 
 }  // namespace usn
 
