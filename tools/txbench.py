@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
-"""tx-direction timing (c4tx): device time of the tx launch (HIP events on
-the launch stream), usn_finalize wall time (it waits for the launch, then
-applies the learned state and runs any host tail) and the classify call's
-wall time (the table rebuild when the previous batch learned), per batch.
+"""tx-direction timing (c4tx): device time of one usn_classify call (the tx
+launch plus the per-endpoint scatter; HIP events on the launch stream),
+usn_finalize wall time (it waits for the launch, then applies the learned
+state and runs any host tail) and the classify call's wall time (the table
+rebuild when the previous batch learned), per batch.
 
-Usage: python tools/txbench.py [n] [batches] [distinct]
+Usage: python tools/txbench.py [n] [batches] [distinct] [libpath] [--rotate R]
   distinct > 1 rotates over that many differently-seeded rings (new flows
   keep learning answer rules); 1 replays one ring (steady state: nothing new).
+  --rotate R: the one ring's frames in R distinct device buffers used in turn
+  (same flows, nothing new learned after the first batch, and R x the ring's
+  bytes touched between two uses of a buffer: with R x 64 MiB > 256 MiB no
+  batch is served from the Infinity Cache -- SURVEY §8d's anti-cache rule).
 """
+import argparse
 import ctypes as C
 import json
 import os
@@ -24,20 +30,27 @@ from usnetd_amd import lib, traffic  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-    nb = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-    distinct = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-    libpath = sys.argv[4] if len(sys.argv) > 4 else None   # an A/B build (build/abl/<v>/libusn.so)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("n", nargs="?", type=int, default=1 << 20)
+    ap.add_argument("batches", nargs="?", type=int, default=8)
+    ap.add_argument("distinct", nargs="?", type=int, default=1)
+    ap.add_argument("libpath", nargs="?", default=None)
+    ap.add_argument("--rotate", type=int, default=1)
+    a = ap.parse_args()
+    n, nb, distinct = a.n, a.batches, a.distinct
     cfgs = [traffic.c4tx(n=n, seed=6 + k) for k in range(distinct)]
-    ctx = lib.Ctx(0, libpath) if libpath else lib.Ctx(0)
+    ctx = lib.Ctx(0, a.libpath) if a.libpath else lib.Ctx(0)
     traffic.install_ctx(ctx, cfgs[0])
     s = ctx.stream()
     batches = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+    for _ in range(a.rotate - 1):   # the same ring again in another buffer
+        batches.append(lib.DeviceBatch(ctx, cfgs[0].frames, cfgs[0].lens, cfgs[0].src,
+                                       stride=cfgs[0].stride))
     results = [lib.DeviceResult(ctx, n) for _ in range(2)]
     ev = [(ctx.event(), ctx.event()) for _ in range(nb)]
     rows = []
     for k in range(nb):
-        b, r = batches[k % distinct], results[k % 2]
+        b, r = batches[k % len(batches)], results[k % 2]
         t0 = time.perf_counter()
         ctx.record(ev[k][0], s)
         ctx.classify(b, r, s)
@@ -45,21 +58,18 @@ def main():
         t1 = time.perf_counter()
         info = ctx.finalize(b, r, s)
         t2 = time.perf_counter()
-        dbg = (C.c_uint32 * 10)()
-        if hasattr(ctx.L, "usn_debug_tx_state"):
-            ctx.L.usn_debug_tx_state.argtypes = [C.c_void_p, C.c_void_p]
-        if hasattr(ctx.L, "usn_debug_tx_state") and ctx.L.usn_debug_tx_state(ctx.h, dbg) == 0:
-            print("tx state", list(dbg), flush=True)
         rows.append({"batch": k, "device_ms": round(ctx.elapsed_ms(*ev[k]), 4),
                      "classify_call_ms": round((t1 - t0) * 1e3, 3),
                      "finalize_ms": round((t2 - t1) * 1e3, 3),
                      "n_learned": int(info.n_learned), "n_host": int(info.n_host),
                      "rules": ctx.rule_count()})
         print(json.dumps(rows[-1]), flush=True)
-    dev = np.array([x["device_ms"] for x in rows[1:]])
-    fin = np.array([x["finalize_ms"] for x in rows[1:]])
-    cal = np.array([x["classify_call_ms"] for x in rows[1:]])
-    out = {"n": n, "batches": nb, "distinct": distinct,
+    steady = rows[max(1, len(batches)):] or rows[1:]
+    dev = np.array([x["device_ms"] for x in steady])
+    fin = np.array([x["finalize_ms"] for x in steady])
+    cal = np.array([x["classify_call_ms"] for x in steady])
+    out = {"n": n, "batches": nb, "distinct": distinct, "rotate_buffers": len(batches),
+           "rotating_bytes": int(len(batches) * n * cfgs[0].stride),
            "device_ms_median": float(np.median(dev)),
            "device_mpps": round(n / np.median(dev) / 1e3, 1),
            "classify_call_ms_median": float(np.median(cal)),

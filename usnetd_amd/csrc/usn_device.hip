@@ -2750,18 +2750,30 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
 }
 
 /* (chunk): its tiles in order, one workgroup of 512 threads (two frames per
- * lane).  Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD
- * remaps them so that an XCD takes a contiguous run of chunks, whose list
- * entries of a bin are adjacent: its L2 assembles each bin's lines before
- * writing them back (cdna_hip_programming.md T1 swizzle, bijective). */
+ * lane).  A tile is ranked in steps of SR rounds (512 frames each): SR = 2
+ * ranks the whole tile at once (16 segments of 64 frames, a 16-byte row of u8
+ * counts per bin); SR = 1 half a tile (8 segments, 8-byte rows) for bin
+ * counts whose 16-byte rows would not fit 64 KiB of LDS (c5 with 4093 pipes).
+ * Every load and store of the loop is unconditional (lanes past a ragged
+ * tile's end store to sink slots past index[n]; the last tile re-reads
+ * itself as its "next"), so hipcc counts them: the wait for the next tile's
+ * decisions leaves this tile's scattered stores in flight instead of
+ * draining them (vmcnt(0)) once per tile.
+ * Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them
+ * so that an XCD takes a contiguous run of chunks, whose list entries of a
+ * bin are adjacent: its L2 assembles each bin's lines before writing them
+ * back (cdna_hip_programming.md T1 swizzle, bijective). */
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
+template <int SR>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
+  typedef typename std::conditional<SR == 2, uint4, uint2>::type Row;
+  constexpr uint32_t SEGB = SR * (NTHREADS / 64);                    // row bytes = segments per step
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint32_t s_scan[16];
   uint32_t *run = reinterpret_cast<uint32_t *>(smem);               // [nbw]
-  uint4 *rows = reinterpret_cast<uint4 *>(smem + (size_t)s.nbw * 4);  // [nbins]: u8 per segment
+  Row *rows = reinterpret_cast<Row *>(smem + (size_t)s.nbw * 4);     // [nbins]: u8 per segment
   uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nwg = s.chunk_base[s.count];
@@ -2799,56 +2811,70 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       pre += B.tot[b];
     }
     if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
-    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = make_uint4(0, 0, 0, 0);
+    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
   }
+  // the loop carries bins, not decisions: the next tile's decisions are
+  // converted at the end of an iteration, where waiting for them leaves this
+  // tile's stores (issued after them) in flight
+  uint32_t bins[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[r], s.n_ep);
   __syncthreads();
   for (uint32_t t = t0; t < t1; ++t) {
     const uint64_t base = (uint64_t)t * TILE;
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
-    uint32_t bins[ROUNDS], rank[ROUNDS];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      const bool v = local < nt;
-      bins[r] = dec_bin(d[r], s.n_ep);
-      const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
-      rank[r] = (uint32_t)__popcll(same & lanemask_lt(lane));
-      if (v && rank[r] == 0) cb[bins[r] * 16 + r * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
-    }
-    if (t + 1 < t1) {   // the next tile's decisions fly under this one
-      const uint64_t nb = base + TILE;
+    {  // the next tile's decisions fly under this one (the last tile reloads itself)
+      const uint64_t nb = (uint64_t)min(t + 1, t1 - 1) * TILE;
       const uint32_t nn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - nb);
 #pragma unroll
       for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[nb + min(r * NTHREADS + tid, nn - 1)];
     }
-    __syncthreads();
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local >= nt) continue;
-      const uint32_t sg = r * (NTHREADS / 64) + wave, b = bins[r];
-      const uint4 wv = rows[b];
-      // frames of bin b in the segments before sg: whole words, then the low bytes of one
-      const uint32_t q = sg >> 2, part = sg & 3u;
-      const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
-      const uint32_t p0 = q > 0 ? wv.x : (wv.x & mpart);
-      const uint32_t p1 = q > 1 ? wv.y : q == 1 ? (wv.y & mpart) : 0u;
-      const uint32_t p2 = q > 2 ? wv.z : q == 2 ? (wv.z & mpart) : 0u;
-      const uint32_t p3 = q == 3 ? (wv.w & mpart) : 0u;
-      const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
-      B.index[run[b] + before + rank[r]] = (uint32_t)(base + local);
-    }
-    __syncthreads();
-    // running += the tile's frames per bin; rows cleared for the next tile
-    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) {
-      const uint4 wv = rows[b];
-      const uint32_t n = byte_sum(wv.x) + byte_sum(wv.y) + byte_sum(wv.z) + byte_sum(wv.w);
-      if (n) {
-        run[b] += n;
-        rows[b] = make_uint4(0, 0, 0, 0);
+    for (uint32_t h = 0; h < ROUNDS / SR; ++h) {
+      uint32_t rank[SR];
+#pragma unroll
+      for (uint32_t k = 0; k < SR; ++k) {
+        const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
+        const bool v = local < nt;
+        const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
+        rank[k] = (uint32_t)__popcll(same & lanemask_lt(lane));
+        if (v && rank[k] == 0) cb[bins[r] * SEGB + k * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
       }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < SR; ++k) {
+        const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
+        const uint32_t sg = k * (NTHREADS / 64) + wave, b = bins[r];
+        // frames of bin b in the segments before sg: whole words, then the low bytes of one
+        const Row wv = rows[b];
+        const uint32_t w[4] = {wv.x, wv.y, SR == 2 ? ((const uint4 &)wv).z : 0u,
+                               SR == 2 ? ((const uint4 &)wv).w : 0u};
+        const uint32_t q = sg >> 2, part = sg & 3u;
+        const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
+        const uint32_t p0 = q > 0 ? w[0] : (w[0] & mpart);
+        const uint32_t p1 = q > 1 ? w[1] : q == 1 ? (w[1] & mpart) : 0u;
+        const uint32_t p2 = q > 2 ? w[2] : q == 2 ? (w[2] & mpart) : 0u;
+        const uint32_t p3 = q == 3 ? (w[3] & mpart) : 0u;
+        const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
+        const bool v = local < nt;
+        const uint32_t pos = v ? run[b] + before + rank[k] : B.n + local;   // sink slots
+        B.index[pos] = (uint32_t)(base + local);
+      }
+      __syncthreads();
+      // running += this step's frames per bin; rows cleared for the next step
+      for (uint32_t b = tid; b < s.nbins; b += NTHREADS) {
+        const Row wv = rows[b];
+        uint32_t n = byte_sum(wv.x) + byte_sum(wv.y);
+        if (SR == 2) n += byte_sum(((const uint4 &)wv).z) + byte_sum(((const uint4 &)wv).w);
+        if (n) {
+          run[b] += n;
+          rows[b] = Row{};
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[r], s.n_ep);
   }
 }
 static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
@@ -2860,17 +2886,13 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t pairs = s.nbw / 2;
   hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
                      dim3(SCAN_THREADS), 0, stream, s);
-  const size_t lds = (size_t)s.nbw * 4 + (size_t)s.nbins * 16;
-  if (lds > 64u * 1024u) {
-    static thread_local bool raised = false;
-    if (!raised) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&scatter_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
-      raised = true;
-    }
-  }
-  hipLaunchKernelGGL(scatter_kernel, dim3(chunks), dim3(NTHREADS), lds, stream, s);
+  // whole tiles (16-byte rows) while they fit 64 KiB of LDS, else half tiles
+  const size_t lds16 = (size_t)s.nbw * 4 + (size_t)s.nbins * 16;
+  if (lds16 <= 64u * 1024u)
+    hipLaunchKernelGGL(scatter_kernel<2>, dim3(chunks), dim3(NTHREADS), lds16, stream, s);
+  else
+    hipLaunchKernelGGL(scatter_kernel<1>, dim3(chunks), dim3(NTHREADS),
+                       (size_t)s.nbw * 4 + (size_t)s.nbins * 8, stream, s);
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512

@@ -1597,7 +1597,8 @@ static Layout layout_for(uint64_t n, uint32_t nbins) {
   Layout L;
   size_t off = 0;
   L.dec = off; off = align256(off + n * 4);
-  L.index = off; off = align256(off + n * 4);
+  L.index = off; off = align256(off + (n + USN_TILE) * 4);   // + a tile of sink slots (the scatter's
+                                                           // lanes past a ragged tile's end)
   L.bin_off = off; off = align256(off + (size_t)(USN_MAX_BINS + 1) * 4);
   L.tiles = off; off = align256(off + nt * sizeof(usn_tile_hdr));
   L.summary = off; off = align256(off + sizeof(usn_summary));
