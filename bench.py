@@ -84,6 +84,9 @@ def parse_args(argv=None):
     ap.add_argument("--launch-probe", type=int, default=150, help="per-launch event pairs")
     ap.add_argument("--ramp", type=int, default=200,
                     help="untimed poll rounds between the probe and the timed steps (clock ramp)")
+    ap.add_argument("--lists-async", type=int, default=0,
+                    help="1: per-endpoint lists on the library's side stream (usn_set_lists_async): "
+                         "a round's scatter overlaps the next round's classify")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: ranks join the process group and report, no GPU")
     return ap.parse_args(argv)
@@ -228,6 +231,13 @@ class Run:
             dist.barrier()
         return t1 - t0, ctx.elapsed_ms(self.ev0, self.ev1)
 
+    def lists_wait(self, ra, cnt, stream):
+        """the stream waits for the lists of one launch (side-stream mode)"""
+        for j in range(cnt):
+            rc = self.L.usn_lists_wait(self.h, C.byref(ra[j]), stream)
+            if rc:
+                _lib().check(rc, "usn_lists_wait")
+
     def launch_probe(self, count):
         """Median duration of one launch (HIP events on the stream it runs on):
         the first launch group of the round, back to back on one stream, so no
@@ -238,11 +248,12 @@ class Run:
         for x in self.streams:
             ctx.sync(x)
         for i, (ea, eb) in enumerate(evs):
-            _, ba, ra, cnt, _, _ = self.groups[i % self.R][0]
+            _, ba, ra, cnt, _, ral = self.groups[i % self.R][0]
             ctx.record(ea, st)
             rc = self.L.usn_classify_multi(self.h, ba, ra, cnt, st)
             if rc:
                 _lib().check(rc, "usn_classify_multi")
+            self.lists_wait(ral, cnt, st)     # the call's lists, wherever they were built
             ctx.record(eb, st)
         ctx.sync(st)
         ms = [ctx.elapsed_ms(a, b) for a, b in evs]
@@ -380,6 +391,8 @@ def main(argv=None):
         if ndev > 0:                       # more ranks than GPUs (a rehearsal): round-robin
             device = local % ndev
     ctx = lib.Ctx(device)
+    if args.lists_async:
+        ctx.set_lists_async(True)
     joined = joined_ranks(dist, rank, device)   # every rank is in the group, on its device
     n = args.frames or DEFAULT_FRAMES[args.config]
     run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong,
@@ -408,6 +421,7 @@ def main(argv=None):
             "parallelism": "replicas%d" % world,
             "rank_devices": [d for _, d in joined],
             "event_ms_per_step": res["event_ms_per_step"],
+            "lists_async": bool(args.lists_async),
             "untimed_ramp_steps": 2 * args.ramp,
             "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],
             "host_stage_frames": res["host_stage_frames"],
@@ -427,6 +441,8 @@ def main(argv=None):
         # configs[1] (the 1M x 64 B, 16-rule slice), measured the same way
         ctx.close()
         ctx = lib.Ctx(device)
+        if args.lists_async:
+            ctx.set_lists_async(True)
         r2 = Run(L, ctx, "c2", DEFAULT_FRAMES["c2"], 0, 1, 0, args.streams, False)
         x = measure(r2, args, None, 1)
         x["workload"] = workload(r2, False)

@@ -294,6 +294,19 @@ int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stre
 int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
                        void *hip_stream);
 
+/* Per-endpoint lists on a side stream (off by default).  With on != 0,
+ * usn_classify / usn_classify_multi of NIC rings enqueue the classify kernel
+ * on the caller's stream and the scatter that builds index / bin_off on a
+ * stream of the library's (one per replica), ordered after it: the caller's
+ * stream does not wait for the lists, so the next batch's classify overlaps
+ * this batch's scatter.  Decisions, tile headers and the summary stay in the
+ * caller's stream order.  The lists are final when usn_finalize returns (it
+ * waits for them), or in the order of `hip_stream` after usn_lists_wait.  A
+ * result is not overwritten by a later classify before its lists are done.
+ * tx batches (learning) always build their lists on the caller's stream. */
+int usn_set_lists_async(usn_ctx *ctx, int on);
+int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
+
 /* Ordered host stage for one classified batch (synchronises the stream).
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
  * frame order and patches decisions and the per-endpoint lists on the device.  Must be called

@@ -270,3 +270,46 @@ def test_classify_multi_matches_separate(name, coracle_mod):
     ra = (lib.Result * 2)(rs[0].desc, rs[1].desc)
     assert ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 2, s) == -22
     ctx.close()
+
+
+@pytest.mark.parametrize("name", ["c2", "c5"])
+def test_lists_async(name, coracle_mod):
+    """usn_set_lists_async: the lists of each batch are built on the library's
+    side stream while the caller's stream classifies the next batches; after
+    usn_lists_wait (or usn_finalize) every batch's lists equal the oracle's
+    ordered per-endpoint lists, and reusing a result waits for its lists."""
+    from usnetd_amd import lib, traffic
+    n = 200003
+    cfgs = [traffic.config(name, n=n, seed=50 + k) for k in range(3)]
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfgs[0])
+    ctx.set_lists_async(True)
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfgs[0])
+    s = ctx.stream()
+    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+    rs = [lib.DeviceResult(ctx, n) for _ in range(2)]
+    wants = [o.forward_batch(c.src, c.frames, c.lens, stride=c.stride) for c in cfgs]
+    for k, (b, want) in enumerate(zip(bs, wants)):
+        r = rs[k % 2]                       # batch 2 reuses batch 0's result
+        ctx.classify(b, r, s)
+        if k == 1:                          # batch 0's lists, joined on the stream
+            ctx.lists_wait(rs[0], s)
+            ctx.sync(s)
+            _check_lists(rs[0], wants[0])
+    ctx.finalize(bs[2], rs[0], s)
+    ctx.finalize(bs[1], rs[1], s)
+    for r, want in ((rs[0], wants[2]), (rs[1], wants[1])):
+        assert np.array_equal(r.decisions() & katrun.PARITY_MASK, want & katrun.PARITY_MASK)
+        _check_lists(r, want)
+    ctx.close()
+
+
+def _check_lists(r, want):
+    from usnetd_amd import lib
+    n_ep = int(r.summary()["n_ep"])
+    got = r.lists(want.shape[0])
+    ref = lib.expected_lists(want, n_ep)
+    assert sorted(got) == sorted(ref)
+    for k in ref:
+        assert np.array_equal(got[k], ref[k]), k

@@ -426,6 +426,10 @@ struct Replica {
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   uint32_t epoch = 0;
+  /* usn_set_lists_async: the scatter's stream, ordered after each classify
+   * launch by the `classified` event */
+  hipStream_t side = nullptr;
+  hipEvent_t classified = nullptr;
 };
 
 struct usn_ctx {
@@ -482,6 +486,12 @@ struct usn_ctx {
    * classified on: usn_finalize acts on the batch's own replica, not on the
    * replica of the source's latest batch */
   std::unordered_map<const void *, uint32_t> batch_rep;
+  /* usn_set_lists_async: lists built on the replica's side stream; each
+   * result's `lists done` event (keyed by its decisions array, created on
+   * its replica's device) */
+  bool lists_async = false;
+  struct ListsEv { hipEvent_t ev = nullptr; int device = -1; bool pending = false; };
+  std::unordered_map<const void *, ListsEv> lists_ev;
 };
 
 namespace {
@@ -1316,6 +1326,16 @@ void usn_ctx_destroy(usn_ctx *c) {
                     (void *)R.counters, (void *)R.listen})
       if (p) (void)hipFree(p);
   }
+  for (auto &kv : c->lists_ev)
+    if (kv.second.ev) {
+      (void)hipSetDevice(kv.second.device);
+      (void)hipEventDestroy(kv.second.ev);
+    }
+  for (Replica &R : c->reps) {
+    (void)hipSetDevice(R.device);
+    if (R.classified) (void)hipEventDestroy(R.classified);
+    if (R.side) (void)hipStreamDestroy(R.side);
+  }
   for (Chain &ch : c->chains)
     for (uint32_t k = 0; k < USN_MAX_REPLICAS; ++k)
       if (ch.done[k]) {
@@ -1901,12 +1921,49 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     c->tx.src = tb.src_endpoint;
     c->tx.replica = rep;
     c->tx.decisions = r[0].decisions;
-  } else if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units))) {
-    HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
   } else {
-    HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+    /* a result whose lists are still being built on the side stream is not
+     * overwritten before they are done */
+    for (uint32_t k = 0; k < count; ++k) {
+      auto it = c->lists_ev.find(r[k].decisions);
+      if (it != c->lists_ev.end() && it->second.pending) {
+        HIPCHK(hipStreamWaitEvent((hipStream_t)stream, it->second.ev, 0));
+        it->second.pending = false;
+      }
+    }
+    if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
+      HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
+    else
+      HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
-  { int st = launch_scatter(m.b, r, count, (hipStream_t)stream); if (st) return st; }
+  if (tx || !c->lists_async) {
+    int st = launch_scatter(m.b, r, count, (hipStream_t)stream);
+    if (st) return st;
+  } else {
+    // the scatter on the side stream, after this launch; the caller's stream
+    // goes on to the next batch (usn_finalize / usn_lists_wait join them)
+    if (!R.side) HIPCHK(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+    if (!R.classified) HIPCHK(hipEventCreateWithFlags(&R.classified, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(R.classified, (hipStream_t)stream));
+    HIPCHK(hipStreamWaitEvent(R.side, R.classified, 0));
+    int st = launch_scatter(m.b, r, count, R.side);
+    if (st) return st;
+    for (uint32_t k = 0; k < count; ++k) {
+      usn_ctx::ListsEv &le = c->lists_ev[r[k].decisions];
+      if (le.ev && le.device != R.device) {
+        (void)hipSetDevice(le.device);
+        (void)hipEventDestroy(le.ev);
+        le.ev = nullptr;
+        HIPCHK(hipSetDevice(R.device));
+      }
+      if (!le.ev) {
+        HIPCHK(hipEventCreateWithFlags(&le.ev, hipEventDisableTiming));
+        le.device = R.device;
+      }
+      HIPCHK(hipEventRecord(le.ev, R.side));
+      le.pending = true;
+    }
+  }
   for (uint32_t k = 0; k < count; ++k) {
     Chain &ch = c->chains[b[k].src_endpoint];
     ch.device_chain = true;
@@ -2353,6 +2410,13 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
+  {  // lists built on the side stream (usn_set_lists_async)
+    auto it = c->lists_ev.find(r->decisions);
+    if (it != c->lists_ev.end() && it->second.pending) {
+      HIPCHK(hipEventSynchronize(it->second.ev));
+      it->second.pending = false;
+    }
+  }
   if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
     if (c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions) {
       const int st = finalize_tx(c, b, r, s, info);
@@ -2502,6 +2566,25 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HIPCHK(hipMemcpy(r->summary, &out, sizeof out, hipMemcpyHostToDevice));
   HIPCHK(hipStreamSynchronize(s));
   if (info) *info = fi;
+  return USN_OK;
+}
+
+int usn_set_lists_async(usn_ctx *c, int on) {
+  if (!c) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->lists_async = on != 0;
+  return USN_OK;
+}
+
+int usn_lists_wait(usn_ctx *c, const usn_result *r, void *stream) {
+  if (!c || !r) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->lists_ev.find(r->decisions);
+  if (it == c->lists_ev.end() || !it->second.ev) return USN_OK;   // built on the batch's stream
+  HIPCHK(hipSetDevice(it->second.device));
+  HIPCHK(hipStreamWaitEvent((hipStream_t)stream, it->second.ev, 0));
   return USN_OK;
 }
 

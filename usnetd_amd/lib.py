@@ -124,9 +124,11 @@ def load(path: str | None = None):
         "usn_ctx_create_group": ([P, U32, C.POINTER(P)], I),
         "usn_ctx_replicas": ([P], I), "usn_replica_select": ([P, U32], I),
         "usn_replica_device": ([P, U32], I),
+        "usn_set_lists_async": ([P, I], I), "usn_lists_wait": ([P, C.POINTER(Result), P], I),
     }
     optional = {"usn_set_frame_reader", "usn_ctx_create_group", "usn_ctx_replicas",
-                "usn_replica_select", "usn_replica_device", "usn_result_bytes_ep"}   # A/B builds of older ABI versions lack these
+                "usn_replica_select", "usn_replica_device", "usn_result_bytes_ep",
+                "usn_set_lists_async", "usn_lists_wait"}   # A/B builds of older ABI versions lack these
     for name, (args, res) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -147,7 +149,8 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_device_sync", "usn_event_create", "usn_event_destroy", "usn_event_record",
             "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi",
             "usn_bridge_set", "usn_table_build", "usn_set_frame_reader", "usn_ctx_create_group",
-            "usn_ctx_replicas", "usn_replica_select", "usn_replica_device"]
+            "usn_ctx_replicas", "usn_replica_select", "usn_replica_device", "usn_set_lists_async",
+            "usn_lists_wait"]
 
 
 def check(rc, what=""):
@@ -364,6 +367,13 @@ class Ctx:
     def classify(self, batch: "DeviceBatch", result: "DeviceResult", stream=None):
         check(self.L.usn_classify(self.h, C.byref(batch.desc), C.byref(result.desc), stream),
               "usn_classify")
+
+    def set_lists_async(self, on=True):
+        """Build the per-endpoint lists on a side stream (usn_set_lists_async)."""
+        check(self.L.usn_set_lists_async(self.h, int(bool(on))), "usn_set_lists_async")
+
+    def lists_wait(self, result: "DeviceResult", stream=None):
+        check(self.L.usn_lists_wait(self.h, C.byref(result.desc), stream), "usn_lists_wait")
 
     def finalize(self, batch: "DeviceBatch", result: "DeviceResult", stream=None) -> FinalizeInfo:
         info = FinalizeInfo()
