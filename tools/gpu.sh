@@ -56,6 +56,10 @@ for s in "$@"; do
     abl) for c in ${ABL_CFGS:-c5}; do
         step abl_$c 600 python tools/abl.py --config $c --json $O/abl_$c.json ${ABL_ARGS:-} ${ABL_VARIANTS:-base}
       done ;;
+    scb) for c in ${SCB_CFGS:-c5 c2}; do
+        if [ $c = c5 ]; then A="--frames 8388608 --multi 2"; else A="--frames 1048576 --multi 8"; fi
+        step scb_$c 300 python tools/scatter_bench.py --config $c $A --json $O/scb_$c.json ${SCB_VARIANTS:-base}
+      done ;;
     stamps) step stamps 300 python tools/stamps.py ${STAMP_ARGS:-c5} ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -2766,6 +2766,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
+#ifndef USN_ABL_SC   /* A/B only: 1 no index stores, 2 coalesced stores, 3 no ranks */
+#define USN_ABL_SC 0
+#endif
 template <int SR>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   typedef typename std::conditional<SR == 2, uint4, uint2>::type Row;
@@ -2836,7 +2839,11 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       for (uint32_t k = 0; k < SR; ++k) {
         const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
         const bool v = local < nt;
+#if USN_ABL_SC == 3
+        const uint64_t same = __ballot(v) & (1ull << lane);
+#else
         const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
+#endif
         rank[k] = (uint32_t)__popcll(same & lanemask_lt(lane));
         if (v && rank[k] == 0) cb[bins[r] * SEGB + k * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
       }
@@ -2858,7 +2865,13 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
         const bool v = local < nt;
         const uint32_t pos = v ? run[b] + before + rank[k] : B.n + local;   // sink slots
+#if USN_ABL_SC == 1   /* A/B only: no index stores (wrong results) */
+        if (pos == 0xFFFFFFFFu) B.index[0] = 0;
+#elif USN_ABL_SC == 2   /* A/B only: coalesced stores in frame order (wrong results) */
+        B.index[(uint32_t)(base + local) + (pos & 0)] = pos;
+#else
         B.index[pos] = (uint32_t)(base + local);
+#endif
       }
       __syncthreads();
       // running += this step's frames per bin; rows cleared for the next step

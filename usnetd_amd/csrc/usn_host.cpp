@@ -2569,6 +2569,19 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   return USN_OK;
 }
 
+/* diagnostics (tools/scatter_bench.py): the per-endpoint scatter of `count`
+ * batches classified together, again, on `stream` (no classify) */
+int usn_debug_scatter(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t count, void *stream) {
+  if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
+  std::lock_guard<std::mutex> g(c->mu);
+  Replica &R = c->reps[c->sel];
+  HIPCHK(hipSetDevice(R.device));
+  usn::ClassifyArgs as[USN_MAX_MULTI];
+  for (uint32_t k = 0; k < count; ++k) fill_args(c, R, &b[k], &r[k], as[k]);
+  return launch_scatter(as, r, count, (hipStream_t)stream);
+}
+
 int usn_set_lists_async(usn_ctx *c, int on) {
   if (!c) return USN_EINVAL;
   if (c->reps.empty()) return USN_ENODEV;
