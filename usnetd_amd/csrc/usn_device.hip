@@ -2673,10 +2673,9 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
  *   scan_agg     (chunk, bin block): the chunk's frames per bin           agg
  *   scan_chunks  (bin pair, one wave): agg := its exclusive scan over the
  *                chunks; tot = the bin's frames
- *   scatter      (chunk, its tiles in order): running[bin] = bin base (block
- *                scan of tot) + agg; per tile each frame's rank among the
- *                tile's frames of its bin, index[running + rank] = frame,
- *                running += the tile's count
+ *   scatter      (chunk): the chunk's frames sorted by bin in an LDS stage,
+ *                then written out in stage order: a bin's frames of the chunk
+ *                leave as one contiguous run of index
  * Algorithmic bytes per frame: 4 (index).  The reference writes each frame
  * straight into its target's ring (endpoint.rs:61-74) and copies FLOOD frames
  * to every other endpoint (:340-363): an endpoint's frames are its list merged
@@ -2691,7 +2690,6 @@ __device__ __forceinline__ uint32_t base_of(const uint32_t *base, uint32_t count
 
 #define SCAN_THREADS 256
 static_assert(USN_SCAN_BINS_PER_BLOCK == 2 * SCAN_THREADS, "two bins per scan thread");
-static_assert(USN_SCAN_MAX_CHUNKS <= 64 * 16, "scan_chunks: 16 chunks per lane");
 
 /* (chunk, bin block): frames of bins 2w, 2w+1 over the chunk's tiles, 8 row
  * loads in flight */
@@ -2720,8 +2718,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_agg_kernel(ScatterArgs s) {
   *reinterpret_cast<uint2 *>(B.agg + (size_t)c * s.nbw + 2 * w) = make_uint2(lo, hi);
 }
 
-/* (bin pair, batch): one wave, lane L owns chunks 16L .. 16L+15: agg of the
- * bin pair over the chunks -> its exclusive scan in place, and the totals */
+/* (bin pair, batch): one wave scans the pair's column of agg in blocks of
+ * 1024 chunks (lane L owns chunks 16L .. 16L+15 of a block): agg := its
+ * exclusive scan in place, tot = the totals */
 __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const ScatterBatch &B = s.b[blockIdx.y];
@@ -2729,54 +2728,60 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
   if (2 * p >= s.nbw) return;
   uint2 *col = reinterpret_cast<uint2 *>(B.agg + 2 * p);
   const uint32_t stride = s.nbw / 2;                           // uint2 per agg row
-  uint2 v[16];
+  uint32_t clo = 0, chi = 0;                                    // blocks before
+  for (uint32_t c0 = 0; c0 < B.nchunks; c0 += 1024) {
+    uint2 v[16];
 #pragma unroll
-  for (uint32_t k = 0; k < 16; ++k) {
-    const uint32_t c = lane * 16 + k;
-    v[k] = c < B.nchunks ? col[(size_t)c * stride] : make_uint2(0, 0);
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t c = c0 + lane * 16 + k;
+      v[k] = c < B.nchunks ? col[(size_t)c * stride] : make_uint2(0, 0);
+    }
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) { lo += v[k].x; hi += v[k].y; }
+    const uint32_t ilo = wave_incl_scan(lo, lane), ihi = wave_incl_scan(hi, lane);
+    uint32_t elo = clo + ilo - lo, ehi = chi + ihi - hi;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t c = c0 + lane * 16 + k;
+      if (c < B.nchunks) col[(size_t)c * stride] = make_uint2(elo, ehi);
+      elo += v[k].x; ehi += v[k].y;
+    }
+    clo += __shfl(ilo, 63, 64);
+    chi += __shfl(ihi, 63, 64);
   }
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 16; ++k) { lo += v[k].x; hi += v[k].y; }
-  const uint32_t ilo = wave_incl_scan(lo, lane), ihi = wave_incl_scan(hi, lane);
-  uint32_t elo = ilo - lo, ehi = ihi - hi;
-#pragma unroll
-  for (uint32_t k = 0; k < 16; ++k) {
-    const uint32_t c = lane * 16 + k;
-    if (c < B.nchunks) col[(size_t)c * stride] = make_uint2(elo, ehi);
-    elo += v[k].x; ehi += v[k].y;
-  }
-  if (lane == 63) *reinterpret_cast<uint2 *>(B.tot + 2 * p) = make_uint2(ilo, ihi);
+  if (lane == 0) *reinterpret_cast<uint2 *>(B.tot + 2 * p) = make_uint2(clo, chi);
 }
 
-/* (chunk): its tiles in order, one workgroup of 512 threads (two frames per
- * lane).  A tile is ranked in steps of SR rounds (512 frames each): SR = 2
- * ranks the whole tile at once (16 segments of 64 frames, a 16-byte row of u8
- * counts per bin); SR = 1 half a tile (8 segments, 8-byte rows) for bin
- * counts whose 16-byte rows would not fit 64 KiB of LDS (c5 with 4093 pipes).
- * Every load and store of the loop is unconditional (lanes past a ragged
- * tile's end store to sink slots past index[n]; the last tile re-reads
- * itself as its "next"), so hipcc counts them: the wait for the next tile's
- * decisions leaves this tile's scattered stores in flight instead of
- * draining them (vmcnt(0)) once per tile.
+/* (chunk of TC tiles): one workgroup of 512 threads.
+ *  1. every decision of the chunk is loaded at once, into registers (2 per
+ *     lane and tile): no load waits inside the tile loop;
+ *  2. off[b] = bin b's base (block scan of the totals) + the chunks before
+ *     (agg) - b's start in the chunk (block scan of the chunk's counts), and
+ *     cur[b] = that start;
+ *  3. per tile, in steps of SR rounds: each frame's rank among the step's
+ *     frames of its bin (bit-sliced ballots; a row of u8 counts per bin and
+ *     64-frame segment) puts it at stage[cur[bin] + rank]: the chunk sorted by
+ *     (bin, frame) in LDS;
+ *  4. the stage is written out in order: index[off[bin] + q] -- contiguous
+ *     runs per bin, one L2 request per run instead of one per frame (c5, 1005
+ *     bins: about 8 frames per run).
  * Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them
- * so that an XCD takes a contiguous run of chunks, whose list entries of a
- * bin are adjacent: its L2 assembles each bin's lines before writing them
- * back (cdna_hip_programming.md T1 swizzle, bijective). */
+ * so that an XCD takes a contiguous run of chunks (cdna_hip_programming.md T1
+ * swizzle, bijective). */
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
-#ifndef USN_ABL_SC   /* A/B only: 1 no index stores, 2 coalesced stores, 3 no ranks */
-#define USN_ABL_SC 0
-#endif
-template <int SR>
+template <int SR, int TC>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   typedef typename std::conditional<SR == 2, uint4, uint2>::type Row;
   constexpr uint32_t SEGB = SR * (NTHREADS / 64);                    // row bytes = segments per step
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint32_t s_scan[16];
-  uint32_t *run = reinterpret_cast<uint32_t *>(smem);               // [nbw]
-  Row *rows = reinterpret_cast<Row *>(smem + (size_t)s.nbw * 4);     // [nbins]: u8 per segment
+  uint32_t *stage = reinterpret_cast<uint32_t *>(smem);              // [TC * TILE]: bin << 16 | frame
+  uint32_t *off = stage + TC * TILE;                                 // [nbw]
+  uint16_t *cur = reinterpret_cast<uint16_t *>(off + s.nbw);         // [nbw]: < TC * TILE
+  Row *rows = reinterpret_cast<Row *>(cur + s.nbw);                  // [nbins]: u8 per segment
   uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t nwg = s.chunk_base[s.count];
@@ -2788,50 +2793,52 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   const uint32_t bi = base_of(s.chunk_base, s.count, g);
   const ScatterBatch &B = s.b[bi];
   const uint32_t c = g - s.chunk_base[bi];
-  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
-  // the first tile's decisions fly while the bases are formed
-  uint32_t d[ROUNDS];
-  {
-    const uint64_t base = (uint64_t)t0 * TILE;
+  const uint32_t t0 = c * TC, ntc = min((uint32_t)TC, B.ntiles - t0);
+  const uint64_t first = (uint64_t)t0 * TILE;                        // the chunk's first frame
+  // 1. every decision of the chunk (tiles past its end re-read its last one)
+  uint32_t d[TC][ROUNDS];
+#pragma unroll
+  for (uint32_t t = 0; t < TC; ++t) {
+    const uint64_t base = first + (uint64_t)min(t, ntc - 1) * TILE;
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
+    for (uint32_t r = 0; r < ROUNDS; ++r) d[t][r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
   }
-  // running[b] = base[b] (frames of the bins before b) + this chunk's offset in b
+  // 2. bases and the chunk's bin starts
   {
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;   // bins per thread, contiguous
     const uint32_t b0 = tid * per;
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < per; ++k)
-      if (b0 + k < s.nbw) sum += B.tot[b0 + k];
+    const uint32_t *ex = B.agg + (size_t)c * s.nbw;           // frames of b in the chunks before
+    const uint32_t *nx = c + 1 < B.nchunks ? ex + s.nbw : B.tot;
+    uint32_t st = 0, sc = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = b0 + k;
+      if (b < s.nbw) { st += B.tot[b]; sc += nx[b] - ex[b]; }
+    }
     uint32_t total;
-    uint32_t pre = block_excl_scan(sum, s_scan, &total);
+    uint32_t pt = block_excl_scan(st, s_scan, &total);
+    uint32_t pc = block_excl_scan(sc, s_scan, &total);
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      run[b] = pre + B.agg[(size_t)c * s.nbw + b];
-      if (c == 0 && b <= s.nbins) B.bin_off[b] = pre;   // pad bins past nbins are empty
-      pre += B.tot[b];
+      off[b] = pt + ex[b] - pc;
+      cur[b] = (uint16_t)pc;
+      if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;          // pad bins past nbins are empty
+      pt += B.tot[b];
+      pc += nx[b] - ex[b];
     }
     if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
     for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
   }
-  // the loop carries bins, not decisions: the next tile's decisions are
-  // converted at the end of an iteration, where waiting for them leaves this
-  // tile's stores (issued after them) in flight
-  uint32_t bins[ROUNDS];
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[r], s.n_ep);
   __syncthreads();
-  for (uint32_t t = t0; t < t1; ++t) {
-    const uint64_t base = (uint64_t)t * TILE;
-    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
-    {  // the next tile's decisions fly under this one (the last tile reloads itself)
-      const uint64_t nb = (uint64_t)min(t + 1, t1 - 1) * TILE;
-      const uint32_t nn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - nb);
+  // 3. rank into the stage, tile by tile
 #pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) d[r] = B.decisions[nb + min(r * NTHREADS + tid, nn - 1)];
-    }
+  for (uint32_t t = 0; t < TC; ++t) {
+    if (t >= ntc) break;
+    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - (first + (uint64_t)t * TILE));
+    uint32_t bins[ROUNDS];
+#pragma unroll
+    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[t][r], s.n_ep);
 #pragma unroll
     for (uint32_t h = 0; h < ROUNDS / SR; ++h) {
       uint32_t rank[SR];
@@ -2839,11 +2846,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       for (uint32_t k = 0; k < SR; ++k) {
         const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
         const bool v = local < nt;
-#if USN_ABL_SC == 3
-        const uint64_t same = __ballot(v) & (1ull << lane);
-#else
         const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
-#endif
         rank[k] = (uint32_t)__popcll(same & lanemask_lt(lane));
         if (v && rank[k] == 0) cb[bins[r] * SEGB + k * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
       }
@@ -2851,6 +2854,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
 #pragma unroll
       for (uint32_t k = 0; k < SR; ++k) {
         const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
+        if (local >= nt) continue;
         const uint32_t sg = k * (NTHREADS / 64) + wave, b = bins[r];
         // frames of bin b in the segments before sg: whole words, then the low bytes of one
         const Row wv = rows[b];
@@ -2863,34 +2867,31 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         const uint32_t p2 = q > 2 ? w[2] : q == 2 ? (w[2] & mpart) : 0u;
         const uint32_t p3 = q == 3 ? (w[3] & mpart) : 0u;
         const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
-        const bool v = local < nt;
-        const uint32_t pos = v ? run[b] + before + rank[k] : B.n + local;   // sink slots
-#if USN_ABL_SC == 1   /* A/B only: no index stores (wrong results) */
-        if (pos == 0xFFFFFFFFu) B.index[0] = 0;
-#elif USN_ABL_SC == 2   /* A/B only: coalesced stores in frame order (wrong results) */
-        B.index[(uint32_t)(base + local) + (pos & 0)] = pos;
-#else
-        B.index[pos] = (uint32_t)(base + local);
-#endif
+        stage[cur[b] + before + rank[k]] = (b << 16) | (t * TILE + local);
       }
       __syncthreads();
-      // running += this step's frames per bin; rows cleared for the next step
+      // cursors past this step's frames; rows cleared for the next step
       for (uint32_t b = tid; b < s.nbins; b += NTHREADS) {
         const Row wv = rows[b];
         uint32_t n = byte_sum(wv.x) + byte_sum(wv.y);
         if (SR == 2) n += byte_sum(((const uint4 &)wv).z) + byte_sum(((const uint4 &)wv).w);
         if (n) {
-          run[b] += n;
+          cur[b] = (uint16_t)(cur[b] + n);
           rows[b] = Row{};
         }
       }
       __syncthreads();
     }
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[r], s.n_ep);
+  }
+  // 4. the stage out, in order
+  const uint32_t nf = (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  for (uint32_t q = tid; q < nf; q += NTHREADS) {
+    const uint32_t e = stage[q];
+    B.index[off[e >> 16] + q] = (uint32_t)first + (e & 0xFFFFu);
   }
 }
 static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
+static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
 
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
@@ -2899,13 +2900,13 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t pairs = s.nbw / 2;
   hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
                      dim3(SCAN_THREADS), 0, stream, s);
-  // whole tiles (16-byte rows) while they fit 64 KiB of LDS, else half tiles
-  const size_t lds16 = (size_t)s.nbw * 4 + (size_t)s.nbins * 16;
-  if (lds16 <= 64u * 1024u)
-    hipLaunchKernelGGL(scatter_kernel<2>, dim3(chunks), dim3(NTHREADS), lds16, stream, s);
-  else
-    hipLaunchKernelGGL(scatter_kernel<1>, dim3(chunks), dim3(NTHREADS),
-                       (size_t)s.nbw * 4 + (size_t)s.nbins * 8, stream, s);
+  const ScatterShape sh = scatter_shape(s.nbins);
+  const dim3 g(chunks), b(NTHREADS);
+#define USN_SC(SR_, TC_) \
+  if (sh.sr == SR_ && sh.tc == TC_) hipLaunchKernelGGL((scatter_kernel<SR_, TC_>), g, b, sh.lds, stream, s)
+  USN_SC(2, 8); else USN_SC(1, 8); else USN_SC(2, 4); else USN_SC(1, 4); else USN_SC(2, 2);
+  else USN_SC(1, 2); else USN_SC(2, 1); else USN_SC(1, 1); else return hipErrorInvalidValue;
+#undef USN_SC
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512

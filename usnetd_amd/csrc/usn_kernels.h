@@ -126,13 +126,13 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
  *   scan_agg     (chunk of tc tiles, bin block): the chunk's frames per bin
  *   scan_chunks  (bin pair, one wave): exclusive scan of agg over the chunks
  *                (in place) and the bin's total
- *   scatter      (chunk, persistent over its tiles): the bin bases (a block
- *                scan of the totals), then per tile each frame's rank among
- *                the tile's frames of its bin (bit-sliced ballots + per-segment
- *                byte counts) and index[running[bin] + rank] = frame
+ *   scatter      (chunk): every decision of the chunk in registers at once;
+ *                bin bases (block scan of the totals); per tile each frame's
+ *                rank among the tile's frames of its bin (bit-sliced ballots +
+ *                per-segment byte counts) gives its slot in the chunk's
+ *                bin-sorted LDS stage; the stage is written out in order, so
+ *                each bin's frames of the chunk leave as one contiguous run
  * Stable: bins in order, frames in frame order inside a bin. */
-#define USN_SCAN_MAX_CHUNKS 1024u      /* chunks per batch (one wave scans them: 16 per lane) */
-#define USN_SCAN_LAUNCH_CHUNKS 1024u   /* scatter workgroups a launch aims at (4 per CU) */
 #define USN_SCAN_BINS_PER_BLOCK 512u   /* scan_agg: 256 threads x 2 bins */
 struct ScatterBatch {
   const uint32_t *decisions;
@@ -149,12 +149,34 @@ struct ScatterArgs {
   uint32_t count;
   uint32_t nbins, nbw, nblk, n_ep, nbits;
 };
-/* scratch bytes of one batch (cnt | agg | tot) and its carve; tc = tiles per
- * chunk, chosen per launch (scatter_tc) */
+/* The scatter kernel's shape for nbins bins: tiles per chunk (tc) and rounds
+ * ranked per step (sr: 2 = whole 1024-frame tiles with 16-byte rows, 1 = half
+ * tiles with 8-byte rows), the most workgroups per CU first (up to 4), then
+ * the larger sr, within 64 KiB of LDS: stage tc x 4 KiB | offsets nbw x 4 |
+ * cursors nbw x 2 | rows nbins x sr x 8. */
+struct ScatterShape { uint32_t sr, tc; size_t lds; };
+inline size_t scatter_lds(uint32_t nbins, uint32_t sr, uint32_t tc) {
+  const size_t nbw = (nbins + 7u) & ~7u;
+  return (size_t)tc * USN_TILE * 4 + nbw * 6 + (size_t)nbins * sr * 8;
+}
+inline ScatterShape scatter_shape(uint32_t nbins) {
+  ScatterShape best{1, 1, scatter_lds(nbins, 1, 1)};
+  uint32_t best_occ = 0;
+  for (uint32_t tc : {8u, 4u, 2u, 1u}) {
+    for (uint32_t sr : {2u, 1u}) {
+      const size_t l = scatter_lds(nbins, sr, tc);
+      if (l > 64u * 1024u) continue;
+      uint32_t occ = (uint32_t)((160u * 1024u) / l);
+      occ = occ > 4 ? 4 : occ;
+      if (occ > best_occ) { best = ScatterShape{sr, tc, l}; best_occ = occ; }
+    }
+    if (best_occ >= 3) break;   // keep chunks long (contiguous runs per bin) once 3 fit per CU
+  }
+  return best;
+}
+/* scratch bytes of one batch (cnt | agg | tot) and its carve */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
-                   uint16_t **cnt);
-uint32_t scatter_tc(uint32_t ntiles, uint32_t launch_tiles);
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt);
 
 }  // namespace usn
 
