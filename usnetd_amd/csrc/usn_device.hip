@@ -2795,6 +2795,18 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   const uint32_t c = g - s.chunk_base[bi];
   const uint32_t t0 = c * TC, ntc = min((uint32_t)TC, B.ntiles - t0);
   const uint64_t first = (uint64_t)t0 * TILE;                        // the chunk's first frame
+  const uint32_t *ex = B.agg + (size_t)c * s.nbw;             // frames of b in the chunks before
+  const uint32_t *nx = c + 1 < B.nchunks ? ex + s.nbw : B.tot;   // ... and in this one too
+  // up to 1024 bins (two per thread): this thread's totals and chunk offsets
+  // are loaded before the decisions, so waiting for them leaves the
+  // decisions in flight
+  const bool pair = s.nbw <= 2 * NTHREADS;
+  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0), vn = make_uint2(0, 0);
+  if (pair && 2 * tid < s.nbw) {
+    vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
+    ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
+    vn = *reinterpret_cast<const uint2 *>(nx + 2 * tid);
+  }
   // 1. every decision of the chunk (tiles past its end re-read its last one)
   uint32_t d[TC][ROUNDS];
 #pragma unroll
@@ -2805,11 +2817,25 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     for (uint32_t r = 0; r < ROUNDS; ++r) d[t][r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
   }
   // 2. bases and the chunk's bin starts
-  {
+  if (pair) {
+    uint32_t total;
+    const uint32_t n0 = vn.x - ve.x, n1 = vn.y - ve.y;
+    const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
+    const uint32_t pc = block_excl_scan(n0 + n1, s_scan, &total);
+    if (2 * tid < s.nbw) {
+      const uint32_t b = 2 * tid;
+      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + n0));
+      *reinterpret_cast<uint32_t *>(cur + b) = (pc & 0xFFFFu) | ((pc + n0) << 16);
+      if (c == 0) {
+        if (b <= s.nbins) B.bin_off[b] = pt;                   // pad bins past nbins are empty
+        if (b + 1 <= s.nbins) B.bin_off[b + 1] = pt + vt.x;
+      }
+    }
+    if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
+  } else {
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;   // bins per thread, contiguous
     const uint32_t b0 = tid * per;
-    const uint32_t *ex = B.agg + (size_t)c * s.nbw;           // frames of b in the chunks before
-    const uint32_t *nx = c + 1 < B.nchunks ? ex + s.nbw : B.tot;
     uint32_t st = 0, sc = 0;
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
@@ -2834,7 +2860,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // 3. rank into the stage, tile by tile
 #pragma unroll
   for (uint32_t t = 0; t < TC; ++t) {
-    if (t >= ntc) break;
+    if (t >= ntc || USN_ABL_SC == 4) break;
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - (first + (uint64_t)t * TILE));
     uint32_t bins[ROUNDS];
 #pragma unroll
@@ -2884,7 +2910,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     }
   }
   // 4. the stage out, in order
-  const uint32_t nf = (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
   for (uint32_t q = tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
     B.index[off[e >> 16] + q] = (uint32_t)first + (e & 0xFFFFu);
@@ -2900,7 +2926,13 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t pairs = s.nbw / 2;
   hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
                      dim3(SCAN_THREADS), 0, stream, s);
-  const ScatterShape sh = scatter_shape(s.nbins);
+  ScatterShape sh = scatter_shape(s.nbins);
+#ifdef USN_SC_SR   /* A/B only: force rounds per step (same tiles per chunk) */
+  if (scatter_lds(s.nbins, USN_SC_SR, sh.tc) <= 64u * 1024u) {
+    sh.sr = USN_SC_SR;
+    sh.lds = scatter_lds(s.nbins, USN_SC_SR, sh.tc);
+  }
+#endif
   const dim3 g(chunks), b(NTHREADS);
 #define USN_SC(SR_, TC_) \
   if (sh.sr == SR_ && sh.tc == TC_) hipLaunchKernelGGL((scatter_kernel<SR_, TC_>), g, b, sh.lds, stream, s)
