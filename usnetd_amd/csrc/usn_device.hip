@@ -2772,6 +2772,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
+#ifndef USN_ABL_SC   /* A/B only: 3 no ranks, 4 no rank loop, 5 no write-out (wrong results) */
+#define USN_ABL_SC 0
+#endif
 template <int SR, int TC>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   typedef typename std::conditional<SR == 2, uint4, uint2>::type Row;
