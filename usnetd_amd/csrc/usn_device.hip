@@ -2867,7 +2867,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - (first + (uint64_t)t * TILE));
     uint32_t bins[ROUNDS];
 #pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = dec_bin(d[t][r], s.n_ep);
+    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = min(dec_bin(d[t][r], s.n_ep), s.nbins - 1u);
 #pragma unroll
     for (uint32_t h = 0; h < ROUNDS / SR; ++h) {
       uint32_t rank[SR];
@@ -2896,7 +2896,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         const uint32_t p2 = q > 2 ? w[2] : q == 2 ? (w[2] & mpart) : 0u;
         const uint32_t p3 = q == 3 ? (w[3] & mpart) : 0u;
         const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
-        stage[cur[b] + before + rank[k]] = (b << 16) | (t * TILE + local);
+        stage[min(cur[b] + before + rank[k], TC * TILE - 1u)] = (b << 16) | (t * TILE + local);
       }
       __syncthreads();
       // cursors past this step's frames; rows cleared for the next step
@@ -2913,10 +2913,14 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     }
   }
   // 4. the stage out, in order
+  // (every address is bounds-checked: counts that disagree with the
+  // decisions, or an A/B build that skips a phase, cannot write past index)
   const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
   for (uint32_t q = tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
-    B.index[off[e >> 16] + q] = (uint32_t)first + (e & 0xFFFFu);
+    const uint32_t b = min(e >> 16, s.nbw - 1u);
+    const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
+    if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
   }
 }
 static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
