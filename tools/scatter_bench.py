@@ -61,6 +61,22 @@ def main():
         print("%-10s scatter %8.2f us (min %8.2f) per %d frames  %.1f GB/s of 12 B/frame  same=%s"
               % (nm, med, min(us), a.frames * a.multi, 12 * a.frames * a.multi / med / 1e3, same),
               flush=True)
+        if nm.startswith("stamps"):   # the diagnostic build: phase medians of the last launch
+            import numpy as np
+            buf = np.zeros(16384 * 16, np.uint64)
+            fn = ctx.L.usn_debug_stamps512
+            fn.argtypes = [C.c_void_p, C.c_size_t]
+            assert fn(buf.ctypes.data, buf.nbytes) == 0
+            chunks = sum(rs[0].ntiles for _ in rs) // 8 or 1
+            st = buf.reshape(16384, 16)[:min(chunks, 16384), :12].astype(np.int64)
+            t0 = st[:, 0].min()
+            names = ["start", "bases+barrier"] + ["tile %d" % k for k in range(8)] + ["loop end", "write-out"]
+            for k in range(1, 12):
+                dk = (st[:, k] - st[:, k - 1]) * 10 / 1000.0   # 100 MHz ticks -> us
+                print("   %-14s median %7.2f us  p90 %7.2f" % (names[k], np.median(dk), np.percentile(dk, 90)))
+            print("   span start %.2f..%.2f us, end %.2f..%.2f us, per chunk %.2f us" % (
+                0, (st[:, 0].max() - t0) / 100, (st[:, 11].min() - t0) / 100, (st[:, 11].max() - t0) / 100,
+                np.median(st[:, 11] - st[:, 0]) / 100), flush=True)
         for b in bs:
             b.free()
         for r in rs:

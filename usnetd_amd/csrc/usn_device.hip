@@ -2798,6 +2798,8 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   const uint32_t c = g - s.chunk_base[bi];
   const uint32_t t0 = c * TC, ntc = min((uint32_t)TC, B.ntiles - t0);
   const uint64_t first = (uint64_t)t0 * TILE;                        // the chunk's first frame
+  STAMP_DECL
+  STAMP(0);
   const uint32_t *ex = B.agg + (size_t)c * s.nbw;             // frames of b in the chunks before
   const uint32_t *nx = c + 1 < B.nchunks ? ex + s.nbw : B.tot;   // ... and in this one too
   // up to 1024 bins (two per thread): this thread's totals and chunk offsets
@@ -2860,6 +2862,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
   }
   __syncthreads();
+  STAMP(1);
   // 3. rank into the stage, tile by tile
 #pragma unroll
   for (uint32_t t = 0; t < TC; ++t) {
@@ -2911,7 +2914,9 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       }
       __syncthreads();
     }
+    if (t < 8) STAMP(2 + t);
   }
+  STAMP(10);
   // 4. the stage out, in order
   // (every address is bounds-checked: counts that disagree with the
   // decisions, or an A/B build that skips a phase, cannot write past index)
@@ -2922,6 +2927,8 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
     if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
   }
+  STAMP(11);
+  STAMP_FLUSH_AT(blockIdx.x);
 }
 static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
 static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
