@@ -2940,7 +2940,7 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t pairs = s.nbw / 2;
   hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
                      dim3(SCAN_THREADS), 0, stream, s);
-  ScatterShape sh = scatter_shape(s.nbins);
+  ScatterShape sh{s.sr, s.tc, scatter_lds(s.nbins, s.sr, s.tc)};
 #ifdef USN_SC_SR   /* A/B only: force rounds per step (same tiles per chunk) */
   if (scatter_lds(s.nbins, USN_SC_SR, sh.tc) <= 64u * 1024u) {
     sh.sr = USN_SC_SR;

@@ -1187,29 +1187,27 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 /* ========================================================================== */
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
- * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32, with
- * chunks of scatter_shape(nbins).tc tiles (monotonic in nbins: fewer tiles
- * per chunk only with more bins) */
+ * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32.  agg
+ * has a row per tile: a launch picks its chunk length (scatter_launch_tc) */
 struct ScatterGeom {
-  uint32_t nbw, ntiles, tc, nchunks;
+  uint32_t nbw, ntiles;
   size_t cnt, agg, tot, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
   g.nbw = (nbins + 7u) & ~7u;
   g.ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
-  g.tc = scatter_shape(nbins).tc;
-  g.nchunks = (g.ntiles + g.tc - 1) / g.tc;
   size_t o = 0;
   auto a256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
   g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw * 2);
-  g.agg = o; o = a256(o + (size_t)g.nchunks * g.nbw * 4);
+  g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.total = o;
   return g;
 }
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins) { return scatter_geom(n, nbins).total; }
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt) {
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
+                   uint16_t **cnt) {
   const ScatterGeom g = scatter_geom(n, nbins);
   uint8_t *p = static_cast<uint8_t *>(scratch);
   *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
@@ -1218,8 +1216,8 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, 
   sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
   sb.n = (uint32_t)n;
   sb.ntiles = g.ntiles;
-  sb.tc = g.tc;
-  sb.nchunks = g.nchunks;
+  sb.tc = tc;
+  sb.nchunks = (g.ntiles + tc - 1) / tc;
 }
 }  // namespace usn
 
@@ -1685,7 +1683,7 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   a.probe_mask = c->probe_mask;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, b->n, a.nbins, sb, &a.cnt);
+  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, sb, &a.cnt);
   a.nbw = (a.nbins + 7u) & ~7u;
   return USN_OK;
 }
@@ -1702,10 +1700,23 @@ static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint
   x.nblk = (x.nbw + USN_SCAN_BINS_PER_BLOCK - 1) / USN_SCAN_BINS_PER_BLOCK;
   x.n_ep = as[0].n_ep;
   x.nbits = as[0].nbits;
+  /* chunk length: the shape's (long chunks: contiguous runs per bin), shorter
+   * when the launch has too few tiles to give every CU its workgroups */
+  const usn::ScatterShape sh = usn::scatter_shape(x.nbins);
+  uint32_t launch_tiles = 0;
+  for (uint32_t k = 0; k < count; ++k) launch_tiles += as[k].ntiles;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
+  uint32_t tc = sh.tc;
+  while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
+  x.sr = sh.sr;
+  x.tc = tc;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
-    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, sb, &cnt);
+    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, sb, &cnt);
     sb.decisions = r[k].decisions;
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;

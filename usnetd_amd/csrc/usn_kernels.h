@@ -148,6 +148,7 @@ struct ScatterArgs {
   uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan_agg / scatter grid: chunks of batch i */
   uint32_t count;
   uint32_t nbins, nbw, nblk, n_ep, nbits;
+  uint32_t sr, tc;                          /* the scatter kernel's shape for this launch */
 };
 /* The scatter kernel's shape for nbins bins: tiles per chunk (tc) and rounds
  * ranked per step (sr: 2 = whole 1024-frame tiles with 16-byte rows, 1 = half
@@ -174,9 +175,15 @@ inline ScatterShape scatter_shape(uint32_t nbins) {
   }
   return best;
 }
-/* scratch bytes of one batch (cnt | agg | tot) and its carve */
+inline uint32_t scatter_occupancy(size_t lds) {
+  const uint32_t occ = (uint32_t)((160u * 1024u) / (lds ? lds : 1));
+  return occ > 4 ? 4 : occ;
+}
+/* scratch bytes of one batch (cnt | agg | tot; agg sized for one-tile
+ * chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, ScatterBatch &sb, uint16_t **cnt);
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
+                   uint16_t **cnt);
 
 }  // namespace usn
 
