@@ -80,7 +80,9 @@ def parse_args(argv=None):
                     help="strong scaling: 64M frames per step for the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the c2 line at N=1")
+    ap.add_argument("--no-extra", action="store_true", help="skip the other configs' keys at N=1")
+    ap.add_argument("--extras", default="c2,c3,c4,c4tx",
+                    help="configs measured under their own keys at N=1")
     ap.add_argument("--launch-probe", type=int, default=150, help="per-launch event pairs")
     ap.add_argument("--ramp", type=int, default=200,
                     help="untimed poll rounds between the probe and the timed steps (clock ramp)")
@@ -357,11 +359,85 @@ def measure(run, args, dist, world):
     }
 
 
+EXTRA_QUEUES = {"c3": 4}   # c3: 4 rx rings of 256K IMIX frames in 2 KiB slots (2 GiB)
+TX_ROTATE = 6              # c4tx: the ring in 6 device buffers (384 MiB > the 256 MiB Infinity Cache)
+
+
+def measure_tx(ctx, args):
+    """configs[3] in the tx direction (c4tx, traffic.c4tx): 1M frames sent by
+    the host endpoint, with ADD_MACS bridge MACs, MAC learning and answer-rule
+    learning (/root/reference/src/endpoint.rs:194-253).  One ring's frames
+    in TX_ROTATE device buffers used in turn: the first pass learns every
+    flow's answer rule, the timed passes learn nothing new, and no pass is
+    served from the Infinity Cache.  A tx batch changes shared state, so
+    each is classified and finalized before the next (the API's order):
+    value = frames / (classify + finalize wall time); the device time of the
+    classify call (tx kernel + per-endpoint scatter, HIP events) gives the
+    roofline."""
+    from usnetd_amd import lib, traffic
+    n = DEFAULT_FRAMES["c4"]
+    cfg = traffic.c4tx(n=n, seed=6)
+    traffic.install_ctx(ctx, cfg)
+    s = ctx.stream()
+    bufs = [lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+            for _ in range(TX_ROTATE)]
+    res = [lib.DeviceResult(ctx, n) for _ in range(2)]
+    for k in range(TX_ROTATE + args.warmup):          # learning pass + warm-up
+        ctx.classify(bufs[k % TX_ROTATE], res[k % 2], s)
+        ctx.finalize(bufs[k % TX_ROTATE], res[k % 2], s)
+    K = max(args.steps, 20)
+    evs = [(ctx.event(), ctx.event()) for _ in range(K)]
+    learned = 0
+    ctx.sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        b, r = bufs[k % TX_ROTATE], res[k % 2]
+        ctx.record(evs[k][0], s)
+        ctx.classify(b, r, s)
+        ctx.record(evs[k][1], s)
+        learned += ctx.finalize(b, r, s).n_learned
+    wall = time.perf_counter() - t0
+    dev_ms = float(np.median([ctx.elapsed_ms(a, e) for a, e in evs]))
+    achieved = ALGO_BYTES * n / (dev_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "tx_kernel + per-endpoint scatter", "kernel_us_median": round(dev_ms * 1e3, 3),
+            "frames_per_launch": n, "algo_bytes_per_frame": ALGO_BYTES}
+    pmc = os.path.join(ROOT, "profiles", "pmc_c4tx.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                pm = json.load(fh)
+            if int(pm.get("frames_per_launch", -1)) == n:
+                roof["traffic"] = pm.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(pmc, ROOT)
+        except (OSError, ValueError):
+            pass
+    x = {"value": round(K * n / wall / 1e6, 2), "unit": "Mpkts/s",
+         "value_basis": "end to end: classify + usn_finalize of each ring in turn",
+         "device_mpps": round(n / (dev_ms * 1e-3) / 1e6, 2), "ms_per_ring": round(wall * 1e3 / K, 4),
+         "rings": K, "learned_in_timed_rings": int(learned),
+         "workload": "c4tx: %d x 64B frames per ring sent by the host endpoint, %d rules after "
+                     "learning, ADD_MACS bridge; ring in %d rotating buffers (%d MiB)"
+                     % (n, ctx.rule_count(), TX_ROTATE, TX_ROTATE * n * cfg.stride >> 20),
+         "roofline": roof}
+    if not args.no_cpu_baseline:
+        x["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_seconds, 3.0))
+    for b in bufs:
+        b.free()
+    for r in res:
+        r.free()
+    return x
+
+
 def workload(run, strong):
     cfg = run.cfg0
-    return ("%s: %d x %dB frames per drained rx ring, %d-rule endpoint table, %d endpoints, NIC rx; "
+    sizes = sorted(set(int(x) for x in np.unique(cfg.lens)))
+    fr = ("%dB frames" % sizes[0]) if len(sizes) == 1 else \
+         ("IMIX frames (%s B) in %d-byte slots" % ("/".join(str(x) for x in sizes[:4]), cfg.stride))
+    return ("%s: %d x %s per drained rx ring, %d-rule endpoint table, %d endpoints, NIC rx; "
             "step = one poll round of %d rx queues per GPU (%d rings per launch, %d streams)%s"
-            % (run.name, run.n, int(cfg.lens[0]), len(cfg.rules), len(cfg.endpoints), run.Q, run.P,
+            % (run.name, run.n, fr, len(cfg.rules), len(cfg.endpoints), run.Q, run.P,
                run.S, "; strong scaling: 64M frames per step in all" if strong else ""))
 
 
@@ -437,19 +513,27 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
         out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, args.cpu_seconds)
     del cfg0
-    if world == 1 and not args.no_extra and args.config != "c2":
-        # configs[1] (the 1M x 64 B, 16-rule slice), measured the same way
-        ctx.close()
-        ctx = lib.Ctx(device)
-        if args.lists_async:
-            ctx.set_lists_async(True)
-        r2 = Run(L, ctx, "c2", DEFAULT_FRAMES["c2"], 0, 1, 0, args.streams, False)
-        x = measure(r2, args, None, 1)
-        x["workload"] = workload(r2, False)
-        if not args.no_cpu_baseline:
-            x["cpu_baseline"] = cpu_baseline(r2.cfg0, min(args.cpu_seconds, 5.0))
-        r2.free()
-        out["c2"] = x
+    if world == 1 and not args.no_extra:
+        # the other BASELINE configs, each measured the same way, under its own
+        # key: configs[1] (c2), configs[2] (c3: IMIX in 2048-byte slots) and
+        # configs[3] in both directions (c4 rx, c4tx: the ADD_MACS learned-MAC
+        # path of a sending endpoint)
+        for name in [x for x in args.extras.split(",") if x and x != args.config]:
+            ctx.close()
+            ctx = lib.Ctx(device)
+            if args.lists_async:
+                ctx.set_lists_async(True)
+            if name == "c4tx":
+                x = measure_tx(ctx, args)
+            else:
+                rx = Run(L, ctx, name, DEFAULT_FRAMES[name], 0, 1, EXTRA_QUEUES.get(name, 0),
+                         args.streams, False)
+                x = measure(rx, args, None, 1)
+                x["workload"] = workload(rx, False)
+                if not args.no_cpu_baseline:
+                    x["cpu_baseline"] = cpu_baseline(rx.cfg0, min(args.cpu_seconds, 3.0))
+                rx.free()
+            out[name] = x
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
