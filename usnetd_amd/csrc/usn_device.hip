@@ -2753,40 +2753,43 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
   if (lane == 0) *reinterpret_cast<uint2 *>(B.tot + 2 * p) = make_uint2(clo, chi);
 }
 
-/* (chunk of TC tiles): one workgroup of 512 threads.
- *  1. every decision of the chunk is loaded at once, into registers (2 per
- *     lane and tile): no load waits inside the tile loop;
- *  2. off[b] = bin b's base (block scan of the totals) + the chunks before
- *     (agg) - b's start in the chunk (block scan of the chunk's counts), and
- *     cur[b] = that start;
- *  3. per tile, in steps of SR rounds: each frame's rank among the step's
- *     frames of its bin (bit-sliced ballots; a row of u8 counts per bin and
- *     64-frame segment) puts it at stage[cur[bin] + rank]: the chunk sorted by
- *     (bin, frame) in LDS;
- *  4. the stage is written out in order: index[off[bin] + q] -- contiguous
- *     runs per bin, one L2 request per run instead of one per frame (c5, 1005
- *     bins: about 8 frames per run).
+/* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
+ * of the chunk.
+ *  1. each wave loads its tile's decisions at once (16 per lane: segment k
+ *     of 64 frames is lane + 64k), every wave in flight together;
+ *  2. per bin: off[b] = bin base (block scan of the totals) + the chunks
+ *     before (agg) - b's start in the chunk (block scan of the chunk's
+ *     counts), and each wave's cursor cur[w][b] = b's start in the chunk +
+ *     b's frames in the chunk's tiles before w (the classify kernel's count
+ *     rows) -- one barrier;
+ *  3. each wave walks its tile's 16 segments in frame order with its own
+ *     cursors, no barrier: a frame's rank among the segment's frames of its
+ *     bin (bit-sliced ballots) puts it at stage[cur[w][bin] + rank], and the
+ *     bin's first lane moves the cursor on: the chunk sorted by (bin, frame)
+ *     in LDS -- one barrier;
+ *  4. the stage is written out in order: index[off[bin] + q], contiguous
+ *     runs per bin (one L2 request per run instead of one per frame; c5,
+ *     1005 bins: about 8 frames per run).
  * Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them
  * so that an XCD takes a contiguous run of chunks (cdna_hip_programming.md T1
  * swizzle, bijective). */
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
-#ifndef USN_ABL_SC   /* A/B only: 3 no ranks, 4 no rank loop, 5 no write-out (wrong results) */
+#ifndef USN_ABL_SC   /* A/B only: 4 no rank walk, 5 no write-out (wrong results) */
 #define USN_ABL_SC 0
 #endif
-template <int SR, int TC>
+template <int TC>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
-  typedef typename std::conditional<SR == 2, uint4, uint2>::type Row;
-  constexpr uint32_t SEGB = SR * (NTHREADS / 64);                    // row bytes = segments per step
+  static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
+  constexpr uint32_t SEGS = TILE / 64;                               // 16 segments per tile
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint32_t s_scan[16];
   uint32_t *stage = reinterpret_cast<uint32_t *>(smem);              // [TC * TILE]: bin << 16 | frame
   uint32_t *off = stage + TC * TILE;                                 // [nbw]
-  uint16_t *cur = reinterpret_cast<uint16_t *>(off + s.nbw);         // [nbw]: < TC * TILE
-  Row *rows = reinterpret_cast<Row *>(cur + s.nbw);                  // [nbins]: u8 per segment
-  uint8_t *cb = reinterpret_cast<uint8_t *>(rows);
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint16_t *cur = reinterpret_cast<uint16_t *>(off + s.nbw);         // [TC][nbw]: < TC * TILE
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nwg = s.chunk_base[s.count];
   uint32_t g = blockIdx.x;
   if (USN_SCATTER_XCD) {
@@ -2801,50 +2804,62 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   STAMP_DECL
   STAMP(0);
   const uint32_t *ex = B.agg + (size_t)c * s.nbw;             // frames of b in the chunks before
-  const uint32_t *nx = c + 1 < B.nchunks ? ex + s.nbw : B.tot;   // ... and in this one too
-  // up to 1024 bins (two per thread): this thread's totals and chunk offsets
-  // are loaded before the decisions, so waiting for them leaves the
-  // decisions in flight
+  // up to 1024 bins (a pair per thread): totals, chunk offsets and the
+  // chunk's count rows are loaded first, then the decisions: waiting for the
+  // former leaves the decisions in flight
   const bool pair = s.nbw <= 2 * NTHREADS;
-  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0), vn = make_uint2(0, 0);
-  if (pair && 2 * tid < s.nbw) {
+  const bool mine = pair && 2 * tid < s.nbw;
+  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
+  uint32_t rc[TC];
+  if (mine) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
-    vn = *reinterpret_cast<const uint2 *>(nx + 2 * tid);
   }
-  // 1. every decision of the chunk (tiles past its end re-read its last one)
-  uint32_t d[TC][ROUNDS];
 #pragma unroll
-  for (uint32_t t = 0; t < TC; ++t) {
-    const uint64_t base = first + (uint64_t)min(t, ntc - 1) * TILE;
-    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - base);
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) d[t][r] = B.decisions[base + min(r * NTHREADS + tid, nt - 1)];
+  for (uint32_t w = 0; w < TC; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
+    const uint32_t t = t0 + min(w, ntc - 1);
+    rc[w] = mine ? reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw)[tid] : 0u;
+    if (w >= ntc) rc[w] = 0;
   }
-  // 2. bases and the chunk's bin starts
+  // 1. this wave's tile (waves past the chunk's end re-read its last tile, unused)
+  const uint32_t wt = min(wave, ntc - 1);
+  const uint64_t tbase = first + (uint64_t)wt * TILE;
+  const uint32_t tn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - tbase);
+  uint32_t d[SEGS];
+#pragma unroll
+  for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
+  // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
+    uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
     uint32_t total;
-    const uint32_t n0 = vn.x - ve.x, n1 = vn.y - ve.y;
     const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
-    const uint32_t pc = block_excl_scan(n0 + n1, s_scan, &total);
-    if (2 * tid < s.nbw) {
+    const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
+    if (mine) {
       const uint32_t b = 2 * tid;
-      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + n0));
-      *reinterpret_cast<uint32_t *>(cur + b) = (pc & 0xFFFFu) | ((pc + n0) << 16);
+      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
+      uint32_t s0 = pc, s1 = pc + c0;
+#pragma unroll
+      for (uint32_t w = 0; w < TC; ++w) {
+        reinterpret_cast<uint32_t *>(cur + (size_t)w * s.nbw)[tid] = (s0 & 0xFFFFu) | (s1 << 16);
+        s0 += rc[w] & 0xFFFFu;
+        s1 += rc[w] >> 16;
+      }
       if (c == 0) {
         if (b <= s.nbins) B.bin_off[b] = pt;                   // pad bins past nbins are empty
         if (b + 1 <= s.nbins) B.bin_off[b + 1] = pt + vt.x;
       }
     }
-    if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
-    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
-  } else {
-    const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;   // bins per thread, contiguous
+  } else {   // more bins: per-thread contiguous runs of bins, the same sums
+    const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
     uint32_t st = 0, sc = 0;
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
-      if (b < s.nbw) { st += B.tot[b]; sc += nx[b] - ex[b]; }
+      if (b >= s.nbw) break;
+      st += B.tot[b];
+      for (uint32_t w = 0; w < ntc; ++w) sc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
     }
     uint32_t total;
     uint32_t pt = block_excl_scan(st, s_scan, &total);
@@ -2853,73 +2868,39 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
       off[b] = pt + ex[b] - pc;
-      cur[b] = (uint16_t)pc;
-      if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;          // pad bins past nbins are empty
+      if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
       pt += B.tot[b];
-      pc += nx[b] - ex[b];
+      for (uint32_t w = 0; w < TC; ++w) {
+        cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
+        if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
+      }
     }
-    if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
-    for (uint32_t b = tid; b < s.nbins; b += NTHREADS) rows[b] = Row{};
   }
+  if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
   __syncthreads();
   STAMP(1);
-  // 3. rank into the stage, tile by tile
+  // 3. each wave ranks its tile into the stage, segment by segment, with its own cursors
+  if (wave < ntc && USN_ABL_SC != 4) {
+    uint16_t *cw = cur + (size_t)wave * s.nbw;
 #pragma unroll
-  for (uint32_t t = 0; t < TC; ++t) {
-    if (t >= ntc || USN_ABL_SC == 4) break;
-    const uint32_t nt = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - (first + (uint64_t)t * TILE));
-    uint32_t bins[ROUNDS];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) bins[r] = min(dec_bin(d[t][r], s.n_ep), s.nbins - 1u);
-#pragma unroll
-    for (uint32_t h = 0; h < ROUNDS / SR; ++h) {
-      uint32_t rank[SR];
-#pragma unroll
-      for (uint32_t k = 0; k < SR; ++k) {
-        const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
-        const bool v = local < nt;
-        const uint64_t same = match_bin(bins[r], __ballot(v), s.nbits);
-        rank[k] = (uint32_t)__popcll(same & lanemask_lt(lane));
-        if (v && rank[k] == 0) cb[bins[r] * SEGB + k * (NTHREADS / 64) + wave] = (uint8_t)__popcll(same);
+    for (uint32_t k = 0; k < SEGS; ++k) {
+      const uint32_t local = k * 64 + lane;
+      const bool v = local < tn;
+      const uint32_t b = min(dec_bin(d[k], s.n_ep), s.nbins - 1u);
+      const uint64_t same = match_bin(b, __ballot(v), s.nbits);
+      const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
+      const uint32_t at = cw[b];
+      if (v) {
+        stage[min(at + rank, TC * TILE - 1u)] = (b << 16) | (wave * TILE + local);
+        if (rank == 0) cw[b] = (uint16_t)(at + __popcll(same));
       }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t k = 0; k < SR; ++k) {
-        const uint32_t r = h * SR + k, local = r * NTHREADS + tid;
-        if (local >= nt) continue;
-        const uint32_t sg = k * (NTHREADS / 64) + wave, b = bins[r];
-        // frames of bin b in the segments before sg: whole words, then the low bytes of one
-        const Row wv = rows[b];
-        const uint32_t w[4] = {wv.x, wv.y, SR == 2 ? ((const uint4 &)wv).z : 0u,
-                               SR == 2 ? ((const uint4 &)wv).w : 0u};
-        const uint32_t q = sg >> 2, part = sg & 3u;
-        const uint32_t mpart = part ? (0xFFFFFFFFu >> (32u - 8u * part)) : 0u;
-        const uint32_t p0 = q > 0 ? w[0] : (w[0] & mpart);
-        const uint32_t p1 = q > 1 ? w[1] : q == 1 ? (w[1] & mpart) : 0u;
-        const uint32_t p2 = q > 2 ? w[2] : q == 2 ? (w[2] & mpart) : 0u;
-        const uint32_t p3 = q == 3 ? (w[3] & mpart) : 0u;
-        const uint32_t before = byte_sum(p0) + byte_sum(p1) + byte_sum(p2) + byte_sum(p3);
-        stage[min(cur[b] + before + rank[k], TC * TILE - 1u)] = (b << 16) | (t * TILE + local);
-      }
-      __syncthreads();
-      // cursors past this step's frames; rows cleared for the next step
-      for (uint32_t b = tid; b < s.nbins; b += NTHREADS) {
-        const Row wv = rows[b];
-        uint32_t n = byte_sum(wv.x) + byte_sum(wv.y);
-        if (SR == 2) n += byte_sum(((const uint4 &)wv).z) + byte_sum(((const uint4 &)wv).w);
-        if (n) {
-          cur[b] = (uint16_t)(cur[b] + n);
-          rows[b] = Row{};
-        }
-      }
-      __syncthreads();
     }
-    if (t < 8) STAMP(2 + t);
   }
+  __syncthreads();
   STAMP(10);
-  // 4. the stage out, in order
-  // (every address is bounds-checked: counts that disagree with the
-  // decisions, or an A/B build that skips a phase, cannot write past index)
+  // 4. the stage out, in order (every address bounds-checked: counts that
+  // disagree with the decisions, or an A/B build that skips a phase, cannot
+  // write past index)
   const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
   for (uint32_t q = tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
@@ -2930,7 +2911,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   STAMP(11);
   STAMP_FLUSH_AT(blockIdx.x);
 }
-static_assert(NTHREADS == 512 && NSEG == 16, "scatter: 16 segments of 64 frames per tile");
+static_assert(NTHREADS == 512, "scatter: 8 waves, a tile each");
 static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
 
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
@@ -2940,19 +2921,15 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t pairs = s.nbw / 2;
   hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
                      dim3(SCAN_THREADS), 0, stream, s);
-  ScatterShape sh{s.sr, s.tc, scatter_lds(s.nbins, s.sr, s.tc)};
-#ifdef USN_SC_SR   /* A/B only: force rounds per step (same tiles per chunk) */
-  if (scatter_lds(s.nbins, USN_SC_SR, sh.tc) <= 64u * 1024u) {
-    sh.sr = USN_SC_SR;
-    sh.lds = scatter_lds(s.nbins, USN_SC_SR, sh.tc);
-  }
-#endif
+  const size_t lds = scatter_lds(s.nbins, s.tc);
   const dim3 g(chunks), b(NTHREADS);
-#define USN_SC(SR_, TC_) \
-  if (sh.sr == SR_ && sh.tc == TC_) hipLaunchKernelGGL((scatter_kernel<SR_, TC_>), g, b, sh.lds, stream, s)
-  USN_SC(2, 8); else USN_SC(1, 8); else USN_SC(2, 4); else USN_SC(1, 4); else USN_SC(2, 2);
-  else USN_SC(1, 2); else USN_SC(2, 1); else USN_SC(1, 1); else return hipErrorInvalidValue;
-#undef USN_SC
+  switch (s.tc) {
+    case 8: hipLaunchKernelGGL(scatter_kernel<8>, g, b, lds, stream, s); break;
+    case 4: hipLaunchKernelGGL(scatter_kernel<4>, g, b, lds, stream, s); break;
+    case 2: hipLaunchKernelGGL(scatter_kernel<2>, g, b, lds, stream, s); break;
+    case 1: hipLaunchKernelGGL(scatter_kernel<1>, g, b, lds, stream, s); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512

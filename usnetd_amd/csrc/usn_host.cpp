@@ -1711,7 +1711,6 @@ static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint
   const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
   uint32_t tc = sh.tc;
   while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
-  x.sr = sh.sr;
   x.tc = tc;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];

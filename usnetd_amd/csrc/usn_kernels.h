@@ -148,32 +148,20 @@ struct ScatterArgs {
   uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan_agg / scatter grid: chunks of batch i */
   uint32_t count;
   uint32_t nbins, nbw, nblk, n_ep, nbits;
-  uint32_t sr, tc;                          /* the scatter kernel's shape for this launch */
+  uint32_t tc;                              /* the scatter kernel's chunk length for this launch */
 };
-/* The scatter kernel's shape for nbins bins: tiles per chunk (tc) and rounds
- * ranked per step (sr: 2 = whole 1024-frame tiles with 16-byte rows, 1 = half
- * tiles with 8-byte rows), the most workgroups per CU first (up to 4), then
- * the larger sr, within 64 KiB of LDS: stage tc x 4 KiB | offsets nbw x 4 |
- * cursors nbw x 2 | rows nbins x sr x 8. */
-struct ScatterShape { uint32_t sr, tc; size_t lds; };
-inline size_t scatter_lds(uint32_t nbins, uint32_t sr, uint32_t tc) {
+/* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
+ * bins: the longest chunk (contiguous runs per bin) whose LDS -- stage
+ * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 -- fits 64 KiB. */
+struct ScatterShape { uint32_t tc; size_t lds; };
+inline size_t scatter_lds(uint32_t nbins, uint32_t tc) {
   const size_t nbw = (nbins + 7u) & ~7u;
-  return (size_t)tc * USN_TILE * 4 + nbw * 6 + (size_t)nbins * sr * 8;
+  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2;
 }
 inline ScatterShape scatter_shape(uint32_t nbins) {
-  ScatterShape best{1, 1, scatter_lds(nbins, 1, 1)};
-  uint32_t best_occ = 0;
-  for (uint32_t tc : {8u, 4u, 2u, 1u}) {
-    for (uint32_t sr : {2u, 1u}) {
-      const size_t l = scatter_lds(nbins, sr, tc);
-      if (l > 64u * 1024u) continue;
-      uint32_t occ = (uint32_t)((160u * 1024u) / l);
-      occ = occ > 4 ? 4 : occ;
-      if (occ > best_occ) { best = ScatterShape{sr, tc, l}; best_occ = occ; }
-    }
-    if (best_occ >= 3) break;   // keep chunks long (contiguous runs per bin) once 3 fit per CU
-  }
-  return best;
+  for (uint32_t tc : {8u, 4u, 2u})
+    if (scatter_lds(nbins, tc) <= 64u * 1024u) return ScatterShape{tc, scatter_lds(nbins, tc)};
+  return ScatterShape{1, scatter_lds(nbins, 1)};
 }
 inline uint32_t scatter_occupancy(size_t lds) {
   const uint32_t occ = (uint32_t)((160u * 1024u) / (lds ? lds : 1));
