@@ -113,4 +113,5 @@ def test_c5_full_bench_batch(coracle_mod):
     assert hits > 0.85 * cfg.n            # the traffic really hits the installed table
     # every endpoint's list, the NIC, FLOOD and DROP lists: the oracle's, in frame order
     check_order_vec(r, want, max(e[0] for e in cfg.endpoints) + 1)
+    assert ctx.scatter_fallbacks() == 0      # every chunk's optimistic ranks were stable
     ctx.close()

@@ -2776,6 +2776,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
+/* chunks that took step 5 (usn_debug_scatter_fallbacks) */
+__device__ uint32_t usn_scatter_fallbacks = 0;
 #ifndef USN_ABL_SC   /* A/B only: 4 no rank walk, 5 no write-out (wrong results) */
 #define USN_ABL_SC 0
 #endif
@@ -2879,40 +2881,88 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
   __syncthreads();
   STAMP(1);
-  // 3. each wave ranks its tile into the stage, segment by segment, with its own cursors
+  // 3. each wave ranks its tile into the stage: one LDS atomic add per frame
+  // on the wave's own cursor of its bin (u16 pairs) returns the frame's stage
+  // slot.  The 16 segments' atomics are issued back to back (a wave's LDS
+  // operations execute in order, so segment k's frames precede segment
+  // k+1's); within one instruction the LDS serves the lanes that hit one word
+  // in lane order (tools/lds_order_check: 0 of 2.5e11 same-word lane pairs
+  // out of order).  That is not an ISA guarantee, so step 4 verifies the
+  // stage and a chunk that is not stably sorted is ranked again the
+  // ballot way (5).
+  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
   if (wave < ntc && USN_ABL_SC != 4) {
-    uint16_t *cw = cur + (size_t)wave * s.nbw;
+    uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
+    uint32_t b[SEGS], at[SEGS];
 #pragma unroll
     for (uint32_t k = 0; k < SEGS; ++k) {
-      const uint32_t local = k * 64 + lane;
-      const bool v = local < tn;
-      const uint32_t b = min(dec_bin(d[k], s.n_ep), s.nbins - 1u);
-      const uint64_t same = match_bin(b, __ballot(v), s.nbits);
-      const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
-      const uint32_t at = cw[b];
-      if (v) {
-        stage[min(at + rank, TC * TILE - 1u)] = (b << 16) | (wave * TILE + local);
-        if (rank == 0) cw[b] = (uint16_t)(at + __popcll(same));
-      }
+      b[k] = min(dec_bin(d[k], s.n_ep), s.nbins - 1u);
+      const uint32_t sh = 16u * (b[k] & 1u);
+      at[k] = k * 64 + lane < tn ? atomicAdd(&cw[b[k] >> 1], 1u << sh) >> sh : 0u;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < SEGS; ++k)
+      if (k * 64 + lane < tn)
+        stage[min(at[k] & 0xFFFFu, TC * TILE - 1u)] = (b[k] << 16) | (wave * TILE + k * 64 + lane);
   }
   __syncthreads();
   STAMP(10);
   // 4. the stage out, in order (every address bounds-checked: counts that
   // disagree with the decisions, or an A/B build that skips a phase, cannot
-  // write past index)
-  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  // write past index), checking that each bin's run is in frame order
+  bool unsorted = false;
   for (uint32_t q = tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
     const uint32_t b = min(e >> 16, s.nbw - 1u);
     const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
     if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
+    const uint32_t p = q ? stage[q - 1] : 0u;
+    unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
   }
   STAMP(11);
+  if (USN_ABL_SC == 0 && __syncthreads_or(unsorted || (s.flags & USN_SCF_SLOW_RANK))) {
+    // 5. (not taken on gfx950 so far) the wave's cursors back to their
+    // seeds (final value - the tile's count), the ranks from bit-sliced
+    // ballots segment by segment, the stage out again
+    if (wave < ntc) {
+      uint16_t *cw = cur + (size_t)wave * s.nbw;
+      const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
+      for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
+#pragma unroll
+      for (uint32_t k = 0; k < SEGS; ++k) {
+        const uint32_t local = k * 64 + lane;
+        const bool v = local < tn;
+        const uint32_t b = min(dec_bin(d[k], s.n_ep), s.nbins - 1u);
+        const uint64_t same = match_bin(b, __ballot(v), s.nbits);
+        const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
+        const uint32_t at = cw[b];
+        if (v) {
+          stage[min(at + rank, TC * TILE - 1u)] = (b << 16) | (wave * TILE + local);
+          if (rank == 0) cw[b] = (uint16_t)(at + __popcll(same));
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < nf; q += NTHREADS) {
+      const uint32_t e = stage[q];
+      const uint32_t b = min(e >> 16, s.nbw - 1u);
+      const uint32_t pos = off[b] + q;
+      if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
+    }
+    if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
+  }
   STAMP_FLUSH_AT(blockIdx.x);
 }
 static_assert(NTHREADS == 512, "scatter: 8 waves, a tile each");
 static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
+
+uint32_t scatter_fallbacks() {
+  uint32_t v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(usn_scatter_fallbacks), sizeof v, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return 0xFFFFFFFFu;
+  return v;
+}
 
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];

@@ -1712,6 +1712,8 @@ static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint
   uint32_t tc = sh.tc;
   while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
+  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
+  x.flags = slow_rank ? USN_SCF_SLOW_RANK : 0u;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
@@ -2580,6 +2582,19 @@ int usn_debug_scatter(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t co
   usn::ClassifyArgs as[USN_MAX_MULTI];
   for (uint32_t k = 0; k < count; ++k) fill_args(c, R, &b[k], &r[k], as[k]);
   return launch_scatter(as, r, count, (hipStream_t)stream);
+}
+
+/* diagnostics: scatter chunks on the selected replica's device whose
+ * optimistic ranks were not stably sorted and were ranked again (the
+ * kernel's step 5; expected 0), since the library was loaded */
+int64_t usn_debug_scatter_fallbacks(usn_ctx *c) {
+  if (!c) return USN_EINVAL;
+  if (c->reps.empty()) return USN_ENODEV;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->reps[c->sel].device));
+  HIPCHK(hipDeviceSynchronize());
+  const uint32_t v = usn_t512::scatter_fallbacks();
+  return v == 0xFFFFFFFFu ? (int64_t)USN_EHIP : (int64_t)v;
 }
 
 int usn_set_lists_async(usn_ctx *c, int on) {

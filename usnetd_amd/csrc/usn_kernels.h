@@ -149,7 +149,10 @@ struct ScatterArgs {
   uint32_t count;
   uint32_t nbins, nbw, nblk, n_ep, nbits;
   uint32_t tc;                              /* the scatter kernel's chunk length for this launch */
+  uint32_t flags;                           /* USN_SCF_* */
 };
+#define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
+                                  ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
  * bins: the longest chunk (contiguous runs per bin) whose LDS -- stage
  * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 -- fits 64 KiB. */
@@ -180,6 +183,7 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, Scatt
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
 hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream);
+uint32_t scatter_fallbacks();   /* chunks the scatter ranked again (current device) */
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }

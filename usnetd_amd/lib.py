@@ -372,6 +372,15 @@ class Ctx:
         """Build the per-endpoint lists on a side stream (usn_set_lists_async)."""
         check(self.L.usn_set_lists_async(self.h, int(bool(on))), "usn_set_lists_async")
 
+    def scatter_fallbacks(self) -> int:
+        """Scatter chunks (on this replica's device, since the library was
+        loaded) whose optimistic ranks were not stably sorted and were ranked
+        again the ballot way (expected 0; usn_debug_scatter_fallbacks)."""
+        f = self.L.usn_debug_scatter_fallbacks
+        f.argtypes = [C.c_void_p]
+        f.restype = C.c_int64
+        return check(f(self.h), "usn_debug_scatter_fallbacks")
+
     def lists_wait(self, result: "DeviceResult", stream=None):
         check(self.L.usn_lists_wait(self.h, C.byref(result.desc), stream), "usn_lists_wait")
 
