@@ -2668,14 +2668,14 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
 /* ===========================================================================
  * Per-endpoint lists: the device-wide stable scatter (usn_kernels.h).
  * The classify / tx kernel leaves each tile's decisions and its count row
- * cnt[tile][bin] (u16).  Three launches turn them into `index` (the batch's
+ * cnt[tile][bin] (u16).  Two launches turn them into `index` (the batch's
  * frame indices grouped by bin, frame order inside a bin) and bin_off:
- *   scan_agg     (chunk, bin block): the chunk's frames per bin           agg
- *   scan_chunks  (bin pair, one wave): agg := its exclusive scan over the
- *                chunks; tot = the bin's frames
- *   scatter      (chunk): the chunk's frames sorted by bin in an LDS stage,
- *                then written out in stage order: a bin's frames of the chunk
- *                leave as one contiguous run of index
+ *   scan     (range of 64 chunks, block of 64 bins): agg[chunk][bin] = the
+ *            bin's frames in the chunks before (exclusive scan over the
+ *            batch's chunks), tot = the bin's frames
+ *   scatter  (chunk): the chunk's frames sorted by bin in an LDS stage, then
+ *            written out in stage order: a bin's frames of the chunk leave as
+ *            one contiguous run of index
  * Algorithmic bytes per frame: 4 (index).  The reference writes each frame
  * straight into its target's ring (endpoint.rs:61-74) and copies FLOOD frames
  * to every other endpoint (:340-363): an endpoint's frames are its list merged
@@ -2689,68 +2689,126 @@ __device__ __forceinline__ uint32_t base_of(const uint32_t *base, uint32_t count
 }
 
 #define SCAN_THREADS 256
-static_assert(USN_SCAN_BINS_PER_BLOCK == 2 * SCAN_THREADS, "two bins per scan thread");
+static_assert(USN_SCAN_RANGE == 64 && USN_SCAN_BLK == 64, "scan: 16 row groups x 4 chunks, 16 lanes x 4 bins");
+#define SCAN_SPIN_TICKS (200u * 100000u)   /* 200 ms of the 100 MHz real-time clock */
 
-/* (chunk, bin block): frames of bins 2w, 2w+1 over the chunk's tiles, 8 row
- * loads in flight */
-__global__ __launch_bounds__(SCAN_THREADS) void scan_agg_kernel(ScatterArgs s) {
-  const uint32_t g = blockIdx.x, bb = blockIdx.y, tid = threadIdx.x;
-  const uint32_t bi = base_of(s.chunk_base, s.count, g);
-  const ScatterBatch &B = s.b[bi];
-  const uint32_t c = g - s.chunk_base[bi];
-  const uint32_t t0 = c * B.tc, t1 = min(t0 + B.tc, B.ntiles);
-  const uint32_t w = bb * SCAN_THREADS + tid;          // bins 2w, 2w + 1
-  if (2 * w >= s.nbw) return;
-  const uint32_t *col = reinterpret_cast<const uint32_t *>(B.cnt) + w;
-  const uint32_t stride = s.nbw / 2;
-  uint32_t lo = 0, hi = 0, t = t0;
-  for (; t + 8 <= t1; t += 8) {
-    uint32_t v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = col[(size_t)(t + k) * stride];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { lo += v[k] & 0xFFFFu; hi += v[k] >> 16; }
-  }
-  for (; t < t1; ++t) {
-    const uint32_t v = col[(size_t)t * stride];
-    lo += v & 0xFFFFu; hi += v >> 16;
-  }
-  *reinterpret_cast<uint2 *>(B.agg + (size_t)c * s.nbw + 2 * w) = make_uint2(lo, hi);
+typedef __attribute__((address_space(1))) unsigned long long gu64s;
+/* a range total: {epoch, value} in one 8-byte agent-scope (sc1) store */
+__device__ __forceinline__ void scan_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
+  __hip_atomic_store((gu64s *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* (bin pair, batch): one wave scans the pair's column of agg in blocks of
- * 1024 chunks (lane L owns chunks 16L .. 16L+15 of a block): agg := its
- * exclusive scan in place, tot = the totals */
-__global__ __launch_bounds__(SCAN_THREADS) void scan_chunks_kernel(ScatterArgs s) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const ScatterBatch &B = s.b[blockIdx.y];
-  const uint32_t p = blockIdx.x * (SCAN_THREADS / 64) + wave;   // bins 2p, 2p + 1
-  if (2 * p >= s.nbw) return;
-  uint2 *col = reinterpret_cast<uint2 *>(B.agg + 2 * p);
-  const uint32_t stride = s.nbw / 2;                           // uint2 per agg row
-  uint32_t clo = 0, chi = 0;                                    // blocks before
-  for (uint32_t c0 = 0; c0 < B.nchunks; c0 += 1024) {
-    uint2 v[16];
+/* (range r of a batch's chunks, bin block bb), range-major so that a
+ * workgroup waits only on workgroups dispatched before it:
+ *  1. thread (rg, l) sums the count rows of chunks 4rg..4rg+3 of the range
+ *     for bins 4l..4l+3 of the block (every load in flight together);
+ *  2. the block's 16 row groups are scanned in LDS: each chunk's prefix
+ *     inside the range, and the range's totals, published as epoch-tagged
+ *     granules gran[r][bin];
+ *  3. carry = the totals of ranges 0..r-1 (their granules, polled; each
+ *     range publishes before it waits, so the wait ends);
+ *  4. agg[chunk][bin] = carry + prefix (16-byte stores); the last range
+ *     writes tot. */
+__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
+  __shared__ uint32_t s_t[16][USN_SCAN_BLK];
+  __shared__ uint32_t s_c[4][USN_SCAN_BLK];
+  __shared__ uint32_t s_tot[USN_SCAN_BLK];
+  const uint32_t tid = threadIdx.x, l = tid & 15, rg = tid >> 4;
+  const uint32_t rgl = blockIdx.x / s.nbb, bb = blockIdx.x - rgl * s.nbb;
+  const uint32_t bi = base_of(s.range_base, s.count, rgl);
+  const ScatterBatch &B = s.b[bi];
+  const uint32_t r = rgl - s.range_base[bi];
+  const uint32_t b0 = bb * USN_SCAN_BLK + 4 * l;             // this thread's 4 bins
+  const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
+  const uint32_t c0 = r * USN_SCAN_RANGE + rg * 4;          // this thread's 4 chunks
+  // 1.
+  uint2 v[4][8];
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-      const uint32_t c = c0 + lane * 16 + k;
-      v[k] = c < B.nchunks ? col[(size_t)c * stride] : make_uint2(0, 0);
+  for (uint32_t j = 0; j < 4; ++j)
+#pragma unroll
+    for (uint32_t w = 0; w < 8; ++w) {
+      const uint32_t t = (c0 + j) * s.tc + w;
+      const bool ok = binok && w < s.tc && t < B.ntiles;
+      v[j][w] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
     }
-    uint32_t lo = 0, hi = 0;
+  uint32_t ex[4][4], tot[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) { lo += v[k].x; hi += v[k].y; }
-    const uint32_t ilo = wave_incl_scan(lo, lane), ihi = wave_incl_scan(hi, lane);
-    uint32_t elo = clo + ilo - lo, ehi = chi + ihi - hi;
+  for (uint32_t j = 0; j < 4; ++j) {
+    uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-      const uint32_t c = c0 + lane * 16 + k;
-      if (c < B.nchunks) col[(size_t)c * stride] = make_uint2(elo, ehi);
-      elo += v[k].x; ehi += v[k].y;
+    for (uint32_t w = 0; w < 8; ++w) {
+      a[0] += v[j][w].x & 0xFFFFu; a[1] += v[j][w].x >> 16;
+      a[2] += v[j][w].y & 0xFFFFu; a[3] += v[j][w].y >> 16;
     }
-    clo += __shfl(ilo, 63, 64);
-    chi += __shfl(ihi, 63, 64);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) { ex[j][i] = tot[i]; tot[i] += a[i]; }
   }
-  if (lane == 0) *reinterpret_cast<uint2 *>(B.tot + 2 * p) = make_uint2(clo, chi);
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) s_t[rg][4 * l + i] = tot[i];
+  __syncthreads();
+  // 2.
+  unsigned long long *gran = B.gran + (size_t)r * s.nbw;
+  if (tid < USN_SCAN_BLK) {
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t x = s_t[k][tid];
+      s_t[k][tid] = run;
+      run += x;
+    }
+    s_tot[tid] = run;
+    if (bb * USN_SCAN_BLK + tid < s.nbw) scan_put(gran + bb * USN_SCAN_BLK + tid, s.epoch, run);
+  }
+  // 3. thread (part, k) sums ranges part, part + 4, ... < r of bin k, four polls in flight
+  {
+    const uint32_t k = tid & 63, part = tid >> 6, bin = bb * USN_SCAN_BLK + k;
+    uint32_t sum = 0;
+    if (bin < s.nbw) {
+      const unsigned long long *col = B.gran + bin;
+      uint64_t t0 = 0;
+      for (uint32_t q = part; q < r; q += 16) {
+        uint32_t got = 0;    // bit u: range q + 4u read
+        for (uint32_t it = 0;; ++it) {
+#pragma unroll
+          for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t rr = q + 4 * u;
+            if (rr < r && !(got & (1u << u))) {
+              const unsigned long long x = __hip_atomic_load((const gu64s *)(col + (size_t)rr * s.nbw),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if ((uint32_t)(x >> 32) == s.epoch) { sum += (uint32_t)x; got |= 1u << u; }
+            }
+          }
+          bool done = true;
+#pragma unroll
+          for (uint32_t u = 0; u < 4; ++u) done &= (q + 4 * u >= r) || (got & (1u << u));
+          if (done) break;
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (it == 0) t0 = now;
+          else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, 1u); break; }   // never seen; lists wrong
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    s_c[part][k] = sum;
+  }
+  __syncthreads();
+  // 4.
+  uint32_t carry[4];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t k = 4 * l + i;
+    carry[i] = s_c[0][k] + s_c[1][k] + s_c[2][k] + s_c[3][k] + s_t[rg][k];
+  }
+  if (binok) {
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+      if (c0 + j < B.nchunks)
+        *reinterpret_cast<uint4 *>(B.agg + (size_t)(c0 + j) * s.nbw + b0) =
+            make_uint4(carry[0] + ex[j][0], carry[1] + ex[j][1], carry[2] + ex[j][2], carry[3] + ex[j][3]);
+  }
+  if (r + 1 == B.nranges && tid < USN_SCAN_BLK && bb * USN_SCAN_BLK + tid < s.nbw)
+    B.tot[bb * USN_SCAN_BLK + tid] = s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid];
 }
 
 /* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
@@ -2967,10 +3025,7 @@ uint32_t scatter_fallbacks() {
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_agg_kernel, dim3(chunks, s.nblk), dim3(SCAN_THREADS), 0, stream, s);
-  const uint32_t pairs = s.nbw / 2;
-  hipLaunchKernelGGL(scan_chunks_kernel, dim3((pairs + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64), s.count),
-                     dim3(SCAN_THREADS), 0, stream, s);
+  hipLaunchKernelGGL(scan_kernel, dim3(s.range_base[s.count] * s.nbb), dim3(SCAN_THREADS), 0, stream, s);
   const size_t lds = scatter_lds(s.nbins, s.tc);
   const dim3 g(chunks), b(NTHREADS);
   switch (s.tc) {

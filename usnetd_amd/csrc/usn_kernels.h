@@ -122,34 +122,38 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
 
 /* ---- per-endpoint lists: the device-wide stable scatter ------------------
  * After the classify (or tx) kernel has written each tile's decisions and its
- * row of per-bin frame counts (cnt[tile][bin], u16), three launches:
- *   scan_agg     (chunk of tc tiles, bin block): the chunk's frames per bin
- *   scan_chunks  (bin pair, one wave): exclusive scan of agg over the chunks
- *                (in place) and the bin's total
- *   scatter      (chunk): every decision of the chunk in registers at once;
- *                bin bases (block scan of the totals); per tile each frame's
- *                rank among the tile's frames of its bin (bit-sliced ballots +
- *                per-segment byte counts) gives its slot in the chunk's
- *                bin-sorted LDS stage; the stage is written out in order, so
- *                each bin's frames of the chunk leave as one contiguous run
+ * row of per-bin frame counts (cnt[tile][bin], u16), two launches:
+ *   scan     (range of USN_SCAN_RANGE chunks, block of USN_SCAN_BLK bins):
+ *            agg[chunk][bin] = frames of the bin in the batch's chunks before
+ *            (ranges hand their totals on through epoch-tagged granules),
+ *            tot[bin] = the bin's frames
+ *   scatter  (chunk of tc tiles): one LDS atomic per frame ranks it in the
+ *            chunk's bin-sorted LDS stage (verified; ballot ranks as the
+ *            fallback); the stage is written out in order, so each bin's
+ *            frames of the chunk leave as one contiguous run
  * Stable: bins in order, frames in frame order inside a bin. */
-#define USN_SCAN_BINS_PER_BLOCK 512u   /* scan_agg: 256 threads x 2 bins */
+#define USN_SCAN_RANGE 64u   /* chunks per scan workgroup */
+#define USN_SCAN_BLK 64u     /* bins per scan workgroup */
 struct ScatterBatch {
   const uint32_t *decisions;
   const uint16_t *cnt;      /* [ntiles][nbw] */
-  uint32_t *agg;            /* [nchunks][nbw]: chunk totals, then their exclusive scan */
+  uint32_t *agg;            /* [nchunks][nbw]: frames per bin in the chunks before */
   uint32_t *tot;            /* [nbw]: frames per bin */
+  unsigned long long *gran; /* [nranges][nbw]: {epoch, range total} */
+  uint32_t *diag;           /* bit 0: a scan wait timed out (the lists are wrong) */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
-  uint32_t n, ntiles, tc, nchunks;
+  uint32_t n, ntiles, tc, nchunks, nranges;
 };
 struct ScatterArgs {
   ScatterBatch b[USN_MAX_MULTI];
-  uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scan_agg / scatter grid: chunks of batch i */
+  uint32_t chunk_base[USN_MAX_MULTI + 1];   /* scatter grid: chunks of batch i */
+  uint32_t range_base[USN_MAX_MULTI + 1];   /* scan grid (x nbb): ranges of batch i */
   uint32_t count;
-  uint32_t nbins, nbw, nblk, n_ep, nbits;
+  uint32_t nbins, nbw, nbb, n_ep, nbits;
   uint32_t tc;                              /* the scatter kernel's chunk length for this launch */
   uint32_t flags;                           /* USN_SCF_* */
+  uint32_t epoch;                           /* this launch's granule tag (never 0) */
 };
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
@@ -170,11 +174,12 @@ inline uint32_t scatter_occupancy(size_t lds) {
   const uint32_t occ = (uint32_t)((160u * 1024u) / (lds ? lds : 1));
   return occ > 4 ? 4 : occ;
 }
-/* scratch bytes of one batch (cnt | agg | tot; agg sized for one-tile
- * chunks) and its carve for chunks of tc tiles */
+/* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
+ * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
 void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
                    uint16_t **cnt);
+void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 
 }  // namespace usn
 
