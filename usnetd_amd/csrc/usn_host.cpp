@@ -22,7 +22,9 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <random>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -40,9 +42,12 @@ using usn::ClassifyArgs;
  * went from 0.75 to 0.65: the kernel does not notice (c5 157.0 vs 158.1 us,
  * c4 160.9 vs 162.5), and placement takes a third of the time (a group of s
  * keys needs ~1/(1-fill)^s trials): 1.19M rules rebuilt in 83 instead of
- * 155 ms (profiles/r02g). */
+ * 155 ms (profiles/r02g).  Round 3: 0.5, so that a key inserted in place
+ * (AddMatch between full builds, refresh_image) finds a free slot under its
+ * group's displacement half the time and its group a new displacement
+ * almost always; a table is rebuilt once its keys pass IMG_MAX_LOAD. */
 #ifndef USN_PH_LOAD
-#define USN_PH_LOAD 0.65
+#define USN_PH_LOAD 0.5
 #endif
 #ifndef USN_PH_GROUP
 #define USN_PH_GROUP 10
@@ -459,6 +464,20 @@ struct usn_ctx {
   uint32_t img_udisp = 0;      // first unit of U's and X's displacements
   uint32_t probe_mask = 0;   // tables holding rules (ClassifyArgs::probe_mask)
   bool proj = std::getenv("USN_NO_PROJ") == nullptr;   // A/B: build U and X
+  /* incremental image updates between full builds (AddMatch / RemoveMatch /
+   * a few learned rules): the registry keys changed since the image was last
+   * brought up to date, each table's displacement groups (slot indices from
+   * the table's first slot; built on first use after a full build), its
+   * keys, and the 16-byte units patched since the last full build, with the
+   * image version that patched them (what a replica uploads) */
+  bool incremental = std::getenv("USN_IMG_FULL") == nullptr;   // A/B: every change rebuilds
+  std::vector<WantKey> img_delta;
+  bool img_groups_ok = false;
+  std::vector<std::vector<uint32_t>> img_groups[4];
+  uint32_t img_nkeys[4] = {0, 0, 0, 0};
+  uint64_t img_full_version = 0;
+  std::vector<std::pair<uint64_t, uint32_t>> img_patches;
+  uint64_t img_builds = 0, img_updates = 0;   // full builds / incremental updates (diagnostics)
   bool bridge_dirty = true;
   uint64_t bridge_version = 0;
   std::vector<unsigned long long> bridge_set;
@@ -492,6 +511,10 @@ struct usn_ctx {
   bool lists_async = false;
   struct ListsEv { hipEvent_t ev = nullptr; int device = -1; bool pending = false; };
   std::unordered_map<const void *, ListsEv> lists_ev;
+  /* the scatter's scan: a tag per launch for its range granules (random
+   * start), and the result scratches whose granules were zeroed */
+  uint32_t scan_epoch = (uint32_t)std::random_device{}();
+  std::unordered_set<uint64_t> scan_zeroed;   // (scratch, frames, bins)
 };
 
 namespace {
@@ -513,10 +536,16 @@ int image_table(const WantKey &k) {
   return -1;
 }
 
-/* registry insert: the device image is rebuilt before the next batch */
+/* a registry key whose rule was added, removed or changed: the image is
+ * brought up to date before the next batch (refresh_image) */
+void note_change(usn_ctx *c, const WantKey &k) {
+  if (!c->table_dirty) c->img_delta.push_back(k);
+}
+
+/* registry insert */
 void rule_insert(usn_ctx *c, const WantKey &k, Rule r) {
   c->rules[k] = r;
-  c->table_dirty = true;
+  note_change(c, k);
 }
 
 /* USN_PROFILE_HOST=1: per-stage wall times of the host stages on stderr */
@@ -702,8 +731,11 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
     clk.mark("partition");
     uint32_t maxc = 0;
     for (uint32_t sh = 0; sh < S; ++sh) maxc = std::max(maxc, off[sh + 1] - off[sh]);
-    const uint32_t m = std::max<uint32_t>(maxc + 1, (uint32_t)((double)maxc / load) + 1);
-    const uint32_t g = std::max<uint32_t>(1, (maxc + group - 1) / group);
+    // at least 64 slots, and groups for the keys the slots hold at `load`: a
+    // small table takes keys in place (refresh_image) before it is rebuilt
+    const uint32_t m = std::max<uint32_t>({maxc + 1, (uint32_t)((double)maxc / load) + 1, 64u});
+    const uint32_t g = std::max<uint32_t>({1u, (maxc + group - 1) / group,
+                                           (uint32_t)(m * load / group)});
     slots.resize((size_t)S * m);
     disp.resize((size_t)S * g);
     std::vector<uint8_t> ok(S, 0);
@@ -916,7 +948,327 @@ int build_image(usn_ctx *c) {
   c->probe_mask = (keys[0].empty() ? 0u : 1u) | (keys[1].empty() ? 0u : 2u) | (proj ? 4u : 0u);
   c->table_dirty = false;
   ++c->table_version;
+  for (int i = 0; i < 4; ++i) c->img_nkeys[i] = (uint32_t)keys[i].size();
+  c->img_delta.clear();
+  c->img_groups_ok = false;
+  c->img_full_version = c->table_version;
+  c->img_patches.clear();
+  ++c->img_builds;
   clk.mark("image");
+  return USN_OK;
+}
+
+/* ---- incremental image updates ---------------------------------------------
+ * An AddMatch or RemoveMatch changes one key: rather than rebuilding the
+ * image (c5: 15-35 ms; the reference's insert is one HashMap insert,
+ * main.rs:266-298), the key's slot is written in place, or, for a new key
+ * whose slot under its group's displacement is taken, its group is placed
+ * again (a new displacement that sends every member to a free slot); the
+ * projection slot in U and the X table follow the same way.  Anything
+ * else -- a group that cannot be placed, a table past IMG_MAX_LOAD or empty
+ * at the last build, a change of the U build condition, more changes than
+ * IMG_MAX_DELTA -- rebuilds the whole image.  The replicas upload only the
+ * patched units (upload_table). */
+#define IMG_MAX_LOAD 0.6
+int g_img_fail = 0;   // diagnostics: why the last in-place insert failed (table * 10 + cause)
+bool img_occupied(int i, const uint4 &e) {
+  return i == 2 ? e.w != USN_U_EMPTY_W : (e.w & USN_SLOT_VALID) != 0;
+}
+uint4 img_empty(int i) { return i == 2 ? make_uint4(0, 0, 0, USN_U_EMPTY_W) : make_uint4(0, 0, 0, 0); }
+uint4 img_hkey(int i, const uint4 &e) {   // the hashed key of an occupied slot
+  return i == 2 ? make_uint4(e.x, 0u, e.w & USN_U_EMASK, 0u)
+                : make_uint4(e.x, e.y, e.z, e.w & USN_KEY_META_MASK);
+}
+void img_patch(usn_ctx *c, uint32_t unit) { c->img_patches.emplace_back(c->table_version + 1, unit); }
+uint16_t *img_disp(usn_ctx *c) { return reinterpret_cast<uint16_t *>(c->img.data()); }
+
+void img_groups_build(usn_ctx *c) {
+  for (int i = 0; i < 4; ++i) {
+    const usn_ph_table &T = c->img_t[i];
+    auto &G = c->img_groups[i];
+    G.assign(T.m ? (size_t)T.g << T.shift : 0, {});
+    if (!T.m) continue;
+    const size_t slots = (size_t)T.m << T.shift;
+    for (size_t q = 0; q < slots; ++q) {
+      const uint4 &e = c->img[T.slot_off + q];
+      if (!img_occupied(i, e)) continue;
+      const uint4 k = img_hkey(i, e);
+      G[usn_ph_group(usn_ph_h1(k.x, k.y, k.z, k.w, T.seed), T.shift, T.g)].push_back((uint32_t)q);
+    }
+  }
+  c->img_groups_ok = true;
+}
+
+/* the image unit holding key k of table i, or -1 */
+int64_t img_find(const usn_ctx *c, int i, const uint4 &k) {
+  const usn_ph_table &T = c->img_t[i];
+  if (!T.m) return -1;
+  const uint32_t h1 = usn_ph_h1(k.x, k.y, k.z, k.w, T.seed);
+  const uint32_t G = usn_ph_group(h1, T.shift, T.g);
+  const uint16_t d = reinterpret_cast<const uint16_t *>(c->img.data())[T.disp_off + G];
+  const size_t u = T.slot_off + (size_t)usn_ph_shard(h1, T.shift) * T.m +
+                   usn_ph_slot(usn_key_hash2(k.x, k.y, k.z, k.w, T.seed), d, T.m);
+  const uint4 &e = c->img[u];
+  if (!img_occupied(i, e)) return -1;
+  const uint4 h = img_hkey(i, e);
+  return (h.x == k.x && h.y == k.y && h.z == k.z && h.w == k.w) ? (int64_t)u : -1;
+}
+
+/* a displacement group of table i being placed again: its entries (the
+ * members, plus a new one) and their slots under the displacement found */
+struct GroupMove {
+  uint32_t G = 0, sh = 0;
+  size_t n = 0;
+  uint4 ent[64];
+  uint32_t hh[64], pos[64];
+  uint32_t d = 0;
+  const GroupMove *avoid = nullptr;   // another group's move whose target slots are taken
+};
+bool img_group_collect(usn_ctx *c, int i, uint32_t G, const uint4 *extra, uint32_t extra_h2,
+                       GroupMove &mv) {
+  const usn_ph_table &T = c->img_t[i];
+  const std::vector<uint32_t> &mem = c->img_groups[i][G];
+  mv.G = G;
+  mv.sh = G / T.g;
+  mv.n = mem.size() + (extra ? 1 : 0);
+  if (mv.n > 64) return false;
+  for (size_t j = 0; j < mem.size(); ++j) {
+    mv.ent[j] = c->img[T.slot_off + mem[j]];
+    const uint4 mk = img_hkey(i, mv.ent[j]);
+    mv.hh[j] = usn_key_hash2(mk.x, mk.y, mk.z, mk.w, T.seed);
+  }
+  if (extra) {
+    mv.ent[mv.n - 1] = *extra;
+    mv.hh[mv.n - 1] = extra_h2;
+  }
+  return true;
+}
+/* the first displacement that sends every entry of mv to a distinct slot
+ * that is free or the group's own (and not a target of mv.avoid); with
+ * `one`, the displacements blocked by exactly one other key are collected */
+bool img_group_search(usn_ctx *c, int i, GroupMove &mv, const GroupMove *avoid,
+                      std::vector<std::pair<uint32_t, uint32_t>> *one) {
+  const usn_ph_table &T = c->img_t[i];
+  const std::vector<uint32_t> &mem = c->img_groups[i][mv.G];
+  const size_t base = T.slot_off + (size_t)mv.sh * T.m;
+  auto own = [&](uint32_t p) {
+    return std::find(mem.begin(), mem.end(), (uint32_t)(mv.sh * T.m + p)) != mem.end();
+  };
+  for (uint32_t d = 0; d < 65536; ++d) {
+    uint32_t blockers = 0, blocker = 0;
+    bool ok = true;
+    for (size_t j = 0; j < mv.n && ok; ++j) {
+      const uint32_t p = usn_ph_slot(mv.hh[j], d, T.m);
+      for (size_t q = 0; q < j; ++q)
+        if (mv.pos[q] == p) { ok = false; break; }
+      if (!ok) break;
+      mv.pos[j] = p;
+      if (avoid && avoid->sh == mv.sh)
+        for (size_t q = 0; q < avoid->n; ++q)
+          if (avoid->pos[q] == p) { ok = false; break; }
+      if (!ok) break;
+      if (img_occupied(i, c->img[base + p]) && !own(p)) {
+        blocker = p;
+        if (++blockers > (one ? 1u : 0u)) ok = false;
+      }
+    }
+    if (!ok) continue;
+    if (blockers == 0) { mv.d = d; return true; }
+    if (one && one->size() < 64) one->emplace_back(d, blocker);
+  }
+  return false;
+}
+/* the group's old slots emptied, its entries written at mv.pos, its
+ * displacement set (every unit patched) */
+void img_group_commit(usn_ctx *c, int i, const GroupMove &mv) {
+  const usn_ph_table &T = c->img_t[i];
+  std::vector<uint32_t> &mem = c->img_groups[i][mv.G];
+  const size_t base = T.slot_off + (size_t)mv.sh * T.m;
+  const uint4 empty = img_empty(i);
+  for (uint32_t q : mem) {
+    c->img[T.slot_off + q] = empty;
+    img_patch(c, (uint32_t)(T.slot_off + q));
+  }
+  mem.clear();
+  for (size_t j = 0; j < mv.n; ++j) {
+    c->img[base + mv.pos[j]] = mv.ent[j];
+    img_patch(c, (uint32_t)(base + mv.pos[j]));
+    mem.push_back((uint32_t)(mv.sh * T.m + mv.pos[j]));
+  }
+  img_disp(c)[T.disp_off + mv.G] = (uint16_t)mv.d;
+  img_patch(c, (T.disp_off + mv.G) / 8);
+}
+
+/* key k of table i gets slot content e (inserted or overwritten) */
+bool img_upsert(usn_ctx *c, int i, const uint4 &k, const uint4 &e) {
+  const int64_t at = img_find(c, i, k);
+  if (at >= 0) {
+    c->img[at] = e;
+    img_patch(c, (uint32_t)at);
+    return true;
+  }
+  const usn_ph_table &T = c->img_t[i];
+  if (!T.m || c->img_nkeys[i] + 1 > IMG_MAX_LOAD * (double)((size_t)T.m << T.shift)) {
+    g_img_fail = i * 10 + 1;
+    return false;
+  }
+  const uint32_t h1 = usn_ph_h1(k.x, k.y, k.z, k.w, T.seed);
+  const uint32_t G = usn_ph_group(h1, T.shift, T.g), sh = usn_ph_shard(h1, T.shift);
+  const size_t base = T.slot_off + (size_t)sh * T.m;   // the shard's first unit
+  uint16_t *D = img_disp(c);
+  const uint32_t h2 = usn_key_hash2(k.x, k.y, k.z, k.w, T.seed);
+  std::vector<uint32_t> &mem = c->img_groups[i][G];   // from the table's first slot
+  const uint32_t p0 = usn_ph_slot(h2, D[T.disp_off + G], T.m);
+  if (!img_occupied(i, c->img[base + p0])) {   // free under the group's displacement
+    c->img[base + p0] = e;
+    img_patch(c, (uint32_t)(base + p0));
+    mem.push_back((uint32_t)(sh * T.m + p0));
+    c->img_nkeys[i]++;
+    return true;
+  }
+  // the group again with a new displacement (img_group_search); if none
+  // exists, one that blocks on a single key of another group, which that
+  // group gives up by taking a new displacement itself
+  GroupMove mv;
+  if (!img_group_collect(c, i, G, &e, h2, mv)) { g_img_fail = i * 10 + 2; return false; }
+  std::vector<std::pair<uint32_t, uint32_t>> one;   // (d, blocking slot) with a single blocker
+  if (img_group_search(c, i, mv, nullptr, &one)) {
+    img_group_commit(c, i, mv);
+    c->img_nkeys[i]++;
+    return true;
+  }
+  for (const auto &cand : one) {
+    mv.d = cand.first;
+    for (size_t j = 0; j < mv.n; ++j) mv.pos[j] = usn_ph_slot(mv.hh[j], mv.d, T.m);
+    const uint4 bk = img_hkey(i, c->img[base + cand.second]);
+    const uint32_t GB = usn_ph_group(usn_ph_h1(bk.x, bk.y, bk.z, bk.w, T.seed), T.shift, T.g);
+    if (GB == G) continue;
+    GroupMove mb;
+    if (!img_group_collect(c, i, GB, nullptr, 0, mb)) continue;
+    mb.avoid = &mv;   // not into the slots G takes (the blocker's among them)
+    if (!img_group_search(c, i, mb, &mv, nullptr)) continue;
+    img_group_commit(c, i, mb);
+    img_group_commit(c, i, mv);
+    c->img_nkeys[i]++;
+    return true;
+  }
+  g_img_fail = i * 10 + 3;
+  return false;
+}
+
+/* key k of table i leaves the image (if it is there) */
+void img_erase(usn_ctx *c, int i, const uint4 &k) {
+  const int64_t at = img_find(c, i, k);
+  if (at < 0) return;
+  const usn_ph_table &T = c->img_t[i];
+  const uint32_t G = usn_ph_group(usn_ph_h1(k.x, k.y, k.z, k.w, T.seed), T.shift, T.g);
+  std::vector<uint32_t> &mem = c->img_groups[i][G];
+  mem.erase(std::find(mem.begin(), mem.end(), (uint32_t)(at - T.slot_off)));
+  c->img[at] = img_empty(i);
+  img_patch(c, (uint32_t)at);
+  c->img_nkeys[i]--;
+}
+
+/* one registry key, brought into the image as build_image would place it
+ * (K1 / K2 slot; U's projection slot and X as proj_keys builds them) */
+bool img_apply_key(usn_ctx *c, const WantKey &k) {
+  const int t = image_table(k);
+  if (t < 0) return true;                        // no frame can hit it: not in the image
+  auto it = c->rules.find(k);
+  const bool present = it != c->rules.end();
+  const uint16_t owner = present ? it->second.owner : 0;
+  const bool nic = present && c->eps[owner].used && c->eps[owner].kind == USN_EP_NIC;
+  const uint4 e = make_uint4(k.dst, k.src, (uint32_t)k.dport | ((uint32_t)k.sport << 16),
+                             usn_key_meta(k.proto, k.present) | (nic ? USN_SLOT_NICOWNER : 0u) |
+                                 ((uint32_t)owner << 16));
+  const uint4 hk = make_uint4(e.x, e.y, e.z, e.w & USN_KEY_META_MASK);
+  if (present) {
+    if (!img_upsert(c, t, hk, e)) return false;
+  } else {
+    img_erase(c, t, hk);
+  }
+  if (!(c->probe_mask & 4u)) return true;
+  const uint32_t has = (k.present & USN_WANT_DPORT) ? 1u : 0u;
+  if (has && usn_u_pidx(k.proto) == 7u) return true;   // never matched (proj_keys skips it)
+  const uint32_t E = usn_u_e(k.proto, has, k.dport);
+  const uint4 uk = make_uint4(k.dst, 0u, E, 0u);
+  const uint32_t code = !present ? USN_U_NONE : nic ? USN_U_NIC : owner;
+  const int64_t at = img_find(c, 2, uk);
+  if (t == 1) {                                  // key2: the projection's K2 owner
+    if (at >= 0) {
+      uint4 u = c->img[at];
+      u.w = E | code << 19;
+      c->img[at] = u;
+      img_patch(c, (uint32_t)at);
+      return true;
+    }
+    if (!present) return true;
+    return img_upsert(c, 2, uk, make_uint4(k.dst, 0u, USN_U_NONE << 16, E | code << 19));
+  }
+  const uint32_t sport = has ? k.sport : 0u;     // key1: inline, or in X
+  if (at < 0) {
+    if (!present) return true;
+    return img_upsert(c, 2, uk, make_uint4(k.dst, k.src, sport | code << 16, E | USN_U_NONE << 19));
+  }
+  uint4 u = c->img[at];
+  const uint32_t o1 = (u.z >> 16) & 0x1FFFu;
+  const bool inline_is_k = o1 != USN_U_NONE && u.y == k.src && (u.z & 0xFFFFu) == sport;
+  if (inline_is_k) {                             // update or empty the inline rule (MORE stays)
+    u.z = (u.z & USN_U_MORE) | (present ? (sport | code << 16) : (USN_U_NONE << 16));
+    if (!present) u.y = 0;
+    c->img[at] = u;
+    img_patch(c, (uint32_t)at);
+    return true;
+  }
+  if (!present) {
+    if (c->img_t[3].m) img_erase(c, 3, hk);
+    return true;
+  }
+  if (c->img_t[3].m && img_find(c, 3, hk) >= 0) return img_upsert(c, 3, hk, e);
+  if (o1 == USN_U_NONE) {                        // the inline place is free
+    u.y = k.src;
+    u.z = (u.z & USN_U_MORE) | sport | code << 16;
+    c->img[at] = u;
+    img_patch(c, (uint32_t)at);
+    return true;
+  }
+  u.z |= USN_U_MORE;
+  c->img[at] = u;
+  img_patch(c, (uint32_t)at);
+  return img_upsert(c, 3, hk, e);                // (X empty at the last build: rebuild)
+}
+
+#define IMG_MAX_DELTA 4096u
+#define IMG_MAX_PATCHES (1u << 16)
+/* the host image brought up to date with the registry: the changed keys in
+ * place, or a full build */
+int refresh_image(usn_ctx *c) {
+  if (c->table_dirty || c->img.empty()) return build_image(c);
+  if (c->img_delta.empty()) return USN_OK;
+  const size_t total = (size_t)c->img_nkeys[0] + c->img_nkeys[1];
+  if (!c->incremental || c->img_delta.size() > IMG_MAX_DELTA + total / 8 ||
+      c->img_patches.size() > IMG_MAX_PATCHES)
+    return build_image(c);
+  if (!c->img_groups_ok) img_groups_build(c);
+  static const bool verbose = std::getenv("USN_PROFILE_HOST") != nullptr;
+  for (const WantKey &k : c->img_delta)
+    if (!img_apply_key(c, k)) {
+      if (verbose)
+        std::fprintf(stderr, "refresh_image: key (table %d, cause %d) not placed in place: rebuild (keys %u %u %u %u)\n",
+                     image_table(k), g_img_fail, c->img_nkeys[0], c->img_nkeys[1], c->img_nkeys[2], c->img_nkeys[3]);
+      return build_image(c);
+    }
+  // the U build condition of build_image, with the counts the keys now have
+  const uint32_t n12 = c->img_nkeys[0] + c->img_nkeys[1];
+  const bool want_proj = c->proj && n12 > 0 && n12 <= USN_U_MAX_KEYS;
+  if (want_proj != ((c->probe_mask & 4u) != 0) ||
+      (n12 > USN_U_MAX_KEYS) != (total > USN_U_MAX_KEYS)) {  // K1/K2 group size changes there
+    if (verbose) std::fprintf(stderr, "refresh_image: U build condition changed: rebuild\n");
+    return build_image(c);
+  }
+  c->img_delta.clear();
+  ++c->table_version;
+  ++c->img_updates;
   return USN_OK;
 }
 
@@ -958,15 +1310,31 @@ void image_probe_u(const usn_ctx *c, uint32_t dst, uint32_t src, uint32_t proto,
 /* the replica's device table at the current image version; no batch still
  * in flight on that device may read the old one */
 int upload_table(usn_ctx *c, Replica &R) {
-  if (c->table_dirty) {
-    const int s = build_image(c);
-    if (s) return s;
-  }
+  { const int s = refresh_image(c); if (s) return s; }
   if (R.table_version == c->table_version) return USN_OK;
   StageClock clk("upload_table");
   const size_t bytes = c->img.size() * sizeof(uint4);
   HIPCHK(hipSetDevice(R.device));
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipDeviceSynchronize());   // no batch in flight on this device reads the old image
+  if (R.d_table && R.table_version >= c->img_full_version && bytes <= R.d_table_cap) {
+    // the replica holds this build's image at an older version: the units
+    // patched since, in runs of consecutive units
+    std::vector<uint32_t> u;
+    for (const auto &pv : c->img_patches)
+      if (pv.first > R.table_version) u.push_back(pv.second);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    for (size_t a = 0; a < u.size();) {
+      size_t b = a + 1;
+      while (b < u.size() && u[b] == u[b - 1] + 1) ++b;
+      HIPCHK(hipMemcpy(R.d_table + u[a], c->img.data() + u[a], (b - a) * sizeof(uint4),
+                       hipMemcpyHostToDevice));
+      a = b;
+    }
+    R.table_version = c->table_version;
+    clk.mark("patch");
+    return USN_OK;
+  }
   if (bytes > R.d_table_cap) {
     if (R.d_table) HIPCHK(hipFree(R.d_table));
     R.d_table = nullptr;
@@ -1187,21 +1555,25 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 /* ========================================================================== */
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
- * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32.  agg
- * has a row per tile: a launch picks its chunk length (scatter_launch_tc) */
+ * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
+ * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized for one-tile
+ * chunks: a launch picks its chunk length (launch_scatter) */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, agg, tot, total;
+  size_t cnt, agg, tot, gran, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
   g.nbw = (nbins + 7u) & ~7u;
   g.ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
+  const size_t ranges = (g.ntiles + USN_SCAN_RANGE - 1) / USN_SCAN_RANGE;
   size_t o = 0;
   auto a256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
   g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw * 2);
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
+  g.gran = o; o = a256(o + ranges * g.nbw * 8);
+  g.diag = o; o = a256(o + 4);
   g.total = o;
   return g;
 }
@@ -1214,10 +1586,20 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, Scatt
   sb.cnt = *cnt;
   sb.agg = reinterpret_cast<uint32_t *>(p + g.agg);
   sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
+  sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
+  sb.diag = reinterpret_cast<uint32_t *>(p + g.diag);
   sb.n = (uint32_t)n;
   sb.ntiles = g.ntiles;
   sb.tc = tc;
   sb.nchunks = (g.ntiles + tc - 1) / tc;
+  sb.nranges = (sb.nchunks + USN_SCAN_RANGE - 1) / USN_SCAN_RANGE;
+}
+/* the granule and diag part of a batch's scratch (zeroed on its first use
+ * with this geometry) */
+void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes) {
+  const ScatterGeom g = scatter_geom(n, nbins);
+  *p = static_cast<uint8_t *>(scratch) + g.gran;
+  *bytes = g.total - g.gran;
 }
 }  // namespace usn
 
@@ -1401,7 +1783,7 @@ int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
   if (it == c->rules.end()) return 0;
   if (it->second.owner != requester) return USN_EPERM;               // main.rs:612-616
   c->rules.erase(it);
-  c->table_dirty = true;
+  note_change(c, k);
   return 1;
 }
 
@@ -1520,10 +1902,7 @@ int64_t usn_debug_image_probe(usn_ctx *c, int table, uint32_t x, uint32_t y, uin
                               uint32_t meta) {
   if (!c || table < 0 || table > 1) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->table_dirty) {
-    const int s = build_image(c);
-    if (s) return s;
-  }
+  { const int s = refresh_image(c); if (s) return s; }
   return (int64_t)image_probe(c, table, x, y, z, meta);
 }
 
@@ -1535,10 +1914,7 @@ int usn_debug_image_probe_rx(usn_ctx *c, uint32_t dst, uint32_t src, uint32_t pr
                              uint32_t dport, uint32_t sport, uint32_t *out4) {
   if (!c || !out4) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->table_dirty) {
-    const int s = build_image(c);
-    if (s) return s;
-  }
+  { const int s = refresh_image(c); if (s) return s; }
   auto norm = [](uint32_t w) {
     return w == 0 ? 0u : 0x10000u | ((w & USN_SLOT_NICOWNER) ? USN_U_NIC : (w >> 16));
   };
@@ -1557,10 +1933,7 @@ int usn_debug_image_probe_rx(usn_ctx *c, uint32_t dst, uint32_t src, uint32_t pr
 int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   if (!c || !out6) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->table_dirty) {
-    const int s = build_image(c);
-    if (s) return s;
-  }
+  { const int s = refresh_image(c); if (s) return s; }
   for (int i = 0; i < 2; ++i) {   // totals over the shards
     out6[2 * i] = c->img_t[i].m << c->img_t[i].shift;
     out6[2 * i + 1] = c->img_t[i].g << c->img_t[i].shift;
@@ -1570,6 +1943,20 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
   out6[7] = c->img_t[3].m << c->img_t[3].shift;
   out6[8] = c->img_t[2].g << c->img_t[2].shift;
   out6[9] = c->img_t[3].g << c->img_t[3].shift;
+  return USN_OK;
+}
+
+/* Test hook: {full image builds, incremental updates, registry changes not
+ * yet in the image, image version} -- after bringing the image up to date
+ * when `refresh` is set */
+int usn_debug_image_stats(usn_ctx *c, int refresh, uint64_t *out4) {
+  if (!c || !out4) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (refresh) { const int s = refresh_image(c); if (s) return s; }
+  out4[0] = c->img_builds;
+  out4[1] = c->img_updates;
+  out4[2] = c->img_delta.size();
+  out4[3] = c->table_version;
   return USN_OK;
 }
 
@@ -1690,15 +2077,14 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
 
 /* the per-endpoint scatter of `count` classified batches (after their
  * classify / tx launch, or after finalize recounted patched tiles) */
-static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint32_t count,
-                          hipStream_t s) {
+static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
+                          uint32_t count, hipStream_t s) {
   usn::ScatterArgs x;
   std::memset(&x, 0, sizeof x);
   x.count = count;
   x.nbins = as[0].nbins;
   x.nbw = as[0].nbw;
-  x.nblk = (x.nbw + USN_SCAN_BINS_PER_BLOCK - 1) / USN_SCAN_BINS_PER_BLOCK;
-  x.n_ep = as[0].n_ep;
+    x.n_ep = as[0].n_ep;
   x.nbits = as[0].nbits;
   /* chunk length: the shape's (long chunks: contiguous runs per bin), shorter
    * when the launch has too few tiles to give every CU its workgroups */
@@ -1714,6 +2100,9 @@ static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = slow_rank ? USN_SCF_SLOW_RANK : 0u;
+  x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
+  if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
+  x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
@@ -1722,6 +2111,17 @@ static int launch_scatter(const usn::ClassifyArgs *as, const usn_result *r, uint
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;
     x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
+    x.range_base[k + 1] = x.range_base[k] + sb.nranges;
+    // granules of a scratch never used before may hold anything: zero them once
+    // (their place depends on the batch's frames and bins)
+    const uint64_t key = (uint64_t)(uintptr_t)r[k].scratch * 0x9E3779B97F4A7C15ull ^
+                         (as[k].n << 16) ^ x.nbins;
+    if (c->scan_zeroed.insert(key).second) {
+      void *p;
+      size_t bytes;
+      usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
+      HIPCHK(hipMemsetAsync(p, 0, bytes, s));
+    }
   }
   HIPCHK(usn_t512::launch_scatter(x, s));
   return USN_OK;
@@ -1939,7 +2339,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
   if (tx || !c->lists_async) {
-    int st = launch_scatter(m.b, r, count, (hipStream_t)stream);
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream);
     if (st) return st;
   } else {
     // the scatter on the side stream, after this launch; the caller's stream
@@ -1948,7 +2348,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (!R.classified) HIPCHK(hipEventCreateWithFlags(&R.classified, hipEventDisableTiming));
     HIPCHK(hipEventRecord(R.classified, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(R.side, R.classified, 0));
-    int st = launch_scatter(m.b, r, count, R.side);
+    int st = launch_scatter(c, m.b, r, count, R.side);
     if (st) return st;
     for (uint32_t k = 0; k < count; ++k) {
       usn_ctx::ListsEv &le = c->lists_ev[r[k].decisions];
@@ -2386,7 +2786,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     ClassifyArgs a;
     fill_args(c, R, b, r, a);
     HIPCHK(usn::launch_recount(a, (uint32_t)(h / USN_TILE), ntiles, s));
-    st = launch_scatter(&a, r, 1, s);
+    st = launch_scatter(c, &a, r, 1, s);
     if (st) return st;
     usn_summary o = sum;
     o.flags |= USN_S_COUT;
@@ -2556,7 +2956,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     t = e;
   }
   if (any) {
-    st = launch_scatter(&a, r, 1, s);
+    st = launch_scatter(c, &a, r, 1, s);
     if (st) return st;
   }
   /* carried-out cache: authoritative from now on */
@@ -2581,7 +2981,7 @@ int usn_debug_scatter(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t co
   HIPCHK(hipSetDevice(R.device));
   usn::ClassifyArgs as[USN_MAX_MULTI];
   for (uint32_t k = 0; k < count; ++k) fill_args(c, R, &b[k], &r[k], as[k]);
-  return launch_scatter(as, r, count, (hipStream_t)stream);
+  return launch_scatter(c, as, r, count, (hipStream_t)stream);
 }
 
 /* diagnostics: scatter chunks on the selected replica's device whose
