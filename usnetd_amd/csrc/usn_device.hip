@@ -2657,6 +2657,19 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   return hipGetLastError();
 }
 
+/* in-place image update (usn_host.cpp upload_table): n patched 16-byte
+ * units, buf = {n values (uint4)} {n unit indices (u32)} */
+__global__ __launch_bounds__(256) void patch_kernel(uint4 *table, const uint4 *buf, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) table[reinterpret_cast<const uint32_t *>(buf + n)[i]] = buf[i];
+}
+hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, table,
+                     static_cast<const uint4 *>(buf), n);
+  return hipGetLastError();
+}
+
 hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream) {
   if (t1 <= t0) return hipSuccess;
   const size_t lds = lds_core_bytes(a.nbins);

@@ -414,6 +414,8 @@ struct Replica {
   uint4 *d_table = nullptr;
   size_t d_table_cap = 0;
   uint64_t table_version = 0;    // image version on the device (0 = none)
+  void *d_patch = nullptr;       // an image patch: {values}{unit indices}
+  size_t d_patch_cap = 0;
   uint64_t *d_bridge = nullptr;
   size_t d_bridge_cap = 0;
   unsigned long long *d_bridge_set = nullptr;   // open addressing, bit 63 = used
@@ -475,6 +477,7 @@ struct usn_ctx {
   bool img_groups_ok = false;
   std::vector<std::vector<uint32_t>> img_groups[4];
   uint32_t img_nkeys[4] = {0, 0, 0, 0};
+  double img_load01 = USN_PH_LOAD;   // slot load K1 / K2 were built at
   uint64_t img_full_version = 0;
   std::vector<std::pair<uint64_t, uint32_t>> img_patches;
   uint64_t img_builds = 0, img_updates = 0;   // full builds / incremental updates (diagnostics)
@@ -494,6 +497,8 @@ struct usn_ctx {
    * synchronous pageable copies */
   uint8_t *h_stage = nullptr;
   size_t h_stage_cap = 0;
+  uint8_t *h_patch = nullptr;    // pinned: an image patch (upload_table)
+  size_t h_patch_cap = 0;
   uint32_t *h_lists = nullptr;   // pinned: the host lists of a batch with many listed tiles
   size_t h_lists_cap = 0;
   uint4 *h_items = nullptr;      // pinned: a tx batch's learned list
@@ -884,6 +889,19 @@ int build_image(usn_ctx *c) {
     // the keys per displacement there places twice as fast (1.19 M rules: 102
     // -> 49 ms of placement on 8 threads) for twice the (L2-resident) bytes
     const bool global_only = keys[0].size() + keys[1].size() > USN_U_MAX_KEYS;
+    // K1 / K2 at the slot load whose image still fits the classify kernel's
+    // LDS copy (LDS_TABLE_MAX_BYTES, 32 KiB) when the default's would not: c3's
+    // 1024 rules fit at 0.65, not at 0.5 (then read from L2: 47.5 vs 37.0 us
+    // per 512K frames, profiles/r03/r03f_bench.log)
+    double load01 = c->ph_load;
+    {
+      const double n12 = (double)(keys[0].size() + keys[1].size());
+      auto kib = [&](double ld) { return (n12 / ld + n12 / c->ph_group / 8 + 136) * 16 / 1024; };
+      if (kib(load01) > 31.0)
+        for (double ld : {0.55, 0.6, 0.65, 0.7})
+          if (ld > load01 && kib(ld) <= 31.0) { load01 = ld; break; }
+    }
+    c->img_load01 = load01;
     auto one = [&](uint32_t i, uint32_t threads) {
       const uint4 empty = i == 2 ? make_uint4(0, 0, 0, USN_U_EMPTY_W) : make_uint4(0, 0, 0, 0);
       // U and X in shards of up to 16K keys: placed in parallel (an AddMatch
@@ -891,7 +909,8 @@ int build_image(usn_ctx *c) {
       const uint32_t shard_keys = i >= 2 ? 16384u : USN_PH_SHARD_KEYS;
       const uint32_t grp0 = (global_only && i < 2) ? std::min(c->ph_group, 5u) : c->ph_group;
       for (uint32_t grp = grp0;; grp /= 2) {   // large groups may not place: smaller ones do
-        if (ph_build(keys[i], t[i], slots[i], disp[i], c->ph_load, grp, threads, empty, shard_keys)) {
+        if (ph_build(keys[i], t[i], slots[i], disp[i], i < 2 ? load01 : c->ph_load, grp, threads, empty,
+                     shard_keys)) {
           placed[i] = true;
           break;
         }
@@ -1108,7 +1127,8 @@ bool img_upsert(usn_ctx *c, int i, const uint4 &k, const uint4 &e) {
     return true;
   }
   const usn_ph_table &T = c->img_t[i];
-  if (!T.m || c->img_nkeys[i] + 1 > IMG_MAX_LOAD * (double)((size_t)T.m << T.shift)) {
+  const double max_load = std::max(IMG_MAX_LOAD, (i < 2 ? c->img_load01 : c->ph_load) + 0.05);
+  if (!T.m || c->img_nkeys[i] + 1 > max_load * (double)((size_t)T.m << T.shift)) {
     g_img_fail = i * 10 + 1;
     return false;
   }
@@ -1319,18 +1339,31 @@ int upload_table(usn_ctx *c, Replica &R) {
   if (R.d_table && R.table_version >= c->img_full_version && bytes <= R.d_table_cap) {
     // the replica holds this build's image at an older version: the units
     // patched since, in runs of consecutive units
+    // patched units, then one copy of {values}{indices} and one patch launch
     std::vector<uint32_t> u;
     for (const auto &pv : c->img_patches)
       if (pv.first > R.table_version) u.push_back(pv.second);
     std::sort(u.begin(), u.end());
     u.erase(std::unique(u.begin(), u.end()), u.end());
-    for (size_t a = 0; a < u.size();) {
-      size_t b = a + 1;
-      while (b < u.size() && u[b] == u[b - 1] + 1) ++b;
-      HIPCHK(hipMemcpy(R.d_table + u[a], c->img.data() + u[a], (b - a) * sizeof(uint4),
-                       hipMemcpyHostToDevice));
-      a = b;
+    const size_t pb = u.size() * (sizeof(uint4) + 4);
+    if (pb > c->h_patch_cap) {
+      if (c->h_patch) HIPCHK(hipHostFree(c->h_patch));
+      c->h_patch = nullptr;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_patch), pb, hipHostMallocDefault));
+      c->h_patch_cap = pb;
     }
+    if (pb > R.d_patch_cap) {
+      if (R.d_patch) HIPCHK(hipFree(R.d_patch));
+      R.d_patch = nullptr;
+      HIPCHK(hipMalloc(&R.d_patch, pb));
+      R.d_patch_cap = pb;
+    }
+    uint4 *hv = reinterpret_cast<uint4 *>(c->h_patch);
+    uint32_t *hi = reinterpret_cast<uint32_t *>(hv + u.size());
+    for (size_t k = 0; k < u.size(); ++k) { hv[k] = c->img[u[k]]; hi[k] = u[k]; }
+    HIPCHK(hipMemcpyAsync(R.d_patch, c->h_patch, pb, hipMemcpyHostToDevice, nullptr));
+    HIPCHK(usn::launch_patch(R.d_table, R.d_patch, (uint32_t)u.size(), nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
     R.table_version = c->table_version;
     clk.mark("patch");
     return USN_OK;
@@ -1694,7 +1727,7 @@ void usn_ctx_destroy(usn_ctx *c) {
   for (Replica &R : c->reps) {
     (void)hipSetDevice(R.device);
     (void)hipDeviceSynchronize();
-    for (void *p : {(void *)R.d_table, (void *)R.d_bridge, (void *)R.d_bridge_set,
+    for (void *p : {(void *)R.d_table, R.d_patch, (void *)R.d_bridge, (void *)R.d_bridge_set,
                     (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
                     (void *)R.counters, (void *)R.listen})
       if (p) (void)hipFree(p);
@@ -1716,6 +1749,7 @@ void usn_ctx_destroy(usn_ctx *c) {
         (void)hipEventDestroy(ch.done[k]);
       }
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_patch) (void)hipHostFree(c->h_patch);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
   if (c->h_items) (void)hipHostFree(c->h_items);
   delete c;

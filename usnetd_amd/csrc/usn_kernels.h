@@ -119,6 +119,8 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
 /* Recount the bin rows and class counts of tiles [t0, t1) from the (patched)
  * decisions (the scatter then runs again). */
 hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
+/* table[idx[k]] = val[k] for the n units of buf = {val[n] (uint4)} {idx[n] (u32)} */
+hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t stream);
 
 /* ---- per-endpoint lists: the device-wide stable scatter ------------------
  * After the classify (or tx) kernel has written each tile's decisions and its
