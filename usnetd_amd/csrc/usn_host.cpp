@@ -378,6 +378,7 @@ struct Ep {
   int kind = 0;
   int for_nic = -1;
   std::vector<Listen> listening;
+  uint64_t listen_ver = 0;   // usn_ctx::listen_gen at the last change of `listening`
   int next_dhcp = -1;
 };
 
@@ -432,11 +433,14 @@ struct Replica {
   uint32_t *counters = nullptr;   // TxArgs::counters
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
+  int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
+  uint64_t listen_ver = 0;
   uint32_t epoch = 0;
   /* usn_set_lists_async: the scatter's stream, ordered after each classify
    * launch by the `classified` event */
   hipStream_t side = nullptr;
   hipEvent_t classified = nullptr;
+  hipEvent_t txstate_ev = nullptr;   // a tx batch's state copies (usn_ctx::h_txstate) landed
 };
 
 struct usn_ctx {
@@ -520,6 +524,13 @@ struct usn_ctx {
    * start), and the result scratches whose granules were zeroed */
   uint32_t scan_epoch = (uint32_t)std::random_device{}();
   std::unordered_set<uint64_t> scan_zeroed;   // (scratch, frames, bins)
+  uint64_t listen_gen = 0;   // Ep::listen_ver source
+  /* a tx batch's summary, tile headers and tx counters, copied to pinned
+   * memory on its stream right after its launch (usn_finalize reads them
+   * after one stream sync) */
+  uint8_t *h_txstate = nullptr;
+  size_t h_txstate_cap = 0;
+  const void *txstate_for = nullptr;   // the result (decisions) whose state it holds
 };
 
 namespace {
@@ -1740,6 +1751,7 @@ void usn_ctx_destroy(usn_ctx *c) {
   for (Replica &R : c->reps) {
     (void)hipSetDevice(R.device);
     if (R.classified) (void)hipEventDestroy(R.classified);
+    if (R.txstate_ev) (void)hipEventDestroy(R.txstate_ev);
     if (R.side) (void)hipStreamDestroy(R.side);
   }
   for (Chain &ch : c->chains)
@@ -1750,6 +1762,7 @@ void usn_ctx_destroy(usn_ctx *c) {
       }
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_patch) (void)hipHostFree(c->h_patch);
+  if (c->h_txstate) (void)hipHostFree(c->h_txstate);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
   if (c->h_items) (void)hipHostFree(c->h_items);
   delete c;
@@ -1769,6 +1782,7 @@ int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
   e.used = true;
   e.kind = kind;
   e.for_nic = for_nic;
+  e.listen_ver = ++c->listen_gen;
   c->n_ep = std::max<uint32_t>(c->n_ep, (uint32_t)id + 1);
   c->chains[id] = Chain();
   return USN_OK;
@@ -1800,6 +1814,7 @@ int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
   if (!e.used) return USN_ENOENT;
   const WantKey k = canon(*w);
   if (c->rules.count(k)) return 0;                                   // main.rs:272-274
+  e.listen_ver = ++c->listen_gen;
   e.listening.push_back(Listen{k.dst, k.proto, (uint8_t)((k.present & USN_WANT_DPORT) ? 1 : 0),
                                k.dport});                            // main.rs:276-279
   if (e.for_nic < 0) return USN_EPERM;                                // main.rs:287-289 panics
@@ -2227,14 +2242,16 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
   return USN_OK;
 }
 
-/* S.listening as {dst, proto | has_port << 8 | port << 16} words on the device */
-static int tx_listen(Replica &T, const Ep &S, uint32_t &n_listen) {
+/* S.listening as {dst, proto | has_port << 8 | port << 16} words on the
+ * device (uploaded when they changed since this replica's last tx batch) */
+static int tx_listen(Replica &T, int src, const Ep &S, uint32_t &n_listen) {
+  n_listen = (uint32_t)S.listening.size();
+  if (T.listen_src == src && T.listen_ver == S.listen_ver) return USN_OK;
   std::vector<uint32_t> v;
   for (const Listen &l : S.listening) {
     v.push_back(l.dst);
     v.push_back((uint32_t)l.proto | ((uint32_t)l.has_port << 8) | ((uint32_t)l.port << 16));
   }
-  n_listen = (uint32_t)S.listening.size();
   if (v.empty()) return USN_OK;
   if (v.size() * 4 > T.listen_cap) {
     if (T.listen) HIPCHK(hipFree(T.listen));
@@ -2243,6 +2260,8 @@ static int tx_listen(Replica &T, const Ep &S, uint32_t &n_listen) {
     T.listen_cap = v.size() * 4;
   }
   HIPCHK(hipMemcpy(T.listen, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  T.listen_src = src;
+  T.listen_ver = S.listen_ver;
   return USN_OK;
 }
 
@@ -2337,7 +2356,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
     t.a = m.b[0];
-    st = tx_listen(R, c->eps[tb.src_endpoint], t.n_listen);
+    st = tx_listen(R, tb.src_endpoint, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
     t.aux = R.aux;
     t.macset = R.macset;
@@ -2375,6 +2394,25 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (tx || !c->lists_async) {
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream);
     if (st) return st;
+    if (tx) {   // what usn_finalize reads first, already on its way to the host
+      const size_t tb = (size_t)m.b[0].ntiles * sizeof(usn_tile_hdr);
+      const size_t need = sizeof(usn_summary) + tb + 32;
+      if (need > c->h_txstate_cap) {
+        if (c->h_txstate) HIPCHK(hipHostFree(c->h_txstate));
+        c->h_txstate = nullptr;
+        c->h_txstate_cap = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), need, hipHostMallocDefault));
+        c->h_txstate_cap = need;
+      }
+      hipStream_t ts = (hipStream_t)stream;
+      HIPCHK(hipMemcpyAsync(c->h_txstate, r[0].summary, sizeof(usn_summary), hipMemcpyDeviceToHost, ts));
+      HIPCHK(hipMemcpyAsync(c->h_txstate + sizeof(usn_summary), r[0].tiles, tb, hipMemcpyDeviceToHost, ts));
+      HIPCHK(hipMemcpyAsync(c->h_txstate + sizeof(usn_summary) + tb, R.counters, 32,
+                            hipMemcpyDeviceToHost, ts));
+      if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(R.txstate_ev, ts));
+      c->txstate_for = r[0].decisions;
+    }
   } else {
     // the scatter on the side stream, after this launch; the caller's stream
     // goes on to the next batch (usn_finalize / usn_lists_wait join them)
@@ -2616,7 +2654,15 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[8];
-  {
+  if (c->txstate_for == r->decisions && R.txstate_ev) {   // copied behind the launch
+    HIPCHK(hipEventSynchronize(R.txstate_ev));
+    const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
+    std::memcpy(&sum, c->h_txstate, sizeof sum);
+    th.resize(ntiles);
+    std::memcpy(th.data(), c->h_txstate + sizeof(usn_summary), tb);
+    std::memcpy(cnt, c->h_txstate + sizeof(usn_summary) + tb, 32);
+    c->txstate_for = nullptr;
+  } else {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters);
     if (e) return e;
   }
