@@ -89,6 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--lists-async", type=int, default=0,
                     help="1: per-endpoint lists on the library's side stream (usn_set_lists_async): "
                          "a round's scatter overlaps the next round's classify")
+    ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
+                    help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: ranks join the process group and report, no GPU")
     return ap.parse_args(argv)
@@ -132,7 +134,8 @@ class Run:
     """The rank's rx queues of one config, resident in HBM, and the launches
     of one poll round."""
 
-    def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong, rings_per_launch=0):
+    def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong, rings_per_launch=0,
+                 rotate_bytes=ROTATE_BYTES):
         from usnetd_amd import shard, traffic
         self.L, self.ctx, self.name, self.n = L, ctx, name, n
         P = rings_per_launch or max(1, min(8, LAUNCH_FRAMES // n))   # rings per launch
@@ -176,7 +179,7 @@ class Run:
                     traffic.install_ctx(ctx, cfg)
                     self.nics = [cfg.src] + traffic.extra_nics(cfg, Q - 1, ctx)
                     frame_bytes = n * cfg.stride
-                    R = max(1, -(-ROTATE_BYTES // (frame_bytes * Q)))
+                    R = max(1, -(-rotate_bytes // (frame_bytes * Q)))
                 self.batches.append(_batch(ctx, cfg, self.nics[j]))
                 self.results.append(_result(ctx, n))
                 del cfg
@@ -472,7 +475,7 @@ def main(argv=None):
     joined = joined_ranks(dist, rank, device)   # every rank is in the group, on its device
     n = args.frames or DEFAULT_FRAMES[args.config]
     run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong,
-              args.rings_per_launch)
+              args.rings_per_launch, args.rotate_mib << 20)
     res = measure(run, args, dist, world)
     out = {
         "metric": METRIC,

@@ -1945,7 +1945,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     T = stab;
   }
   if (tile == 0) {   // carried-in cache of this source; counters for phase 2 (all wait for tile 0)
-    if (tid < 3) __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 5 && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
+      __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
       for (int k = 0; k < 6; ++k) {
@@ -2533,9 +2534,31 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     H->class_count[3] = (uint16_t)fl;
     H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
+    if (s_misc[1]) atomicAdd(t.counters + 4, s_misc[1]);   // after phase 2: tile 0 zeroed it
   }
   STAMP(11);
   STAMP_FLUSH_AT(tile);
+}
+
+/* what usn_finalize of a tx batch reads first, gathered by one wave into
+ * host memory behind the batch's kernels: {summary flags, counters[0..4],
+ * bin_off[n_ep .. n_ep + 3]} (the NIC, FLOOD and DROP bins follow the
+ * endpoint bins, so the class totals are differences of bin_off) */
+__global__ __launch_bounds__(64) void txstate_kernel(const usn_summary *sum, const uint32_t *counters,
+                                                     const uint32_t *bin_off, uint32_t n_ep,
+                                                     uint32_t *out) {
+  const uint32_t l = threadIdx.x;
+  uint32_t v = 0;
+  if (l == 0) v = sum->flags;
+  else if (l <= 5) v = __hip_atomic_load((const gu32 *)(counters + l - 1), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  else if (l <= 9) v = bin_off[n_ep + l - 6];
+  if (l < 10) out[l] = v;
+}
+hipError_t launch_txstate(const usn_summary *sum, const uint32_t *counters, const uint32_t *bin_off,
+                          uint32_t n_ep, uint32_t *out, hipStream_t stream) {
+  hipLaunchKernelGGL(txstate_kernel, dim3(1), dim3(64), 0, stream, sum, counters, bin_off, n_ep, out);
+  return hipGetLastError();
 }
 
 static inline size_t table_lds_bytes(uint32_t table_units);
@@ -2685,7 +2708,8 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
  * frame indices grouped by bin, frame order inside a bin) and bin_off:
  *   scan     (range of 64 chunks, block of 64 bins): agg[chunk][bin] = the
  *            bin's frames in the chunks before (exclusive scan over the
- *            batch's chunks), tot = the bin's frames
+ *            batch's chunks); the last range: base = the bin's first place
+ *            in index (bin_off)
  *   scatter  (chunk): the chunk's frames sorted by bin in an LDS stage, then
  *            written out in stage order: a bin's frames of the chunk leave as
  *            one contiguous run of index
@@ -2702,7 +2726,7 @@ __device__ __forceinline__ uint32_t base_of(const uint32_t *base, uint32_t count
 }
 
 #define SCAN_THREADS 256
-static_assert(USN_SCAN_RANGE == 64 && USN_SCAN_BLK == 64, "scan: 16 row groups x 4 chunks, 16 lanes x 4 bins");
+static_assert(USN_SCAN_BLK == 64, "scan: 16 lanes x 4 bins");
 #define SCAN_SPIN_TICKS (200u * 100000u)   /* 200 ms of the 100 MHz real-time clock */
 
 typedef __attribute__((address_space(1))) unsigned long long gu64s;
@@ -2712,17 +2736,19 @@ __device__ __forceinline__ void scan_put(unsigned long long *g, uint32_t epoch, 
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* (range r of a batch's chunks, bin block bb), range-major so that a
+/* (range r of 16 CPT chunks of a batch, bin block bb), range-major so that a
  * workgroup waits only on workgroups dispatched before it:
- *  1. thread (rg, l) sums the count rows of chunks 4rg..4rg+3 of the range
+ *  1. thread (rg, l) sums the count rows of its CPT chunks of the range
  *     for bins 4l..4l+3 of the block (every load in flight together);
  *  2. the block's 16 row groups are scanned in LDS: each chunk's prefix
  *     inside the range, and the range's totals, published as epoch-tagged
  *     granules gran[r][bin];
  *  3. carry = the totals of ranges 0..r-1 (their granules, polled; each
  *     range publishes before it waits, so the wait ends);
- *  4. agg[chunk][bin] = carry + prefix (16-byte stores); the last range
- *     writes tot. */
+ *  4. agg[chunk][bin] = carry + prefix (16-byte stores);
+ *  5. the last range: its bins' totals scanned, plus the totals of the bin
+ *     blocks before (one granule per block): base and bin_off. */
+template <int CPT>   // chunks per thread: a range is 16 * CPT chunks
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   __shared__ uint32_t s_t[16][USN_SCAN_BLK];
   __shared__ uint32_t s_c[4][USN_SCAN_BLK];
@@ -2734,20 +2760,20 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   const uint32_t r = rgl - s.range_base[bi];
   const uint32_t b0 = bb * USN_SCAN_BLK + 4 * l;             // this thread's 4 bins
   const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
-  const uint32_t c0 = r * USN_SCAN_RANGE + rg * 4;          // this thread's 4 chunks
+  const uint32_t c0 = r * 16 * CPT + rg * CPT;              // this thread's CPT chunks
   // 1.
-  uint2 v[4][8];
+  uint2 v[CPT][8];
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j)
+  for (uint32_t j = 0; j < CPT; ++j)
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) {
       const uint32_t t = (c0 + j) * s.tc + w;
       const bool ok = binok && w < s.tc && t < B.ntiles;
       v[j][w] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
     }
-  uint32_t ex[4][4], tot[4] = {0, 0, 0, 0};
+  uint32_t ex[CPT][4], tot[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
+  for (uint32_t j = 0; j < CPT; ++j) {
     uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) {
@@ -2815,32 +2841,60 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   }
   if (binok) {
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
+    for (uint32_t j = 0; j < CPT; ++j)
       if (c0 + j < B.nchunks)
         *reinterpret_cast<uint4 *>(B.agg + (size_t)(c0 + j) * s.nbw + b0) =
             make_uint4(carry[0] + ex[j][0], carry[1] + ex[j][1], carry[2] + ex[j][2], carry[3] + ex[j][3]);
   }
-  if (r + 1 == B.nranges && tid < USN_SCAN_BLK && bb * USN_SCAN_BLK + tid < s.nbw)
-    B.tot[bb * USN_SCAN_BLK + tid] = s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid];
+  if (r + 1 != B.nranges) return;
+  // 5. (the batch's last range) bin bases: the block's totals scanned, the
+  // blocks before handed on through one granule each; bin_off
+  __shared__ uint32_t s_base[USN_SCAN_BLK], s_blk;
+  const uint32_t bin = bb * USN_SCAN_BLK + tid;
+  if (tid == 0) s_blk = 0;
+  if (tid < USN_SCAN_BLK) {
+    const uint32_t tv = bin < s.nbw ? s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid] : 0u;
+    const uint32_t inc = wave_incl_scan(tv, tid);
+    s_base[tid] = inc - tv;
+    if (tid == USN_SCAN_BLK - 1) scan_put(B.gblk + bb, s.epoch, inc);
+  }
+  __syncthreads();
+  if (tid < bb) {
+    uint64_t t0 = 0;
+    for (uint32_t it = 0;; ++it) {
+      const unsigned long long x =
+          __hip_atomic_load((const gu64s *)(B.gblk + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(x >> 32) == s.epoch) { atomicAdd(&s_blk, (uint32_t)x); break; }
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (it == 0) t0 = now;
+      else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, 1u); break; }   // never seen; lists wrong
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (tid < USN_SCAN_BLK && bin < s.nbw) {
+    const uint32_t base = s_blk + s_base[tid];
+    B.base[bin] = base;
+    if (bin < s.nbins) B.bin_off[bin] = base;
+  }
+  if (bb == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
 }
 
 /* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
  * of the chunk.
  *  1. each wave loads its tile's decisions at once (16 per lane: segment k
  *     of 64 frames is lane + 64k), every wave in flight together;
- *  2. per bin: off[b] = bin base (block scan of the totals) + the chunks
- *     before (agg) - b's start in the chunk (block scan of the chunk's
- *     counts), and each wave's cursor cur[w][b] = b's start in the chunk +
- *     b's frames in the chunk's tiles before w (the classify kernel's count
- *     rows) -- one barrier;
- *  3. each wave walks its tile's 16 segments in frame order with its own
- *     cursors, no barrier: a frame's rank among the segment's frames of its
- *     bin (bit-sliced ballots) puts it at stage[cur[w][bin] + rank], and the
- *     bin's first lane moves the cursor on: the chunk sorted by (bin, frame)
- *     in LDS -- one barrier;
+ *  2. per bin: off[b] = bin base (the scan's) + the chunks before (agg) -
+ *     b's start in the chunk (block scan of the chunk's counts), and each
+ *     wave's cursor cur[w][b] = b's start in the chunk + b's frames in the
+ *     chunk's tiles before w (the classify kernel's count rows) -- one
+ *     barrier;
+ *  3. each wave ranks its tile's frames with one LDS atomic each on its own
+ *     cursors (below): the chunk sorted by (bin, frame) in LDS -- one
+ *     barrier;
  *  4. the stage is written out in order: index[off[bin] + q], contiguous
  *     runs per bin (one L2 request per run instead of one per frame; c5,
- *     1005 bins: about 8 frames per run).
+ *     1005 bins: about 8 frames per run), and checked to be stably sorted.
  * Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them
  * so that an XCD takes a contiguous run of chunks (cdna_hip_programming.md T1
  * swizzle, bijective). */
@@ -2882,10 +2936,10 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // former leaves the decisions in flight
   const bool pair = s.nbw <= 2 * NTHREADS;
   const bool mine = pair && 2 * tid < s.nbw;
-  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
+  uint2 vb = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
   if (mine) {
-    vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
+    vb = *reinterpret_cast<const uint2 *>(B.base + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
 #pragma unroll
@@ -2907,11 +2961,9 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
     uint32_t total;
-    const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
     const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
     if (mine) {
-      const uint32_t b = 2 * tid;
-      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
+      *reinterpret_cast<uint2 *>(off + 2 * tid) = make_uint2(vb.x + ve.x - pc, vb.y + ve.y - (pc + c0));
       uint32_t s0 = pc, s1 = pc + c0;
 #pragma unroll
       for (uint32_t w = 0; w < TC; ++w) {
@@ -2919,37 +2971,28 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         s0 += rc[w] & 0xFFFFu;
         s1 += rc[w] >> 16;
       }
-      if (c == 0) {
-        if (b <= s.nbins) B.bin_off[b] = pt;                   // pad bins past nbins are empty
-        if (b + 1 <= s.nbins) B.bin_off[b + 1] = pt + vt.x;
-      }
     }
   } else {   // more bins: per-thread contiguous runs of bins, the same sums
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
-    uint32_t st = 0, sc = 0;
+    uint32_t sc = 0;
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      st += B.tot[b];
       for (uint32_t w = 0; w < ntc; ++w) sc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
     }
     uint32_t total;
-    uint32_t pt = block_excl_scan(st, s_scan, &total);
     uint32_t pc = block_excl_scan(sc, s_scan, &total);
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      off[b] = pt + ex[b] - pc;
-      if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
-      pt += B.tot[b];
+      off[b] = B.base[b] + ex[b] - pc;
       for (uint32_t w = 0; w < TC; ++w) {
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
         if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       }
     }
   }
-  if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
   __syncthreads();
   STAMP(1);
   // 3. each wave ranks its tile into the stage: one LDS atomic add per frame
@@ -3038,7 +3081,13 @@ uint32_t scatter_fallbacks() {
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_kernel, dim3(s.range_base[s.count] * s.nbb), dim3(SCAN_THREADS), 0, stream, s);
+  const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
+  switch (s.cpt) {
+    case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
+    case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
+    case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;
+    default: return hipErrorInvalidValue;
+  }
   const size_t lds = scatter_lds(s.nbins, s.tc);
   const dim3 g(chunks), b(NTHREADS);
   switch (s.tc) {

@@ -525,9 +525,9 @@ struct usn_ctx {
   uint32_t scan_epoch = (uint32_t)std::random_device{}();
   std::unordered_set<uint64_t> scan_zeroed;   // (scratch, frames, bins)
   uint64_t listen_gen = 0;   // Ep::listen_ver source
-  /* a tx batch's summary, tile headers and tx counters, copied to pinned
-   * memory on its stream right after its launch (usn_finalize reads them
-   * after one stream sync) */
+  /* a tx batch's summary flags, counters and class totals, written into
+   * host-mapped memory by a one-wave kernel right after its launch
+   * (usn_finalize of a batch that learned nothing reads only these) */
   uint8_t *h_txstate = nullptr;
   size_t h_txstate_cap = 0;
   const void *txstate_for = nullptr;   // the result (decisions) whose state it holds
@@ -1599,44 +1599,46 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 /* ========================================================================== */
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
- * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
- * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized for one-tile
- * chunks: a launch picks its chunk length (launch_scatter) */
+ * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | base[nbw] u32 |
+ * gran[nranges][nbw] u64 | gblk[nbb] u64 | diag u32.  agg and gran are sized
+ * for one-tile chunks: a launch picks its chunk length (launch_scatter) */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, agg, tot, gran, diag, total;
+  size_t cnt, agg, tot, gran, gblk, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
   g.nbw = (nbins + 7u) & ~7u;
   g.ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
-  const size_t ranges = (g.ntiles + USN_SCAN_RANGE - 1) / USN_SCAN_RANGE;
+  const size_t ranges = (g.ntiles + USN_SCAN_RANGE_MIN - 1) / USN_SCAN_RANGE_MIN;
   size_t o = 0;
   auto a256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
   g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw * 2);
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.gran = o; o = a256(o + ranges * g.nbw * 8);
+  g.gblk = o; o = a256(o + (g.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK * 8);
   g.diag = o; o = a256(o + 4);
   g.total = o;
   return g;
 }
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins) { return scatter_geom(n, nbins).total; }
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
-                   uint16_t **cnt) {
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
+                   ScatterBatch &sb, uint16_t **cnt) {
   const ScatterGeom g = scatter_geom(n, nbins);
   uint8_t *p = static_cast<uint8_t *>(scratch);
   *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
   sb.cnt = *cnt;
   sb.agg = reinterpret_cast<uint32_t *>(p + g.agg);
-  sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
+  sb.base = reinterpret_cast<uint32_t *>(p + g.tot);
   sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
+  sb.gblk = reinterpret_cast<unsigned long long *>(p + g.gblk);
   sb.diag = reinterpret_cast<uint32_t *>(p + g.diag);
   sb.n = (uint32_t)n;
   sb.ntiles = g.ntiles;
   sb.tc = tc;
   sb.nchunks = (g.ntiles + tc - 1) / tc;
-  sb.nranges = (sb.nchunks + USN_SCAN_RANGE - 1) / USN_SCAN_RANGE;
+  sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
 }
 /* the granule and diag part of a batch's scratch (zeroed on its first use
  * with this geometry) */
@@ -2119,7 +2121,7 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   a.probe_mask = c->probe_mask;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, sb, &a.cnt);
+  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, 1, sb, &a.cnt);
   a.nbw = (a.nbins + 7u) & ~7u;
   return USN_OK;
 }
@@ -2150,12 +2152,18 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = slow_rank ? USN_SCF_SLOW_RANK : 0u;
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
+  static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
+    const char *e = std::getenv("USN_SCAN_CPT");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
+  }();
+  x.cpt = cpt_knob ? cpt_knob : 4u;
   if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
   x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
-    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, sb, &cnt);
+    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, x.cpt, sb, &cnt);
     sb.decisions = r[k].decisions;
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;
@@ -2394,21 +2402,16 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (tx || !c->lists_async) {
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream);
     if (st) return st;
-    if (tx) {   // what usn_finalize reads first, already on its way to the host
-      const size_t tb = (size_t)m.b[0].ntiles * sizeof(usn_tile_hdr);
-      const size_t need = sizeof(usn_summary) + tb + 32;
-      if (need > c->h_txstate_cap) {
-        if (c->h_txstate) HIPCHK(hipHostFree(c->h_txstate));
-        c->h_txstate = nullptr;
-        c->h_txstate_cap = 0;
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), need, hipHostMallocDefault));
-        c->h_txstate_cap = need;
+    if (tx) {   // what usn_finalize reads first, gathered into host memory behind the launch
+      if (!c->h_txstate) {
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), 64,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        c->h_txstate_cap = 64;
       }
+      uint32_t *dp = nullptr;
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&dp), c->h_txstate, 0));
       hipStream_t ts = (hipStream_t)stream;
-      HIPCHK(hipMemcpyAsync(c->h_txstate, r[0].summary, sizeof(usn_summary), hipMemcpyDeviceToHost, ts));
-      HIPCHK(hipMemcpyAsync(c->h_txstate + sizeof(usn_summary), r[0].tiles, tb, hipMemcpyDeviceToHost, ts));
-      HIPCHK(hipMemcpyAsync(c->h_txstate + sizeof(usn_summary) + tb, R.counters, 32,
-                            hipMemcpyDeviceToHost, ts));
+      HIPCHK(usn::launch_txstate(r[0].summary, R.counters, r[0].bin_off, m.b[0].n_ep, dp, ts));
       if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
       HIPCHK(hipEventRecord(R.txstate_ev, ts));
       c->txstate_for = r[0].decisions;
@@ -2654,15 +2657,27 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[8];
-  if (c->txstate_for == r->decisions && R.txstate_ev) {   // copied behind the launch
+  if (c->txstate_for == r->decisions && R.txstate_ev) {   // gathered behind the launch
     HIPCHK(hipEventSynchronize(R.txstate_ev));
-    const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
-    std::memcpy(&sum, c->h_txstate, sizeof sum);
-    th.resize(ntiles);
-    std::memcpy(th.data(), c->h_txstate + sizeof(usn_summary), tb);
-    std::memcpy(cnt, c->h_txstate + sizeof(usn_summary) + tb, 32);
     c->txstate_for = nullptr;
-  } else {
+    const volatile uint32_t *q = reinterpret_cast<const volatile uint32_t *>(c->h_txstate);
+    uint32_t v[10];
+    for (int k = 0; k < 10; ++k) v[k] = q[k];
+    if (v[1] == 0 && v[2] == 0 && v[4] != R.epoch && v[5] == 0) {
+      // nothing learned, nothing for the host stage, no timeout: the
+      // results are final; class totals from bin_off (EP bins, NIC, FLOOD, DROP)
+      usn_finalize_info fi;
+      std::memset(&fi, 0, sizeof fi);
+      fi.flags = v[0];
+      fi.class_count[USN_CLS_EP] = v[6];
+      fi.class_count[USN_CLS_NIC] = v[7] - v[6];
+      fi.class_count[USN_CLS_FLOOD] = v[8] - v[7];
+      fi.class_count[USN_CLS_DROP] = v[9] - v[8];
+      if (info) *info = fi;
+      return USN_OK;
+    }
+  }
+  {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters);
     if (e) return e;
   }

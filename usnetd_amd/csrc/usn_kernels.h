@@ -98,7 +98,8 @@ struct TxArgs {
   uint4 *learned;             /* items appended by tx_decide: {frame, kind 0 mac | 1 rule},
                                  {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
   uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with
-                                 items, [3] epoch of a batch whose tile waits timed out */
+                                 items, [3] epoch of a batch whose tile waits timed out, [4] frames
+                                 listed for the host stage */
   uint32_t learned_cap;
   const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
   uint32_t bridge_mask;
@@ -110,6 +111,9 @@ struct TxArgs {
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
+/* out[0..9] (host-mapped) = {summary flags, counters[0..4], bin_off[n_ep .. n_ep + 3]} */
+hipError_t launch_txstate(const usn_summary *sum, const uint32_t *counters, const uint32_t *bin_off,
+                          uint32_t n_ep, uint32_t *out, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds);
@@ -125,23 +129,24 @@ hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t s
 /* ---- per-endpoint lists: the device-wide stable scatter ------------------
  * After the classify (or tx) kernel has written each tile's decisions and its
  * row of per-bin frame counts (cnt[tile][bin], u16), two launches:
- *   scan     (range of USN_SCAN_RANGE chunks, block of USN_SCAN_BLK bins):
+ *   scan     (range of 16 x cpt chunks, block of USN_SCAN_BLK bins):
  *            agg[chunk][bin] = frames of the bin in the batch's chunks before
  *            (ranges hand their totals on through epoch-tagged granules),
- *            tot[bin] = the bin's frames
+ *            base[bin] = bin_off[bin] (bin blocks hand on their totals)
  *   scatter  (chunk of tc tiles): one LDS atomic per frame ranks it in the
  *            chunk's bin-sorted LDS stage (verified; ballot ranks as the
  *            fallback); the stage is written out in order, so each bin's
  *            frames of the chunk leave as one contiguous run
  * Stable: bins in order, frames in frame order inside a bin. */
-#define USN_SCAN_RANGE 64u   /* chunks per scan workgroup */
+#define USN_SCAN_RANGE_MIN 16u   /* chunks per scan workgroup: 16 x cpt (1, 2, 4) */
 #define USN_SCAN_BLK 64u     /* bins per scan workgroup */
 struct ScatterBatch {
   const uint32_t *decisions;
   const uint16_t *cnt;      /* [ntiles][nbw] */
   uint32_t *agg;            /* [nchunks][nbw]: frames per bin in the chunks before */
-  uint32_t *tot;            /* [nbw]: frames per bin */
+  uint32_t *base;           /* [nbw]: the bin's first place in index (= bin_off) */
   unsigned long long *gran; /* [nranges][nbw]: {epoch, range total} */
+  unsigned long long *gblk; /* [nbb]: {epoch, the bin block's total} */
   uint32_t *diag;           /* bit 0: a scan wait timed out (the lists are wrong) */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
@@ -156,6 +161,7 @@ struct ScatterArgs {
   uint32_t tc;                              /* the scatter kernel's chunk length for this launch */
   uint32_t flags;                           /* USN_SCF_* */
   uint32_t epoch;                           /* this launch's granule tag (never 0) */
+  uint32_t cpt;                             /* scan: chunks per thread (1, 2, 4) */
 };
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
@@ -179,8 +185,8 @@ inline uint32_t scatter_occupancy(size_t lds) {
 /* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, ScatterBatch &sb,
-                   uint16_t **cnt);
+void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
+                   ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 
 }  // namespace usn
