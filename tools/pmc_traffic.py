@@ -6,11 +6,11 @@ FETCH_SIZE is doubled because on gfx950 it tallies the 128-byte requests of
 coalesced streaming reads at 64 B; the known read volume of a call (64 B
 window + 2 B length per frame) checks the factor (fetch_vs_algorithmic).
 
-One usn_classify_multi call = classify_rx_kernel + the per-endpoint scatter
-(scan_agg_kernel, scan_off_kernel, scatter_kernel): the counters of every
-dispatch of these kernels are summed per kernel name and divided by the
-number of classify dispatches covering `frames` frames (every call of the
-run has that shape).
+One usn_classify_multi call = classify_rx_kernel (or tx_kernel) + the
+per-endpoint scatter (scan_kernel, scatter_kernel; tx: txstate_kernel): the
+counters of every dispatch of these kernels are summed per kernel name and
+divided by the number of classify / tx dispatches covering `frames` frames
+(every call of the run has that shape).
 usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json>"""
 import csv
 import glob
@@ -19,7 +19,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("classify_rx_kernel", "scan_agg_kernel", "scan_off_kernel", "scatter_kernel")
+KERNELS = ("classify_rx_kernel", "tx_kernel", "scan_kernel", "scatter_kernel", "txstate_kernel")
+MAIN = ("classify_rx_kernel", "tx_kernel")
 
 
 def per_kernel(d, counter, frames):
@@ -35,7 +36,7 @@ def per_kernel(d, counter, frames):
             if k is None:
                 continue
             tot[k] += float(r["Counter_Value"])
-            if k == "classify_rx_kernel" and int(r["Grid_Size"]) in (frames // 4, frames // 2):
+            if k in MAIN and int(r["Grid_Size"]) in (frames // 4, frames // 2):
                 calls += 1
     return tot, calls
 
