@@ -2157,7 +2157,15 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     const int v = e ? std::atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
   }();
-  x.cpt = cpt_knob ? cpt_knob : 4u;
+  // chunks per scan thread: 4 (a workgroup per 64 chunks) while that gives
+  // the launch >= 256 workgroups, else fewer (A/B, profiles/r03/r03i: c5 16M
+  // 56.6 / 57.3 / 60.3 us for scan + scatter at 4 / 2 / 1; c2 8M, 19 bins:
+  // 32.1 / 30.4 / 29.4)
+  uint32_t chunks = 0;
+  for (uint32_t k = 0; k < count; ++k) chunks += (as[k].ntiles + tc - 1) / tc;
+  uint32_t cpt = 4;
+  while (cpt > 1 && (chunks / (16 * cpt)) * x.nbb < 256) cpt /= 2;
+  x.cpt = cpt_knob ? cpt_knob : cpt;
   if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
   x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
