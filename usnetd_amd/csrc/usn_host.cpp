@@ -1376,6 +1376,9 @@ int upload_table(usn_ctx *c, Replica &R) {
     HIPCHK(usn::launch_patch(R.d_table, R.d_patch, (uint32_t)u.size(), nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
     R.table_version = c->table_version;
+    bool all = true;   // every replica current: the log starts afresh
+    for (const Replica &Q : c->reps) all &= Q.table_version == c->table_version;
+    if (all) c->img_patches.clear();
     clk.mark("patch");
     return USN_OK;
   }
