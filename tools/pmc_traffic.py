@@ -7,7 +7,7 @@ coalesced streaming reads at 64 B; the known read volume of a call (64 B
 window + 2 B length per frame) checks the factor (fetch_vs_algorithmic).
 
 One usn_classify_multi call = classify_rx_kernel (or tx_kernel) + the
-per-endpoint scatter (scan_kernel, scatter_kernel; tx: txstate_kernel): the
+per-endpoint scatter (scan_kernel, scatter_kernel): the
 counters of every dispatch of these kernels are summed per kernel name and
 divided by the number of classify / tx dispatches covering `frames` frames
 (every call of the run has that shape).

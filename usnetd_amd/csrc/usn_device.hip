@@ -2540,26 +2540,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   STAMP_FLUSH_AT(tile);
 }
 
-/* what usn_finalize of a tx batch reads first, gathered by one wave into
- * host memory behind the batch's kernels: {summary flags, counters[0..4],
- * bin_off[n_ep .. n_ep + 3]} (the NIC, FLOOD and DROP bins follow the
- * endpoint bins, so the class totals are differences of bin_off) */
-__global__ __launch_bounds__(64) void txstate_kernel(const usn_summary *sum, const uint32_t *counters,
-                                                     const uint32_t *bin_off, uint32_t n_ep,
-                                                     uint32_t *out) {
-  const uint32_t l = threadIdx.x;
-  uint32_t v = 0;
-  if (l == 0) v = sum->flags;
-  else if (l <= 5) v = __hip_atomic_load((const gu32 *)(counters + l - 1), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-  else if (l <= 9) v = bin_off[n_ep + l - 6];
-  if (l < 10) out[l] = v;
-}
-hipError_t launch_txstate(const usn_summary *sum, const uint32_t *counters, const uint32_t *bin_off,
-                          uint32_t n_ep, uint32_t *out, hipStream_t stream) {
-  hipLaunchKernelGGL(txstate_kernel, dim3(1), dim3(64), 0, stream, sum, counters, bin_off, n_ep, out);
-  return hipGetLastError();
-}
 
 static inline size_t table_lds_bytes(uint32_t table_units);
 
@@ -2708,8 +2688,7 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
  * frame indices grouped by bin, frame order inside a bin) and bin_off:
  *   scan     (range of 64 chunks, block of 64 bins): agg[chunk][bin] = the
  *            bin's frames in the chunks before (exclusive scan over the
- *            batch's chunks); the last range: base = the bin's first place
- *            in index (bin_off)
+ *            batch's chunks), tot = the bin's frames
  *   scatter  (chunk): the chunk's frames sorted by bin in an LDS stage, then
  *            written out in stage order: a bin's frames of the chunk leave as
  *            one contiguous run of index
@@ -2745,9 +2724,10 @@ __device__ __forceinline__ void scan_put(unsigned long long *g, uint32_t epoch, 
  *     granules gran[r][bin];
  *  3. carry = the totals of ranges 0..r-1 (their granules, polled; each
  *     range publishes before it waits, so the wait ends);
- *  4. agg[chunk][bin] = carry + prefix (16-byte stores);
- *  5. the last range: its bins' totals scanned, plus the totals of the bin
- *     blocks before (one granule per block): base and bin_off. */
+ *  4. agg[chunk][bin] = carry + prefix (16-byte stores); the last range
+ *     writes tot.  (Bin bases here too, handed on between bin blocks, cost
+ *     the scan's last ranges one more round trip: 15.4 against 13.9 us for
+ *     c5, more than the scatter's block scan they saved, profiles/r03.) */
 template <int CPT>   // chunks per thread: a range is 16 * CPT chunks
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   __shared__ uint32_t s_t[16][USN_SCAN_BLK];
@@ -2799,29 +2779,33 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
     s_tot[tid] = run;
     if (bb * USN_SCAN_BLK + tid < s.nbw) scan_put(gran + bb * USN_SCAN_BLK + tid, s.epoch, run);
   }
-  // 3. thread (part, k) sums ranges part, part + 4, ... < r of bin k, four polls in flight
+  // 3. thread (part, k) sums ranges part, part + 4, ... < r of bin k: the
+  // loads of 16 ranges issued together (what is still pending is fixed
+  // before they issue, so none waits for another), then checked
   {
     const uint32_t k = tid & 63, part = tid >> 6, bin = bb * USN_SCAN_BLK + k;
     uint32_t sum = 0;
     if (bin < s.nbw) {
       const unsigned long long *col = B.gran + bin;
       uint64_t t0 = 0;
-      for (uint32_t q = part; q < r; q += 16) {
-        uint32_t got = 0;    // bit u: range q + 4u read
+      for (uint32_t q0 = part; q0 < r; q0 += 64) {
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 16; ++u) pend |= (q0 + 4 * u < r ? 1u : 0u) << u;
         for (uint32_t it = 0;; ++it) {
+          unsigned long long x[16];
 #pragma unroll
-          for (uint32_t u = 0; u < 4; ++u) {
-            const uint32_t rr = q + 4 * u;
-            if (rr < r && !(got & (1u << u))) {
-              const unsigned long long x = __hip_atomic_load((const gu64s *)(col + (size_t)rr * s.nbw),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((uint32_t)(x >> 32) == s.epoch) { sum += (uint32_t)x; got |= 1u << u; }
+          for (uint32_t u = 0; u < 16; ++u)
+            x[u] = ((pend >> u) & 1u) ? __hip_atomic_load((const gu64s *)(col + (size_t)(q0 + 4 * u) * s.nbw),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0ull;
+#pragma unroll
+          for (uint32_t u = 0; u < 16; ++u)
+            if (((pend >> u) & 1u) && (uint32_t)(x[u] >> 32) == s.epoch) {
+              sum += (uint32_t)x[u];
+              pend &= ~(1u << u);
             }
-          }
-          bool done = true;
-#pragma unroll
-          for (uint32_t u = 0; u < 4; ++u) done &= (q + 4 * u >= r) || (got & (1u << u));
-          if (done) break;
+          if (!pend) break;
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (it == 0) t0 = now;
           else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, 1u); break; }   // never seen; lists wrong
@@ -2846,46 +2830,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
         *reinterpret_cast<uint4 *>(B.agg + (size_t)(c0 + j) * s.nbw + b0) =
             make_uint4(carry[0] + ex[j][0], carry[1] + ex[j][1], carry[2] + ex[j][2], carry[3] + ex[j][3]);
   }
-  if (r + 1 != B.nranges) return;
-  // 5. (the batch's last range) bin bases: the block's totals scanned, the
-  // blocks before handed on through one granule each; bin_off
-  __shared__ uint32_t s_base[USN_SCAN_BLK], s_blk;
-  const uint32_t bin = bb * USN_SCAN_BLK + tid;
-  if (tid == 0) s_blk = 0;
-  if (tid < USN_SCAN_BLK) {
-    const uint32_t tv = bin < s.nbw ? s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid] : 0u;
-    const uint32_t inc = wave_incl_scan(tv, tid);
-    s_base[tid] = inc - tv;
-    if (tid == USN_SCAN_BLK - 1) scan_put(B.gblk + bb, s.epoch, inc);
-  }
-  __syncthreads();
-  if (tid < bb) {
-    uint64_t t0 = 0;
-    for (uint32_t it = 0;; ++it) {
-      const unsigned long long x =
-          __hip_atomic_load((const gu64s *)(B.gblk + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)(x >> 32) == s.epoch) { atomicAdd(&s_blk, (uint32_t)x); break; }
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (it == 0) t0 = now;
-      else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, 1u); break; }   // never seen; lists wrong
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  if (tid < USN_SCAN_BLK && bin < s.nbw) {
-    const uint32_t base = s_blk + s_base[tid];
-    B.base[bin] = base;
-    if (bin < s.nbins) B.bin_off[bin] = base;
-  }
-  if (bb == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+  if (r + 1 == B.nranges && tid < USN_SCAN_BLK && bb * USN_SCAN_BLK + tid < s.nbw)
+    B.tot[bb * USN_SCAN_BLK + tid] = s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid];
 }
 
 /* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
  * of the chunk.
  *  1. each wave loads its tile's decisions at once (16 per lane: segment k
  *     of 64 frames is lane + 64k), every wave in flight together;
- *  2. per bin: off[b] = bin base (the scan's) + the chunks before (agg) -
- *     b's start in the chunk (block scan of the chunk's counts), and each
+ *  2. per bin: off[b] = bin base (block scan of the totals) + the chunks
+ *     before (agg) - b's start in the chunk (block scan of the chunk's
+ *     counts), and each
  *     wave's cursor cur[w][b] = b's start in the chunk + b's frames in the
  *     chunk's tiles before w (the classify kernel's count rows) -- one
  *     barrier;
@@ -2936,10 +2891,10 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // former leaves the decisions in flight
   const bool pair = s.nbw <= 2 * NTHREADS;
   const bool mine = pair && 2 * tid < s.nbw;
-  uint2 vb = make_uint2(0, 0), ve = make_uint2(0, 0);
+  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
   if (mine) {
-    vb = *reinterpret_cast<const uint2 *>(B.base + 2 * tid);
+    vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
 #pragma unroll
@@ -2961,9 +2916,11 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
     uint32_t total;
+    const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
     const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
     if (mine) {
-      *reinterpret_cast<uint2 *>(off + 2 * tid) = make_uint2(vb.x + ve.x - pc, vb.y + ve.y - (pc + c0));
+      const uint32_t b = 2 * tid;
+      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
       uint32_t s0 = pc, s1 = pc + c0;
 #pragma unroll
       for (uint32_t w = 0; w < TC; ++w) {
@@ -2971,27 +2928,47 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         s0 += rc[w] & 0xFFFFu;
         s1 += rc[w] >> 16;
       }
+      if (c == 0) {
+        if (b <= s.nbins) B.bin_off[b] = pt;                   // pad bins past nbins are empty
+        if (b + 1 <= s.nbins) B.bin_off[b + 1] = pt + vt.x;
+        if (s.txs_out && bi == 0) {   // tx: the class totals for usn_finalize (host memory)
+          if (b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
+          if (b + 1 >= s.n_ep && b + 1 < s.n_ep + 3) s.txs_out[7 + b - s.n_ep] = pt + vt.x;
+        }
+      }
     }
   } else {   // more bins: per-thread contiguous runs of bins, the same sums
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
-    uint32_t sc = 0;
+    uint32_t st = 0, sc = 0;
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
+      st += B.tot[b];
       for (uint32_t w = 0; w < ntc; ++w) sc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
     }
     uint32_t total;
+    uint32_t pt = block_excl_scan(st, s_scan, &total);
     uint32_t pc = block_excl_scan(sc, s_scan, &total);
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      off[b] = B.base[b] + ex[b] - pc;
+      off[b] = pt + ex[b] - pc;
+      if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
+      if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
+      pt += B.tot[b];
       for (uint32_t w = 0; w < TC; ++w) {
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
         if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       }
     }
+  }
+  if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+  if (c == 0 && bi == 0 && s.txs_out && tid < 6) {   // tx: summary flags, counters[0..4], n
+    uint32_t v = tid == 0 ? s.txs_sum->flags
+                          : __hip_atomic_load(s.txs_counters + tid - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s.txs_out[tid] = v;
+    if (tid == 0) s.txs_out[9] = B.n;
   }
   __syncthreads();
   STAMP(1);

@@ -526,8 +526,8 @@ struct usn_ctx {
   std::unordered_set<uint64_t> scan_zeroed;   // (scratch, frames, bins)
   uint64_t listen_gen = 0;   // Ep::listen_ver source
   /* a tx batch's summary flags, counters and class totals, written into
-   * host-mapped memory by a one-wave kernel right after its launch
-   * (usn_finalize of a batch that learned nothing reads only these) */
+   * host-mapped memory by the scatter's first chunk (usn_finalize of a
+   * batch that learned nothing reads only these) */
   uint8_t *h_txstate = nullptr;
   size_t h_txstate_cap = 0;
   const void *txstate_for = nullptr;   // the result (decisions) whose state it holds
@@ -1602,12 +1602,12 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 /* ========================================================================== */
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
- * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | base[nbw] u32 |
- * gran[nranges][nbw] u64 | gblk[nbb] u64 | diag u32.  agg and gran are sized
+ * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
+ * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized
  * for one-tile chunks: a launch picks its chunk length (launch_scatter) */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, agg, tot, gran, gblk, diag, total;
+  size_t cnt, agg, tot, gran, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
@@ -1620,7 +1620,6 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.gran = o; o = a256(o + ranges * g.nbw * 8);
-  g.gblk = o; o = a256(o + (g.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK * 8);
   g.diag = o; o = a256(o + 4);
   g.total = o;
   return g;
@@ -1633,9 +1632,8 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
   sb.cnt = *cnt;
   sb.agg = reinterpret_cast<uint32_t *>(p + g.agg);
-  sb.base = reinterpret_cast<uint32_t *>(p + g.tot);
+  sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
   sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
-  sb.gblk = reinterpret_cast<unsigned long long *>(p + g.gblk);
   sb.diag = reinterpret_cast<uint32_t *>(p + g.diag);
   sb.n = (uint32_t)n;
   sb.ntiles = g.ntiles;
@@ -2132,7 +2130,8 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
 /* the per-endpoint scatter of `count` classified batches (after their
  * classify / tx launch, or after finalize recounted patched tiles) */
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
-                          uint32_t count, hipStream_t s) {
+                          uint32_t count, hipStream_t s, uint32_t *txs_out = nullptr,
+                          const uint32_t *txs_counters = nullptr) {
   usn::ScatterArgs x;
   std::memset(&x, 0, sizeof x);
   x.count = count;
@@ -2169,6 +2168,9 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   uint32_t cpt = 4;
   while (cpt > 1 && (chunks / (16 * cpt)) * x.nbb < 256) cpt /= 2;
   x.cpt = cpt_knob ? cpt_knob : cpt;
+  x.txs_out = txs_out;
+  x.txs_counters = txs_counters;
+  x.txs_sum = r[0].summary;
   if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
   x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
@@ -2411,20 +2413,20 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
   if (tx || !c->lists_async) {
-    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream);
-    if (st) return st;
-    if (tx) {   // what usn_finalize reads first, gathered into host memory behind the launch
+    uint32_t *txs = nullptr;
+    if (tx) {   // what usn_finalize reads first: written into host memory by the scatter's chunk 0
       if (!c->h_txstate) {
         HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), 64,
                              hipHostMallocMapped | hipHostMallocCoherent));
         c->h_txstate_cap = 64;
       }
-      uint32_t *dp = nullptr;
-      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&dp), c->h_txstate, 0));
-      hipStream_t ts = (hipStream_t)stream;
-      HIPCHK(usn::launch_txstate(r[0].summary, R.counters, r[0].bin_off, m.b[0].n_ep, dp, ts));
+      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&txs), c->h_txstate, 0));
+    }
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
+    if (st) return st;
+    if (tx) {
       if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(R.txstate_ev, ts));
+      HIPCHK(hipEventRecord(R.txstate_ev, (hipStream_t)stream));
       c->txstate_for = r[0].decisions;
     }
   } else {

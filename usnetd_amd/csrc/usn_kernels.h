@@ -111,9 +111,6 @@ struct TxArgs {
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
-/* out[0..9] (host-mapped) = {summary flags, counters[0..4], bin_off[n_ep .. n_ep + 3]} */
-hipError_t launch_txstate(const usn_summary *sum, const uint32_t *counters, const uint32_t *bin_off,
-                          uint32_t n_ep, uint32_t *out, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds);
@@ -132,7 +129,7 @@ hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t s
  *   scan     (range of 16 x cpt chunks, block of USN_SCAN_BLK bins):
  *            agg[chunk][bin] = frames of the bin in the batch's chunks before
  *            (ranges hand their totals on through epoch-tagged granules),
- *            base[bin] = bin_off[bin] (bin blocks hand on their totals)
+ *            tot[bin] = the bin's frames
  *   scatter  (chunk of tc tiles): one LDS atomic per frame ranks it in the
  *            chunk's bin-sorted LDS stage (verified; ballot ranks as the
  *            fallback); the stage is written out in order, so each bin's
@@ -144,9 +141,8 @@ struct ScatterBatch {
   const uint32_t *decisions;
   const uint16_t *cnt;      /* [ntiles][nbw] */
   uint32_t *agg;            /* [nchunks][nbw]: frames per bin in the chunks before */
-  uint32_t *base;           /* [nbw]: the bin's first place in index (= bin_off) */
+  uint32_t *tot;            /* [nbw]: frames per bin */
   unsigned long long *gran; /* [nranges][nbw]: {epoch, range total} */
-  unsigned long long *gblk; /* [nbb]: {epoch, the bin block's total} */
   uint32_t *diag;           /* bit 0: a scan wait timed out (the lists are wrong) */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
@@ -162,6 +158,11 @@ struct ScatterArgs {
   uint32_t flags;                           /* USN_SCF_* */
   uint32_t epoch;                           /* this launch's granule tag (never 0) */
   uint32_t cpt;                             /* scan: chunks per thread (1, 2, 4) */
+  /* tx: chunk 0 of batch 0 also writes {summary flags, counters[0..4],
+   * bin_off[n_ep .. n_ep + 3]} into host-mapped memory (usn_finalize) */
+  uint32_t *txs_out;
+  const uint32_t *txs_counters;
+  const usn_summary *txs_sum;
 };
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
