@@ -328,11 +328,11 @@ def measure(run, args, dist, world):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": None,
-        "kernel": "classify_rx_kernel + per-endpoint scatter (scan_agg, scan_off, scatter_kernel)",
+        "kernel": "classify_rx_kernel + per-endpoint scatter (scan_kernel, scatter_kernel)",
         "kernel_us_median": round(kern_ms * 1e3, 3) if kern_ms else None,
         "frames_per_launch": probe_frames,
         "algo_bytes_per_frame": ALGO_BYTES,
-        "achieved_basis": "algorithmic bytes of one usn_classify_multi call (its four kernels) / "
+        "achieved_basis": "algorithmic bytes of one usn_classify_multi call (its three kernels) / "
                           "its median duration (HIP events on its stream, calls serialised on one "
                           "stream)",
         # the timed region (launches overlapping on the streams): per GPU,

@@ -2144,9 +2144,18 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   const usn::ScatterShape sh = usn::scatter_shape(x.nbins);
   uint32_t launch_tiles = 0;
   for (uint32_t k = 0; k < count; ++k) launch_tiles += as[k].ntiles;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int cus = 256;   // the replica's CUs, queried once
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      for (Replica &R : c->reps)
+        if (R.device == dev) {
+          if (!R.n_cu) (void)hipDeviceGetAttribute(&R.n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+          if (R.n_cu > 0) cus = R.n_cu;
+          break;
+        }
+    }
+  }
   const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
   uint32_t tc = sh.tc;
   while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
@@ -2461,8 +2470,10 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     ch.tiles = r[k].tiles;
     ch.ntiles = m.b[k].ntiles;
     ch.summary = r[k].summary;
-    if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
-    HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
+    if (c->reps.size() > 1) {   // only a move to another replica reads the chain on the host
+      if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
+      HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
+    }
     c->batch_rep[r[k].decisions] = rep;
   }
   return USN_OK;
