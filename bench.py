@@ -225,6 +225,7 @@ class Run:
             ctx.wait_event(x, self.ev0)
         for i in range(steps):
             self.step(i)
+        self.enqueue_s = time.perf_counter() - t0     # host time to enqueue the steps
         for x, ej in zip(self.streams[1:], self.joins[1:]):
             ctx.record(ej, x)
             ctx.wait_event(main, ej)
@@ -354,6 +355,8 @@ def measure(run, args, dist, world):
         "value": round(frames / elapsed / 1e6, 2),
         "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
         "event_ms_per_step": round(ev_ms / args.steps, 5),
+        # the host's own time to enqueue a step's calls (close to ms_per_step: host-bound)
+        "enqueue_ms_per_step": round(run.enqueue_s * 1e3 / args.steps, 5),
         "frames_per_step_per_gpu": run.frames_per_step(),
         "host_stage_frames": int(host_frames),
         "summary_flags": int(flags),
@@ -500,6 +503,7 @@ def main(argv=None):
             "parallelism": "replicas%d" % world,
             "rank_devices": [d for _, d in joined],
             "event_ms_per_step": res["event_ms_per_step"],
+            "enqueue_ms_per_step": res["enqueue_ms_per_step"],
             "lists_async": bool(args.lists_async),
             "untimed_ramp_steps": 2 * args.ramp,
             "frames_per_step_per_gpu": res["frames_per_step_per_gpu"],

@@ -2891,9 +2891,10 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // former leaves the decisions in flight
   const bool pair = s.nbw <= 2 * NTHREADS;
   const bool mine = pair && 2 * tid < s.nbw;
+  const bool noscan = (s.flags & USN_SCF_NOSCAN) != 0;   // one chunk per batch: its counts are the batch's
   uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
-  if (mine) {
+  if (mine && !noscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
@@ -2915,6 +2916,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
+    if (noscan) vt = make_uint2(c0, c1);
     uint32_t total;
     const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
     const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
@@ -2944,8 +2946,10 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      st += B.tot[b];
-      for (uint32_t w = 0; w < ntc; ++w) sc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
+      uint32_t cb = 0;
+      for (uint32_t w = 0; w < ntc; ++w) cb += B.cnt[(size_t)(t0 + w) * s.nbw + b];
+      sc += cb;
+      st += noscan ? cb : B.tot[b];
     }
     uint32_t total;
     uint32_t pt = block_excl_scan(st, s_scan, &total);
@@ -2953,10 +2957,14 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
-      off[b] = pt + ex[b] - pc;
+      off[b] = pt + (noscan ? 0u : ex[b]) - pc;
       if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
       if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
-      pt += B.tot[b];
+      if (noscan) {
+        for (uint32_t w = 0; w < ntc; ++w) pt += B.cnt[(size_t)(t0 + w) * s.nbw + b];
+      } else {
+        pt += B.tot[b];
+      }
       for (uint32_t w = 0; w < TC; ++w) {
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
         if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
@@ -3059,7 +3067,7 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  switch (s.cpt) {
+  if (!(s.flags & USN_SCF_NOSCAN)) switch (s.cpt) {
     case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
     case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
     case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;

@@ -2157,11 +2157,16 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     }
   }
   const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
-  uint32_t tc = sh.tc;
-  while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
+  uint32_t tc = sh.tc, max_tiles = 0;
+  for (uint32_t k = 0; k < count; ++k) max_tiles = std::max(max_tiles, as[k].ntiles);
+  // batches of at most one chunk each (a daemon's drained rings): no scan
+  // launch, the scatter's one chunk per batch has the whole batch
+  const bool noscan = max_tiles <= sh.tc;
+  if (!noscan)
+    while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  x.flags = slow_rank ? USN_SCF_SLOW_RANK : 0u;
+  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = std::getenv("USN_SCAN_CPT");

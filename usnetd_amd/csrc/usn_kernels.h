@@ -164,6 +164,8 @@ struct ScatterArgs {
   const uint32_t *txs_counters;
   const usn_summary *txs_sum;
 };
+#define USN_SCF_NOSCAN 2u      /* every batch is one chunk: no scan launch; the chunk's own counts
+                                  are the batch's (agg = 0, tot = the chunk's sums) */
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
