@@ -2976,7 +2976,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     uint32_t v = tid == 0 ? s.txs_sum->flags
                           : __hip_atomic_load(s.txs_counters + tid - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s.txs_out[tid] = v;
-    if (tid == 0) s.txs_out[9] = B.n;
+    if (tid == 0) { s.txs_out[9] = B.n; s.txs_out[10] = *B.diag; }
   }
   __syncthreads();
   STAMP(1);

@@ -1641,6 +1641,10 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.nchunks = (g.ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
 }
+/* the scan's diag word of a batch's scratch (bit 0: a wait timed out) */
+uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
+  return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(n, nbins).diag);
+}
 /* the granule and diag part of a batch's scratch (zeroed on its first use
  * with this geometry) */
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes) {
@@ -2573,11 +2577,21 @@ bool retains(uint32_t d) {
  * listed tile, or one bulk copy of the whole area when many tiles list frames */
 /* summary + tile headers (+ the tx counters when cnt) of a classified batch,
  * through the context's pinned staging buffer on stream s */
+/* a scan wait of the batch's lists timed out (never seen; the kernel gave up
+ * after 200 ms): report it once, loudly */
+int lists_failed(uint32_t diag, uint32_t *d_diag, hipStream_t s) {
+  if (!diag) return USN_OK;
+  HIPCHK(hipMemsetAsync(d_diag, 0, 4, s));
+  HIPCHK(hipStreamSynchronize(s));
+  g_last_hip = (int)hipErrorLaunchTimeOut;
+  return USN_EHIP;
+}
+
 int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
                       usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
-                      const uint32_t *d_counters = nullptr) {
+                      const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
-  const size_t need = sizeof(usn_summary) + tb + 32;
+  const size_t need = sizeof(usn_summary) + tb + 32 + 4;
   if (need > c->h_stage_cap) {
     if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
     c->h_stage = nullptr;
@@ -2591,11 +2605,17 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   if (tb) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary), r->tiles, tb, hipMemcpyDeviceToHost, s));
   if (cnt)
     HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, 32, hipMemcpyDeviceToHost, s));
+  if (d_diag) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb + 32, d_diag, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   std::memcpy(&sum, p, sizeof sum);
   th.resize(ntiles);
   if (tb) std::memcpy(th.data(), p + sizeof(usn_summary), tb);
   if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, 32);
+  if (d_diag) {
+    uint32_t dg;
+    std::memcpy(&dg, p + sizeof(usn_summary) + tb + 32, 4);
+    return lists_failed(dg, d_diag, s);
+  }
   return USN_OK;
 }
 
@@ -2690,8 +2710,9 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     HIPCHK(hipEventSynchronize(R.txstate_ev));
     c->txstate_for = nullptr;
     const volatile uint32_t *q = reinterpret_cast<const volatile uint32_t *>(c->h_txstate);
-    uint32_t v[10];
-    for (int k = 0; k < 10; ++k) v[k] = q[k];
+    uint32_t v[11];
+    for (int k = 0; k < 11; ++k) v[k] = q[k];
+    { const int e = lists_failed(v[10], usn::scatter_diag(r->scratch, n, c->n_ep + 3), s); if (e) return e; }
     if (v[1] == 0 && v[2] == 0 && v[4] != R.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
       // results are final; class totals from bin_off (EP bins, NIC, FLOOD, DROP)
@@ -2707,7 +2728,8 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     }
   }
   {
-    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters);
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters,
+                                    usn::scatter_diag(r->scratch, n, c->n_ep + 3));
     if (e) return e;
   }
   // a tile wait of the kernel timed out (counters[3] = this epoch): the whole
@@ -2968,7 +2990,8 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   {
-    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr);
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr,
+                                    usn::scatter_diag(r->scratch, b->n, c->n_ep + 3));
     if (e) return e;
   }
   usn_finalize_info fi;

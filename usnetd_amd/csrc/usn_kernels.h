@@ -159,7 +159,8 @@ struct ScatterArgs {
   uint32_t epoch;                           /* this launch's granule tag (never 0) */
   uint32_t cpt;                             /* scan: chunks per thread (1, 2, 4) */
   /* tx: chunk 0 of batch 0 also writes {summary flags, counters[0..4],
-   * bin_off[n_ep .. n_ep + 3]} into host-mapped memory (usn_finalize) */
+   * bin_off[n_ep .. n_ep + 3], the scan's diag} into host-mapped memory
+   * (usn_finalize) */
   uint32_t *txs_out;
   const uint32_t *txs_counters;
   const usn_summary *txs_sum;
@@ -191,6 +192,7 @@ size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
 void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
                    ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
+uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
 
 }  // namespace usn
 
