@@ -1,0 +1,3 @@
+# round-3 session: kernel breakdown of the bench (all configs) and of the tx rings
+bash tools/gpu.sh r03n rocprof || exit 1
+TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh r03n txprof
