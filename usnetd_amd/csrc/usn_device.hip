@@ -2858,6 +2858,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
 #endif
 /* chunks that took step 5 (usn_debug_scatter_fallbacks) */
 __device__ uint32_t usn_scatter_fallbacks = 0;
+#ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
+#define USN_SC_GROUP 1
+#endif
 #ifndef USN_ABL_SC   /* A/B only: 4 no rank walk, 5 no write-out (wrong results) */
 #define USN_ABL_SC 0
 #endif
@@ -3010,7 +3013,31 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // disagree with the decisions, or an A/B build that skips a phase, cannot
   // write past index), checking that each bin's run is in frame order
   bool unsorted = false;
-  for (uint32_t q = tid; q < nf; q += NTHREADS) {
+  uint32_t q0 = 0;
+  if (USN_ABL_SC != 4 && USN_SC_GROUP) {
+    // groups of 8 entries per thread: every stage read of the group, then
+    // every offset read, then the stores (the LDS round trips overlap)
+    constexpr uint32_t G = 8;
+    for (; q0 + G * NTHREADS <= nf; q0 += G * NTHREADS) {
+      uint32_t e[G], p[G], o[G];
+#pragma unroll
+      for (uint32_t j = 0; j < G; ++j) {
+        const uint32_t q = q0 + j * NTHREADS + tid;
+        e[j] = stage[q];
+        p[j] = q ? stage[q - 1] : 0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < G; ++j) o[j] = off[min(e[j] >> 16, s.nbw - 1u)];
+#pragma unroll
+      for (uint32_t j = 0; j < G; ++j) {
+        const uint32_t q = q0 + j * NTHREADS + tid;
+        const uint32_t pos = o[j] + q;
+        if (pos < B.n) B.index[pos] = (uint32_t)first + (e[j] & 0xFFFFu);
+        unsorted |= q && (p[j] >> 16) == (e[j] >> 16) && (p[j] & 0xFFFFu) >= (e[j] & 0xFFFFu);
+      }
+    }
+  }
+  for (uint32_t q = q0 + tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
     const uint32_t b = min(e >> 16, s.nbw - 1u);
     const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
