@@ -555,7 +555,15 @@ int image_table(const WantKey &k) {
 /* a registry key whose rule was added, removed or changed: the image is
  * brought up to date before the next batch (refresh_image) */
 void note_change(usn_ctx *c, const WantKey &k) {
-  if (!c->table_dirty) c->img_delta.push_back(k);
+  if (c->table_dirty) return;
+  c->img_delta.push_back(k);
+  // more changes than refresh_image would apply in place (or a registry-only
+  // context that never refreshes): the next refresh rebuilds; stop queueing
+  if (c->img_delta.size() > 4096u + ((size_t)c->img_nkeys[0] + c->img_nkeys[1]) / 8) {
+    c->table_dirty = true;
+    c->img_delta.clear();
+    c->img_delta.shrink_to_fit();
+  }
 }
 
 /* registry insert */
