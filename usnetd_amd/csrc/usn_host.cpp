@@ -2169,11 +2169,16 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     }
   }
   const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
-  uint32_t tc = sh.tc, max_tiles = 0;
+  static const uint32_t tc_knob = [] {   // A/B: USN_SCATTER_TC=1|2|4|8 (at most the shape's)
+    const char *e = std::getenv("USN_SCATTER_TC");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? (uint32_t)v : 0u;
+  }();
+  uint32_t tc = tc_knob ? std::min(tc_knob, sh.tc) : sh.tc, max_tiles = 0;
   for (uint32_t k = 0; k < count; ++k) max_tiles = std::max(max_tiles, as[k].ntiles);
   // batches of at most one chunk each (a daemon's drained rings): no scan
   // launch, the scatter's one chunk per batch has the whole batch
-  const bool noscan = max_tiles <= sh.tc;
+  const bool noscan = max_tiles <= tc;
   if (!noscan)
     while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
