@@ -233,7 +233,8 @@ int usn_endpoint_remove(usn_ctx *ctx, uint16_t id);
 
 /* add_listening_match (main.rs:266-298): 1 inserted, 0 key exists ("ER"),
  * USN_EPERM owner is a NIC (the reference panics). Clears the owner's NIC
- * decision cache and records the listening triple. */
+ * decision cache and records the listening triple.  The device image takes
+ * the key in place before the next classify (a few slots, not a rebuild). */
 int usn_add_match(usn_ctx *ctx, const usn_want *w, uint16_t owner, int sticky);
 /* act_on RemoveMatch (main.rs:608-625): 1 removed, 0 absent, USN_EPERM if
  * requester is not the owner.  Does NOT clear any cache (as the reference). */
@@ -311,7 +312,10 @@ int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
  * frame order and patches decisions and the per-endpoint lists on the device.  Must be called
  * before the next usn_classify of the same source whenever the summary has
- * n_host > 0 or flags != 0; calling it always is allowed. */
+ * n_host > 0 or flags != 0; calling it always is allowed.  USN_EHIP with
+ * usn_last_hip_error() == hipErrorLaunchTimeOut (702): the device gave up
+ * waiting inside the lists' scan (bounded at 200 ms; never observed) and this
+ * batch's index / bin_off are not valid. */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
                  usn_finalize_info *info);
 
