@@ -1,0 +1,95 @@
+#!/bin/bash
+# Round-3 GPU sessions (each a sequence of tools/gpu.sh steps):
+#   bash tools/r03.sh <session>   output under gpurun_out/<session>/
+set -o pipefail
+S=${1:?session}
+case $S in
+  r03i)
+    # round-3 session: parity of the scan/base change and the tx fast path,
+    # scan chunks-per-thread A/B, c3 LDS-DMA A/B, tx timing on rotating buffers
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py tests/test_gpu_parity.py tests/test_gpu_tx.py tests/test_gpu_group.py" bash tools/gpu.sh r03i tests || exit 1
+    for k in 4 2 1; do
+      USN_SCAN_CPT=$k SCB_CFGS="c5 c2" bash tools/gpu.sh r03i scb || exit 1
+      mv gpurun_out/r03i/scb_c5.log gpurun_out/r03i/scb_c5_cpt$k.log
+      mv gpurun_out/r03i/scb_c2.log gpurun_out/r03i/scb_c2_cpt$k.log
+    done
+    TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh r03i txbench || exit 1
+    ABL_CFGS=c3 ABL_VARIANTS="base c3glds" bash tools/gpu.sh r03i abl
+    ;;
+  r03j)
+    # round-3 session: c5 bench launch shapes (one stream; the scatter on the side
+    # stream; two streams of one 2-ring launch each), PMC traffic of c5/c2/c4 and
+    # of the tx call, rocprof of the default bench
+    B="--steps 40 --warmup 5 --no-cpu-baseline --no-extra"
+    O=gpurun_out/r03j
+    BENCH_ARGS="$B" bash tools/gpu.sh r03j bench || exit 1; mv $O/bench.log $O/bench_default.log
+    BENCH_ARGS="$B --lists-async 1" bash tools/gpu.sh r03j bench || exit 1; mv $O/bench.log $O/bench_async.log
+    BENCH_ARGS="$B --streams 2 --queues 4 --rings-per-launch 2" bash tools/gpu.sh r03j bench || exit 1; mv $O/bench.log $O/bench_s2.log
+    PMC_CFGS="c5 c2 c4" bash tools/gpu.sh r03j pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh r03j txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json > $O/pmct_c4tx.log 2>&1
+    bash tools/gpu.sh r03j rocprof
+    ;;
+  r03k)
+    # round-3 session: parity after the scan poll / tx state changes, scatter and tx timing, full bench, c3 stream shapes
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py tests/test_gpu_tx.py tests/test_gpu_parity.py" bash tools/gpu.sh r03k tests || exit 1
+    SCB_CFGS="c5 c2" bash tools/gpu.sh r03k scb || exit 1
+    TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh r03k txbench || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03k bench || exit 1
+    mv gpurun_out/r03k/bench.log gpurun_out/r03k/bench_full.log
+    BENCH_ARGS="--config c3 --queues 4 --streams 4 --steps 40 --warmup 5 --no-cpu-baseline --no-extra" bash tools/gpu.sh r03k bench || exit 1
+    mv gpurun_out/r03k/bench.log gpurun_out/r03k/bench_c3_s4.log
+    ;;
+  r03l)
+    # round-3 session: bench c5 twice (variance), the HBM streaming floor of the access pattern, group/daemon tests
+    B="--steps 40 --warmup 5 --no-cpu-baseline --no-extra"
+    BENCH_ARGS="$B" bash tools/gpu.sh r03l bench || exit 1; mv gpurun_out/r03l/bench.log gpurun_out/r03l/bench1.log
+    BENCH_ARGS="$B" bash tools/gpu.sh r03l bench || exit 1; mv gpurun_out/r03l/bench.log gpurun_out/r03l/bench2.log
+    timeout -k 10 120 build/hbm_floor 8388608 50 > gpurun_out/r03l/hbm_floor.log 2>&1 || exit 1
+    TESTS="tests/test_gpu_group.py tests/test_daemon_gpu.py tests/test_gpu_multiproc.py tests/test_gpu_bench.py" bash tools/gpu.sh r03l tests
+    ;;
+  r03m)
+    # round-3 session: the whole GPU suite (noscan path for small batches), smoke, full bench
+    bash tools/gpu.sh r03m tests || exit 1
+    bash tools/gpu.sh r03m smoke || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03m bench
+    ;;
+  r03n)
+    # round-3 session: kernel breakdown of the bench (all configs) and of the tx
+    # rings; A/B of the scatter's grouped write-out
+    SCB_CFGS="c5 c2" SCB_VARIANTS="base scg0" bash tools/gpu.sh r03n scb || exit 1
+    bash tools/gpu.sh r03n rocprof || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh r03n txprof
+    ;;
+  r03o)
+    # round-3 session: scan chunks-per-thread A/B after the poll change; PMC traffic of the final kernels
+    O=gpurun_out/r03o
+    for k in 4 2; do
+      USN_SCAN_CPT=$k SCB_CFGS="c5" bash tools/gpu.sh r03o scb || exit 1
+      mv $O/scb_c5.log $O/scb_c5_cpt$k.log
+    done
+    PMC_CFGS="c5 c2 c4 c3" bash tools/gpu.sh r03o pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh r03o txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json > $O/pmct_c4tx.log 2>&1
+    ;;
+  r03p)
+    # round-3 session: scatter chunk length A/B (c5/c2 through scatter_bench, tx
+    # rings through txbench); c5 calls of 4 and 8 rings
+    O=gpurun_out/r03p
+    mkdir -p $O
+    for k in 8 4; do
+      USN_SCATTER_TC=$k SCB_CFGS="c5 c2" bash tools/gpu.sh r03p scb || exit 1
+      mv $O/scb_c5.log $O/scb_c5_tc$k.log; mv $O/scb_c2.log $O/scb_c2_tc$k.log
+    done
+    for k in 1 4 8; do
+      USN_SCATTER_TC=$k TXB_ARGS="1048576 30 1 --rotate 6" bash tools/gpu.sh r03p txbench || exit 1
+      mv $O/txbench.log $O/txbench_tc$k.log
+    done
+    B="--steps 30 --warmup 5 --no-cpu-baseline --no-extra"
+    for q in 2 4 8; do
+      BENCH_ARGS="$B --queues $q --rings-per-launch $q" bash tools/gpu.sh r03p bench || exit 1
+      mv $O/bench.log $O/bench_q$q.log
+    done
+    ;;
+  *) echo "unknown session $S"; exit 2 ;;
+esac
