@@ -91,5 +91,13 @@ case $S in
       mv $O/bench.log $O/bench_q$q.log
     done
     ;;
+  r03q)
+    # round-3 final check of the tree: the whole GPU suite, smoke, the default
+    # bench line, and a rocprof of the default bench
+    bash tools/gpu.sh r03q tests || exit 1
+    bash tools/gpu.sh r03q smoke || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03q bench || exit 1
+    bash tools/gpu.sh r03q rocprof
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
