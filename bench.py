@@ -365,7 +365,12 @@ def measure(run, args, dist, world):
     }
 
 
-EXTRA_QUEUES = {"c3": 4}   # c3: 4 rx rings of 256K IMIX frames in 2 KiB slots (2 GiB)
+# c3: 8 rx rings of 256K IMIX frames in 2 KiB slots (4 GiB), two calls of 4
+# rings on two streams.  With 4 rings in two calls of 2 the step was bound by
+# the host's enqueue (3 launches per call, ~6 us each): 17-28 Gpkt/s between
+# runs; 8 rings in calls of 4: 29.2, enqueue 0.043 of a 0.072 ms step
+# (profiles/r03/r03r)
+EXTRA_QUEUES = {"c3": 8}
 TX_ROTATE = 6              # c4tx: the ring in 6 device buffers (384 MiB > the 256 MiB Infinity Cache)
 
 

@@ -99,5 +99,20 @@ case $S in
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03q bench || exit 1
     bash tools/gpu.sh r03q rocprof
     ;;
+  r03r)
+    # round-3 session: c3 launch shapes (host-enqueue bound at 2 rings per call on
+    # 2 streams: 17-28 Gpkt/s between runs), HIP API times of the c3 bench
+    O=gpurun_out/r03r
+    mkdir -p $O
+    B="--config c3 --steps 40 --warmup 5 --no-cpu-baseline --no-extra"
+    for v in "4 2 2" "4 4 1" "8 8 1" "8 4 2"; do
+      set -- $v
+      BENCH_ARGS="$B --queues $1 --rings-per-launch $2 --streams $3" bash tools/gpu.sh r03r bench || exit 1
+      mv $O/bench.log $O/bench_q$1_p$2_s$3.log
+    done
+    rm -rf $O/rt
+    timeout -k 10 300 rocprofv3 --runtime-trace --stats --output-format csv -d $O/rt -o run -- \
+      python3 bench.py $B --queues 4 --launch-probe 20 --ramp 20 > $O/rt.log 2>&1 || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
