@@ -75,3 +75,78 @@ def test_scatter_ballot_ranks_forced():
     out = _run({"USN_SCATTER_SLOW_RANK": "1"})
     assert out.strip().endswith("ok")
     assert all(not l.endswith(" 0") for l in out.splitlines()[:-1]), out
+
+
+def _tile_plan(bins_of, rng, n_tiles):
+    """Frame indices of a batch whose tiles hold bins with 254, 255, 256,
+    511, 1020 and 1024 frames, the rest random, each tile shuffled."""
+    from collections import defaultdict
+    by = defaultdict(list)
+    for i, b in enumerate(bins_of):
+        by[int(b)].append(i)
+    big = sorted(by, key=lambda b: -len(by[b]))[:6]
+    allidx = np.arange(bins_of.size)
+    plans = [
+        {big[0]: 1024},
+        {big[0]: 255, big[1]: 256, big[2]: 254},
+        {big[0]: 255, big[1]: 255, big[2]: 255, big[3]: 255},
+        {big[4]: 1020},
+        {big[5]: 511, big[1]: 257},
+    ]
+    tiles = []
+    for t in range(n_tiles):
+        want = plans[t % (len(plans) + 2)] if t % (len(plans) + 2) < len(plans) else {}
+        sel = []
+        for b, k in want.items():
+            sel.append(rng.choice(by[b], size=k, replace=True))
+        rest = 1024 - sum(want.values())
+        if rest:
+            sel.append(rng.choice(allidx, size=rest, replace=True))
+        tile = np.concatenate(sel)
+        rng.shuffle(tile)
+        tiles.append(tile)
+    return np.concatenate(tiles)
+
+
+@pytest.mark.parametrize("name", ["c5", "c2"])
+def test_count_rows_heavy_bins(name):
+    """Tiles whose frames crowd into few bins (a whole tile in one bin; bins
+    at 254-256 frames, the edge of a one-byte count row, measured and
+    rejected in DESIGN.md 6.1): decisions and the per-endpoint lists equal
+    the oracle's.  c5 (1005 bins, a scan over 48 chunks) and c2 (19 bins)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import coracle
+    import katrun
+    from usnetd_amd import lib, traffic
+    coracle.build()
+    base = traffic.config(name, n=1 << 18, seed=77)
+    o = coracle.Oracle()
+    coracle.install_oracle(o, base)
+    d0 = o.forward_batch(base.src, base.frames, base.lens, stride=base.stride)
+    n_ep = max(e[0] for e in base.endpoints) + 1
+    rng = np.random.default_rng(5)
+    idx = _tile_plan(lib.dec_bin(d0, n_ep), rng, 384)
+    st = base.stride
+    rows = np.asarray(base.frames, np.uint8)[: base.n * st].reshape(base.n, st)
+    frames = np.concatenate([rows[idx].reshape(-1), np.zeros(64, np.uint8)])
+    lens = np.asarray(base.lens)[idx]
+    n = idx.size
+    o2 = coracle.Oracle()
+    coracle.install_oracle(o2, base)
+    want = o2.forward_batch(base.src, frames, lens, stride=st)
+    bins = lib.dec_bin(want, n_ep)
+    counts = np.bincount((np.arange(n) // 1024) * (n_ep + 3) + bins)
+    assert (counts == 255).any() and (counts == 1024).any() and (counts == 256).any()
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, base)
+    s = ctx.stream()
+    b = lib.DeviceBatch(ctx, frames, lens, base.src, stride=st)
+    r = lib.DeviceResult(ctx, n)
+    ctx.classify(b, r, s)
+    ctx.finalize(b, r, s)
+    got = r.decisions()
+    assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK)
+    off = r.bin_off()
+    assert np.array_equal(np.diff(off.astype(np.int64)), np.bincount(bins, minlength=n_ep + 3))
+    assert np.array_equal(r.index(n), np.argsort(bins, kind="stable").astype(np.uint32))
+    b.free(); r.free(); ctx.close()

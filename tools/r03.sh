@@ -114,5 +114,25 @@ case $S in
     timeout -k 10 300 rocprofv3 --runtime-trace --stats --output-format csv -d $O/rt -o run -- \
       python3 bench.py $B --queues 4 --launch-probe 20 --ramp 20 > $O/rt.log 2>&1 || exit 1
     ;;
+  r03s)
+    # round-3 session: u8 count rows (255 escapes to a u16 row): parity incl.
+    # the escape cases, scan + scatter timing, the default bench
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py tests/test_gpu_parity.py tests/test_gpu_tx.py" bash tools/gpu.sh r03s tests || exit 1
+    SCB_CFGS="c5 c2" bash tools/gpu.sh r03s scb || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03s bench
+    ;;
+  r03t)
+    # round-3 session: A/B of the u8 count rows against the u16 ones (build/abl/u16 =
+    # the tree before them), whole calls interleaved in one process, and scan +
+    # scatter alone; c4's DROP bin escapes in every tile
+    O=gpurun_out/r03t
+    mkdir -p $O
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="u8 u16" bash tools/gpu.sh r03t abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="u8 u16" bash tools/gpu.sh r03t abl || exit 1
+    for c in c5 c4 c2; do
+      if [ $c = c5 ]; then A="--frames 8388608 --multi 2"; else A="--frames 1048576 --multi 8"; fi
+      timeout -k 10 300 python tools/scatter_bench.py --config $c $A --json $O/scb_$c.json u8 u16 u8 u16 > $O/scb_$c.log 2>&1 || exit 1
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
