@@ -5,11 +5,12 @@ The loop a host runs per drained ring: pinned-host header
 windows + lengths -> hipMemcpyAsync H2D -> usn_classify -> usn_finalize (the
 ordered host stage: it reads the batch summary and tile headers, and patches
 results when a batch needs it) -> D2H of the decisions and the per-endpoint
-order.  Batches go round-robin over S streams, one NIC rx queue each; a
+lists (index + bin_off, ABI v3).  Batches go round-robin over S streams, one NIC rx queue each; a
 stream's previous batch is finalized and copied back right before its next
 batch is enqueued, so the copies and host stage of one stream overlap the
 kernels of the others.  At the end every batch's returned decisions are
-compared with the C oracle (bits [23:0]).  Reported in DESIGN.md; never the
+compared with the C oracle (bits [23:0]) and its returned lists with the
+stable sort of the oracle's decisions by bin.  Reported in DESIGN.md; never the
 bench value.  usage: hostio.py [config] [frames] [batches] [streams] [rounds]"""
 import ctypes as C
 import json
@@ -38,7 +39,8 @@ def main():
     nics = [cfg0.src] + traffic.extra_nics(cfg0, S - 1, ctx)
     W = cfg0.stride
     fbytes, lbytes = n * W, n * 2
-    obytes = n * 4 + n * 2
+    n_ep = max(max(e[0] for e in cfg0.endpoints), max(nics)) + 1   # the extra NICs are endpoints too
+    obytes = n * 4 + n * 4 + (n_ep + 4) * 4   # decisions | index | bin_off
     host = []
     for cfg in cfgs:
         hp = C.c_void_p()
@@ -64,7 +66,8 @@ def main():
         host_frames[0] += info.n_host
         hp = host[k]
         lib.check(L.usn_memcpy_d2h(ctx.h, hp + fbytes + lbytes, r.desc.decisions, n * 4, s))
-        lib.check(L.usn_memcpy_d2h(ctx.h, hp + fbytes + lbytes + n * 4, r.desc.order, n * 2, s))
+        lib.check(L.usn_memcpy_d2h(ctx.h, hp + fbytes + lbytes + n * 4, r.desc.index, n * 4, s))
+        lib.check(L.usn_memcpy_d2h(ctx.h, hp + fbytes + lbytes + n * 8, r.desc.bin_off, (n_ep + 4) * 4, s))
         pending[si] = None
 
     def one(k, si):
@@ -97,23 +100,30 @@ def main():
     # every batch's decisions made the round trip and equal the oracle's
     import coracle
     coracle.build()
-    bad = 0
+    bad = bad_lists = 0
     for k, cfg in enumerate(cfgs):
         o = coracle.Oracle()
         coracle.install_oracle(o, cfg0)
         want = o.forward_batch(cfg0.src, cfg.frames, cfg.lens, stride=W)
         got = np.frombuffer((C.c_uint8 * (n * 4)).from_address(host[k] + fbytes + lbytes), np.uint32)
         bad += int(((got ^ want) & lib.PARITY_MASK).astype(bool).sum())
+        bins = lib.dec_bin(want, n_ep)
+        idx = np.frombuffer((C.c_uint8 * (n * 4)).from_address(host[k] + fbytes + lbytes + n * 4), np.uint32)
+        off = np.frombuffer((C.c_uint8 * ((n_ep + 4) * 4)).from_address(host[k] + fbytes + lbytes + n * 8),
+                            np.uint32)
+        want_off = np.concatenate([[0], np.cumsum(np.bincount(bins, minlength=n_ep + 3))])
+        bad_lists += int(not np.array_equal(idx, np.argsort(bins, kind="stable").astype(np.uint32)))
+        bad_lists += int(not np.array_equal(off.astype(np.int64), want_off))
     res = {"config": name, "mpps_median": round(float(np.median(rates)), 1),
            "mpps_all": [round(x, 1) for x in rates], "frames_per_batch": n, "streams": S,
-           "h2d_bytes_per_frame": W + 2, "d2h_bytes_per_frame": 6,
-           "pcie_gbs_equiv": round(float(np.median(rates)) * (W + 8) / 1e3, 1),
+           "h2d_bytes_per_frame": W + 2, "d2h_bytes_per_frame": 8,
+           "pcie_gbs_equiv": round(float(np.median(rates)) * (W + 10) / 1e3, 1),
            "host_stage_frames": host_frames[0], "decisions_checked": nb * n,
-           "decisions_differing_from_oracle": bad,
-           "loop": "H2D windows+lens, usn_classify, usn_finalize, D2H decisions+order; "
+           "decisions_differing_from_oracle": bad, "batches_with_lists_differing": bad_lists,
+           "loop": "H2D windows+lens, usn_classify, usn_finalize, D2H decisions+index+bin_off; "
                    "%d streams, a stream's previous batch finalized before its next" % S}
     print(json.dumps(res))
-    assert bad == 0
+    assert bad == 0 and bad_lists == 0
 
 
 if __name__ == "__main__":

@@ -134,5 +134,24 @@ case $S in
       timeout -k 10 300 python tools/scatter_bench.py --config $c $A --json $O/scb_$c.json u8 u16 u8 u16 > $O/scb_$c.log 2>&1 || exit 1
     done
     ;;
+  r03u)
+    # round-3 session: the tree after the u8 A/B (u16 rows), the whole GPU suite,
+    # smoke, the default bench line (c3 in its new shape), c5 at one ring per call
+    O=gpurun_out/r03u
+    mkdir -p $O
+    bash tools/gpu.sh r03u tests || exit 1
+    bash tools/gpu.sh r03u smoke || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03u bench || exit 1
+    mv $O/bench.log $O/bench_full.log
+    B="--steps 40 --warmup 5 --no-cpu-baseline --no-extra"
+    HOSTIO_ARGS="c2 1048576 8 4 6" bash tools/gpu.sh r03u hostio || exit 1
+    mv $O/hostio.log $O/hostio_c2.log
+    HOSTIO_ARGS="c5 1048576 8 4 6" bash tools/gpu.sh r03u hostio || exit 1
+    mv $O/hostio.log $O/hostio_c5.log
+    for s in 1 2; do
+      BENCH_ARGS="$B --queues 2 --rings-per-launch 1 --streams $s" bash tools/gpu.sh r03u bench || exit 1
+      mv $O/bench.log $O/bench_p1_s$s.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
