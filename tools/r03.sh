@@ -153,5 +153,26 @@ case $S in
       mv $O/bench.log $O/bench_p1_s$s.log
     done
     ;;
+  r03v)
+    # round-3 session: the scan at 8 bins per lane (16-byte loads, USN_SCAN_LW=8):
+    # parity with it, scan + scatter A/B against 4 bins per lane, bench with it;
+    # the PCIe-inclusive loop with the lists (hostio.py, ABI v3)
+    O=gpurun_out/r03v
+    mkdir -p $O
+    USN_SCAN_LW=8 TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py tests/test_gpu_parity.py" bash tools/gpu.sh r03v tests || exit 1
+    for k in 4 8 4 8; do
+      USN_SCAN_LW=$k SCB_CFGS="c5" bash tools/gpu.sh r03v scb || exit 1
+      cat $O/scb_c5.log >> $O/scb_c5_lw$k.log
+    done
+    B="--steps 40 --warmup 5 --no-cpu-baseline --no-extra"
+    for k in 4 8; do
+      USN_SCAN_LW=$k BENCH_ARGS="$B" bash tools/gpu.sh r03v bench || exit 1
+      mv $O/bench.log $O/bench_lw$k.log
+    done
+    HOSTIO_ARGS="c2 1048576 8 4 6" bash tools/gpu.sh r03v hostio || exit 1
+    mv $O/hostio.log $O/hostio_c2.log
+    HOSTIO_ARGS="c5 1048576 8 4 6" bash tools/gpu.sh r03v hostio || exit 1
+    mv $O/hostio.log $O/hostio_c5.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
