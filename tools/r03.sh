@@ -174,5 +174,16 @@ case $S in
     HOSTIO_ARGS="c5 1048576 8 4 6" bash tools/gpu.sh r03v hostio || exit 1
     mv $O/hostio.log $O/hostio_c5.log
     ;;
+  r03w)
+    # round-3 session: where the tx ring's time goes now (phase stamps of the tx
+    # kernel, the launch without rule probes) and the c5 classify's phases
+    O=gpurun_out/r03w
+    mkdir -p $O
+    timeout -k 10 300 python tools/stamps.py c4tx 1048576 > $O/stamps_c4tx.log 2>&1 || exit 1
+    timeout -k 10 300 python tools/stamps.py c5 8388608 > $O/stamps_c5.log 2>&1 || exit 1
+    for v in base txnoprobe base txnoprobe; do
+      timeout -k 10 300 python tools/txbench.py 1048576 30 1 build/abl/$v/libusn.so --rotate 6 >> $O/txbench_$v.log 2>&1 || exit 1
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
