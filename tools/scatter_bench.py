@@ -63,12 +63,12 @@ def main():
               flush=True)
         if nm.startswith("stamps"):   # the diagnostic build: phase medians of the last launch
             import numpy as np
-            buf = np.zeros(16384 * 16, np.uint64)
+            buf = np.zeros(2 * 16384 * 16, np.uint64)   # the scatter's stamps: slots 16384..
             fn = ctx.L.usn_debug_stamps512
             fn.argtypes = [C.c_void_p, C.c_size_t]
             assert fn(buf.ctypes.data, buf.nbytes) == 0
             chunks = sum(rs[0].ntiles for _ in rs) // 8 or 1
-            st = buf.reshape(16384, 16)[:min(chunks, 16384), :12].astype(np.int64)
+            st = buf.reshape(2 * 16384, 16)[16384:16384 + min(chunks, 16384), :12].astype(np.int64)
             t0 = st[:, 0].min()
             names = ["start", "bases+barrier"] + ["tile %d" % k for k in range(8)] + ["loop end", "write-out"]
             for k in range(1, 12):

@@ -44,10 +44,17 @@ def main():
     ctx.sync(s)
     ntiles = (n + 1023) // 1024
     buf = np.zeros(16384 * 16, np.uint64)
-    fn = ctx.L.usn_debug_stamps512 if os.environ.get("STAMPS512") == "1" else ctx.L.usn_debug_stamps
-    fn.argtypes = [C.c_void_p, C.c_size_t]
-    rc = fn(buf.ctypes.data, buf.nbytes)
-    assert rc == 0, rc
+    # the build that ran: the 512-thread one (every config now) or the 256-thread
+    # one (STAMPS512=0 forces it); the other's buffer is all zero
+    names_fn = ["usn_debug_stamps"] if os.environ.get("STAMPS512") == "0" else ["usn_debug_stamps512",
+                                                                               "usn_debug_stamps"]
+    for nm in names_fn:
+        fn = getattr(ctx.L, nm)
+        fn.argtypes = [C.c_void_p, C.c_size_t]
+        rc = fn(buf.ctypes.data, buf.nbytes)
+        assert rc == 0, rc
+        if buf.any():
+            break
     st = buf.reshape(16384, 16)[:ntiles, :12].astype(np.int64)
     t0 = st[:, 0].min()
     us = lambda x: x / 100.0   # 100 MHz ticks -> us

@@ -68,7 +68,9 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 #endif
 #if USN_STAMPS
 #define USN_NSTAMP 16
-__device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
+/* slots 0..16383: the classify / tx kernels' workgroups; 16384..32767: the
+ * scatter kernel's (a classify call runs both) */
+__device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 /* stamps live in registers until the end: a global store per stamp would
  * queue behind the header loads and time the memory queue instead */
 #ifndef USN_STAMP_MIN   /* 1: only the first and last stamp (registers as in the product) */
@@ -87,14 +89,16 @@ __device__ unsigned long long usn_stamp_buf[16384 * USN_NSTAMP];
   do {                                                                           \
     if (threadIdx.x == 0)                                                        \
       for (int k_ = 0; k_ < 12; ++k_)                                            \
-        usn_stamp_buf[((slot) & 16383) * USN_NSTAMP + k_] = stamp_t[k_];         \
+        usn_stamp_buf[((slot) & 32767) * USN_NSTAMP + k_] = stamp_t[k_];         \
   } while (0)
 #define STAMP_FLUSH() STAMP_FLUSH_AT(blockIdx.x)
+#define STAMP_FLUSH_SCATTER(slot) STAMP_FLUSH_AT(16384 + ((slot) & 16383))
 #else
 #define STAMP(k) do { } while (0)
 #define STAMP_DECL
 #define STAMP_FLUSH() do { } while (0)
 #define STAMP_FLUSH_AT(slot) do { } while (0)
+#define STAMP_FLUSH_SCATTER(slot) do { } while (0)
 #endif
 
 #ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
@@ -3077,7 +3081,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     }
     if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
   }
-  STAMP_FLUSH_AT(blockIdx.x);
+  STAMP_FLUSH_SCATTER(blockIdx.x);
 }
 static_assert(NTHREADS == 512, "scatter: 8 waves, a tile each");
 static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
