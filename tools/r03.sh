@@ -185,5 +185,13 @@ case $S in
       timeout -k 10 300 python tools/txbench.py 1048576 30 1 build/abl/$v/libusn.so --rotate 6 >> $O/txbench_$v.log 2>&1 || exit 1
     done
     ;;
+  r03x)
+    # round-3 session: phase stamps of the tx kernel and the c5 classify (the
+    # 512-thread build's buffer)
+    O=gpurun_out/r03x
+    mkdir -p $O
+    timeout -k 10 300 python tools/stamps.py c4tx 1048576 > $O/stamps_c4tx.log 2>&1 || exit 1
+    timeout -k 10 300 python tools/stamps.py c5 8388608 > $O/stamps_c5.log 2>&1 || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
