@@ -313,3 +313,41 @@ def _check_lists(r, want):
     assert sorted(got) == sorted(ref)
     for k in ref:
         assert np.array_equal(got[k], ref[k]), k
+
+
+def test_endpoint_added_before_finalize(coracle_mod):
+    """An rx batch whose later fragments need the host stage, then an endpoint
+    added (the endpoint count grows) before its usn_finalize: the batch keeps
+    the bins it was classified with (scratch, count rows, lists), and its
+    decisions and lists equal the oracle's.  (Before round 3's fix, finalize
+    carved the scratch with the grown endpoint count.)"""
+    from gpu_backend import check_order
+    from usnetd_amd import lib, traffic
+    n = 1 << 16
+    cfg = traffic.config("c2", n=n, seed=91)
+    fr = np.asarray(cfg.frames, np.uint8)
+    H = fr[: n * cfg.stride].reshape(n, cfg.stride)
+    # frame 100: a first fragment (MF, offset 0); frames 2000 and 40000: later
+    # fragments of the same datagram (offset 24 B), decided by the host stage
+    H[100, 20:22] = [0x20, 0x00]
+    for j in (2000, 40000):
+        H[j, :] = H[100, :]
+        H[j, 20:22] = [0x00, 0x03]
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfg)
+    want = o.forward_batch(cfg.src, fr, cfg.lens, stride=cfg.stride)
+    n_ep = max(e[0] for e in cfg.endpoints) + 1
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s = ctx.stream()
+    b = lib.DeviceBatch(ctx, fr, cfg.lens, cfg.src, stride=cfg.stride)
+    r = lib.DeviceResult(ctx, n)
+    ctx.classify(b, r, s)
+    ctx.endpoint_add(n_ep + 40, lib.EP_PIPE, 0)      # 43 more bins from now on
+    info = ctx.finalize(b, r, s)
+    assert info.n_host >= 2
+    got = r.decisions()
+    assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK)
+    assert int(r.summary()["n_bins"]) == n_ep + 3
+    check_order(r, got)
+    b.free(); r.free(); ctx.close()

@@ -193,5 +193,11 @@ case $S in
     timeout -k 10 300 python tools/stamps.py c4tx 1048576 > $O/stamps_c4tx.log 2>&1 || exit 1
     timeout -k 10 300 python tools/stamps.py c5 8388608 > $O/stamps_c5.log 2>&1 || exit 1
     ;;
+  r03y)
+    # round-3 session: a batch keeps its classify-time bins through usn_finalize
+    # (endpoints added in between); the whole GPU suite and smoke on the tree
+    bash tools/gpu.sh r03y tests || exit 1
+    bash tools/gpu.sh r03y smoke
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -513,7 +513,11 @@ struct usn_ctx {
   /* the replica each classified result (keyed by its decisions array) was
    * classified on: usn_finalize acts on the batch's own replica, not on the
    * replica of the source's latest batch */
-  std::unordered_map<const void *, uint32_t> batch_rep;
+  /* per classified batch (by its decisions): the replica it ran on and its
+   * bin count (endpoints can be added before its usn_finalize: the batch's
+   * scratch, count rows and lists keep the bins it was classified with) */
+  struct BatchRec { uint32_t rep, nbins; };
+  std::unordered_map<const void *, BatchRec> batch_rep;
   /* usn_set_lists_async: lists built on the replica's side stream; each
    * result's `lists done` event (keyed by its decisions array, created on
    * its replica's device) */
@@ -2101,6 +2105,18 @@ int usn_result_bind(void *mem, size_t bytes, uint64_t n, usn_result *out) {
 }
 
 /* ---- the hot path ----------------------------------------------------------- */
+/* a batch's bins (nbins = endpoints + 3) in its classify args, and the
+ * count rows carved for them */
+static void set_bins(const usn_result *r, uint64_t n, uint32_t nbins, usn::ClassifyArgs &a) {
+  a.nbins = nbins;
+  a.n_ep = nbins - 3;
+  a.nbits = 1;
+  while ((1u << a.nbits) < a.nbins) ++a.nbits;
+  usn::ScatterBatch sb;
+  usn::scatter_carve(r->scratch, n, nbins, 1, 1, sb, &a.cnt);
+  a.nbw = (nbins + 7u) & ~7u;
+}
+
 static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn_result *r,
                      ClassifyArgs &a) {
   std::memset(&a, 0, sizeof a);
@@ -2496,7 +2512,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
-    c->batch_rep[r[k].decisions] = rep;
+    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins};
   }
   return USN_OK;
 }
@@ -2967,7 +2983,10 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   const bool txb = c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions;
   const auto br = c->batch_rep.find(r->decisions);
   const uint32_t rep = txb ? c->tx.replica
-                     : br != c->batch_rep.end() ? br->second : c->chains[b->src_endpoint].replica;
+                     : br != c->batch_rep.end() ? br->second.rep : c->chains[b->src_endpoint].replica;
+  // the bins the batch was classified with (an rx batch's endpoints may have
+  // grown since; a tx batch blocks every registry change until it is final)
+  const uint32_t nb0 = br != c->batch_rep.end() ? br->second.nbins : c->n_ep + 3;
   HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
@@ -3004,7 +3023,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   std::vector<usn_tile_hdr> th;
   {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr,
-                                    usn::scatter_diag(r->scratch, b->n, c->n_ep + 3));
+                                    usn::scatter_diag(r->scratch, b->n, nb0));
     if (e) return e;
   }
   usn_finalize_info fi;
@@ -3103,9 +3122,17 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   }
   st = advance(b->n);
   if (st) return st;
-  /* patched tiles: recount their bin rows, then the lists again */
+  /* patched tiles: recount their bin rows, then the lists again, with the
+   * bins the batch was classified with -- unless a decision of the host stage
+   * names an endpoint added since (then every tile, with today's bins) */
+  uint32_t nb = nb0;
+  for (uint32_t j : hosts)
+    if (USN_DEC_CLASS(hv.dec[j]) == USN_CLS_EP && (hv.dec[j] & 0xFFFFu) + 3 >= nb) nb = c->n_ep + 3;
+  if (nb > r->max_bins) return USN_ERANGE;
+  if (nb != nb0) std::fill(dirty.begin(), dirty.end(), 1);
   ClassifyArgs a;
   fill_args(c, c->reps[rep], b, r, a);
+  set_bins(r, b->n, nb, a);
   bool any = false;
   for (uint32_t t = 0; t < ntiles;) {
     if (!dirty[t]) { ++t; continue; }
@@ -3121,6 +3148,9 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   }
   /* carried-out cache: authoritative from now on */
   usn_summary out = sum;
+  out.n_ep = nb - 3;
+  out.n_bins = nb;
+  if (nb != nb0) c->batch_rep[r->decisions].nbins = nb;
   out.flags |= USN_S_COUT;
   out.cout_state = cs.valid ? USN_CS_VALID : 0u;
   out.cout_dst = cs.dst;
