@@ -315,7 +315,10 @@ int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
  * n_host > 0 or flags != 0; calling it always is allowed.  USN_EHIP with
  * usn_last_hip_error() == hipErrorLaunchTimeOut (702): the device gave up
  * waiting inside the lists' scan (bounded at 200 ms; never observed) and this
- * batch's index / bin_off are not valid. */
+ * batch's index / bin_off are not valid.  The batch keeps the bins it was
+ * classified with (summary n_bins) when endpoints were added since; only a
+ * host-stage decision naming such an endpoint rebuilds its lists with
+ * today's bins (summary n_ep / n_bins updated; USN_ERANGE past max_bins). */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
                  usn_finalize_info *info);
 
