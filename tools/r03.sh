@@ -199,5 +199,15 @@ case $S in
     bash tools/gpu.sh r03y tests || exit 1
     bash tools/gpu.sh r03y smoke
     ;;
+  r03z)
+    # round-3 session: the tx probes' slot reads non-temporal (USN_TX_SLOT_NT,
+    # build/abl/txslotnt) against the default, alternating, on rotating buffers
+    O=gpurun_out/r03z
+    mkdir -p $O
+    for v in base txslotnt base txslotnt; do
+      timeout -k 10 300 python tools/txbench.py 1048576 30 1 build/abl/$v/libusn.so --rotate 6 > $O/tmp.log 2>&1 || exit 1
+      grep '^{"n"' $O/tmp.log >> $O/txbench_$v.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
