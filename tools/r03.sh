@@ -209,5 +209,11 @@ case $S in
       grep '^{"n"' $O/tmp.log >> $O/txbench_$v.log
     done
     ;;
+  r03f)
+    # round-3 final tree: the default bench line (as the driver runs it) and a
+    # rocprof of the bench
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh r03f bench || exit 1
+    bash tools/gpu.sh r03f rocprof
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
