@@ -51,14 +51,16 @@ clean:
 
 # A/B experiment builds (tools/abl.py): build/abl/<variant>/libusn.so,
 # one variant per line of tools/abl_variants.txt: "<name> <extra hipcc flags>"
+# (USN_AB_BUILD=1: the A/B-only knobs that give wrong results are allowed
+# here and nowhere else, usn_device.hip)
 # (ABL_ONLY="v1 v2": only those)
 abl: build/usn_host.o
 	@while read -r name flags; do \
 	  case "$$name" in ''|'#'*) continue;; esac; \
 	  case " $(ABL_ONLY) " in "  ") ;; *" $$name "*) ;; *) continue;; esac; \
 	  mkdir -p build/abl/$$name; echo "variant $$name: $$flags"; \
-	  $(HIPCC) $(HIPFLAGS) $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip & \
-	  $(HIPCC) $(HIPFLAGS) -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 $$flags -c -o build/abl/$$name/dev512.o $(CSRC)/usn_device.hip & \
+	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip & \
+	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 $$flags -c -o build/abl/$$name/dev512.o $(CSRC)/usn_device.hip & \
 	  wait; \
 	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/abl/$$name/dev512.o build/usn_host.o || exit 1; \
 	done < tools/abl_variants.txt

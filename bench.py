@@ -372,6 +372,7 @@ def measure(run, args, dist, world):
 # (profiles/r03/r03r)
 EXTRA_QUEUES = {"c3": 8}
 TX_ROTATE = 6              # c4tx: the ring in 6 device buffers (384 MiB > the 256 MiB Infinity Cache)
+TX_RINGS = 100             # c4tx: timed rings (and device event pairs) at least
 
 
 def measure_tx(ctx, args):
@@ -396,7 +397,9 @@ def measure_tx(ctx, args):
     for k in range(TX_ROTATE + args.warmup):          # learning pass + warm-up
         ctx.classify(bufs[k % TX_ROTATE], res[k % 2], s)
         ctx.finalize(bufs[k % TX_ROTATE], res[k % 2], s)
-    K = max(args.steps, 20)
+    # >= 100 rings (about 8 ms) and as many event pairs for the device median
+    # (the anti-cache rule of BASELINE.md: >= 100 launches)
+    K = max(args.steps, TX_RINGS)
     evs = [(ctx.event(), ctx.event()) for _ in range(K)]
     learned = 0
     ctx.sync()
@@ -525,6 +528,10 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
         out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, args.cpu_seconds)
     del cfg0
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_extra:
+        # configs[0], the CPU-only config, in both traffic variants
+        for name in ("c1", "c1fixed"):
+            out[name] = measure_c1(name, min(args.cpu_seconds, 3.0))
     if world == 1 and not args.no_extra:
         # the other BASELINE configs, each measured the same way, under its own
         # key: configs[1] (c2), configs[2] (c3: IMIX in 2048-byte slots) and
@@ -580,6 +587,14 @@ def launch_check(rank, world):
         dist.destroy_process_group()
 
 
+def frames_desc(cfg):
+    """What a config's frames are, for the CPU baselines' sample strings."""
+    sizes = sorted(set(int(x) for x in np.unique(cfg.lens)))
+    if len(sizes) == 1:
+        return "%dB frames" % sizes[0]
+    return "IMIX frames (%s B) in %d-byte slots" % ("/".join(str(x) for x in sizes[:4]), cfg.stride)
+
+
 def cpu_baseline(cfg, seconds):
     """The sequential C oracle (restatement of the reference matcher, one
     thread) timed on this host on the rank's first batch, repeated for about
@@ -598,13 +613,16 @@ def cpu_baseline(cfg, seconds):
             break
     return {"value": round(passes * cfg.n / el / 1e6, 3), "unit": "Mpkts/s", "cores": 1,
             "kind": "port",
-            "sample": "%d passes over one %s batch (%d x 64B frames), sequential C restatement "
-                      "with the 1-entry cache, %.1f s" % (passes, cfg.name, cfg.n, el)}
+            "sample": "%d passes over one %s batch (%d x %s), sequential C restatement "
+                      "with the 1-entry cache, %.1f s" % (passes, cfg.name, cfg.n, frames_desc(cfg), el)}
 
 
 def _cpu_worker(arg):
-    """One core: its own oracle, its own rx queue (batch), passes for ~seconds."""
-    name, n, seed, seconds = arg
+    """One core: its own oracle, its own rx queue (batch), passes for ~seconds;
+    pinned to `core` when one is given (taskset-style, os.sched_setaffinity)."""
+    name, n, seed, seconds, core = arg
+    if core is not None:
+        os.sched_setaffinity(0, {core})
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
     from usnetd_amd import traffic
@@ -615,29 +633,88 @@ def _cpu_worker(arg):
     while time.perf_counter() - t0 < seconds:
         o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
         passes += 1
-    return passes * cfg.n, time.perf_counter() - t0
+    aff = sorted(os.sched_getaffinity(0))
+    return passes * cfg.n, time.perf_counter() - t0, frames_desc(cfg), aff
 
 
-def cpu_baseline_ncores(name, seconds):
+def host_cpus():
+    """The CPUs this job may run on (its affinity set; the GPU box gives a
+    share of a larger machine)."""
+    try:
+        return sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return list(range(os.cpu_count() or 1))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline_ncores(name, seconds, pin=False, nshard=1 << 18):
     """SURVEY §8d's N-core variant: the sequential oracle sharded by rx queue,
     one process per core, N = the host CPUs this job may use (at most 16 on
-    the GPU box).  Aggregate frames / slowest worker's time."""
+    the GPU box); with `pin`, worker k runs on the k-th of those CPUs only.
+    Aggregate frames / slowest worker's time."""
     import multiprocessing as mp
-    try:
-        ncores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncores = os.cpu_count() or 1
-    ncores = max(1, min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores)), 16))
-    nshard = 1 << 18   # each core's queue: a quarter-million frames keeps memory small
+    cpus = host_cpus()
+    ncores = max(1, min(len(cpus), int(os.environ.get("OMP_NUM_THREADS", len(cpus))), 16))
     ctx = mp.get_context("spawn")
     with ctx.Pool(ncores) as pool:
-        res = pool.map(_cpu_worker, [(name, nshard, 1000 + k, seconds) for k in range(ncores)])
+        res = pool.map(_cpu_worker, [(name, nshard, 1000 + k, seconds, cpus[k] if pin else None)
+                                     for k in range(ncores)])
     frames = sum(r[0] for r in res)
     el = max(r[1] for r in res)
     return {"value": round(frames / el / 1e6, 3), "unit": "Mpkts/s", "cores": ncores,
-            "kind": "port",
-            "sample": "%d processes, each the sequential C restatement over its own %s rx queue "
-                      "(%d x 64B frames) for %.1f s" % (ncores, name, nshard, el)}
+            "kind": "port", "pinned": bool(pin),
+            "sample": "%d processes%s, each the sequential C restatement over its own %s rx queue "
+                      "(%d x %s) for %.1f s" % (ncores, " (one per CPU, pinned)" if pin else "", name,
+                                                nshard, res[0][2], el)}
+
+
+def cpu_pinned_1core(name, seconds, nshard=1 << 18):
+    """BASELINE configs[0] as the reference measured it: the matcher on ONE
+    pinned core (`taskset -c 6`, /root/reference/eval/Makefile:22).  One
+    spawned process pinned with os.sched_setaffinity to one CPU of this job's
+    set (CPU 6 when the set holds it)."""
+    import multiprocessing as mp
+    cpus = host_cpus()
+    core = 6 if 6 in cpus else cpus[min(len(cpus) - 1, 6)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(1) as pool:
+        frames, el, desc, aff = pool.map(_cpu_worker, [(name, nshard, 1000, seconds, core)])[0]
+    return {"value": round(frames / el / 1e6, 3), "unit": "Mpkts/s", "cores": 1, "kind": "port",
+            "pinned_cpu": core, "affinity_seen_by_worker": aff,
+            "sample": "one process pinned to CPU %d, the sequential C restatement (1-entry cache) "
+                      "over one %s rx queue (%d x %s) for %.1f s" % (core, name, nshard, desc, el)}
+
+
+C1_KEYS = {"c1": "random UDP source port per frame (smolbench-style flood)",
+           "c1fixed": "fixed 5-tuple (pkt-gen -f tx), every frame a 1-entry-cache hit"}
+
+
+def measure_c1(name, seconds):
+    """configs[0] ("CPU reference, no GPU"): the reference's own CPU
+    measurement setup -- 64 B UDP to UDP:3333 of the host, the 4-rule table
+    of DEBUG_PORTS TCP:22 + 3 pipes (/root/reference/eval/enp6s0f0config:1-6,
+    eval/Makefile:11-28) -- timed on this host, 1 core pinned and N cores,
+    with the host CPU named."""
+    cpus = host_cpus()
+    one = cpu_pinned_1core(name, seconds)
+    return {"value": one["value"], "unit": "Mpkts/s", "device": "cpu",
+            "traffic": C1_KEYS[name],
+            "workload": "%s: 64B IPv4/UDP frames to the host's UDP:3333, 4-rule table "
+                        "(DEBUG_PORTS TCP:22 + 3 static pipes)" % name,
+            "cpu_model": cpu_model(), "host_cpus": len(cpus),
+            "cpu_baseline": one,
+            "cpu_baseline_ncores": cpu_baseline_ncores(name, seconds, pin=True)}
 
 
 if __name__ == "__main__":

@@ -51,6 +51,8 @@ extern "C" {
 #define USN_ENODEV (-19)     /* no gfx950 device */
 #define USN_ERANGE (-34)
 #define USN_EBUSY (-16)      /* a tx batch awaits usn_finalize (shared state not final yet) */
+#define USN_ELIST (-74)      /* EBADMSG: the device found the batch's per-bin counts disagreeing with
+                                its decisions; index / bin_off of that batch are not valid */
 
 /* ---- decision word (u32), one per frame --------------------------------
  *   [15:0]  endpoint id (0xFFFF = none)            Target::Endpoint/EndpointRef
@@ -176,7 +178,8 @@ typedef struct {
                               and list offsets) */
   uint64_t n;
   uint32_t max_bins;       /* bins the scratch holds (a batch with more endpoints: USN_ERANGE) */
-  uint32_t _pad;
+  uint32_t bind_tag;       /* internal: distinct per usn_result_bind call (the scratch's state
+                              is re-initialised on the first classify after a bind) */
 } usn_result;
 #define USN_MAX_BINS (USN_MAX_ENDPOINTS + 3)
 
@@ -312,13 +315,17 @@ int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
  * frame order and patches decisions and the per-endpoint lists on the device.  Must be called
  * before the next usn_classify of the same source whenever the summary has
- * n_host > 0 or flags != 0; calling it always is allowed.  USN_EHIP with
- * usn_last_hip_error() == hipErrorLaunchTimeOut (702): the device gave up
- * waiting inside the lists' scan (bounded at 200 ms; never observed) and this
- * batch's index / bin_off are not valid.  The batch keeps the bins it was
- * classified with (summary n_bins) when endpoints were added since; only a
- * host-stage decision naming such an endpoint rebuilds its lists with
- * today's bins (summary n_ep / n_bins updated; USN_ERANGE past max_bins). */
+ * n_host > 0 or flags != 0; calling it always is allowed.  The batch's
+ * index / bin_off are not valid when it returns USN_ELIST (the scatter found
+ * a decision naming a bin past the batch's bins, or per-tile counts that
+ * disagree with the decisions) or USN_EHIP with usn_last_hip_error() ==
+ * hipErrorLaunchTimeOut (702: the device gave up waiting inside the lists'
+ * scan, bounded at 200 ms); neither has been observed outside the test hook
+ * that forces them.  The batch keeps the bins it was classified with
+ * (summary n_bins) when endpoints were added since; only a host-stage
+ * decision naming such an endpoint rebuilds its lists with today's bins
+ * (summary n_ep / n_bins updated).  USN_ERANGE, before any side effect: the
+ * batch needs the host stage and today's bins exceed the result's max_bins. */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
                  usn_finalize_info *info);
 

@@ -54,3 +54,23 @@ def test_result_layout():
     assert small < nbytes
     assert L.usn_result_bind(base, small, n, ctypes.byref(r)) == 0 and 1005 <= r.max_bins < 1016
     assert L.usn_result_bind(base, L.usn_result_bytes_ep(n, 0) - 1, n, ctypes.byref(r)) == -34
+
+
+def test_ab_only_knobs_refused_in_product_builds():
+    """the ablation knobs that give wrong results on purpose
+    compile only with USN_AB_BUILD=1 (the Makefile's `abl` builds); a product
+    build that sets one stops at usn_device.hip's static_assert."""
+    import shutil
+    import subprocess
+    import pytest
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc) and not shutil.which("hipcc"):
+        pytest.skip("no hipcc")
+    src = os.path.join(ROOT, "usnetd_amd", "csrc", "usn_device.hip")
+    base = [hipcc, "-std=c++17", "--offload-arch=gfx950", "-fsyntax-only", "-DUSN_NTHREADS=512",
+            "-DUSN_NS=usn_t512", src]
+    bad = subprocess.run(base + ["-DUSN_ABL_NOPROBE=1"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "A/B-only knob" in bad.stderr, bad.stderr[-2000:]
+    ok = subprocess.run(base + ["-DUSN_ABL_NOPROBE=1", "-DUSN_AB_BUILD=1"], capture_output=True,
+                        text=True)
+    assert ok.returncode == 0, ok.stderr[-2000:]

@@ -351,3 +351,52 @@ def test_endpoint_added_before_finalize(coracle_mod):
     assert int(r.summary()["n_bins"]) == n_ep + 3
     check_order(r, got)
     b.free(); r.free(); ctx.close()
+
+
+def test_stale_walk_names_endpoint_added_after_classify(coracle_mod):
+    """the stale-prefix walk of usn_finalize resolves frames with
+    today's registry.  A NIC's cached decision goes stale (RemoveMatch,
+    main.rs:608-625); the next batch repeats the cached flow past tile 0 and
+    then sends ONE frame of another flow; between that batch's classify and
+    its finalize an endpoint and a rule for that flow are added.  The walk
+    resolves the frame to the new endpoint (an id past the batch's bins), so
+    the lists are rebuilt with today's bins: decisions and lists equal the
+    oracle's, run with the same registry change before that frame."""
+    from gpu_backend import check_order
+    from usnetd_amd import lib, traffic
+    n = 1 << 14
+    k = 5000                                  # past tile 0: the walk, not the device, reaches it
+    cfg = traffic.config("c1", n=n, variant="fixed")
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfg)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s = ctx.stream()
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, 0, stride=cfg.stride)
+    r1, r2 = lib.DeviceResult(ctx, n), lib.DeviceResult(ctx, n)
+    ctx.classify(b, r1, s)
+    ctx.finalize(b, r1, s)
+    o.forward_batch(0, cfg.frames, cfg.lens, stride=cfg.stride)
+    assert ctx.remove_match(lib.make_want(traffic.LOCAL, 17, 3333), 2) == 1
+    assert o.remove_match(coracle_mod.make_want(traffic.LOCAL, 17, 3333), 2) == 1
+    frames = np.asarray(cfg.frames, np.uint8).copy()
+    frames[k * 64 + 36:k * 64 + 38] = [0x12, 0x34]          # dport 4660 (UDP checksum untouched)
+    n_ep = max(e[0] for e in cfg.endpoints) + 1
+    new_id = n_ep + 40
+    b2 = lib.DeviceBatch(ctx, frames, cfg.lens, 0, stride=cfg.stride)
+    ctx.classify(b2, r2, s)
+    ctx.endpoint_add(new_id, lib.EP_PIPE, 0)
+    assert ctx.add_match(lib.make_want(traffic.LOCAL, 17, 0x1234), new_id) == 1
+    info = ctx.finalize(b2, r2, s)
+    got = r2.decisions()
+    want0 = o.forward_batch(0, frames[: k * 64], cfg.lens[:k], stride=cfg.stride)
+    o.add_endpoint(new_id, lib.EP_PIPE, 0)
+    assert o.add_match(coracle_mod.make_want(traffic.LOCAL, 17, 0x1234), new_id) == 1
+    want1 = o.forward_batch(0, frames[k * 64:], cfg.lens[k:], stride=cfg.stride)
+    want = np.concatenate([want0, want1])
+    assert info.flags & lib.S_STALE
+    assert (got[k] & 0xFFFF) == new_id and ((got[k] >> 16) & 0xF) == lib.CLS_EP
+    assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK)
+    assert int(r2.summary()["n_bins"]) == new_id + 1 + 3
+    check_order(r2, got)
+    b.free(); b2.free(); r1.free(); r2.free(); ctx.close()

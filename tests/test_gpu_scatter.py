@@ -150,3 +150,43 @@ def test_count_rows_heavy_bins(name):
     assert np.array_equal(np.diff(off.astype(np.int64)), np.bincount(bins, minlength=n_ep + 3))
     assert np.array_equal(r.index(n), np.argsort(bins, kind="stable").astype(np.uint32))
     b.free(); r.free(); ctx.close()
+
+
+CORRUPT_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [%(root)r]
+from usnetd_amd import lib, traffic
+for name, n in (("c5", 1 << 20), ("c2", 1 << 16), ("c4tx", 1 << 16)):
+    cfg = traffic.c4tx(n=n, seed=6) if name == "c4tx" else traffic.config(name, n=n, seed=4242)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s = ctx.stream()
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+    r = lib.DeviceResult(ctx, n)
+    ctx.classify(b, r, s)
+    try:
+        ctx.finalize(b, r, s)
+        print(name, "no error", flush=True)
+    except lib.UsnError as e:
+        print(name, "error", str(e), flush=True)
+    b.free(); r.free(); ctx.close()
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_scatter_reports_inconsistent_counts(mode):
+    """a count row that disagrees with the decisions (test
+    hook USN_DEBUG_CORRUPT=1: +257 frames in one bin of the first tile) or a
+    decision naming an endpoint past the batch's bins (=2) is reported by
+    usn_finalize as USN_ELIST, on the rx path (c5 with the scan, c2) and on
+    the tx path (c4tx, the finalize state gathered on the device)."""
+    env = dict(os.environ, USN_DEBUG_CORRUPT=mode)
+    p = subprocess.run([sys.executable, "-c", CORRUPT_CHILD % {"root": ROOT}], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    lines = p.stdout.strip().splitlines()
+    assert lines[-1] == "ok", p.stdout
+    for line in lines[:-1]:
+        assert " error " in line and "ELIST" in line, line
+    assert len(lines) == 4, lines

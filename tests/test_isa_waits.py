@@ -31,12 +31,12 @@ def test_hand_counted_waits(build):
 
 
 def test_check_fails_on_an_extra_load():
-    text = _asm("t512_perturb1", BUILDS["t512"] + ("USN_ISA_PERTURB=1",))
+    text = _asm("t512_perturb1", BUILDS["t512"] + ("USN_ISA_PERTURB=1", "USN_AB_BUILD=1"))
     findings, _ = isa_check.check(text, lambda n: "classify_rx_kernelILi2ELb1" in n)
     assert any(f.kind == "loose" for f in findings), findings
 
 
 def test_check_fails_on_a_stale_count():
-    text = _asm("t512_perturb2", BUILDS["t512"] + ("USN_ISA_PERTURB=2",))
+    text = _asm("t512_perturb2", BUILDS["t512"] + ("USN_ISA_PERTURB=2", "USN_AB_BUILD=1"))
     findings, _ = isa_check.check(text, lambda n: "classify_rx_kernelILi2ELb1" in n)
     assert any(f.kind == "hazard" for f in findings), findings

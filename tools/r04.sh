@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-4 GPU sessions (each a sequence of tools/gpu.sh steps):
+#   bash tools/r04.sh <session>   output under gpurun_out/<session>/
+set -o pipefail
+S=${1:?session}
+O=gpurun_out/$S
+mkdir -p $O
+export TMPDIR=/tmp
+case $S in
+  r04a)
+    # round-4 first session: the whole GPU suite (loud scatter errors, the
+    # stale walk naming a new endpoint), smoke, the default bench (c1 keys,
+    # c4tx at 100 rings), and the FETCH_SIZE calibration of one scattered
+    # window read per 2048-byte slot (c3's pattern) from TCC_EA0_RDREQ
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    timeout -k 10 60 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
+    for c in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" FETCH_SIZE; do
+      n=$(echo $c | cut -d' ' -f1)
+      rm -rf $O/sf_$n
+      timeout -k 10 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/sf_$n -o run -- build/stride_floor 4194304 2048 6 > $O/sf_$n.log 2>&1 || exit 1
+    done
+    ;;
+  *) echo "unknown session $S"; exit 2 ;;
+esac
+echo "== session $S done"

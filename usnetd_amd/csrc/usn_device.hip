@@ -1,22 +1,27 @@
 /*
- * usn_device.hip -- gfx950 kernels of the usnetd match path.
+ * usn_device.hip -- gfx950 kernels of the usnetd match path (DESIGN.md §3).
  *
- * classify: one workgroup (256 threads, 4 waves) per tile of USN_TILE = 1024
- * frames, one frame per lane per round, four rounds.  Per frame:
- *   1. the 64-byte header window + the 2-byte length: windows stream into a
- *      wave-private LDS stage by LDS-DMA (glds, non-temporal), one round in
- *      flight while the previous one is decided;
+ * classify_rx_kernel: one workgroup per tile of USN_TILE = 1024 frames, 512
+ * threads (two rounds per lane; the 256-thread build, four rounds, only where
+ * its smaller header stage is what lets the rule image fit LDS).  Per frame:
+ *   1. the header window + the 2-byte length: fixed-stride layouts stream
+ *      bytes 12..43 into a wave-private LDS stage by LDS-DMA (glds, `nt`),
+ *      round 1 in flight while round 0 is parsed; offsets layouts and wide
+ *      strides use per-lane 16-byte register loads;
  *   2. extract_pkt_info in registers, branch-free    /root/reference/src/pkt.rs:158-218
- *   3. get_endpoint: exact-match probes of the bucketed rule table (LDS copy
- *      when it fits, else L2-resident), only for key shapes the table holds
+ *   3. get_endpoint: perfect-hash probes of the rule image (whole image in
+ *      LDS when it fits; else displacements in LDS and slots from L2: one U
+ *      slot answers key1 and key2, X only for shared projections)
  *                                                      /root/reference/src/endpoint.rs:307-338
  *   4. the decision of find_forward for a NIC source    /root/reference/src/endpoint.rs:172-296
- *   5. stable per-endpoint order of the tile: bit-sliced wave ballots give
- *      every frame the mask of lanes holding the same bin (no data-dependent
- *      loop), hence its rank in its 64-frame segment and per-segment counts;
- *      a column scan over the 16 segments and one block scan over bins give
- *      the slots and the bin runs; sorted tile-local indices are written with
- *      coalesced stores.
+ *   5. the tile's frames per bin (LDS histogram) -> its count row; frames
+ *      that need ordered state are listed for usn_finalize.
+ * tx_kernel: the sending-endpoint direction in one launch (learning, the
+ * inner L2 bridge, epoch-tagged cross-tile hand-offs; §3.4).
+ * scan_kernel + scatter_kernel: the device-wide per-endpoint lists (index,
+ * bin_off) from the decisions and the count rows (§3.2): stable, frame order
+ * inside each bin; a count row that disagrees with the decisions is reported
+ * (diag USN_DIAG_LISTS -> usn_finalize USN_ELIST), never hidden.
  * No MFMA: byte parsing and hash probing, bounded by HBM reads.
  *
  * Order-dependent state (fragment map, DHCP next endpoint, a stale carried
@@ -101,6 +106,12 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #define STAMP_FLUSH_SCATTER(slot) do { } while (0)
 #endif
 
+/* A/B-only knobs below give WRONG results on purpose (ablations timed by
+ * tools/abl.py).  Those builds define USN_AB_BUILD=1 (the Makefile's `abl`
+ * target, tests/isa_check.py); a product build that sets one fails here. */
+#ifndef USN_AB_BUILD
+#define USN_AB_BUILD 0
+#endif
 #ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
 #define USN_ABL_NOTAGS 0
 #endif
@@ -121,6 +132,16 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #ifndef USN_ABL_LOADONLY   /* A/B only: loads and stores, no parse/probe/decide */
 #define USN_ABL_LOADONLY 0
 #endif
+#ifndef USN_ABL_SC   /* A/B only: scatter_kernel 4 no rank walk, 5 no write-out */
+#define USN_ABL_SC 0
+#endif
+#ifndef USN_ISA_PERTURB   /* tests/test_isa_waits.py only: 1 an extra load, 2 a stale wait count */
+#define USN_ISA_PERTURB 0
+#endif
+static_assert(USN_AB_BUILD || !(USN_ABL_NOTAGS || USN_ABL_TXNOPROBE || USN_ABL_NOPROBE ||
+                                USN_ABL_NODISPCOPY || USN_ABL_LOADONLY || USN_ABL_SC ||
+                                USN_ISA_PERTURB),
+              "an A/B-only knob (wrong results) in a build without USN_AB_BUILD=1");
 
 /* 16-byte header load (`nt` streaming hint only when USN_LOAD_NT) */
 __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
@@ -2812,7 +2833,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
           if (!pend) break;
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (it == 0) t0 = now;
-          else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, 1u); break; }   // never seen; lists wrong
+          else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(B.diag, USN_DIAG_TIMEOUT); break; }   // never seen; lists wrong
           __builtin_amdgcn_s_sleep(1);
         }
       }
@@ -2864,9 +2885,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
 __device__ uint32_t usn_scatter_fallbacks = 0;
 #ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
 #define USN_SC_GROUP 1
-#endif
-#ifndef USN_ABL_SC   /* A/B only: 4 no rank walk, 5 no write-out (wrong results) */
-#define USN_ABL_SC 0
 #endif
 template <int TC>
 __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
@@ -2978,6 +2996,13 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
       }
     }
   }
+  // every stage slot starts empty: a slot still empty at the write-out means
+  // the count rows disagree with the decisions (reported, never hidden)
+  {
+    uint4 *st4 = reinterpret_cast<uint4 *>(stage);
+#pragma unroll
+    for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
   if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
   if (c == 0 && bi == 0 && s.txs_out && tid < 6) {   // tx: summary flags, counters[0..4], n
     uint32_t v = tid == 0 ? s.txs_sum->flags
@@ -2997,19 +3022,27 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
   // stage and a chunk that is not stably sorted is ranked again the
   // ballot way (5).
   const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  // bad: a decision naming a bin past the batch's bins, a rank past the
+  // chunk, an empty stage slot or a list position past n -- the count rows
+  // and the decisions disagree.  Every access stays in bounds regardless, and
+  // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
+  bool bad = false;
   if (wave < ntc && USN_ABL_SC != 4) {
     uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
     uint32_t b[SEGS], at[SEGS];
 #pragma unroll
     for (uint32_t k = 0; k < SEGS; ++k) {
-      b[k] = min(dec_bin(d[k], s.n_ep), s.nbins - 1u);
+      const uint32_t raw = dec_bin(d[k], s.n_ep);
+      b[k] = min(raw, s.nbins - 1u);
       const uint32_t sh = 16u * (b[k] & 1u);
-      at[k] = k * 64 + lane < tn ? atomicAdd(&cw[b[k] >> 1], 1u << sh) >> sh : 0u;
+      const bool v = k * 64 + lane < tn;
+      at[k] = v ? (atomicAdd(&cw[b[k] >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+      bad |= v && (raw >= s.nbins || at[k] >= nf);
     }
 #pragma unroll
     for (uint32_t k = 0; k < SEGS; ++k)
       if (k * 64 + lane < tn)
-        stage[min(at[k] & 0xFFFFu, TC * TILE - 1u)] = (b[k] << 16) | (wave * TILE + k * 64 + lane);
+        stage[min(at[k], TC * TILE - 1u)] = (b[k] << 16) | (wave * TILE + k * 64 + lane);
   }
   __syncthreads();
   STAMP(10);
@@ -3037,6 +3070,7 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
         const uint32_t q = q0 + j * NTHREADS + tid;
         const uint32_t pos = o[j] + q;
         if (pos < B.n) B.index[pos] = (uint32_t)first + (e[j] & 0xFFFFu);
+        bad |= pos >= B.n || e[j] == ~0u;
         unsorted |= q && (p[j] >> 16) == (e[j] >> 16) && (p[j] & 0xFFFFu) >= (e[j] & 0xFFFFu);
       }
     }
@@ -3046,10 +3080,15 @@ __global__ __launch_bounds__(NTHREADS) void scatter_kernel(ScatterArgs s) {
     const uint32_t b = min(e >> 16, s.nbw - 1u);
     const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
     if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
+    bad |= pos >= B.n || e == ~0u;
     const uint32_t p = q ? stage[q - 1] : 0u;
     unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
   }
   STAMP(11);
+  if (USN_ABL_SC == 0 && __ballot(bad) && lane == 0) {   // rare: one report per wave
+    atomicOr(B.diag, USN_DIAG_LISTS);
+    if (s.txs_out) s.txs_out[11] = USN_DIAG_LISTS;   // tx: beside chunk 0's copy of the scan's word
+  }
   if (USN_ABL_SC == 0 && __syncthreads_or(unsorted || (s.flags & USN_SCF_SLOW_RANK))) {
     // 5. (not taken on gfx950 so far) the wave's cursors back to their
     // seeds (final value - the tile's count), the ranks from bit-sliced

@@ -23,6 +23,7 @@
 #include <new>
 #include <thread>
 #include <random>
+#include <atomic>
 #include <unordered_map>
 #include <unordered_set>
 #include <utility>
@@ -527,7 +528,10 @@ struct usn_ctx {
   /* the scatter's scan: a tag per launch for its range granules (random
    * start), and the result scratches whose granules were zeroed */
   uint32_t scan_epoch = (uint32_t)std::random_device{}();
-  std::unordered_set<uint64_t> scan_zeroed;   // (scratch, frames, bins)
+  /* per scratch: the bind tag and geometry (frames, bins) its granules were
+   * last zeroed for (one entry per scratch, not per geometry) */
+  struct Zeroed { uint32_t tag; uint64_t geo; };
+  std::unordered_map<const void *, Zeroed> scan_zeroed;
   uint64_t listen_gen = 0;   // Ep::listen_ver source
   /* a tx batch's summary flags, counters and class totals, written into
    * host-mapped memory by the scatter's first chunk (usn_finalize of a
@@ -1683,6 +1687,7 @@ const char *usn_strerror(int s) {
     case USN_ENODEV: return "no gfx950 device";
     case USN_ERANGE: return "out of range";
     case USN_EBUSY: return "a tx batch awaits usn_finalize";
+    case USN_ELIST: return "per-endpoint lists inconsistent with the decisions";
     default: return "unknown";
   }
 }
@@ -2100,7 +2105,10 @@ int usn_result_bind(void *mem, size_t bytes, uint64_t n, usn_result *out) {
   out->scratch = b + L.scratch;
   out->n = n;
   out->max_bins = lo;
-  out->_pad = 0;
+  static std::atomic<uint32_t> tags{0};
+  uint32_t t;
+  do t = tags.fetch_add(1, std::memory_order_relaxed) + 1; while (t == 0);
+  out->bind_tag = t;
   return USN_OK;
 }
 
@@ -2229,17 +2237,29 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     sb.bin_off = r[k].bin_off;
     x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
     x.range_base[k + 1] = x.range_base[k] + sb.nranges;
-    // granules of a scratch never used before may hold anything: zero them once
-    // (their place depends on the batch's frames and bins)
-    const uint64_t key = (uint64_t)(uintptr_t)r[k].scratch * 0x9E3779B97F4A7C15ull ^
-                         (as[k].n << 16) ^ x.nbins;
-    if (c->scan_zeroed.insert(key).second) {
+    // granules of a scratch never used before may hold anything: zero them
+    // after every bind, and again when the geometry moves them (their place
+    // depends on the batch's frames and bins)
+    const uint64_t geo = (as[k].n << 16) ^ x.nbins;
+    auto zi = c->scan_zeroed.find(r[k].scratch);
+    if (zi == c->scan_zeroed.end() || zi->second.tag != r[k].bind_tag || zi->second.geo != geo) {
+      c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo};
       void *p;
       size_t bytes;
       usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
       HIPCHK(hipMemsetAsync(p, 0, bytes, s));
     }
   }
+  // test hook (tests/test_gpu_scatter.py, read once per process):
+  // USN_DEBUG_CORRUPT=1 adds 257 to bin 0 of batch 0's first count row, =2
+  // makes frame 0's decision name endpoint 0x0FF0 (past every batch's bins);
+  // the scatter must report either (usn_finalize: USN_ELIST)
+  static const int corrupt = [] {
+    const char *e = std::getenv("USN_DEBUG_CORRUPT");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (corrupt == 1) HIPCHK(hipMemsetAsync(const_cast<uint16_t *>(x.b[0].cnt), 0x01, 2, s));
+  if (corrupt == 2) HIPCHK(hipMemsetD32Async(r[0].decisions, (int)((1u << 16) | 0x0FF0u), 1, s));
   HIPCHK(usn_t512::launch_scatter(x, s));
   return USN_OK;
 }
@@ -2468,6 +2488,9 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         c->h_txstate_cap = 64;
       }
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&txs), c->h_txstate, 0));
+      // word 11: set by any scatter chunk that finds inconsistent lists (the
+      // previous tx batch's kernels are done: its usn_finalize synchronised)
+      reinterpret_cast<volatile uint32_t *>(c->h_txstate)[11] = 0;
     }
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
     if (st) return st;
@@ -2606,14 +2629,25 @@ bool retains(uint32_t d) {
  * listed tile, or one bulk copy of the whole area when many tiles list frames */
 /* summary + tile headers (+ the tx counters when cnt) of a classified batch,
  * through the context's pinned staging buffer on stream s */
-/* a scan wait of the batch's lists timed out (never seen; the kernel gave up
- * after 200 ms): report it once, loudly */
+/* the batch's lists are not valid (usn_kernels.h USN_DIAG_*): a scan wait
+ * timed out (never seen; the kernel gave up after 200 ms), or the scatter
+ * found counts that disagree with the decisions.  Reported once, loudly; the
+ * word is cleared for the scratch's next batch. */
 int lists_failed(uint32_t diag, uint32_t *d_diag, hipStream_t s) {
   if (!diag) return USN_OK;
   HIPCHK(hipMemsetAsync(d_diag, 0, 4, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (diag & USN_DIAG_LISTS) return USN_ELIST;
   g_last_hip = (int)hipErrorLaunchTimeOut;
   return USN_EHIP;
+}
+/* the same after a scatter that usn_finalize launched itself (the stream is
+ * synchronised by the caller) */
+int lists_check(uint32_t *d_diag, hipStream_t s) {
+  uint32_t dg = 0;
+  HIPCHK(hipMemcpyAsync(&dg, d_diag, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return lists_failed(dg, d_diag, s);
 }
 
 int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
@@ -2739,9 +2773,9 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     HIPCHK(hipEventSynchronize(R.txstate_ev));
     c->txstate_for = nullptr;
     const volatile uint32_t *q = reinterpret_cast<const volatile uint32_t *>(c->h_txstate);
-    uint32_t v[11];
-    for (int k = 0; k < 11; ++k) v[k] = q[k];
-    { const int e = lists_failed(v[10], usn::scatter_diag(r->scratch, n, c->n_ep + 3), s); if (e) return e; }
+    uint32_t v[12];
+    for (int k = 0; k < 12; ++k) v[k] = q[k];
+    { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, n, c->n_ep + 3), s); if (e) return e; }
     if (v[1] == 0 && v[2] == 0 && v[4] != R.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
       // results are final; class totals from bin_off (EP bins, NIC, FLOOD, DROP)
@@ -2970,6 +3004,8 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     std::memcpy(o.cout_info, cs.info.w, 16);
     HIPCHK(hipMemcpy(r->summary, &o, sizeof o, hipMemcpyHostToDevice));
     HIPCHK(hipStreamSynchronize(s));
+    st = lists_check(usn::scatter_diag(r->scratch, n, c->n_ep + 3), s);
+    if (st) return st;
   }
   if (info) *info = fi;
   return USN_OK;
@@ -3041,6 +3077,11 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     if (info) *info = fi;
     return USN_OK;   // device results are final; the device chain carries the cache
   }
+  // the host stage may name an endpoint added since the classify: its lists
+  // then need today's bins.  Refused here, before any side effect, when the
+  // result cannot hold them (a retry would otherwise repeat the map, DHCP
+  // and cache steps).
+  if (c->n_ep + 3 > nb0 && c->n_ep + 3 > r->max_bins) return USN_ERANGE;
   const int src = b->src_endpoint;
   HostView hv{c, b, r, s, {}, {}, false, false};
   int st = hv.fetch_dec();
@@ -3049,6 +3090,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   std::vector<uint8_t> buf;
   uint32_t len = 0;
   std::vector<char> dirty(ntiles, 0);
+  bool new_ep = false;   // a resolved decision names an endpoint id >= the batch's n_ep
   CacheState cs;
   cs.valid = sum.cin_state & USN_CS_VALID;
   cs.dst = sum.cin_dst;
@@ -3081,6 +3123,8 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     bool learned;
     const uint32_t d = host_step(c, src, buf.data(), len, cs, learned) | USN_F_HOST;
     const uint32_t old = hv.dec[j];
+    // every resolved frame counts, host-listed or walked in a stale prefix
+    if (USN_DEC_CLASS(d) == USN_CLS_EP && (d & 0xFFFFu) + 3 >= nb0) new_ep = true;
     if ((old & USN_PARITY_MASK) != (d & USN_PARITY_MASK)) {
       fi.n_patched++;
       fi.class_count[USN_DEC_CLASS(old)]--;
@@ -3125,10 +3169,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   /* patched tiles: recount their bin rows, then the lists again, with the
    * bins the batch was classified with -- unless a decision of the host stage
    * names an endpoint added since (then every tile, with today's bins) */
-  uint32_t nb = nb0;
-  for (uint32_t j : hosts)
-    if (USN_DEC_CLASS(hv.dec[j]) == USN_CLS_EP && (hv.dec[j] & 0xFFFFu) + 3 >= nb) nb = c->n_ep + 3;
-  if (nb > r->max_bins) return USN_ERANGE;
+  const uint32_t nb = new_ep ? c->n_ep + 3 : nb0;   // <= max_bins: checked before any side effect
   if (nb != nb0) std::fill(dirty.begin(), dirty.end(), 1);
   ClassifyArgs a;
   fill_args(c, c->reps[rep], b, r, a);
@@ -3157,6 +3198,10 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   std::memcpy(out.cout_info, cs.info.w, 16);
   HIPCHK(hipMemcpy(r->summary, &out, sizeof out, hipMemcpyHostToDevice));
   HIPCHK(hipStreamSynchronize(s));
+  if (any) {
+    st = lists_check(usn::scatter_diag(r->scratch, b->n, nb), s);
+    if (st) return st;
+  }
   if (info) *info = fi;
   return USN_OK;
 }

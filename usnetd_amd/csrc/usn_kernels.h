@@ -143,7 +143,7 @@ struct ScatterBatch {
   uint32_t *agg;            /* [nchunks][nbw]: frames per bin in the chunks before */
   uint32_t *tot;            /* [nbw]: frames per bin */
   unsigned long long *gran; /* [nranges][nbw]: {epoch, range total} */
-  uint32_t *diag;           /* bit 0: a scan wait timed out (the lists are wrong) */
+  uint32_t *diag;           /* USN_DIAG_*: the lists are wrong (usn_finalize reports it) */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
   uint32_t n, ntiles, tc, nchunks, nranges;
@@ -165,6 +165,8 @@ struct ScatterArgs {
   const uint32_t *txs_counters;
   const usn_summary *txs_sum;
 };
+#define USN_DIAG_TIMEOUT 1u     /* a scan wait timed out (200 ms; never observed) */
+#define USN_DIAG_LISTS 2u       /* the scatter found count rows that disagree with the decisions */
 #define USN_SCF_NOSCAN 2u      /* every batch is one chunk: no scan launch; the chunk's own counts
                                   are the batch's (agg = 0, tot = the chunk's sums) */
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the

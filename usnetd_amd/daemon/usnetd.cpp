@@ -191,6 +191,7 @@ class Daemon {
   PcapWriter pcap_;
   uint64_t class_count_[4] = {0, 0, 0, 0};
   bool end_ = false;
+  uint32_t ep_limit_ = 0;   // max endpoint id ever added + 1: the context's n_ep (it never shrinks)
   unsigned cleanup_secs_ = 90;
   int write_wait_ms_ = 5;     // USNETD_WRITE_WAIT_MS: back-pressure before a frame is dropped
 
@@ -274,6 +275,7 @@ bool Daemon::register_dev(const DevP &d) {
     return false;
   }
   devices_.push_back(d);
+  ep_limit_ = std::max<uint32_t>(ep_limit_, (uint32_t)d->id + 1);
   LOGI("added endpoint %u (kind %d)", d->id, d->kind);
   return true;
 }
@@ -962,7 +964,10 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
       uint8_t *o = B.h_out + s.out_off;
       select(s.dev->rep);
       usn_memcpy_d2h(ctx_, o, s.res.summary, sizeof(usn_summary), B.stream);
-      usn_memcpy_d2h(ctx_, o + OUT_BINS, s.res.bin_off, (size_t)(USN_MAX_BINS + 1) * 4, B.stream);
+      // bin_off entries the batch can use: its bins are at most today's
+      // n_ep + 3 (not the whole USN_MAX_BINS + 1 array per source)
+      const size_t nbo = std::min<size_t>((size_t)ep_limit_ + 4, USN_MAX_BINS + 1);
+      usn_memcpy_d2h(ctx_, o + OUT_BINS, s.res.bin_off, nbo * 4, B.stream);
       usn_memcpy_d2h(ctx_, o + OUT_HEAD, s.res.index, (size_t)s.n * 4, B.stream);
     }
     k = e;

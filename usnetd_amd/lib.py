@@ -27,8 +27,9 @@ F_CACHE, F_FRAG1, F_FRAGN, F_DHCP, F_HOST, F_LEARN = (1 << 24, 1 << 25, 1 << 26,
                                                       1 << 28, 1 << 29)
 S_STALE, S_STALE_EXTENDS, S_COUT = 1, 2, 8
 STATUS = {0: "ok", -22: "EINVAL", -12: "ENOMEM", -17: "EEXIST", -2: "ENOENT", -1: "EPERM",
-          -5: "EHIP", -19: "ENODEV", -34: "ERANGE", -16: "EBUSY"}
+          -5: "EHIP", -19: "ENODEV", -34: "ERANGE", -16: "EBUSY", -74: "ELIST"}
 USN_EBUSY = -16
+USN_ELIST = -74
 
 
 class UsnError(RuntimeError):
@@ -56,7 +57,7 @@ class Result(C.Structure):
     _fields_ = [("decisions", C.c_void_p), ("index", C.c_void_p), ("bin_off", C.c_void_p),
                 ("tiles", C.c_void_p), ("summary", C.c_void_p), ("host_list", C.c_void_p),
                 ("scratch", C.c_void_p), ("n", C.c_uint64), ("max_bins", C.c_uint32),
-                ("_pad", C.c_uint32)]
+                ("bind_tag", C.c_uint32)]
 
 
 class FinalizeInfo(C.Structure):
