@@ -22,6 +22,19 @@ case $S in
       timeout -k 10 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/sf_$n -o run -- build/stride_floor 4194304 2048 6 > $O/sf_$n.log 2>&1 || exit 1
     done
     ;;
+  r04b)
+    # tx lists built inside the tx launch (tx_lists): the GPU suite, tx ring
+    # timing inline vs the scan + scatter launches, the scatter at 3 vs 2
+    # workgroups per CU (80 vs 85 VGPRs), the default bench
+    bash tools/gpu.sh $S testsall || exit 1
+    TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh $S txbench || exit 1
+    mv $O/txbench.log $O/txbench_inline.log
+    USN_TX_LISTS_LAUNCHES=1 TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh $S txbench || exit 1
+    mv $O/txbench.log $O/txbench_launches.log
+    SCB_CFGS="c5 c2" SCB_VARIANTS="base scwpe4" bash tools/gpu.sh $S scb || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txprof
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -432,6 +432,9 @@ struct Replica {
   uint4 *learned = nullptr;
   uint32_t learned_cap = 0;
   uint32_t *counters = nullptr;   // TxArgs::counters
+  unsigned long long *lg = nullptr;   // TxArgs::lg, the inline lists' granules (epoch-tagged)
+  size_t lg_bytes = 0;
+  uint32_t tx_inline_launches = 0;    // tx launches that built their lists inline (diagnostics)
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
@@ -1764,7 +1767,7 @@ void usn_ctx_destroy(usn_ctx *c) {
     (void)hipDeviceSynchronize();
     for (void *p : {(void *)R.d_table, R.d_patch, (void *)R.d_bridge, (void *)R.d_bridge_set,
                     (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
-                    (void *)R.counters, (void *)R.listen})
+                    (void *)R.counters, (void *)R.listen, (void *)R.lg})
       if (p) (void)hipFree(p);
   }
   for (auto &kv : c->lists_ev)
@@ -2045,6 +2048,7 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
     HIPCHK(hipMemcpy(out10, R.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   out10[8] = R.epoch;
+  out10[9] = R.tx_inline_launches;
   return USN_OK;
 }
 
@@ -2163,6 +2167,22 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   return USN_OK;
 }
 
+/* granules and diag word of a result's scratch never used before may hold
+ * anything: zero them after every bind, and again when the geometry moves
+ * them (their place depends on the batch's frames and bins) */
+static int scratch_tail_zeroed(usn_ctx *c, const usn_result &r, uint64_t n, uint32_t nbins,
+                               hipStream_t s) {
+  const uint64_t geo = (n << 16) ^ nbins;
+  auto zi = c->scan_zeroed.find(r.scratch);
+  if (zi != c->scan_zeroed.end() && zi->second.tag == r.bind_tag && zi->second.geo == geo) return USN_OK;
+  c->scan_zeroed[r.scratch] = usn_ctx::Zeroed{r.bind_tag, geo};
+  void *p;
+  size_t bytes;
+  usn::scatter_tail(r.scratch, n, nbins, &p, &bytes);
+  HIPCHK(hipMemsetAsync(p, 0, bytes, s));
+  return USN_OK;
+}
+
 /* the per-endpoint scatter of `count` classified batches (after their
  * classify / tx launch, or after finalize recounted patched tiles) */
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
@@ -2237,18 +2257,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     sb.bin_off = r[k].bin_off;
     x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
     x.range_base[k + 1] = x.range_base[k] + sb.nranges;
-    // granules of a scratch never used before may hold anything: zero them
-    // after every bind, and again when the geometry moves them (their place
-    // depends on the batch's frames and bins)
-    const uint64_t geo = (as[k].n << 16) ^ x.nbins;
-    auto zi = c->scan_zeroed.find(r[k].scratch);
-    if (zi == c->scan_zeroed.end() || zi->second.tag != r[k].bind_tag || zi->second.geo != geo) {
-      c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo};
-      void *p;
-      size_t bytes;
-      usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
-      HIPCHK(hipMemsetAsync(p, 0, bytes, s));
-    }
+    { const int e = scratch_tail_zeroed(c, r[k], as[k].n, x.nbins, s); if (e) return e; }
   }
   // test hook (tests/test_gpu_scatter.py, read once per process):
   // USN_DEBUG_CORRUPT=1 adds 257 to bin 0 of batch 0's first count row, =2
@@ -2289,7 +2298,7 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
 
 /* device scratch of a tx batch of n frames on replica R; the epoch-tagged
  * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
-static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
+static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, size_t lg_bytes) {
   if (n > T.learned_frames) {
     if (T.learned) HIPCHK(hipFree(T.learned));
     T.learned = nullptr;
@@ -2308,6 +2317,14 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
     HIPCHK(hipMalloc(&T.counters, 8 * sizeof(uint32_t)));
     HIPCHK(hipMemset(T.counters, 0, 8 * sizeof(uint32_t)));
   }
+  if (lg_bytes > T.lg_bytes) {   // zeroed: no granule holds an epoch yet
+    if (T.lg) HIPCHK(hipFree(T.lg));
+    T.lg = nullptr;
+    T.lg_bytes = 0;
+    HIPCHK(hipMalloc(&T.lg, lg_bytes));
+    HIPCHK(hipMemset(T.lg, 0, lg_bytes));
+    T.lg_bytes = lg_bytes;
+  }
   const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
   bool clear = false;
   if (slots > T.set_slots) {
@@ -2325,6 +2342,7 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
     HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
     HIPCHK(hipMemset(T.counters + 3, 0, sizeof(uint32_t)));
+    if (T.lg) HIPCHK(hipMemset(T.lg, 0, T.lg_bytes));
     T.epoch = 1;
   }
   return USN_OK;
@@ -2437,9 +2455,11 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     }
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
+  bool tx_inline = false;   // tx: the per-endpoint lists built inside the tx launch
   if (tx) {
     const usn_batch &tb = b[0];
-    int st = tx_prepare(R, tb.n, m.b[0].ntiles);
+    const size_t lg_bytes = ((size_t)m.b[0].ntiles * (m.b[0].nbw / 2 + m.b[0].nbw) + m.b[0].nbw) * 8;
+    int st = tx_prepare(R, tb.n, m.b[0].ntiles, lg_bytes);
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
@@ -2458,6 +2478,21 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
+    // USN_TX_LISTS_LAUNCHES (A/B) and the USN_DEBUG_CORRUPT test hook: the
+    // lists by the scan and scatter launches
+    static const bool inline_off = std::getenv("USN_TX_LISTS_LAUNCHES") != nullptr ||
+                                   std::getenv("USN_DEBUG_CORRUPT") != nullptr;
+    t.lists_inline = !inline_off && (c->tx512 ? usn_t512::tx_lists_fit(t) : usn::tx_lists_fit(t));
+    if (t.lists_inline) {
+      t.index = r[0].index;
+      t.bin_off = r[0].bin_off;
+      t.diag = usn::scatter_diag(r[0].scratch, tb.n, t.a.nbins);
+      t.lg = R.lg;
+      st = scratch_tail_zeroed(c, r[0], tb.n, t.a.nbins, (hipStream_t)stream);
+      if (st) return st;
+      tx_inline = true;
+      ++R.tx_inline_launches;
+    }
     if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
     else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
     c->tx.pending = true;
@@ -2492,8 +2527,20 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       // previous tx batch's kernels are done: its usn_finalize synchronised)
       reinterpret_cast<volatile uint32_t *>(c->h_txstate)[11] = 0;
     }
-    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
-    if (st) return st;
+    if (tx_inline) {   // the lists are built: one wave gathers what usn_finalize reads first
+      usn::TxState xs;
+      xs.out = txs;
+      xs.counters = R.counters;
+      xs.sum = r[0].summary;
+      xs.bin_off = r[0].bin_off;
+      xs.diag = usn::scatter_diag(r[0].scratch, b[0].n, m.b[0].nbins);
+      xs.n = (uint32_t)b[0].n;
+      xs.n_ep = m.b[0].n_ep;
+      HIPCHK(usn_t512::launch_txstate(xs, (hipStream_t)stream));
+    } else {
+      int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
+      if (st) return st;
+    }
     if (tx) {
       if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
       HIPCHK(hipEventRecord(R.txstate_ev, (hipStream_t)stream));
@@ -3228,8 +3275,8 @@ int64_t usn_debug_scatter_fallbacks(usn_ctx *c) {
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->reps[c->sel].device));
   HIPCHK(hipDeviceSynchronize());
-  const uint32_t v = usn_t512::scatter_fallbacks();
-  return v == 0xFFFFFFFFu ? (int64_t)USN_EHIP : (int64_t)v;
+  const uint32_t v = usn_t512::scatter_fallbacks(), w = usn::scatter_fallbacks();
+  return v == 0xFFFFFFFFu || w == 0xFFFFFFFFu ? (int64_t)USN_EHIP : (int64_t)v + w;
 }
 
 int usn_set_lists_async(usn_ctx *c, int on) {
