@@ -243,10 +243,7 @@ def test_c4tx_more_tiles_than_resident(coracle_mod):
 
 
 def _tx_inline_launches(ctx):
-    import ctypes
-    out = (ctypes.c_uint32 * 10)()
-    assert ctx.L.usn_debug_tx_state(ctx.h, out) == 0
-    return int(out[9])
+    return ctx.lists_inline()[1]
 
 
 @pytest.mark.parametrize("n", [3000, 1 << 20])

@@ -42,7 +42,8 @@ for s in "$@"; do
         F=$(python3 -c "import bench; print(bench.launch_frames('$c'))")
         pmc_pass pmcf_$c FETCH_SIZE python3 bench.py --config $c --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
         pmc_pass pmcw_$c WRITE_SIZE python3 bench.py --config $c --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
-        step pmct_$c 60 python3 tools/pmc_traffic.py $O/pmcf_$c $O/pmcw_$c $F $O/pmc_$c.json
+        FF=""; [ $c = c3 ] && FF="classify_rx_kernel=1"   # one 64-B request per 2048-B slot
+        step pmct_$c 60 python3 tools/pmc_traffic.py $O/pmcf_$c $O/pmcw_$c $F $O/pmc_$c.json $FF
       done ;;
     txbench) step txbench 300 python tools/txbench.py ${TXB_ARGS:-1048576 12 1} ;;
     txprof) rm -rf $O/txprof

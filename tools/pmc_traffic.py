@@ -11,7 +11,12 @@ per-endpoint scatter (scan_kernel, scatter_kernel): the
 counters of every dispatch of these kernels are summed per kernel name and
 divided by the number of classify / tx dispatches covering `frames` frames
 (every call of the run has that shape).
-usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json>"""
+usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json> [KERNEL=F ...]
+KERNEL=F: that kernel's FETCH_SIZE counted xF instead of x2.  c3's classify
+reads one window per 2048-byte slot inside the first 64-byte half of a line:
+a 64-byte EA request, which FETCH_SIZE (= TCC_EA0_RDREQ x 64 B) counts
+exactly, so c3 uses classify_rx_kernel=1 (calibration: tools/stride_floor.hip
+under --pmc, profiles/r04/r04a/stride_floor_pmc.json)."""
 import csv
 import glob
 import json
@@ -43,11 +48,15 @@ def per_kernel(d, counter, frames):
 
 def main():
     fd, wd, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    factor = {}
+    for kv in sys.argv[5:]:
+        k, f = kv.split("=", 1)
+        factor[k] = float(f)
     fetch, nf = per_kernel(fd, "FETCH_SIZE", frames)
     write, nw = per_kernel(wd, "WRITE_SIZE", frames)
     if not nf or not nw:
         sys.exit("no classify dispatch of %d frames in %s / %s" % (frames, fd, wd))
-    rd = {k: 2 * v * 1024 / nf for k, v in fetch.items()}
+    rd = {k: factor.get(k, 2.0) * v * 1024 / nf for k, v in fetch.items()}
     wr = {k: v * 1024 / nw for k, v in write.items()}
     read_algo = frames * (64 + 2)
     write_algo = frames * (4 + 4)
@@ -63,7 +72,8 @@ def main():
         "fetch_vs_algorithmic": round(sum(rd.values()) / read_algo, 4),
         "write_vs_algorithmic": round(sum(wr.values()) / write_algo, 4),
         "traffic_vs_algorithmic": round((sum(rd.values()) + sum(wr.values())) / (frames * 74), 4),
-        "correction": "FETCH_SIZE x2 (gfx950, 128-B requests tallied at 64 B), WRITE_SIZE x1",
+        "correction": "FETCH_SIZE x2 (gfx950, 128-B requests tallied at 64 B), WRITE_SIZE x1" +
+                      "".join("; %s FETCH_SIZE x%g" % (k, f) for k, f in sorted(factor.items())),
     }
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:

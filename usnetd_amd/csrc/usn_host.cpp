@@ -435,6 +435,7 @@ struct Replica {
   unsigned long long *lg = nullptr;   // TxArgs::lg, the inline lists' granules (epoch-tagged)
   size_t lg_bytes = 0;
   uint32_t tx_inline_launches = 0;    // tx launches that built their lists inline (diagnostics)
+  uint32_t rx_inline_launches = 0;    // classify launches that built their lists inline
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
@@ -520,7 +521,8 @@ struct usn_ctx {
   /* per classified batch (by its decisions): the replica it ran on and its
    * bin count (endpoints can be added before its usn_finalize: the batch's
    * scratch, count rows and lists keep the bins it was classified with) */
-  struct BatchRec { uint32_t rep, nbins; };
+  struct BatchRec { uint32_t rep, nbins; bool inl; };   // inl: lists built by the classify launch
+  bool rx_inline = std::getenv("USN_RX_LISTS_LAUNCHES") == nullptr;   // A/B: lists by the launches
   std::unordered_map<const void *, BatchRec> batch_rep;
   /* usn_set_lists_async: lists built on the replica's side stream; each
    * result's `lists done` event (keyed by its decisions array, created on
@@ -530,7 +532,10 @@ struct usn_ctx {
   std::unordered_map<const void *, ListsEv> lists_ev;
   /* the scatter's scan: a tag per launch for its range granules (random
    * start), and the result scratches whose granules were zeroed */
-  uint32_t scan_epoch = (uint32_t)std::random_device{}();
+  /* granule tags of the lists' scans (scan_kernel and the inline lists), in
+   * [2^31, 2^32): never 0 (zeroed granules) and never a count or offset (an
+   * inline G1 granule lives where the scan's agg rows are) */
+  uint32_t scan_epoch = (uint32_t)std::random_device{}() | 0x80000000u;
   /* per scratch: the bind tag and geometry (frames, bins) its granules were
    * last zeroed for (one entry per scratch, not per geometry) */
   struct Zeroed { uint32_t tag; uint64_t geo; };
@@ -1622,11 +1627,14 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
  * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
- * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized
- * for one-tile chunks: a launch picks its chunk length (launch_scatter) */
+ * gran[nranges][nbw] u64 | inl[ntiles][nbw] u64 | diag u32.  agg and gran
+ * are sized for one-tile chunks: a launch picks its chunk length
+ * (launch_scatter).  inl (batches of at most USN_INLINE_MAX_TILES tiles):
+ * G2 of the lists a classify launch builds itself (usn_device.hip
+ * inline_lists; G1 lives in agg, G3 in gran). */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, agg, tot, gran, diag, total;
+  size_t cnt, agg, tot, gran, inl, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
@@ -1639,6 +1647,7 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.gran = o; o = a256(o + ranges * g.nbw * 8);
+  g.inl = o; o = a256(o + (g.ntiles <= USN_INLINE_MAX_TILES ? (size_t)g.ntiles * g.nbw * 8 : 0));
   g.diag = o; o = a256(o + 4);
   g.total = o;
   return g;
@@ -1660,7 +1669,16 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.nchunks = (g.ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
 }
-/* the scan's diag word of a batch's scratch (bit 0: a wait timed out) */
+/* the granules of the lists a classify launch builds itself (G1 | G2 | G3) */
+void scatter_inline(void *scratch, uint64_t n, uint32_t nbins, unsigned long long **g1,
+                    unsigned long long **g2, unsigned long long **g3) {
+  const ScatterGeom g = scatter_geom(n, nbins);
+  uint8_t *p = static_cast<uint8_t *>(scratch);
+  *g1 = reinterpret_cast<unsigned long long *>(p + g.agg);
+  *g2 = reinterpret_cast<unsigned long long *>(p + g.inl);
+  *g3 = reinterpret_cast<unsigned long long *>(p + g.gran);
+}
+/* the scan's diag word of a batch's scratch (USN_DIAG_*) */
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
   return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(n, nbins).diag);
 }
@@ -2052,6 +2070,17 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
   return USN_OK;
 }
 
+/* diagnostics: launches of the selected replica that built their
+ * per-endpoint lists themselves: out2[0] classify, out2[1] tx */
+int usn_debug_lists_inline(usn_ctx *c, uint32_t *out2) {
+  if (!c || !out2 || c->reps.empty()) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  const Replica &R = c->reps[c->sel];
+  out2[0] = R.rx_inline_launches;
+  out2[1] = R.tx_inline_launches;
+  return USN_OK;
+}
+
 int usn_cache_clear(usn_ctx *c, uint16_t ep) {
   if (!c || ep >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -2167,6 +2196,11 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   return USN_OK;
 }
 
+static uint32_t next_scan_epoch(usn_ctx *c) {
+  if (++c->scan_epoch == 0) c->scan_epoch = 0x80000000u;
+  return c->scan_epoch;
+}
+
 /* granules and diag word of a result's scratch never used before may hold
  * anything: zero them after every bind, and again when the geometry moves
  * them (their place depends on the batch's frames and bins) */
@@ -2246,8 +2280,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.txs_out = txs_out;
   x.txs_counters = txs_counters;
   x.txs_sum = r[0].summary;
-  if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
-  x.epoch = c->scan_epoch;
+  x.epoch = next_scan_epoch(c);
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
@@ -2509,12 +2542,33 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         it->second.pending = false;
       }
     }
-    if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
-      HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
-    else
-      HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+    const bool t512 = c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units));
+    // small launches (every tile resident at once) build their lists
+    // themselves: no scan / scatter launch behind them
+    static const bool corrupt_hook = std::getenv("USN_DEBUG_CORRUPT") != nullptr;
+    if (c->rx_inline && !corrupt_hook &&
+        (t512 ? usn_t512::classify_lists_fit(m) : usn::classify_lists_fit(m))) {
+      const uint32_t ep = next_scan_epoch(c);
+      for (uint32_t k = 0; k < count; ++k) {
+        ClassifyArgs &a = m.b[k];
+        a.index = r[k].index;
+        a.bin_off = r[k].bin_off;
+        a.diag = usn::scatter_diag(r[k].scratch, a.n, a.nbins);
+        usn::scatter_inline(r[k].scratch, a.n, a.nbins, &a.lg1, &a.lg2, &a.lg3);
+        a.lepoch = ep;
+        int st = scratch_tail_zeroed(c, r[k], a.n, a.nbins, (hipStream_t)stream);
+        if (st) return st;
+      }
+      m.lists_inline = 1;
+      ++R.rx_inline_launches;
+    }
+    if (t512) HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
+    else HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
-  if (tx || !c->lists_async) {
+  if (!tx && m.lists_inline) {
+    // the lists are built (a result whose lists a side stream still builds
+    // was waited for above)
+  } else if (tx || !c->lists_async) {
     uint32_t *txs = nullptr;
     if (tx) {   // what usn_finalize reads first: written into host memory by the scatter's chunk 0
       if (!c->h_txstate) {
@@ -2582,7 +2636,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
-    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins};
+    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins, m.lists_inline != 0};
   }
   return USN_OK;
 }
@@ -2699,7 +2753,8 @@ int lists_check(uint32_t *d_diag, hipStream_t s) {
 
 int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
                       usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
-                      const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr) {
+                      const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr,
+                      uint32_t *diag_out = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
   const size_t need = sizeof(usn_summary) + tb + 32 + 4;
   if (need > c->h_stage_cap) {
@@ -2724,6 +2779,7 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   if (d_diag) {
     uint32_t dg;
     std::memcpy(&dg, p + sizeof(usn_summary) + tb + 32, 4);
+    if (diag_out) { *diag_out = dg; return USN_OK; }   // the caller decides
     return lists_failed(dg, d_diag, s);
   }
   return USN_OK;
@@ -3105,8 +3161,22 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   {
-    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr,
-                                    usn::scatter_diag(r->scratch, b->n, nb0));
+    uint32_t *d_diag = usn::scatter_diag(r->scratch, b->n, nb0), dg = 0;
+    int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr, d_diag, &dg);
+    if (e) return e;
+    if (dg == USN_DIAG_TIMEOUT && br != c->batch_rep.end() && br->second.inl) {
+      // a wait of the launch's inline lists gave up (never seen): the lists
+      // again by the scan and scatter launches
+      HIPCHK(hipMemsetAsync(d_diag, 0, 4, s));
+      ClassifyArgs a;
+      fill_args(c, c->reps[rep], b, r, a);
+      set_bins(r, b->n, nb0, a);
+      e = launch_scatter(c, &a, r, 1, s);
+      if (e) return e;
+      e = lists_check(d_diag, s);
+    } else {
+      e = lists_failed(dg, d_diag, s);
+    }
     if (e) return e;
   }
   usn_finalize_info fi;
