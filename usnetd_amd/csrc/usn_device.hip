@@ -1004,6 +1004,7 @@ struct InlineG {
   unsigned long long *g1, *g2, *g3;
   uint32_t *index, *bin_off, *diag;
   uint32_t epoch;
+  uint32_t flags;   // USN_SCF_SLOW_RANK (test hook): the ballot ranks as well
 };
 /* chunks / tiles whose ranks were redone by ballots (usn_debug_scatter_fallbacks) */
 __device__ uint32_t usn_scatter_fallbacks = 0;
@@ -1122,7 +1123,8 @@ __device__ __forceinline__ void inline_lists(const ClassifyArgs &a, const Inline
     const uint32_t p = q ? stage[q - 1] : 0u;
     unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
   }
-  if (__syncthreads_or(unsorted)) {   // (not seen on gfx950) ballot ranks, then the stage again
+  if (__syncthreads_or(unsorted || (g.flags & USN_SCF_SLOW_RANK))) {   // (not seen on gfx950)
+    // ballot ranks, then the stage again
     if (tid == 0) {   // cursors back to the bins' starts in the tile
       uint32_t run = 0;
       for (uint32_t b = 0; b < nbw; ++b) {
@@ -1702,7 +1704,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
                                                            : TM == TM_DISPLDS ? table_lds_units(disp_lds_units(a))
                                                                               : 0u));
       uint32_t *off = stage + TILE;
-      const InlineG g{a.lg1, a.lg2, a.lg3, a.index, a.bin_off, a.diag, a.lepoch};
+      const InlineG g{a.lg1, a.lg2, a.lg3, a.index, a.bin_off, a.diag, a.lepoch, a.lflags};
       RxPoll poll{a.lepoch, a.diag};
       inline_lists(a, g, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw), poll);
     }
@@ -2850,7 +2852,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (t.lists_inline) {   // the records' LDS is free: stage | offsets | cursors
     uint32_t *stage = reinterpret_cast<uint32_t *>(srec);
     uint32_t *off = stage + TILE;
-    const InlineG g{tx_g1(t), tx_g2(t), tx_g3(t), t.index, t.bin_off, t.diag, t.epoch};
+    const InlineG g{tx_g1(t), tx_g2(t), tx_g3(t), t.index, t.bin_off, t.diag, t.epoch, a.lflags};
     TxPoll poll{t};
     inline_lists(a, g, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw), poll);
   }

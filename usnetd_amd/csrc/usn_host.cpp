@@ -2196,6 +2196,13 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   return USN_OK;
 }
 
+/* test hook USN_SCATTER_SLOW_RANK=1 (read once): every chunk / inline tile
+ * also ranks by ballots and writes its stage out again */
+static bool slow_rank_hook() {
+  static const bool on = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
+  return on;
+}
+
 static uint32_t next_scan_epoch(usn_ctx *c) {
   if (++c->scan_epoch == 0) c->scan_epoch = 0x80000000u;
   return c->scan_epoch;
@@ -2260,8 +2267,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   if (!noscan)
     while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
-  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
+  x.flags = (slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = std::getenv("USN_SCAN_CPT");
@@ -2521,6 +2527,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       t.bin_off = r[0].bin_off;
       t.diag = usn::scatter_diag(r[0].scratch, tb.n, t.a.nbins);
       t.lg = R.lg;
+      t.a.lflags = slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u;
       st = scratch_tail_zeroed(c, r[0], tb.n, t.a.nbins, (hipStream_t)stream);
       if (st) return st;
       tx_inline = true;
@@ -2556,6 +2563,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         a.diag = usn::scatter_diag(r[k].scratch, a.n, a.nbins);
         usn::scatter_inline(r[k].scratch, a.n, a.nbins, &a.lg1, &a.lg2, &a.lg3);
         a.lepoch = ep;
+        a.lflags = slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u;
         int st = scratch_tail_zeroed(c, r[k], a.n, a.nbins, (hipStream_t)stream);
         if (st) return st;
       }

@@ -63,6 +63,7 @@ struct ClassifyArgs {
   uint32_t *index, *bin_off, *diag;
   unsigned long long *lg1, *lg2, *lg3;
   uint32_t lepoch;
+  uint32_t lflags;          /* USN_SCF_SLOW_RANK: the inline lists also rank by ballots (test hook) */
 };
 
 /* Several batches (distinct sources) classified by one launch: workgroup w

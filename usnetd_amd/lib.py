@@ -387,7 +387,10 @@ class Ctx:
         per-endpoint lists themselves (every tile resident: no scan /
         scatter launch; usn_debug_lists_inline)."""
         out = (C.c_uint32 * 2)()
-        check(self.L.usn_debug_lists_inline(self.h, out), "usn_debug_lists_inline")
+        f = self.L.usn_debug_lists_inline
+        f.argtypes = [C.c_void_p, C.c_void_p]
+        f.restype = C.c_int
+        check(f(self.h, out), "usn_debug_lists_inline")
         return int(out[0]), int(out[1])
 
     def lists_wait(self, result: "DeviceResult", stream=None):
