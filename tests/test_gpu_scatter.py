@@ -191,67 +191,3 @@ def test_scatter_reports_inconsistent_counts(mode):
         assert " error " in line and "ELIST" in line, line
     assert len(lines) == 4, lines
 
-
-INLINE_CHILD = r"""
-import sys, ctypes as C, numpy as np
-sys.path[:0] = [%(root)r, %(root)r + '/oracle', %(root)r + '/tests']
-import coracle, katrun
-from usnetd_amd import lib, traffic
-coracle.build()
-# (config, frames per ring, rings per call): c3 as the bench calls it (4 x
-# 256K IMIX rings in 2 KiB slots = 1024 tiles), c2 at one 1M ring, c5 with
-# 1005 bins at 2 x 64K, c4 at 3 rings of 100K (a ragged last tile)
-for name, n, rings in (("c3", 1 << 18, 4), ("c2", 1 << 20, 1), ("c5", 1 << 16, 2), ("c4", 100000, 3)):
-    ctx = lib.Ctx(0)
-    cfg0 = traffic.config(name, n=n, seed=11)
-    traffic.install_ctx(ctx, cfg0)
-    nics = [cfg0.src] + traffic.extra_nics(cfg0, rings - 1, ctx)
-    o = coracle.Oracle()
-    coracle.install_oracle(o, cfg0)
-    for nid in nics[1:]:
-        o.add_endpoint(nid, 0, -1)
-    cfgs = [traffic.config(name, n=n, seed=11 + k) for k in range(rings)]
-    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[k], stride=c.stride) for k, c in enumerate(cfgs)]
-    rs = [lib.DeviceResult(ctx, n) for _ in cfgs]
-    s = ctx.stream()
-    ba = (lib.Batch * rings)(*[b.desc for b in bs])
-    ra = (lib.Result * rings)(*[r.desc for r in rs])
-    lib.check(ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), rings, s))
-    for k, c in enumerate(cfgs):
-        ctx.finalize(bs[k], rs[k], s)
-        want = o.forward_batch(nics[k], c.frames, c.lens, stride=c.stride)
-        got = rs[k].decisions()
-        assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK), (name, k)
-        n_ep = int(rs[k].summary()["n_ep"])
-        assert np.array_equal(rs[k].index(n), np.argsort(lib.dec_bin(want, n_ep), kind="stable").astype(np.uint32)), (name, k)
-    print(name, "inline", ctx.lists_inline()[0], "fallbacks", ctx.scatter_fallbacks(), flush=True)
-    for x in bs + rs:
-        x.free()
-    ctx.close()
-print("ok")
-"""
-
-
-@pytest.mark.parametrize("launches", [False, True])
-def test_small_launch_lists_inline(launches):
-    """A classify launch whose tiles are all resident builds its own lists
-    (inline_lists: the tiles hand their counts on through epoch-tagged
-    granules; no scan or scatter launch): c3's 4 x 256K-frame call, a 1M c2
-    ring, c5's 1005 bins, c4 with ragged rings -- lists equal the oracle's
-    stable sort by bin.  USN_RX_LISTS_LAUNCHES=1 (read once per process)
-    takes the scan + scatter launches for the same calls."""
-    env = dict(os.environ)
-    if launches:
-        env["USN_RX_LISTS_LAUNCHES"] = "1"
-    p = subprocess.run([sys.executable, "-c", INLINE_CHILD % {"root": ROOT}], env=env,
-                       capture_output=True, text=True, timeout=280)
-    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
-    lines = p.stdout.strip().splitlines()
-    assert lines[-1] == "ok", p.stdout
-    for line in lines[:-1]:
-        name, _, inl, _, fb = line.split()
-        assert int(fb) == 0, line
-        if launches:
-            assert int(inl) == 0, line
-        elif name in ("c3", "c2"):
-            assert int(inl) == 1, line

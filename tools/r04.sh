@@ -35,6 +35,20 @@ case $S in
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txprof
     ;;
+  r04c)
+    # tx inline lists with one polling wave per tile; rx inline removed (slower,
+    # and two concurrent launches could each hold half the CUs); the suite,
+    # tx ring timing inline vs launches, c3 PMC traffic with the x1 classify
+    # fetch factor, the default bench
+    bash tools/gpu.sh $S testsall || exit 1
+    TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh $S txbench || exit 1
+    mv $O/txbench.log $O/txbench_inline.log
+    USN_TX_LISTS_LAUNCHES=1 TXB_ARGS="1048576 40 1 --rotate 6" bash tools/gpu.sh $S txbench || exit 1
+    mv $O/txbench.log $O/txbench_launches.log
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txprof || exit 1
+    PMC_CFGS="c3" bash tools/gpu.sh $S pmc || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

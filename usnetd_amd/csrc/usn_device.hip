@@ -980,221 +980,6 @@ __device__ __forceinline__ void g_put(unsigned long long *g, uint32_t epoch, uin
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* ---- per-endpoint lists built inside the classify / tx launch -------------
- * When every tile of a launch is resident at once (the host checks the grid
- * against the occupancy query: launch_tx / launch_classify), the scan that
- * scan_kernel + scatter_kernel do in two more launches is done by hand-offs
- * between the tiles of each batch, through epoch-tagged granules {epoch,
- * value} (sc1 stores and loads, MI355X guide Guideline 16 R2):
- *   P1  each tile publishes its count row: G1[tile][pair] = the u16 counts
- *       of bins 2 pair, 2 pair + 1;
- *   P2  tile t scans pairs t, t + ntiles, ... over the batch's tiles:
- *       G2[u][bin] = the bin's frames in tiles before u, G3[bin] = its frames;
- *   P3  each tile takes its row of G2 and all of G3: the bin bases (an
- *       exclusive scan of G3 over bins) and its offsets; one wave ranks the
- *       tile's frames into a (bin, frame)-sorted LDS stage with one LDS atomic
- *       each (the scatter kernel's ranks: checked, and redone by ballots when
- *       not stably sorted), and the stage goes out as the tile's runs of index.
- * Every store is bounds-checked; a count that disagrees with the decisions
- * sets USN_DIAG_LISTS.  A wait that times out gives up (the poller's policy:
- * the tx kernel marks the batch for the host stage, the classify kernel sets
- * USN_DIAG_TIMEOUT and usn_finalize rebuilds the lists by the launches). */
-#define INL_TPT 4   /* tiles per thread in P2: a batch of <= INL_TPT * NTHREADS tiles */
-struct InlineG {
-  unsigned long long *g1, *g2, *g3;
-  uint32_t *index, *bin_off, *diag;
-  uint32_t epoch;
-  uint32_t flags;   // USN_SCF_SLOW_RANK (test hook): the ballot ranks as well
-};
-/* chunks / tiles whose ranks were redone by ballots (usn_debug_scatter_fallbacks) */
-__device__ uint32_t usn_scatter_fallbacks = 0;
-
-__host__ __device__ inline size_t inline_lds_bytes(uint32_t nbw) {   /* stage | offsets | cursors */
-  return (size_t)TILE * 4 + (size_t)nbw * 4 + (size_t)nbw * 2;
-}
-
-template <class Poll>
-__device__ __forceinline__ void inline_lists(const ClassifyArgs &a, const InlineG &g, uint32_t tile,
-                                             uint32_t nt, const Lds &L, const uint16_t *bins16,
-                                             uint32_t *stage, uint32_t *off, uint16_t *cur, Poll &poll) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nbw = a.nbw, np = nbw / 2, ntiles = a.ntiles;
-  // P1 (the histogram is complete: a barrier after tile_hist)
-  for (uint32_t k = tid; k < np; k += NTHREADS) g_put(g.g1 + (size_t)tile * np + k, g.epoch, L.hist[k]);
-  // P2: this tile's pairs, thread k holding tiles k*TPT .. k*TPT + TPT - 1
-  for (uint32_t pr = tile; pr < np; pr += ntiles) {
-    uint32_t lo[INL_TPT], hi[INL_TPT], slo = 0, shi = 0, v[INL_TPT];
-    const unsigned long long *gp[INL_TPT];
-#pragma unroll
-    for (uint32_t j = 0; j < INL_TPT; ++j) {
-      const uint32_t u = tid * INL_TPT + j;
-      gp[j] = u < ntiles ? g.g1 + (size_t)u * np + pr : nullptr;
-    }
-    poll(gp, v);   // false: gave up (values unused beyond bounds-checked stores)
-#pragma unroll
-    for (uint32_t j = 0; j < INL_TPT; ++j) {
-      lo[j] = v[j] & 0xFFFFu;
-      hi[j] = v[j] >> 16;
-      slo += lo[j];
-      shi += hi[j];
-    }
-    uint32_t tlo, thi;
-    uint32_t elo = block_excl_scan(slo, L.scratch, &tlo);
-    uint32_t ehi = block_excl_scan(shi, L.scratch, &thi);
-#pragma unroll
-    for (uint32_t j = 0; j < INL_TPT; ++j) {
-      const uint32_t u = tid * INL_TPT + j;
-      if (u < ntiles) {
-        g_put(g.g2 + (size_t)u * nbw + 2 * pr, g.epoch, elo);
-        g_put(g.g2 + (size_t)u * nbw + 2 * pr + 1, g.epoch, ehi);
-      }
-      elo += lo[j];
-      ehi += hi[j];
-    }
-    if (tid == 0) {
-      g_put(g.g3 + 2 * pr, g.epoch, tlo);
-      g_put(g.g3 + 2 * pr + 1, g.epoch, thi);
-    }
-  }
-  // P3: this tile's offsets (thread k: bins 2k, 2k+1; nbw <= 2 NTHREADS)
-  {
-    const bool mine = 2 * tid < nbw;
-    uint32_t v[4] = {0, 0, 0, 0};
-    if (mine) {
-      const unsigned long long *gp[4] = {g.g2 + (size_t)tile * nbw + 2 * tid, g.g2 + (size_t)tile * nbw + 2 * tid + 1,
-                                         g.g3 + 2 * tid, g.g3 + 2 * tid + 1};
-      poll(gp, v);
-    }
-    const uint32_t hw = mine ? L.hist[tid] : 0u;
-    const uint32_t c0 = hw & 0xFFFFu, c1 = hw >> 16;
-    uint32_t total;
-    const uint32_t pt = block_excl_scan(v[2] + v[3], L.scratch, &total);   // bin bases
-    const uint32_t pc = block_excl_scan(c0 + c1, L.scratch, &total);       // the bins' starts in the tile
-    if (mine) {
-      const uint32_t b = 2 * tid;
-      off[b] = pt + v[0] - pc;
-      off[b + 1] = pt + v[2] + v[1] - (pc + c0);
-      reinterpret_cast<uint32_t *>(cur)[tid] = (pc & 0xFFFFu) | ((pc + c0) << 16);
-      if (tile == 0) {
-        if (b <= a.nbins) g.bin_off[b] = pt;
-        if (b + 1 <= a.nbins) g.bin_off[b + 1] = pt + v[2];
-      }
-    }
-    for (uint32_t q4 = tid; q4 < TILE / 4; q4 += NTHREADS)
-      reinterpret_cast<uint4 *>(stage)[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
-  }
-  __syncthreads();
-  // ranks: wave 0, the tile's 16 segments in order (one LDS atomic per frame)
-  bool bad = false;
-  if (wave == 0) {   // in two halves of 8 segments (the kernels' VGPR budget); a wave's
-                     // LDS operations execute in order either way
-    uint32_t *cw = reinterpret_cast<uint32_t *>(cur);
-#pragma unroll
-    for (uint32_t h = 0; h < TILE / 64; h += 8) {
-      uint32_t at[8];
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t f = (h + k) * 64 + lane;
-        const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u);
-        const uint32_t sh = 16u * (b & 1u);
-        at[k] = f < nt ? atomicAdd(&cw[b >> 1], 1u << sh) >> sh : 0u;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t f = (h + k) * 64 + lane;
-        if (f < nt) {
-          const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u), q = at[k] & 0xFFFFu;
-          bad |= q >= nt;
-          stage[min(q, (uint32_t)TILE - 1u)] = (b << 16) | f;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // the stage out in order: the tile's run of each bin at off[bin] + q
-  const uint64_t base = (uint64_t)tile * TILE;
-  bool unsorted = false;
-  for (uint32_t q = tid; q < nt; q += NTHREADS) {
-    const uint32_t e = stage[q];
-    const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
-    if (pos < a.n) g.index[pos] = (uint32_t)base + (e & 0xFFFFu);
-    bad |= pos >= a.n || e == ~0u;
-    const uint32_t p = q ? stage[q - 1] : 0u;
-    unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
-  }
-  if (__syncthreads_or(unsorted || (g.flags & USN_SCF_SLOW_RANK))) {   // (not seen on gfx950)
-    // ballot ranks, then the stage again
-    if (tid == 0) {   // cursors back to the bins' starts in the tile
-      uint32_t run = 0;
-      for (uint32_t b = 0; b < nbw; ++b) {
-        cur[b] = (uint16_t)run;
-        run += hist_get(L.hist, b);
-      }
-    }
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll 1
-      for (uint32_t k = 0; k < TILE / 64; ++k) {
-        const uint32_t local = k * 64 + lane;
-        const bool v = local < nt;
-        const uint32_t b = min((uint32_t)bins16[min(local, nt - 1)], a.nbins - 1u);
-        const uint64_t same = match_bin(b, __ballot(v), a.nbits);
-        const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
-        const uint32_t at = cur[b];
-        if (v) {
-          stage[min(at + rank, (uint32_t)TILE - 1u)] = (b << 16) | local;
-          if (rank == 0) cur[b] = (uint16_t)(at + __popcll(same));
-        }
-      }
-    }
-    __syncthreads();
-    for (uint32_t q = tid; q < nt; q += NTHREADS) {
-      const uint32_t e = stage[q];
-      const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
-      if (pos < a.n) g.index[pos] = (uint32_t)base + (e & 0xFFFFu);
-    }
-    if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
-  }
-  if (__ballot(bad) && lane == 0) atomicOr(g.diag, USN_DIAG_LISTS);
-  if (tile == 0 && tid == 0) g.bin_off[a.nbins] = (uint32_t)a.n;
-}
-
-/* the classify kernel's waits: bounded; a timeout sets USN_DIAG_TIMEOUT in the
- * batch's diag word (later waits then give up at once) and usn_finalize
- * rebuilds that batch's lists by the scan and scatter launches */
-#define INL_SPIN_TICKS (200u * 100000u)   /* 200 ms of the 100 MHz real-time clock */
-struct RxPoll {
-  uint32_t epoch;
-  uint32_t *diag;
-  template <int N>
-  __device__ __forceinline__ bool operator()(const unsigned long long *const (&g)[N], uint32_t (&v)[N]) {
-    uint64_t t0 = 0;
-    for (uint32_t it = 0;; ++it) {
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < N; ++k) {
-        const unsigned long long x =
-            g[k] ? __hip_atomic_load((gu64 *)g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                 : (unsigned long long)epoch << 32;
-        v[k] = (uint32_t)x;
-        ok &= (uint32_t)(x >> 32) == epoch;
-      }
-      if (ok) return true;
-      if (__hip_atomic_load((gu32 *)diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & USN_DIAG_TIMEOUT)
-        return false;
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (it == 0) {
-        t0 = now;
-      } else if (now - t0 > INL_SPIN_TICKS) {
-        atomicOr(diag, USN_DIAG_TIMEOUT);
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-};
-
 /* units of the displacements TM_DISPLDS copies to LDS: U's and X's when U is
  * built (one slot read per frame), else K1's and K2's */
 __host__ __device__ inline uint32_t disp_lds_units(const ClassifyArgs &a) {
@@ -1231,9 +1016,7 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 #else
 #define USN_RX_ATTR
 #endif
-/* INL: the launch builds its per-endpoint lists (m.lists_inline); its own
- * instantiation, so that the large launches' kernel is not changed by it */
-template <int TM, bool GLDS, bool INL>
+template <int TM, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
@@ -1693,21 +1476,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
       if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
     }
-    if (INL) {
-      // the lists by the launch (every tile resident): bins to the order row
-      // (the header stage's bytes when GLDS: every wave is past its stage
-      // reads at the barrier above), stage | offsets | cursors after the image
-#pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) L.order[r * NTHREADS + tid] = (uint16_t)bins[r];
-      uint32_t *stage = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(L.table) +
-                                                     16 * (TM == TM_LDS ? table_lds_units(a.table_units)
-                                                           : TM == TM_DISPLDS ? table_lds_units(disp_lds_units(a))
-                                                                              : 0u));
-      uint32_t *off = stage + TILE;
-      const InlineG g{a.lg1, a.lg2, a.lg3, a.index, a.bin_off, a.diag, a.lepoch, a.lflags};
-      RxPoll poll{a.lepoch, a.diag};
-      inline_lists(a, g, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw), poll);
-    }
     STAMP(11);
     STAMP_FLUSH_AT(w);
     if (!USN_PERSIST || w + gridDim.x >= ntiles_launch) break;
@@ -2081,35 +1849,6 @@ __device__ __forceinline__ bool g_getn(const unsigned long long *g, const TxArgs
   }
 }
 
-/* the same for N granules anywhere (g[k] == nullptr: none, v[k] = 0); the
- * loads of a poll fly together */
-template <int N>
-__device__ __forceinline__ bool g_getp(const unsigned long long *const (&g)[N], const TxArgs &t,
-                                       uint32_t (&v)[N]) {
-  uint64_t t0 = 0;
-  for (uint32_t it = 0;; ++it) {
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-      const unsigned long long x =
-          g[k] ? __hip_atomic_load((gu64 *)g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-               : (unsigned long long)t.epoch << 32;
-      v[k] = (uint32_t)x;
-      ok &= (uint32_t)(x >> 32) == t.epoch;
-    }
-    if (ok) return true;
-    if (tx_timed_out(t)) return false;
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (it == 0) {
-      t0 = now;
-    } else if (now - t0 > TX_SPIN_TICKS) {
-      atomicMax(t.counters + 3, t.epoch);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
 /* one read of granule g: true (and v) when it carries the batch epoch */
 __device__ __forceinline__ bool g_try(const unsigned long long *g, const TxArgs &t, uint32_t &v) {
   const unsigned long long x = __hip_atomic_load((gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2187,21 +1926,240 @@ __device__ __forceinline__ void tx_load_cin(const TxArgs &t, uint32_t *cin) {
   for (int k = 0; k < 6; ++k) cin[k] = ok ? v[k] : 0u;
 }
 
-/* the tx kernel's waits: give up once any wait of the batch has timed out
- * (the batch then goes to the host stage, which rebuilds the lists) */
-struct TxPoll {
-  const TxArgs &t;
-  template <int N>
-  __device__ __forceinline__ bool operator()(const unsigned long long *const (&g)[N], uint32_t (&v)[N]) {
-    return g_getp<N>(g, t, v);
-  }
-};
+/* ---- the per-endpoint lists inside the tx launch (TxArgs.lists_inline) ----
+ * When every tile of a tx batch is resident at once (tx_lists_fit checks the
+ * grid against the occupancy query), the scan that scan_kernel +
+ * scatter_kernel do in two more launches is done by hand-offs between the
+ * batch's tiles, through epoch-tagged granules (sc1 stores and loads, MI355X
+ * guide Guideline 16 R1/R2):
+ *   P1  each tile publishes its count row: G1[tile][pair] = the u16 counts
+ *       of bins 2 pair, 2 pair + 1 (each granule is its own flag);
+ *   P2  tile t scans pairs t, t + ntiles, ... over the tiles: one wave
+ *       gathers the pair's G1 granules of every tile into LDS, the block
+ *       scans them, G2[u][bin] = the bin's frames in tiles before u, G3[bin] =
+ *       its frames; then DONE[t] (after every wave drained its stores);
+ *   P3  one wave polls the DONE flags of the handler tiles, then the block
+ *       reads its row of G2 and all of G3: the bin bases (an exclusive scan of
+ *       G3 over bins) and its offsets; one wave ranks the tile's frames into a
+ *       (bin, frame)-sorted LDS stage with one LDS atomic each (the scatter
+ *       kernel's ranks: checked, and redone by ballots when not stably
+ *       sorted), and the stage goes out as the tile's runs of index.
+ * Polling is one wave per tile (every thread polling its own granules loaded
+ * the memory system enough to cost the launch 26 us per 1M-frame ring).  A
+ * wait that times out marks the batch as the kernel's other waits do
+ * (counters[3]): usn_finalize then decides it on the host and rebuilds the
+ * lists by the scan and scatter launches.  Every store is bounds-checked; a
+ * count that disagrees with the decisions sets USN_DIAG_LISTS. */
+#define TXL_TPT 4   /* tiles per thread in P2: a batch of <= TXL_TPT * NTHREADS tiles */
 __device__ __forceinline__ unsigned long long *tx_g1(const TxArgs &t) { return t.lg; }
 __device__ __forceinline__ unsigned long long *tx_g2(const TxArgs &t) {
   return t.lg + (size_t)t.a.ntiles * (t.a.nbw / 2);
 }
 __device__ __forceinline__ unsigned long long *tx_g3(const TxArgs &t) {
   return tx_g2(t) + (size_t)t.a.ntiles * t.a.nbw;
+}
+__device__ __forceinline__ unsigned long long *tx_done(const TxArgs &t) { return tx_g3(t) + t.a.nbw; }
+__host__ __device__ inline size_t tx_lists_lds_bytes(uint32_t nbw) {   /* stage | offsets | cursors */
+  return (size_t)TILE * 4 + (size_t)nbw * 4 + (size_t)nbw * 2;
+}
+/* chunks / tiles whose ranks were redone by ballots (usn_debug_scatter_fallbacks) */
+__device__ uint32_t usn_scatter_fallbacks = 0;
+
+/* one wave: out[u] = the value of granule g[u * stride] for u < count, once
+ * each carries the batch epoch (TXG_DEPTH per lane in flight per poll); false after
+ * a timeout of any wait of the batch */
+#define TXG_DEPTH 4   /* granules per lane in flight per poll (the kernel's VGPR budget) */
+__device__ __forceinline__ bool tx_gather(const TxArgs &t, const unsigned long long *g, uint32_t stride,
+                                          uint32_t count, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63;
+  bool ok = true;
+  for (uint32_t b0 = 0; b0 < count && ok; b0 += 64 * TXG_DEPTH) {
+    uint32_t pend = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < TXG_DEPTH; ++j) pend |= (b0 + j * 64 + lane < count ? 1u : 0u) << j;
+    uint64_t t0 = 0;
+    for (uint32_t it = 0; pend; ++it) {
+      unsigned long long x[TXG_DEPTH];
+#pragma unroll
+      for (uint32_t j = 0; j < TXG_DEPTH; ++j)
+        x[j] = ((pend >> j) & 1u)
+                   ? __hip_atomic_load((gu64 *)(g + (size_t)(b0 + j * 64 + lane) * stride), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT)
+                   : 0ull;
+#pragma unroll
+      for (uint32_t j = 0; j < TXG_DEPTH; ++j)
+        if (((pend >> j) & 1u) && (uint32_t)(x[j] >> 32) == t.epoch) {
+          out[b0 + j * 64 + lane] = (uint32_t)x[j];
+          pend &= ~(1u << j);
+        }
+      if (!pend) break;
+      if (tx_timed_out(t)) { ok = false; break; }
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (it == 0) {
+        t0 = now;
+      } else if (now - t0 > TX_SPIN_TICKS) {
+        atomicMax(t.counters + 3, t.epoch);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  return ok;
+}
+
+__device__ __forceinline__ void tx_lists(const TxArgs &t, uint32_t tile, uint32_t nt, const Lds &L,
+                                         const uint16_t *bins16, uint32_t *stage, uint32_t *off,
+                                         uint16_t *cur) {
+  const ClassifyArgs &a = t.a;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nbw = a.nbw, np = nbw / 2, ntiles = a.ntiles, nh = min(np, ntiles);
+  unsigned long long *G1 = tx_g1(t), *G2 = tx_g2(t), *G3 = tx_g3(t), *DONE = tx_done(t);
+  // P1 (the histogram is complete: a barrier after tile_hist)
+  for (uint32_t k = tid; k < np; k += NTHREADS) g_put(G1 + (size_t)tile * np + k, t.epoch, L.hist[k]);
+  // P2: this tile's pairs; the stage holds one pair's counts of every tile
+  for (uint32_t pr = tile; pr < np; pr += ntiles) {
+    if (wave == 0) tx_gather(t, G1 + pr, np, ntiles, stage);   // false: gave up (marked)
+    __syncthreads();
+    uint32_t lo[TXL_TPT], hi[TXL_TPT], slo = 0, shi = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < TXL_TPT; ++j) {
+      const uint32_t u = tid * TXL_TPT + j;
+      const uint32_t v = u < ntiles ? stage[u] : 0u;
+      lo[j] = v & 0xFFFFu;
+      hi[j] = v >> 16;
+      slo += lo[j];
+      shi += hi[j];
+    }
+    uint32_t tlo, thi;
+    uint32_t elo = block_excl_scan(slo, L.scratch, &tlo);   // (its barriers: the stage is free after)
+    uint32_t ehi = block_excl_scan(shi, L.scratch, &thi);
+#pragma unroll
+    for (uint32_t j = 0; j < TXL_TPT; ++j) {
+      const uint32_t u = tid * TXL_TPT + j;
+      if (u < ntiles) {
+        g_put(G2 + (size_t)u * nbw + 2 * pr, t.epoch, elo);
+        g_put(G2 + (size_t)u * nbw + 2 * pr + 1, t.epoch, ehi);
+      }
+      elo += lo[j];
+      ehi += hi[j];
+    }
+    if (tid == 0) {
+      g_put(G3 + 2 * pr, t.epoch, tlo);
+      g_put(G3 + 2 * pr + 1, t.epoch, thi);
+    }
+  }
+  if (tile < nh) {   // DONE after every wave's G2 / G3 stores have landed (R1)
+    vm_drain();
+    __syncthreads();
+    if (tid == 0) g_put(DONE + tile, t.epoch, 1u);
+  }
+  // P3: the handlers are done; then this tile's offsets (thread k: bins 2k, 2k+1)
+  if (wave == 0) tx_gather(t, DONE, 1, nh, reinterpret_cast<uint32_t *>(off));   // (values unused)
+  __syncthreads();
+  {
+    const bool mine = 2 * tid < nbw;
+    uint32_t v[4] = {0, 0, 0, 0};
+    if (mine) {
+      const unsigned long long *gp[4] = {G2 + (size_t)tile * nbw + 2 * tid, G2 + (size_t)tile * nbw + 2 * tid + 1,
+                                         G3 + 2 * tid, G3 + 2 * tid + 1};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[k] = (uint32_t)__hip_atomic_load((gu64 *)gp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t hw = mine ? L.hist[tid] : 0u;
+    const uint32_t c0 = hw & 0xFFFFu, c1 = hw >> 16;
+    uint32_t total;
+    const uint32_t pt = block_excl_scan(v[2] + v[3], L.scratch, &total);   // bin bases
+    const uint32_t pc = block_excl_scan(c0 + c1, L.scratch, &total);       // the bins' starts in the tile
+    if (mine) {
+      const uint32_t b = 2 * tid;
+      off[b] = pt + v[0] - pc;
+      off[b + 1] = pt + v[2] + v[1] - (pc + c0);
+      reinterpret_cast<uint32_t *>(cur)[tid] = (pc & 0xFFFFu) | ((pc + c0) << 16);
+      if (tile == 0) {
+        if (b <= a.nbins) t.bin_off[b] = pt;
+        if (b + 1 <= a.nbins) t.bin_off[b + 1] = pt + v[2];
+      }
+    }
+    for (uint32_t q4 = tid; q4 < TILE / 4; q4 += NTHREADS)
+      reinterpret_cast<uint4 *>(stage)[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+  __syncthreads();
+  // ranks: wave 0, the tile's 16 segments in order (one LDS atomic per frame)
+  bool bad = false;
+  if (wave == 0) {   // in two halves of 8 segments (the kernel's VGPR budget); a wave's
+                     // LDS operations execute in order either way
+    uint32_t *cw = reinterpret_cast<uint32_t *>(cur);
+#pragma unroll
+    for (uint32_t h = 0; h < TILE / 64; h += 8) {
+      uint32_t at[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t f = (h + k) * 64 + lane;
+        const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u);
+        const uint32_t sh = 16u * (b & 1u);
+        at[k] = f < nt ? atomicAdd(&cw[b >> 1], 1u << sh) >> sh : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t f = (h + k) * 64 + lane;
+        if (f < nt) {
+          const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u), q = at[k] & 0xFFFFu;
+          bad |= q >= nt;
+          stage[min(q, (uint32_t)TILE - 1u)] = (b << 16) | f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // the stage out in order: the tile's run of each bin at off[bin] + q
+  const uint64_t base = (uint64_t)tile * TILE;
+  bool unsorted = false;
+  for (uint32_t q = tid; q < nt; q += NTHREADS) {
+    const uint32_t e = stage[q];
+    const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
+    if (pos < a.n) t.index[pos] = (uint32_t)base + (e & 0xFFFFu);
+    bad |= pos >= a.n || e == ~0u;
+    const uint32_t p = q ? stage[q - 1] : 0u;
+    unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
+  }
+  if (__syncthreads_or(unsorted || (a.lflags & USN_SCF_SLOW_RANK))) {   // (not seen on gfx950)
+    // ballot ranks, then the stage again
+    if (tid == 0) {   // cursors back to the bins' starts in the tile
+      uint32_t run = 0;
+      for (uint32_t b = 0; b < nbw; ++b) {
+        cur[b] = (uint16_t)run;
+        run += hist_get(L.hist, b);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll 1
+      for (uint32_t k = 0; k < TILE / 64; ++k) {
+        const uint32_t local = k * 64 + lane;
+        const bool v = local < nt;
+        const uint32_t b = min((uint32_t)bins16[min(local, nt - 1)], a.nbins - 1u);
+        const uint64_t same = match_bin(b, __ballot(v), a.nbits);
+        const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
+        const uint32_t at = cur[b];
+        if (v) {
+          stage[min(at + rank, (uint32_t)TILE - 1u)] = (b << 16) | local;
+          if (rank == 0) cur[b] = (uint16_t)(at + __popcll(same));
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < nt; q += NTHREADS) {
+      const uint32_t e = stage[q];
+      const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
+      if (pos < a.n) t.index[pos] = (uint32_t)base + (e & 0xFFFFu);
+    }
+    if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(t.diag, USN_DIAG_LISTS);
+  if (tile == 0 && tid == 0) t.bin_off[a.nbins] = (uint32_t)a.n;
 }
 
 /* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge.
@@ -2852,9 +2810,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (t.lists_inline) {   // the records' LDS is free: stage | offsets | cursors
     uint32_t *stage = reinterpret_cast<uint32_t *>(srec);
     uint32_t *off = stage + TILE;
-    const InlineG g{tx_g1(t), tx_g2(t), tx_g3(t), t.index, t.bin_off, t.diag, t.epoch, a.lflags};
-    TxPoll poll{t};
-    inline_lists(a, g, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw), poll);
+    tx_lists(t, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw));
   }
   STAMP(11);
   STAMP_FLUSH_AT(tile);
@@ -2878,9 +2834,9 @@ static uint32_t resident_grid(K fn, size_t lds);
 
 bool tx_lists_fit(const TxArgs &t) {
   const ClassifyArgs &a = t.a;
-  if (a.ntiles == 0 || a.ntiles > INL_TPT * NTHREADS || a.nbw > 2 * NTHREADS) return false;
+  if (a.ntiles == 0 || a.ntiles > TXL_TPT * NTHREADS || a.nbw > 2 * NTHREADS) return false;
   // stage | offsets | cursors in the records' LDS
-  if (inline_lds_bytes(a.nbw) > tx_lds_head(a.nbins) - lds_core_bytes(a.nbins)) return false;
+  if (tx_lists_lds_bytes(a.nbw) > tx_lds_head(a.nbins) - lds_core_bytes(a.nbins)) return false;
   bool in_lds;
   size_t lds;
   tx_shape(t, &in_lds, &lds);
@@ -2971,33 +2927,12 @@ static uint32_t resident_grid(K fn, size_t lds) {
   return blocks;
 }
 
-/* the classify launch's dynamic LDS (the inline lists' stage | offsets |
- * cursors after the image when m.lists_inline) */
-static size_t classify_lds(const MultiArgs &m, int tm, bool glds, bool inl) {
+/* the classify launch's dynamic LDS */
+static size_t classify_lds(const MultiArgs &m, int tm, bool glds) {
   const ClassifyArgs &a = m.b[0];
   return lds_core_bytes(a.nbins, !glds) +
          (tm == TM_LDS ? table_lds_bytes(a.table_units)
-          : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0) +
-         (inl ? inline_lds_bytes(a.nbw) : 0);
-}
-
-bool classify_lists_fit(const MultiArgs &m) {
-  const uint32_t tiles = m.tile_base[m.count];
-  const ClassifyArgs &a = m.b[0];
-  if (tiles == 0 || USN_PERSIST || a.nbw > 2 * NTHREADS) return false;
-  for (uint32_t k = 0; k < m.count; ++k)
-    if (m.b[k].ntiles > USN_INLINE_MAX_TILES || m.b[k].ntiles > INL_TPT * NTHREADS) return false;
-  const int tm = table_mode(a);
-  const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds(m, tm, glds, true);
-  if (lds > 64u * 1024u) return false;
-  uint32_t res = 0;   // every tile of the launch resident at once (0 = unknown: no)
-#define USN_RES(T_, G_) res = resident_grid(classify_rx_kernel<T_, G_, true>, lds)
-  if (tm == TM_LDS) { if (glds) USN_RES(TM_LDS, true); else USN_RES(TM_LDS, false); }
-  else if (tm == TM_DISPLDS) { if (glds) USN_RES(TM_DISPLDS, true); else USN_RES(TM_DISPLDS, false); }
-  else { if (glds) USN_RES(TM_GLOBAL, true); else USN_RES(TM_GLOBAL, false); }
-#undef USN_RES
-  return tiles <= res;
+          : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
 }
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
@@ -3006,22 +2941,19 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const int tm = table_mode(a);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds(m, tm, glds, m.lists_inline != 0);
+  const size_t lds = classify_lds(m, tm, glds);
   const dim3 b(NTHREADS);
   // a grid of at most what the chip holds (0 = the query failed: one per tile)
 #define USN_LAUNCH(T_, G_)                                                              \
   do {                                                                                  \
     uint32_t grid = tiles;                                                              \
     if (USN_PERSIST == 1) {                                                             \
-      const uint32_t res = resident_grid(classify_rx_kernel<T_, G_, false>, lds);       \
+      const uint32_t res = resident_grid(classify_rx_kernel<T_, G_>, lds);              \
       if (res) grid = min(grid, res);                                                   \
     } else if (USN_PERSIST > 1) {                                                       \
       grid = (tiles + USN_PERSIST - 1) / USN_PERSIST;                                   \
     }                                                                                   \
-    if (m.lists_inline)                                                                 \
-      hipLaunchKernelGGL((classify_rx_kernel<T_, G_, true>), dim3(grid), b, lds, stream, m); \
-    else                                                                                \
-      hipLaunchKernelGGL((classify_rx_kernel<T_, G_, false>), dim3(grid), b, lds, stream, m); \
+    hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(grid), b, lds, stream, m);    \
   } while (0)
   if (tm == TM_LDS) { if (glds) USN_LAUNCH(TM_LDS, true); else USN_LAUNCH(TM_LDS, false); }
   else if (tm == TM_DISPLDS) { if (glds) USN_LAUNCH(TM_DISPLDS, true); else USN_LAUNCH(TM_DISPLDS, false); }

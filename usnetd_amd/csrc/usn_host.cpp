@@ -435,7 +435,6 @@ struct Replica {
   unsigned long long *lg = nullptr;   // TxArgs::lg, the inline lists' granules (epoch-tagged)
   size_t lg_bytes = 0;
   uint32_t tx_inline_launches = 0;    // tx launches that built their lists inline (diagnostics)
-  uint32_t rx_inline_launches = 0;    // classify launches that built their lists inline
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
@@ -521,8 +520,7 @@ struct usn_ctx {
   /* per classified batch (by its decisions): the replica it ran on and its
    * bin count (endpoints can be added before its usn_finalize: the batch's
    * scratch, count rows and lists keep the bins it was classified with) */
-  struct BatchRec { uint32_t rep, nbins; bool inl; };   // inl: lists built by the classify launch
-  bool rx_inline = std::getenv("USN_RX_LISTS_LAUNCHES") == nullptr;   // A/B: lists by the launches
+  struct BatchRec { uint32_t rep, nbins; };
   std::unordered_map<const void *, BatchRec> batch_rep;
   /* usn_set_lists_async: lists built on the replica's side stream; each
    * result's `lists done` event (keyed by its decisions array, created on
@@ -1627,14 +1625,11 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
  * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
- * gran[nranges][nbw] u64 | inl[ntiles][nbw] u64 | diag u32.  agg and gran
- * are sized for one-tile chunks: a launch picks its chunk length
- * (launch_scatter).  inl (batches of at most USN_INLINE_MAX_TILES tiles):
- * G2 of the lists a classify launch builds itself (usn_device.hip
- * inline_lists; G1 lives in agg, G3 in gran). */
+ * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized
+ * for one-tile chunks: a launch picks its chunk length (launch_scatter) */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, agg, tot, gran, inl, diag, total;
+  size_t cnt, agg, tot, gran, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
@@ -1647,7 +1642,6 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.gran = o; o = a256(o + ranges * g.nbw * 8);
-  g.inl = o; o = a256(o + (g.ntiles <= USN_INLINE_MAX_TILES ? (size_t)g.ntiles * g.nbw * 8 : 0));
   g.diag = o; o = a256(o + 4);
   g.total = o;
   return g;
@@ -1668,15 +1662,6 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.tc = tc;
   sb.nchunks = (g.ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
-}
-/* the granules of the lists a classify launch builds itself (G1 | G2 | G3) */
-void scatter_inline(void *scratch, uint64_t n, uint32_t nbins, unsigned long long **g1,
-                    unsigned long long **g2, unsigned long long **g3) {
-  const ScatterGeom g = scatter_geom(n, nbins);
-  uint8_t *p = static_cast<uint8_t *>(scratch);
-  *g1 = reinterpret_cast<unsigned long long *>(p + g.agg);
-  *g2 = reinterpret_cast<unsigned long long *>(p + g.inl);
-  *g3 = reinterpret_cast<unsigned long long *>(p + g.gran);
 }
 /* the scan's diag word of a batch's scratch (USN_DIAG_*) */
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
@@ -2071,12 +2056,13 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
 }
 
 /* diagnostics: launches of the selected replica that built their
- * per-endpoint lists themselves: out2[0] classify, out2[1] tx */
+ * per-endpoint lists themselves: out2[0] classify (none: every classify
+ * launch hands them to the scan and scatter launches), out2[1] tx */
 int usn_debug_lists_inline(usn_ctx *c, uint32_t *out2) {
   if (!c || !out2 || c->reps.empty()) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   const Replica &R = c->reps[c->sel];
-  out2[0] = R.rx_inline_launches;
+  out2[0] = 0;
   out2[1] = R.tx_inline_launches;
   return USN_OK;
 }
@@ -2497,7 +2483,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   bool tx_inline = false;   // tx: the per-endpoint lists built inside the tx launch
   if (tx) {
     const usn_batch &tb = b[0];
-    const size_t lg_bytes = ((size_t)m.b[0].ntiles * (m.b[0].nbw / 2 + m.b[0].nbw) + m.b[0].nbw) * 8;
+    // the inline lists' granules: G1 | G2 | G3 | DONE (usn_device.hip tx_lists)
+    const size_t lg_bytes = ((size_t)m.b[0].ntiles * (m.b[0].nbw / 2 + m.b[0].nbw + 1) + m.b[0].nbw) * 8;
     int st = tx_prepare(R, tb.n, m.b[0].ntiles, lg_bytes);
     if (st) return st;
     usn::TxArgs t;
@@ -2550,33 +2537,10 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       }
     }
     const bool t512 = c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units));
-    // small launches (every tile resident at once) build their lists
-    // themselves: no scan / scatter launch behind them
-    static const bool corrupt_hook = std::getenv("USN_DEBUG_CORRUPT") != nullptr;
-    if (c->rx_inline && !corrupt_hook &&
-        (t512 ? usn_t512::classify_lists_fit(m) : usn::classify_lists_fit(m))) {
-      const uint32_t ep = next_scan_epoch(c);
-      for (uint32_t k = 0; k < count; ++k) {
-        ClassifyArgs &a = m.b[k];
-        a.index = r[k].index;
-        a.bin_off = r[k].bin_off;
-        a.diag = usn::scatter_diag(r[k].scratch, a.n, a.nbins);
-        usn::scatter_inline(r[k].scratch, a.n, a.nbins, &a.lg1, &a.lg2, &a.lg3);
-        a.lepoch = ep;
-        a.lflags = slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u;
-        int st = scratch_tail_zeroed(c, r[k], a.n, a.nbins, (hipStream_t)stream);
-        if (st) return st;
-      }
-      m.lists_inline = 1;
-      ++R.rx_inline_launches;
-    }
     if (t512) HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
     else HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
-  if (!tx && m.lists_inline) {
-    // the lists are built (a result whose lists a side stream still builds
-    // was waited for above)
-  } else if (tx || !c->lists_async) {
+  if (tx || !c->lists_async) {
     uint32_t *txs = nullptr;
     if (tx) {   // what usn_finalize reads first: written into host memory by the scatter's chunk 0
       if (!c->h_txstate) {
@@ -2644,7 +2608,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
-    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins, m.lists_inline != 0};
+    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins};
   }
   return USN_OK;
 }
@@ -2761,8 +2725,7 @@ int lists_check(uint32_t *d_diag, hipStream_t s) {
 
 int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStream_t s,
                       usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
-                      const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr,
-                      uint32_t *diag_out = nullptr) {
+                      const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
   const size_t need = sizeof(usn_summary) + tb + 32 + 4;
   if (need > c->h_stage_cap) {
@@ -2787,7 +2750,6 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   if (d_diag) {
     uint32_t dg;
     std::memcpy(&dg, p + sizeof(usn_summary) + tb + 32, 4);
-    if (diag_out) { *diag_out = dg; return USN_OK; }   // the caller decides
     return lists_failed(dg, d_diag, s);
   }
   return USN_OK;
@@ -3169,22 +3131,8 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   {
-    uint32_t *d_diag = usn::scatter_diag(r->scratch, b->n, nb0), dg = 0;
-    int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr, d_diag, &dg);
-    if (e) return e;
-    if (dg == USN_DIAG_TIMEOUT && br != c->batch_rep.end() && br->second.inl) {
-      // a wait of the launch's inline lists gave up (never seen): the lists
-      // again by the scan and scatter launches
-      HIPCHK(hipMemsetAsync(d_diag, 0, 4, s));
-      ClassifyArgs a;
-      fill_args(c, c->reps[rep], b, r, a);
-      set_bins(r, b->n, nb0, a);
-      e = launch_scatter(c, &a, r, 1, s);
-      if (e) return e;
-      e = lists_check(d_diag, s);
-    } else {
-      e = lists_failed(dg, d_diag, s);
-    }
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr,
+                                    usn::scatter_diag(r->scratch, b->n, nb0));
     if (e) return e;
   }
   usn_finalize_info fi;

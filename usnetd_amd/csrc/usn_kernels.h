@@ -57,13 +57,7 @@ struct ClassifyArgs {
   const usn_tile_hdr *prev_tiles;
   uint32_t prev_ntiles;
   const usn_summary *prev_summary;
-  /* per-endpoint lists built inside the classify launch (MultiArgs.lists_inline;
-   * usn_device.hip inline_lists): outputs, and the epoch-tagged granules G1
-   * (the scratch's agg area), G2 (its inline area) and G3 (its gran area) */
-  uint32_t *index, *bin_off, *diag;
-  unsigned long long *lg1, *lg2, *lg3;
-  uint32_t lepoch;
-  uint32_t lflags;          /* USN_SCF_SLOW_RANK: the inline lists also rank by ballots (test hook) */
+  uint32_t lflags;          /* tx inline lists: USN_SCF_SLOW_RANK (test hook: ballot ranks too) */
 };
 
 /* Several batches (distinct sources) classified by one launch: workgroup w
@@ -73,7 +67,6 @@ struct MultiArgs {
   ClassifyArgs b[USN_MAX_MULTI];
   uint32_t tile_base[USN_MAX_MULTI + 1];
   uint32_t count;
-  uint32_t lists_inline;   /* every tile of the launch resident: lists built by the launch */
 };
 static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 
@@ -145,10 +138,6 @@ size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_ld
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
-/* the launch can build its lists inline (every tile resident at once, each
- * batch within inline_lists' mapping); m.lists_inline is then set by the caller */
-bool classify_lists_fit(const MultiArgs &m);
-#define USN_INLINE_MAX_TILES 1024u   /* batches the scratch carries the inline area for */
 /* Recount the bin rows and class counts of tiles [t0, t1) from the (patched)
  * decisions (the scatter then runs again). */
 hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
@@ -227,8 +216,6 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
                    ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
-void scatter_inline(void *scratch, uint64_t n, uint32_t nbins, unsigned long long **g1,
-                    unsigned long long **g2, unsigned long long **g3);
 uint32_t scatter_fallbacks();   /* tiles the 256-thread tx kernel's inline lists ranked again */
 
 }  // namespace usn
@@ -242,7 +229,6 @@ uint32_t scatter_fallbacks();   /* chunks the scatter (and tiles the tx kernel's
                                    ranked again (current device) */
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
 bool tx_lists_fit(const usn::TxArgs &t);
-bool classify_lists_fit(const usn::MultiArgs &m);
 hipError_t launch_txstate(const usn::TxState &x, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }
