@@ -56,11 +56,21 @@ DEFAULT_FRAMES = {"c1": 1 << 20, "c1fixed": 1 << 20, "c2": 1 << 20, "c3": 1 << 1
                   "c5": 1 << 23}
 
 
-def launch_frames(name):
+def launch_frames(name, queues=0):
     """Frames per classify launch of a config in the bench's launch shape
-    (Run: up to 8 rings of the config's batch size, at most 16M frames)."""
+    (Run: up to 8 rings of the config's batch size, at most 16M frames, the
+    rings of `queues` rx queues dealt over the streams)."""
     n = DEFAULT_FRAMES[name]
-    return n * max(1, min(8, LAUNCH_FRAMES // n))
+    P = max(1, min(8, LAUNCH_FRAMES // n))
+    S = 1 if P * n >= LAUNCH_FRAMES else 2
+    Q = queues or P * S
+    S = min(S, Q)
+    return n * min(P, -(-Q // S))
+
+
+def extra_queues(name):
+    """rx queues per rank of a config measured under its own key at N=1"""
+    return EXTRA_QUEUES.get(name, 0)
 
 
 def parse_args(argv=None):

@@ -241,35 +241,3 @@ def test_c4tx_more_tiles_than_resident(coracle_mod):
     infos = _run(traffic.config("c4tx", n=1 << 22), coracle_mod, batches=2)
     assert [i.n_host for i in infos] == [0, 0]
 
-
-def _tx_inline_launches(ctx):
-    return ctx.lists_inline()[1]
-
-
-@pytest.mark.parametrize("n", [3000, 1 << 20])
-def test_tx_lists_built_inline(n, coracle_mod):
-    """A tx ring whose tiles are all resident builds its per-endpoint lists
-    inside the tx launch (tx_lists: the tiles hand their counts to each other
-    through epoch-tagged granules; no scan / scatter launch): decisions and
-    lists equal the oracle's, over three rings that learn and then repeat."""
-    from usnetd_amd import lib, traffic
-    cfg = traffic.config("c4tx", n=n)
-    o = coracle_mod.Oracle()
-    coracle_mod.install_oracle(o, cfg)
-    ctx = lib.Ctx(0)
-    traffic.install_ctx(ctx, cfg)
-    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
-    for k in range(3):
-        want = o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
-        r = lib.DeviceResult(ctx, cfg.n)
-        ctx.classify(b, r)
-        info = ctx.finalize(b, r)
-        got = r.decisions()
-        assert np.array_equal(got & katrun.PARITY_MASK, want & katrun.PARITY_MASK), k
-        check_order(r, got)
-        assert info.n_host == 0
-        r.free()
-    assert _tx_inline_launches(ctx) == 3
-    assert ctx.scatter_fallbacks() == 0
-    b.free()
-    ctx.close()

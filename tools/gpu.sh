@@ -39,9 +39,11 @@ for s in "$@"; do
       step trace_summary 60 python3 tools/trace_summary.py $O/prof/run_kernel_trace.csv ;;
     pmc)  # FETCH_SIZE / WRITE_SIZE passes per config of PMC_CFGS through bench.py's launch shape
       for c in ${PMC_CFGS:-c5 c2}; do
-        F=$(python3 -c "import bench; print(bench.launch_frames('$c'))")
-        pmc_pass pmcf_$c FETCH_SIZE python3 bench.py --config $c --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
-        pmc_pass pmcw_$c WRITE_SIZE python3 bench.py --config $c --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
+        # the launch shape the bench line uses for the config (c3: its 8 queues)
+        QA=$(python3 -c "import bench; q = bench.extra_queues('$c'); print('--queues %d' % q if q else '')")
+        F=$(python3 -c "import bench; print(bench.launch_frames('$c', bench.extra_queues('$c')))")
+        pmc_pass pmcf_$c FETCH_SIZE python3 bench.py --config $c $QA --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
+        pmc_pass pmcw_$c WRITE_SIZE python3 bench.py --config $c $QA --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0
         FF=""; [ $c = c3 ] && FF="classify_rx_kernel=1"   # one 64-B request per 2048-B slot
         step pmct_$c 60 python3 tools/pmc_traffic.py $O/pmcf_$c $O/pmcw_$c $F $O/pmc_$c.json $FF
       done ;;

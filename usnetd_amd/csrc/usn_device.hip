@@ -802,7 +802,7 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw) {
  * workgroup 0: the state after the last cache-touching frame of the previous
  * batch (its tiles are scanned in parallel), or that batch's own carried-in
  * state when none of its frames touched the cache.  out[0..5] in LDS. */
-__device__ __forceinline__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *scratch) {
+__device__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *scratch) {
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const bool chain = a.carry_mode == CARRY_CHAIN && !(a.prev_summary->flags & USN_S_COUT);
   uint32_t best = 0;   // 1 + index of the last previous tile with a touching frame
@@ -968,22 +968,6 @@ __device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) q[k] = ld_stream(w + k);
   q[3] = make_uint4(0, 0, 0, 0);
-}
-
-/* epoch-tagged granules {epoch, value}: one agent-scope (sc1) 8-byte store
- * each, polled by sc1 loads (MI355X guide, Guideline 16 R2) */
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) uint32_t gu32;
-
-__device__ __forceinline__ void g_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
-  __hip_atomic_store((gu64 *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-/* units of the displacements TM_DISPLDS copies to LDS: U's and X's when U is
- * built (one slot read per frame), else K1's and K2's */
-__host__ __device__ inline uint32_t disp_lds_units(const ClassifyArgs &a) {
-  return (a.probe_mask & 4u) ? a.u_end_unit - a.u_disp_unit : a.table_units - a.disp_unit;
 }
 
 /* Which batch of a launch tile w belongs to: tile_base[] is increasing, so
@@ -1660,7 +1644,7 @@ __device__ __forceinline__ void key1_of(const uint4 &r0, uint32_t &x, uint32_t &
 
 /* Exclusive prefix max, in tile-local frame order, of v[r] (frame r*256+tid).
  * Values are <= TILE.  Uses L.order as a u16 scratch row and L.scratch. */
-__device__ __forceinline__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t out[ROUNDS]) {
+__device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t out[ROUNDS]) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) L.order[r * NTHREADS + tid] = (uint16_t)v[r];
@@ -1814,6 +1798,13 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
 static_assert(TXG_CIN + 6 <= TXA_GRANULES, "aux granules");
 #define TX_SPIN_TICKS (200u * 100000u)   /* 200 ms of the 100 MHz real-time clock */
 
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ void g_put(unsigned long long *g, uint32_t epoch, uint32_t v) {
+  __hip_atomic_store((gu64 *)g, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void g_put4(unsigned long long *g, uint32_t epoch, const uint4 &v) {
   g_put(g, epoch, v.x); g_put(g + 1, epoch, v.y); g_put(g + 2, epoch, v.z); g_put(g + 3, epoch, v.w);
 }
@@ -1825,7 +1816,7 @@ __device__ __forceinline__ bool tx_timed_out(const TxArgs &t) {
  * loads of a poll fly together); false after TX_SPIN_TICKS or once any wait
  * of the batch has timed out */
 template <int N>
-__device__ __forceinline__ bool g_getn(const unsigned long long *g, const TxArgs &t, uint32_t (&v)[N]) {
+__device__ bool g_getn(const unsigned long long *g, const TxArgs &t, uint32_t (&v)[N]) {
   uint64_t t0 = 0;
   for (uint32_t it = 0;; ++it) {
     bool ok = true;
@@ -1866,7 +1857,7 @@ __device__ __forceinline__ bool g_try(const unsigned long long *g, const TxArgs 
  * the caller); false after a timeout. */
 #define TX_LB_PER_THREAD 4
 #define TX_LOOKBACK (NTHREADS * TX_LB_PER_THREAD)
-__device__ __forceinline__ bool tx_lookback(const TxArgs &t, uint32_t tile, uint32_t *ins_out, uint32_t *head_out) {
+__device__ bool tx_lookback(const TxArgs &t, uint32_t tile, uint32_t *ins_out, uint32_t *head_out) {
   const uint32_t tid = threadIdx.x;
   uint32_t ins = 0, head = 0;
   bool ok = true;
@@ -1895,7 +1886,7 @@ __device__ __forceinline__ bool tx_lookback(const TxArgs &t, uint32_t tile, uint
 /* The OR of EARLY over tiles [0, tile), the same way as tx_lookback (EARLY
  * goes out long before INS: a tile whose predecessors flag nothing to learn
  * need not wait for their claims). */
-__device__ __forceinline__ bool tx_lookback_early(const TxArgs &t, uint32_t tile, uint32_t *early_out) {
+__device__ bool tx_lookback_early(const TxArgs &t, uint32_t tile, uint32_t *early_out) {
   const uint32_t tid = threadIdx.x;
   uint32_t e = 0;
   bool ok = true;
@@ -1924,242 +1915,6 @@ __device__ __forceinline__ void tx_load_cin(const TxArgs &t, uint32_t *cin) {
   uint32_t v[6];
   const bool ok = g_getn<6>(t.aux + TXG_CIN, t, v);
   for (int k = 0; k < 6; ++k) cin[k] = ok ? v[k] : 0u;
-}
-
-/* ---- the per-endpoint lists inside the tx launch (TxArgs.lists_inline) ----
- * When every tile of a tx batch is resident at once (tx_lists_fit checks the
- * grid against the occupancy query), the scan that scan_kernel +
- * scatter_kernel do in two more launches is done by hand-offs between the
- * batch's tiles, through epoch-tagged granules (sc1 stores and loads, MI355X
- * guide Guideline 16 R1/R2):
- *   P1  each tile publishes its count row: G1[tile][pair] = the u16 counts
- *       of bins 2 pair, 2 pair + 1 (each granule is its own flag);
- *   P2  tile t scans pairs t, t + ntiles, ... over the tiles: one wave
- *       gathers the pair's G1 granules of every tile into LDS, the block
- *       scans them, G2[u][bin] = the bin's frames in tiles before u, G3[bin] =
- *       its frames; then DONE[t] (after every wave drained its stores);
- *   P3  one wave polls the DONE flags of the handler tiles, then the block
- *       reads its row of G2 and all of G3: the bin bases (an exclusive scan of
- *       G3 over bins) and its offsets; one wave ranks the tile's frames into a
- *       (bin, frame)-sorted LDS stage with one LDS atomic each (the scatter
- *       kernel's ranks: checked, and redone by ballots when not stably
- *       sorted), and the stage goes out as the tile's runs of index.
- * Polling is one wave per tile (every thread polling its own granules loaded
- * the memory system enough to cost the launch 26 us per 1M-frame ring).  A
- * wait that times out marks the batch as the kernel's other waits do
- * (counters[3]): usn_finalize then decides it on the host and rebuilds the
- * lists by the scan and scatter launches.  Every store is bounds-checked; a
- * count that disagrees with the decisions sets USN_DIAG_LISTS. */
-#define TXL_TPT 4   /* tiles per thread in P2: a batch of <= TXL_TPT * NTHREADS tiles */
-__device__ __forceinline__ unsigned long long *tx_g1(const TxArgs &t) { return t.lg; }
-__device__ __forceinline__ unsigned long long *tx_g2(const TxArgs &t) {
-  return t.lg + (size_t)t.a.ntiles * (t.a.nbw / 2);
-}
-__device__ __forceinline__ unsigned long long *tx_g3(const TxArgs &t) {
-  return tx_g2(t) + (size_t)t.a.ntiles * t.a.nbw;
-}
-__device__ __forceinline__ unsigned long long *tx_done(const TxArgs &t) { return tx_g3(t) + t.a.nbw; }
-__host__ __device__ inline size_t tx_lists_lds_bytes(uint32_t nbw) {   /* stage | offsets | cursors */
-  return (size_t)TILE * 4 + (size_t)nbw * 4 + (size_t)nbw * 2;
-}
-/* chunks / tiles whose ranks were redone by ballots (usn_debug_scatter_fallbacks) */
-__device__ uint32_t usn_scatter_fallbacks = 0;
-
-/* one wave: out[u] = the value of granule g[u * stride] for u < count, once
- * each carries the batch epoch (TXG_DEPTH per lane in flight per poll); false after
- * a timeout of any wait of the batch */
-#define TXG_DEPTH 4   /* granules per lane in flight per poll (the kernel's VGPR budget) */
-__device__ __forceinline__ bool tx_gather(const TxArgs &t, const unsigned long long *g, uint32_t stride,
-                                          uint32_t count, uint32_t *out) {
-  const uint32_t lane = threadIdx.x & 63;
-  bool ok = true;
-  for (uint32_t b0 = 0; b0 < count && ok; b0 += 64 * TXG_DEPTH) {
-    uint32_t pend = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < TXG_DEPTH; ++j) pend |= (b0 + j * 64 + lane < count ? 1u : 0u) << j;
-    uint64_t t0 = 0;
-    for (uint32_t it = 0; pend; ++it) {
-      unsigned long long x[TXG_DEPTH];
-#pragma unroll
-      for (uint32_t j = 0; j < TXG_DEPTH; ++j)
-        x[j] = ((pend >> j) & 1u)
-                   ? __hip_atomic_load((gu64 *)(g + (size_t)(b0 + j * 64 + lane) * stride), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT)
-                   : 0ull;
-#pragma unroll
-      for (uint32_t j = 0; j < TXG_DEPTH; ++j)
-        if (((pend >> j) & 1u) && (uint32_t)(x[j] >> 32) == t.epoch) {
-          out[b0 + j * 64 + lane] = (uint32_t)x[j];
-          pend &= ~(1u << j);
-        }
-      if (!pend) break;
-      if (tx_timed_out(t)) { ok = false; break; }
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (it == 0) {
-        t0 = now;
-      } else if (now - t0 > TX_SPIN_TICKS) {
-        atomicMax(t.counters + 3, t.epoch);
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  return ok;
-}
-
-__device__ __forceinline__ void tx_lists(const TxArgs &t, uint32_t tile, uint32_t nt, const Lds &L,
-                                         const uint16_t *bins16, uint32_t *stage, uint32_t *off,
-                                         uint16_t *cur) {
-  const ClassifyArgs &a = t.a;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nbw = a.nbw, np = nbw / 2, ntiles = a.ntiles, nh = min(np, ntiles);
-  unsigned long long *G1 = tx_g1(t), *G2 = tx_g2(t), *G3 = tx_g3(t), *DONE = tx_done(t);
-  // P1 (the histogram is complete: a barrier after tile_hist)
-  for (uint32_t k = tid; k < np; k += NTHREADS) g_put(G1 + (size_t)tile * np + k, t.epoch, L.hist[k]);
-  // P2: this tile's pairs; the stage holds one pair's counts of every tile
-  for (uint32_t pr = tile; pr < np; pr += ntiles) {
-    if (wave == 0) tx_gather(t, G1 + pr, np, ntiles, stage);   // false: gave up (marked)
-    __syncthreads();
-    uint32_t lo[TXL_TPT], hi[TXL_TPT], slo = 0, shi = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < TXL_TPT; ++j) {
-      const uint32_t u = tid * TXL_TPT + j;
-      const uint32_t v = u < ntiles ? stage[u] : 0u;
-      lo[j] = v & 0xFFFFu;
-      hi[j] = v >> 16;
-      slo += lo[j];
-      shi += hi[j];
-    }
-    uint32_t tlo, thi;
-    uint32_t elo = block_excl_scan(slo, L.scratch, &tlo);   // (its barriers: the stage is free after)
-    uint32_t ehi = block_excl_scan(shi, L.scratch, &thi);
-#pragma unroll
-    for (uint32_t j = 0; j < TXL_TPT; ++j) {
-      const uint32_t u = tid * TXL_TPT + j;
-      if (u < ntiles) {
-        g_put(G2 + (size_t)u * nbw + 2 * pr, t.epoch, elo);
-        g_put(G2 + (size_t)u * nbw + 2 * pr + 1, t.epoch, ehi);
-      }
-      elo += lo[j];
-      ehi += hi[j];
-    }
-    if (tid == 0) {
-      g_put(G3 + 2 * pr, t.epoch, tlo);
-      g_put(G3 + 2 * pr + 1, t.epoch, thi);
-    }
-  }
-  if (tile < nh) {   // DONE after every wave's G2 / G3 stores have landed (R1)
-    vm_drain();
-    __syncthreads();
-    if (tid == 0) g_put(DONE + tile, t.epoch, 1u);
-  }
-  // P3: the handlers are done; then this tile's offsets (thread k: bins 2k, 2k+1)
-  if (wave == 0) tx_gather(t, DONE, 1, nh, reinterpret_cast<uint32_t *>(off));   // (values unused)
-  __syncthreads();
-  {
-    const bool mine = 2 * tid < nbw;
-    uint32_t v[4] = {0, 0, 0, 0};
-    if (mine) {
-      const unsigned long long *gp[4] = {G2 + (size_t)tile * nbw + 2 * tid, G2 + (size_t)tile * nbw + 2 * tid + 1,
-                                         G3 + 2 * tid, G3 + 2 * tid + 1};
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        v[k] = (uint32_t)__hip_atomic_load((gu64 *)gp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint32_t hw = mine ? L.hist[tid] : 0u;
-    const uint32_t c0 = hw & 0xFFFFu, c1 = hw >> 16;
-    uint32_t total;
-    const uint32_t pt = block_excl_scan(v[2] + v[3], L.scratch, &total);   // bin bases
-    const uint32_t pc = block_excl_scan(c0 + c1, L.scratch, &total);       // the bins' starts in the tile
-    if (mine) {
-      const uint32_t b = 2 * tid;
-      off[b] = pt + v[0] - pc;
-      off[b + 1] = pt + v[2] + v[1] - (pc + c0);
-      reinterpret_cast<uint32_t *>(cur)[tid] = (pc & 0xFFFFu) | ((pc + c0) << 16);
-      if (tile == 0) {
-        if (b <= a.nbins) t.bin_off[b] = pt;
-        if (b + 1 <= a.nbins) t.bin_off[b + 1] = pt + v[2];
-      }
-    }
-    for (uint32_t q4 = tid; q4 < TILE / 4; q4 += NTHREADS)
-      reinterpret_cast<uint4 *>(stage)[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
-  }
-  __syncthreads();
-  // ranks: wave 0, the tile's 16 segments in order (one LDS atomic per frame)
-  bool bad = false;
-  if (wave == 0) {   // in two halves of 8 segments (the kernel's VGPR budget); a wave's
-                     // LDS operations execute in order either way
-    uint32_t *cw = reinterpret_cast<uint32_t *>(cur);
-#pragma unroll
-    for (uint32_t h = 0; h < TILE / 64; h += 8) {
-      uint32_t at[8];
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t f = (h + k) * 64 + lane;
-        const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u);
-        const uint32_t sh = 16u * (b & 1u);
-        at[k] = f < nt ? atomicAdd(&cw[b >> 1], 1u << sh) >> sh : 0u;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t f = (h + k) * 64 + lane;
-        if (f < nt) {
-          const uint32_t b = min((uint32_t)bins16[f], a.nbins - 1u), q = at[k] & 0xFFFFu;
-          bad |= q >= nt;
-          stage[min(q, (uint32_t)TILE - 1u)] = (b << 16) | f;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // the stage out in order: the tile's run of each bin at off[bin] + q
-  const uint64_t base = (uint64_t)tile * TILE;
-  bool unsorted = false;
-  for (uint32_t q = tid; q < nt; q += NTHREADS) {
-    const uint32_t e = stage[q];
-    const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
-    if (pos < a.n) t.index[pos] = (uint32_t)base + (e & 0xFFFFu);
-    bad |= pos >= a.n || e == ~0u;
-    const uint32_t p = q ? stage[q - 1] : 0u;
-    unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
-  }
-  if (__syncthreads_or(unsorted || (a.lflags & USN_SCF_SLOW_RANK))) {   // (not seen on gfx950)
-    // ballot ranks, then the stage again
-    if (tid == 0) {   // cursors back to the bins' starts in the tile
-      uint32_t run = 0;
-      for (uint32_t b = 0; b < nbw; ++b) {
-        cur[b] = (uint16_t)run;
-        run += hist_get(L.hist, b);
-      }
-    }
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll 1
-      for (uint32_t k = 0; k < TILE / 64; ++k) {
-        const uint32_t local = k * 64 + lane;
-        const bool v = local < nt;
-        const uint32_t b = min((uint32_t)bins16[min(local, nt - 1)], a.nbins - 1u);
-        const uint64_t same = match_bin(b, __ballot(v), a.nbits);
-        const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
-        const uint32_t at = cur[b];
-        if (v) {
-          stage[min(at + rank, (uint32_t)TILE - 1u)] = (b << 16) | local;
-          if (rank == 0) cur[b] = (uint16_t)(at + __popcll(same));
-        }
-      }
-    }
-    __syncthreads();
-    for (uint32_t q = tid; q < nt; q += NTHREADS) {
-      const uint32_t e = stage[q];
-      const uint32_t pos = off[min(e >> 16, nbw - 1u)] + q;
-      if (pos < a.n) t.index[pos] = (uint32_t)base + (e & 0xFFFFu);
-    }
-    if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
-  }
-  if (__ballot(bad) && lane == 0) atomicOr(t.diag, USN_DIAG_LISTS);
-  if (tile == 0 && tid == 0) t.bin_off[a.nbins] = (uint32_t)a.n;
 }
 
 /* LDS of the tx kernel: core | records | decisions | table (LDS) | bridge.
@@ -2767,7 +2522,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       my_info = make_uint4(rec[r].x & TXR_I0_MASK, rec[r].y, rec[r].z, rec[r].w);
     }
     bins[r] = dec_bin(dec[r], a.n_ep);
-    L.order[local] = (uint16_t)bins[r];   // the inline lists' ranks (tile_prefix_max is done with it)
     const bool host = valid && (dec[r] & (USN_F_HOST | USN_F_FRAG1 | USN_F_LEARN));
     if (__ballot(host))
       if (host) hl[atomicAdd(&s_misc[1], 1u)] = (uint32_t)(base + local);
@@ -2807,11 +2561,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
     if (s_misc[1]) atomicAdd(t.counters + 4, s_misc[1]);   // after phase 2: tile 0 zeroed it
   }
-  if (t.lists_inline) {   // the records' LDS is free: stage | offsets | cursors
-    uint32_t *stage = reinterpret_cast<uint32_t *>(srec);
-    uint32_t *off = stage + TILE;
-    tx_lists(t, tile, nt, L, L.order, stage, off, reinterpret_cast<uint16_t *>(off + a.nbw));
-  }
   STAMP(11);
   STAMP_FLUSH_AT(tile);
 }
@@ -2819,41 +2568,16 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
 
 static inline size_t table_lds_bytes(uint32_t table_units);
 
-/* the tx kernel's variant (rule image in LDS or not) and dynamic LDS */
-static void tx_shape(const TxArgs &t, bool *in_lds, size_t *lds) {
-  const ClassifyArgs &a = t.a;
-  const size_t head = tx_lds_head(a.nbins);
-  const size_t bridge = t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0;
-  const size_t with_table = head + table_lds_bytes(a.table_units) + bridge;
-  *in_lds = table_fits_lds(a.nbins, a.table_units) && with_table <= 64u * 1024u;
-  *lds = *in_lds ? with_table : head + bridge;
-}
-
-template <typename K>
-static uint32_t resident_grid(K fn, size_t lds);
-
-bool tx_lists_fit(const TxArgs &t) {
-  const ClassifyArgs &a = t.a;
-  if (a.ntiles == 0 || a.ntiles > TXL_TPT * NTHREADS || a.nbw > 2 * NTHREADS) return false;
-  // stage | offsets | cursors in the records' LDS
-  if (tx_lists_lds_bytes(a.nbw) > tx_lds_head(a.nbins) - lds_core_bytes(a.nbins)) return false;
-  bool in_lds;
-  size_t lds;
-  tx_shape(t, &in_lds, &lds);
-  // every tile resident at once (the occupancy query; 0 = unknown: no)
-  const uint32_t res = in_lds ? resident_grid(tx_kernel<true>, lds) : resident_grid(tx_kernel<false>, lds);
-  return a.ntiles <= res;
-}
-
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const ClassifyArgs &a = t.a;
   if (a.ntiles == 0) return hipSuccess;
   const dim3 g(a.ntiles), b(NTHREADS);
-  bool in_lds;
-  size_t lds;
-  tx_shape(t, &in_lds, &lds);
-  if (in_lds) hipLaunchKernelGGL(tx_kernel<true>, g, b, lds, stream, t);
-  else hipLaunchKernelGGL(tx_kernel<false>, g, b, lds, stream, t);
+  const size_t head = tx_lds_head(a.nbins);
+  const size_t bridge = t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0;
+  const size_t with_table = head + table_lds_bytes(a.table_units) + bridge;
+  const bool in_lds = table_fits_lds(a.nbins, a.table_units) && with_table <= 64u * 1024u;
+  if (in_lds) hipLaunchKernelGGL(tx_kernel<true>, g, b, with_table, stream, t);
+  else hipLaunchKernelGGL(tx_kernel<false>, g, b, head + bridge, stream, t);
   return hipGetLastError();
 }
 
@@ -2879,6 +2603,11 @@ bool table_fits_lds(uint32_t nbins, uint32_t table_units) {
 #ifndef USN_DISP_LDS_MAX
 #define USN_DISP_LDS_MAX (26u * 1024u)
 #endif
+/* units of the displacements TM_DISPLDS copies to LDS: U's and X's when U is
+ * built (one slot read per frame), else K1's and K2's */
+static uint32_t disp_lds_units(const ClassifyArgs &a) {
+  return (a.probe_mask & 4u) ? a.u_end_unit - a.u_disp_unit : a.table_units - a.disp_unit;
+}
 static int table_mode(const ClassifyArgs &a) {
   if (table_fits_lds(a.nbins, a.table_units)) return TM_LDS;
   const size_t disp = (size_t)disp_lds_units(a) * 16;
@@ -2927,21 +2656,15 @@ static uint32_t resident_grid(K fn, size_t lds) {
   return blocks;
 }
 
-/* the classify launch's dynamic LDS */
-static size_t classify_lds(const MultiArgs &m, int tm, bool glds) {
-  const ClassifyArgs &a = m.b[0];
-  return lds_core_bytes(a.nbins, !glds) +
-         (tm == TM_LDS ? table_lds_bytes(a.table_units)
-          : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
-}
-
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const int tm = table_mode(a);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-  const size_t lds = classify_lds(m, tm, glds);
+  const size_t lds = lds_core_bytes(a.nbins, !glds) +
+                     (tm == TM_LDS ? table_lds_bytes(a.table_units)
+                      : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
   const dim3 b(NTHREADS);
   // a grid of at most what the chip holds (0 = the query failed: one per tile)
 #define USN_LAUNCH(T_, G_)                                                              \
@@ -3158,14 +2881,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
 #ifndef USN_SCATTER_XCD
 #define USN_SCATTER_XCD 1
 #endif
+/* chunks that took step 5 (usn_debug_scatter_fallbacks) */
+__device__ uint32_t usn_scatter_fallbacks = 0;
 #ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
 #define USN_SC_GROUP 1
 #endif
-#ifndef USN_SCATTER_WPE   /* waves per SIMD the scatter is compiled for (6: 3 workgroups per CU, <= 80 VGPRs) */
+#ifndef USN_SCATTER_WPE   /* waves per SIMD the scatter is compiled for: 6 = 3 workgroups per CU
+                             (80 VGPRs, a few spilled): c5 scan + scatter 57.5 vs 61.7 us per 16M
+                             frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
 #endif
 template <int TC>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SCATTER_WPE))) void scatter_kernel(ScatterArgs s) {
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SCATTER_WPE)))
+void scatter_kernel(ScatterArgs s) {
   static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
   constexpr uint32_t SEGS = TILE / 64;                               // 16 segments per tile
   extern __shared__ __align__(16) uint8_t smem[];
@@ -3382,8 +3110,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SC
       for (uint32_t k = 0; k < SEGS; ++k) {
         const uint32_t local = k * 64 + lane;
         const bool v = local < tn;
-        // the decision again from memory: keeping d[] live to here cost the
-        // common path 16 VGPRs (and 3 workgroups per CU)
+        // the decision again from memory: keeping d[] live to here costs the
+        // common path VGPRs
         const uint32_t dk = B.decisions[tbase + min(local, tn - 1)];
         const uint32_t b = min(dec_bin(dk, s.n_ep), s.nbins - 1u);
         const uint64_t same = match_bin(b, __ballot(v), s.nbits);
@@ -3409,22 +3137,12 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SC
 static_assert(NTHREADS == 512, "scatter: 8 waves, a tile each");
 static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
 
-
-/* tx: the state usn_finalize reads first (usn_kernels.h TxState), behind
- * a tx launch that built its lists inline */
-__global__ __launch_bounds__(64) void txstate_kernel(TxState x) {
-  const uint32_t tid = threadIdx.x;
+uint32_t scatter_fallbacks() {
   uint32_t v = 0;
-  if (tid == 0) v = x.sum->flags;
-  else if (tid < 6) v = __hip_atomic_load(x.counters + tid - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else if (tid < 9) v = x.bin_off[x.n_ep + tid - 6];
-  else if (tid == 9) v = x.n;
-  else if (tid == 10) v = *x.diag;
-  if (tid < 11) x.out[tid] = v;
-}
-hipError_t launch_txstate(const TxState &x, hipStream_t stream) {
-  hipLaunchKernelGGL(txstate_kernel, dim3(1), dim3(64), 0, stream, x);
-  return hipGetLastError();
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(usn_scatter_fallbacks), sizeof v, 0, hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return 0xFFFFFFFFu;
+  return v;
 }
 
 hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
@@ -3449,14 +3167,6 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512
-
-uint32_t scatter_fallbacks() {
-  uint32_t v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(usn_scatter_fallbacks), sizeof v, 0, hipMemcpyDeviceToHost) !=
-      hipSuccess)
-    return 0xFFFFFFFFu;
-  return v;
-}
 
 }  // namespace USN_NS
 

@@ -432,9 +432,6 @@ struct Replica {
   uint4 *learned = nullptr;
   uint32_t learned_cap = 0;
   uint32_t *counters = nullptr;   // TxArgs::counters
-  unsigned long long *lg = nullptr;   // TxArgs::lg, the inline lists' granules (epoch-tagged)
-  size_t lg_bytes = 0;
-  uint32_t tx_inline_launches = 0;    // tx launches that built their lists inline (diagnostics)
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
@@ -530,10 +527,7 @@ struct usn_ctx {
   std::unordered_map<const void *, ListsEv> lists_ev;
   /* the scatter's scan: a tag per launch for its range granules (random
    * start), and the result scratches whose granules were zeroed */
-  /* granule tags of the lists' scans (scan_kernel and the inline lists), in
-   * [2^31, 2^32): never 0 (zeroed granules) and never a count or offset (an
-   * inline G1 granule lives where the scan's agg rows are) */
-  uint32_t scan_epoch = (uint32_t)std::random_device{}() | 0x80000000u;
+  uint32_t scan_epoch = (uint32_t)std::random_device{}();
   /* per scratch: the bind tag and geometry (frames, bins) its granules were
    * last zeroed for (one entry per scratch, not per geometry) */
   struct Zeroed { uint32_t tag; uint64_t geo; };
@@ -1663,7 +1657,7 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.nchunks = (g.ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
 }
-/* the scan's diag word of a batch's scratch (USN_DIAG_*) */
+/* the scan's diag word of a batch's scratch (bit 0: a wait timed out) */
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
   return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(n, nbins).diag);
 }
@@ -1770,7 +1764,7 @@ void usn_ctx_destroy(usn_ctx *c) {
     (void)hipDeviceSynchronize();
     for (void *p : {(void *)R.d_table, R.d_patch, (void *)R.d_bridge, (void *)R.d_bridge_set,
                     (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
-                    (void *)R.counters, (void *)R.listen, (void *)R.lg})
+                    (void *)R.counters, (void *)R.listen})
       if (p) (void)hipFree(p);
   }
   for (auto &kv : c->lists_ev)
@@ -2051,19 +2045,6 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
     HIPCHK(hipMemcpy(out10, R.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   out10[8] = R.epoch;
-  out10[9] = R.tx_inline_launches;
-  return USN_OK;
-}
-
-/* diagnostics: launches of the selected replica that built their
- * per-endpoint lists themselves: out2[0] classify (none: every classify
- * launch hands them to the scan and scatter launches), out2[1] tx */
-int usn_debug_lists_inline(usn_ctx *c, uint32_t *out2) {
-  if (!c || !out2 || c->reps.empty()) return USN_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  const Replica &R = c->reps[c->sel];
-  out2[0] = 0;
-  out2[1] = R.tx_inline_launches;
   return USN_OK;
 }
 
@@ -2182,34 +2163,6 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   return USN_OK;
 }
 
-/* test hook USN_SCATTER_SLOW_RANK=1 (read once): every chunk / inline tile
- * also ranks by ballots and writes its stage out again */
-static bool slow_rank_hook() {
-  static const bool on = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  return on;
-}
-
-static uint32_t next_scan_epoch(usn_ctx *c) {
-  if (++c->scan_epoch == 0) c->scan_epoch = 0x80000000u;
-  return c->scan_epoch;
-}
-
-/* granules and diag word of a result's scratch never used before may hold
- * anything: zero them after every bind, and again when the geometry moves
- * them (their place depends on the batch's frames and bins) */
-static int scratch_tail_zeroed(usn_ctx *c, const usn_result &r, uint64_t n, uint32_t nbins,
-                               hipStream_t s) {
-  const uint64_t geo = (n << 16) ^ nbins;
-  auto zi = c->scan_zeroed.find(r.scratch);
-  if (zi != c->scan_zeroed.end() && zi->second.tag == r.bind_tag && zi->second.geo == geo) return USN_OK;
-  c->scan_zeroed[r.scratch] = usn_ctx::Zeroed{r.bind_tag, geo};
-  void *p;
-  size_t bytes;
-  usn::scatter_tail(r.scratch, n, nbins, &p, &bytes);
-  HIPCHK(hipMemsetAsync(p, 0, bytes, s));
-  return USN_OK;
-}
-
 /* the per-endpoint scatter of `count` classified batches (after their
  * classify / tx launch, or after finalize recounted patched tiles) */
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
@@ -2253,7 +2206,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   if (!noscan)
     while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
-  x.flags = (slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
+  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
+  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = std::getenv("USN_SCAN_CPT");
@@ -2272,7 +2226,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.txs_out = txs_out;
   x.txs_counters = txs_counters;
   x.txs_sum = r[0].summary;
-  x.epoch = next_scan_epoch(c);
+  if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
+  x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
@@ -2282,7 +2237,18 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     sb.bin_off = r[k].bin_off;
     x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
     x.range_base[k + 1] = x.range_base[k] + sb.nranges;
-    { const int e = scratch_tail_zeroed(c, r[k], as[k].n, x.nbins, s); if (e) return e; }
+    // granules of a scratch never used before may hold anything: zero them
+    // after every bind, and again when the geometry moves them (their place
+    // depends on the batch's frames and bins)
+    const uint64_t geo = (as[k].n << 16) ^ x.nbins;
+    auto zi = c->scan_zeroed.find(r[k].scratch);
+    if (zi == c->scan_zeroed.end() || zi->second.tag != r[k].bind_tag || zi->second.geo != geo) {
+      c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo};
+      void *p;
+      size_t bytes;
+      usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
+      HIPCHK(hipMemsetAsync(p, 0, bytes, s));
+    }
   }
   // test hook (tests/test_gpu_scatter.py, read once per process):
   // USN_DEBUG_CORRUPT=1 adds 257 to bin 0 of batch 0's first count row, =2
@@ -2323,7 +2289,7 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
 
 /* device scratch of a tx batch of n frames on replica R; the epoch-tagged
  * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
-static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, size_t lg_bytes) {
+static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
   if (n > T.learned_frames) {
     if (T.learned) HIPCHK(hipFree(T.learned));
     T.learned = nullptr;
@@ -2342,14 +2308,6 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, size_t lg_bytes) 
     HIPCHK(hipMalloc(&T.counters, 8 * sizeof(uint32_t)));
     HIPCHK(hipMemset(T.counters, 0, 8 * sizeof(uint32_t)));
   }
-  if (lg_bytes > T.lg_bytes) {   // zeroed: no granule holds an epoch yet
-    if (T.lg) HIPCHK(hipFree(T.lg));
-    T.lg = nullptr;
-    T.lg_bytes = 0;
-    HIPCHK(hipMalloc(&T.lg, lg_bytes));
-    HIPCHK(hipMemset(T.lg, 0, lg_bytes));
-    T.lg_bytes = lg_bytes;
-  }
   const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
   bool clear = false;
   if (slots > T.set_slots) {
@@ -2367,7 +2325,6 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, size_t lg_bytes) 
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
     HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
     HIPCHK(hipMemset(T.counters + 3, 0, sizeof(uint32_t)));
-    if (T.lg) HIPCHK(hipMemset(T.lg, 0, T.lg_bytes));
     T.epoch = 1;
   }
   return USN_OK;
@@ -2480,12 +2437,9 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     }
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
-  bool tx_inline = false;   // tx: the per-endpoint lists built inside the tx launch
   if (tx) {
     const usn_batch &tb = b[0];
-    // the inline lists' granules: G1 | G2 | G3 | DONE (usn_device.hip tx_lists)
-    const size_t lg_bytes = ((size_t)m.b[0].ntiles * (m.b[0].nbw / 2 + m.b[0].nbw + 1) + m.b[0].nbw) * 8;
-    int st = tx_prepare(R, tb.n, m.b[0].ntiles, lg_bytes);
+    int st = tx_prepare(R, tb.n, m.b[0].ntiles);
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
@@ -2504,22 +2458,6 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
-    // USN_TX_LISTS_LAUNCHES (A/B) and the USN_DEBUG_CORRUPT test hook: the
-    // lists by the scan and scatter launches
-    static const bool inline_off = std::getenv("USN_TX_LISTS_LAUNCHES") != nullptr ||
-                                   std::getenv("USN_DEBUG_CORRUPT") != nullptr;
-    t.lists_inline = !inline_off && (c->tx512 ? usn_t512::tx_lists_fit(t) : usn::tx_lists_fit(t));
-    if (t.lists_inline) {
-      t.index = r[0].index;
-      t.bin_off = r[0].bin_off;
-      t.diag = usn::scatter_diag(r[0].scratch, tb.n, t.a.nbins);
-      t.lg = R.lg;
-      t.a.lflags = slow_rank_hook() ? USN_SCF_SLOW_RANK : 0u;
-      st = scratch_tail_zeroed(c, r[0], tb.n, t.a.nbins, (hipStream_t)stream);
-      if (st) return st;
-      tx_inline = true;
-      ++R.tx_inline_launches;
-    }
     if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
     else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
     c->tx.pending = true;
@@ -2536,9 +2474,10 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         it->second.pending = false;
       }
     }
-    const bool t512 = c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units));
-    if (t512) HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
-    else HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+    if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
+      HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
+    else
+      HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
   if (tx || !c->lists_async) {
     uint32_t *txs = nullptr;
@@ -2553,20 +2492,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       // previous tx batch's kernels are done: its usn_finalize synchronised)
       reinterpret_cast<volatile uint32_t *>(c->h_txstate)[11] = 0;
     }
-    if (tx_inline) {   // the lists are built: one wave gathers what usn_finalize reads first
-      usn::TxState xs;
-      xs.out = txs;
-      xs.counters = R.counters;
-      xs.sum = r[0].summary;
-      xs.bin_off = r[0].bin_off;
-      xs.diag = usn::scatter_diag(r[0].scratch, b[0].n, m.b[0].nbins);
-      xs.n = (uint32_t)b[0].n;
-      xs.n_ep = m.b[0].n_ep;
-      HIPCHK(usn_t512::launch_txstate(xs, (hipStream_t)stream));
-    } else {
-      int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
-      if (st) return st;
-    }
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
+    if (st) return st;
     if (tx) {
       if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
       HIPCHK(hipEventRecord(R.txstate_ev, (hipStream_t)stream));
@@ -3301,8 +3228,8 @@ int64_t usn_debug_scatter_fallbacks(usn_ctx *c) {
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->reps[c->sel].device));
   HIPCHK(hipDeviceSynchronize());
-  const uint32_t v = usn_t512::scatter_fallbacks(), w = usn::scatter_fallbacks();
-  return v == 0xFFFFFFFFu || w == 0xFFFFFFFFu ? (int64_t)USN_EHIP : (int64_t)v + w;
+  const uint32_t v = usn_t512::scatter_fallbacks();
+  return v == 0xFFFFFFFFu ? (int64_t)USN_EHIP : (int64_t)v;
 }
 
 int usn_set_lists_async(usn_ctx *c, int on) {

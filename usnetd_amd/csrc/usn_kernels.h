@@ -57,7 +57,6 @@ struct ClassifyArgs {
   const usn_tile_hdr *prev_tiles;
   uint32_t prev_ntiles;
   const usn_summary *prev_summary;
-  uint32_t lflags;          /* tx inline lists: USN_SCF_SLOW_RANK (test hook: ballot ranks too) */
 };
 
 /* Several batches (distinct sources) classified by one launch: workgroup w
@@ -91,11 +90,6 @@ static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 
 struct TxArgs {
   ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
-  /* per-endpoint lists built inside the launch (usn_device.hip tx_lists),
-   * when every tile is resident at once; else scan + scatter launches */
-  uint32_t lists_inline;
-  uint32_t *index, *bin_off, *diag;
-  unsigned long long *lg;     /* G1 [ntiles][nbw/2] | G2 [ntiles][nbw] | G3 [nbw], epoch-tagged */
   unsigned long long *aux;    /* per tile x TXA_GRANULES {epoch, value}: what crosses a tile boundary */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
@@ -115,21 +109,6 @@ struct TxArgs {
 };
 
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
-/* tx: what usn_finalize reads first, gathered by one wave behind the launch
- * into host-mapped memory: {summary flags, counters[0..4], bin_off[n_ep ..
- * n_ep + 3), n, diag} (the scatter's chunk 0 does it when the lists are
- * built by the scan and scatter launches) */
-struct TxState {
-  uint32_t *out;
-  const uint32_t *counters;
-  const usn_summary *sum;
-  const uint32_t *bin_off;
-  const uint32_t *diag;
-  uint32_t n, n_ep;
-};
-/* the tx launch can build its lists inline: every tile resident at once and
- * the batch within tx_lists' thread mapping (usn_device.hip) */
-bool tx_lists_fit(const TxArgs &t);
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
@@ -216,7 +195,6 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
                    ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
-uint32_t scatter_fallbacks();   /* tiles the 256-thread tx kernel's inline lists ranked again */
 
 }  // namespace usn
 
@@ -225,11 +203,8 @@ uint32_t scatter_fallbacks();   /* tiles the 256-thread tx kernel's inline lists
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
 hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream);
-uint32_t scatter_fallbacks();   /* chunks the scatter (and tiles the tx kernel's inline lists)
-                                   ranked again (current device) */
+uint32_t scatter_fallbacks();   /* chunks the scatter ranked again (current device) */
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
-bool tx_lists_fit(const usn::TxArgs &t);
-hipError_t launch_txstate(const usn::TxState &x, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 }
 

@@ -382,17 +382,6 @@ class Ctx:
         f.restype = C.c_int64
         return check(f(self.h), "usn_debug_scatter_fallbacks")
 
-    def lists_inline(self):
-        """(classify, tx) launches of the selected replica that built their
-        per-endpoint lists themselves (every tile resident: no scan /
-        scatter launch; usn_debug_lists_inline)."""
-        out = (C.c_uint32 * 2)()
-        f = self.L.usn_debug_lists_inline
-        f.argtypes = [C.c_void_p, C.c_void_p]
-        f.restype = C.c_int
-        check(f(self.h, out), "usn_debug_lists_inline")
-        return int(out[0]), int(out[1])
-
     def lists_wait(self, result: "DeviceResult", stream=None):
         check(self.L.usn_lists_wait(self.h, C.byref(result.desc), stream), "usn_lists_wait")
 
