@@ -289,7 +289,13 @@ int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
  * which must stay allocated until this call's work has been enqueued.
  * A batch sent by a non-NIC endpoint (tx: find_forward with incoming ==
  * false) learns bridge MACs and answer rules; until its usn_finalize every
- * other call that reads or changes the registry returns USN_EBUSY. */
+ * other call that reads or changes the registry returns USN_EBUSY, except
+ * the source's next tx ring on the same stream: at most two tx batches are
+ * in flight and they are finalized in order (a later one first: USN_EBUSY).
+ * The second ran against the state the first started from; when the first's
+ * usn_finalize changed that state (it learned, or ran a host tail that left
+ * another carried cache or DHCP steering), the second's usn_finalize decides
+ * it again on the host from its first frame. */
 int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream);
 /* Several drained rings of DISTINCT sources (e.g. the rx queues of the NICs
  * polled in one poll() round, main.rs:1029-1046) in one launch: b[k] -> r[k],
@@ -311,7 +317,8 @@ int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t
 int usn_set_lists_async(usn_ctx *ctx, int on);
 int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
 
-/* Ordered host stage for one classified batch (synchronises the stream).
+/* Ordered host stage for one classified batch (synchronises the stream; for
+ * a tx batch, waits for that batch's own launches only).
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
  * frame order and patches decisions and the per-endpoint lists on the device.  Must be called
  * before the next usn_classify of the same source whenever the summary has

@@ -241,3 +241,86 @@ def test_c4tx_more_tiles_than_resident(coracle_mod):
     infos = _run(traffic.config("c4tx", n=1 << 22), coracle_mod, batches=2)
     assert [i.n_host for i in infos] == [0, 0]
 
+
+
+def _pipelined(cfgs, coracle_mod, n_rings):
+    """Rings of one sending endpoint, ring k + 1 classified before ring k's
+    usn_finalize; decisions, lists and the registry against the sequential
+    oracle, ring by ring."""
+    from usnetd_amd import lib, traffic
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfgs[0])
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfgs[0])
+    s = ctx.stream()
+    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
+    rs = [lib.DeviceResult(ctx, cfgs[0].n) for _ in range(2)]
+    infos = []
+    ctx.classify(bs[0], rs[0], s)
+    for k in range(n_rings):
+        if k + 1 < n_rings:
+            ctx.classify(bs[(k + 1) % len(bs)], rs[(k + 1) % 2], s)
+        info = ctx.finalize(bs[k % len(bs)], rs[k % 2], s)
+        c = cfgs[k % len(cfgs)]
+        want = o.forward_batch(c.src, c.frames, c.lens, stride=c.stride)
+        got = rs[k % 2].decisions()
+        bad = np.nonzero((got & katrun.PARITY_MASK) != (want & katrun.PARITY_MASK))[0]
+        assert bad.size == 0, "ring %d: %d mismatches, first %d: got %#x want %#x" % (
+            k, bad.size, bad[0], got[bad[0]], want[bad[0]])
+        check_order(rs[k % 2], got)
+        infos.append(info)
+    assert sorted(o.rules()) == _registry_gpu(ctx)
+    assert o.bridge_count() == ctx.bridge_count()
+    ctx.close()
+    return infos
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_tx_pipelined_rings(n, coracle_mod):
+    """ring k + 1 enqueued before ring k's usn_finalize.  Ring
+    0 learns, so ring 1 (which ran against the state ring 0 started from) is
+    decided again on the host; rings 2.. run against the learned state and
+    are final on the device."""
+    from usnetd_amd import traffic
+    infos = _pipelined([traffic.config("c4tx", n=n)], coracle_mod, 5)
+    assert infos[0].n_learned > 0
+    assert infos[1].n_host == n                  # redone on the host
+    assert [i.n_host for i in infos[2:]] == [0, 0, 0]
+
+
+def test_tx_pipelined_rings_all_learn(coracle_mod):
+    """Back-to-back rings that all learn (new flows in every ring): each ring
+    after the first is redone on the host, and every decision, the registry
+    and the bridge equal the sequential oracle's."""
+    from usnetd_amd import traffic
+    cfgs = [traffic.c4tx(n=1 << 16, seed=6 + k) for k in range(4)]
+    infos = _pipelined(cfgs, coracle_mod, 4)
+    assert all(i.n_learned > 0 for i in infos)
+    assert [i.n_host for i in infos[1:]] == [1 << 16] * 3
+
+
+def test_tx_pipeline_order_and_busy(coracle_mod):
+    """At most two tx rings in flight, of one source on one stream, finalized
+    in order; nothing else while they are (USN_EBUSY)."""
+    import ctypes as C
+    from usnetd_amd import lib, traffic
+    cfg = traffic.config("c4tx", n=4096)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s, s2 = ctx.stream(), ctx.stream()
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+    r0, r1, r2 = (lib.DeviceResult(ctx, cfg.n) for _ in range(3))
+    L = ctx.L
+    ctx.classify(b, r0, s)
+    assert L.usn_classify(ctx.h, C.byref(b.desc), C.byref(r1.desc), s2) == lib.USN_EBUSY   # other stream
+    ctx.classify(b, r1, s)
+    assert L.usn_classify(ctx.h, C.byref(b.desc), C.byref(r2.desc), s) == lib.USN_EBUSY    # a third
+    info = lib.FinalizeInfo()
+    assert L.usn_finalize(ctx.h, C.byref(b.desc), C.byref(r1.desc), s, C.byref(info)) == lib.USN_EBUSY
+    w = lib.make_want(traffic.LOCAL, 17, 4444)
+    assert ctx.L.usn_add_match(ctx.h, C.byref(w), 2, 0) == lib.USN_EBUSY
+    ctx.finalize(b, r0, s)
+    ctx.finalize(b, r1, s)
+    ctx.classify(b, r2, s)
+    ctx.finalize(b, r2, s)
+    ctx.close()

@@ -49,6 +49,13 @@ case $S in
     PMC_CFGS="c3" bash tools/gpu.sh $S pmc || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
     ;;
+  r04d)
+    # tx rings pipelined (ring k + 1 before ring k's finalize): the suite, the
+    # bench (c4tx pipelined + sequential), c3 PMC at the bench's launch shape
+    bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    PMC_CFGS="c3" bash tools/gpu.sh $S pmc
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <deque>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -423,15 +424,21 @@ struct Replica {
   unsigned long long *d_bridge_set = nullptr;   // open addressing, bit 63 = used
   size_t d_bridge_set_cap = 0;
   uint64_t bridge_version = 0;
-  /* tx scratch */
-  uint64_t learned_frames = 0;
+  /* tx scratch.  Epoch-tagged (aux granules, the learning sets): shared by
+   * the batches in flight.  What usn_finalize of a batch reads after the
+   * next batch has launched (its counters, its learned list, its gathered
+   * state) lives in one of two slots, alternating (usn_ctx::txq) */
   unsigned long long *aux = nullptr;   // TXA_GRANULES per tile, tagged with the epoch
   uint32_t aux_tiles = 0;
   unsigned long long *macset = nullptr, *ruleset = nullptr;
   uint32_t set_slots = 0;
-  uint4 *learned = nullptr;
-  uint32_t learned_cap = 0;
-  uint32_t *counters = nullptr;   // TxArgs::counters
+  struct TxSlot {
+    uint4 *learned = nullptr;
+    uint64_t learned_frames = 0;
+    uint32_t learned_cap = 0;
+    uint32_t *counters = nullptr;       // TxArgs::counters
+    hipEvent_t txstate_ev = nullptr;    // the batch's gathered state (usn_ctx::h_txstate) landed
+  } txs[2];
   uint32_t *listen = nullptr;
   size_t listen_cap = 0;
   int listen_src = -1;           // the endpoint / version whose listening triples `listen` holds
@@ -441,8 +448,9 @@ struct Replica {
    * launch by the `classified` event */
   hipStream_t side = nullptr;
   hipEvent_t classified = nullptr;
-  hipEvent_t txstate_ev = nullptr;   // a tx batch's state copies (usn_ctx::h_txstate) landed
 };
+
+constexpr size_t TXSTATE_BYTES = 64;   // a tx batch's gathered state (16 words) per slot
 
 struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
@@ -490,13 +498,24 @@ struct usn_ctx {
   uint64_t bridge_version = 0;
   std::vector<unsigned long long> bridge_set;
   uint32_t bridge_mask = 0;
-  /* the tx batch in flight (one per context: it changes shared state) */
+  /* tx batches in flight: classified, not finalized, so the registry is not
+   * final (every registry call returns USN_EBUSY).  At most two, of one
+   * source, on one stream and replica: ring k + 1 may be enqueued before ring
+   * k's usn_finalize (the device is not left idle while the host finalizes).
+   * Ring k + 1 ran against the state ring k started from; when ring k's
+   * finalize changed that state (it learned, or ran a host tail), ring k + 1
+   * is decided again on the host from its first frame (tx_redo_next). */
   struct Tx {
-    bool pending = false;   // classified, not finalized: registry not final
-    int src = -1;
-    uint32_t replica = 0;
     const uint32_t *decisions = nullptr;
-  } tx;
+    int src = -1;
+    uint32_t replica = 0, slot = 0, epoch = 0;
+    hipStream_t stream = nullptr;
+  };
+  std::deque<Tx> txq;
+  uint32_t tx_next_slot = 0;
+  bool tx_redo_next = false;     // the next batch in txq is redone on the host from frame 0
+  bool tx_cout_valid = false;    // ... from this carried cache (the previous batch's host tail)
+  uint32_t tx_cout[6] = {0, 0, 0, 0, 0, 0};   // {state, dst, info[4]}
   /* pinned staging for usn_finalize's small reads (summary, tile headers,
    * tx counters): async copies and one stream sync instead of three
    * synchronous pageable copies */
@@ -536,9 +555,9 @@ struct usn_ctx {
   /* a tx batch's summary flags, counters and class totals, written into
    * host-mapped memory by the scatter's first chunk (usn_finalize of a
    * batch that learned nothing reads only these) */
-  uint8_t *h_txstate = nullptr;
+  uint8_t *h_txstate = nullptr;      // 2 slots x TXSTATE_BYTES
   size_t h_txstate_cap = 0;
-  const void *txstate_for = nullptr;   // the result (decisions) whose state it holds
+  const void *txstate_for[2] = {nullptr, nullptr};   // the result (decisions) each slot holds
 };
 
 namespace {
@@ -1763,8 +1782,9 @@ void usn_ctx_destroy(usn_ctx *c) {
     (void)hipSetDevice(R.device);
     (void)hipDeviceSynchronize();
     for (void *p : {(void *)R.d_table, R.d_patch, (void *)R.d_bridge, (void *)R.d_bridge_set,
-                    (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.learned,
-                    (void *)R.counters, (void *)R.listen})
+                    (void *)R.aux, (void *)R.macset, (void *)R.ruleset, (void *)R.txs[0].learned,
+                    (void *)R.txs[0].counters, (void *)R.txs[1].learned, (void *)R.txs[1].counters,
+                    (void *)R.listen})
       if (p) (void)hipFree(p);
   }
   for (auto &kv : c->lists_ev)
@@ -1775,7 +1795,8 @@ void usn_ctx_destroy(usn_ctx *c) {
   for (Replica &R : c->reps) {
     (void)hipSetDevice(R.device);
     if (R.classified) (void)hipEventDestroy(R.classified);
-    if (R.txstate_ev) (void)hipEventDestroy(R.txstate_ev);
+    for (auto &x : R.txs)
+      if (x.txstate_ev) (void)hipEventDestroy(x.txstate_ev);
     if (R.side) (void)hipStreamDestroy(R.side);
   }
   for (Chain &ch : c->chains)
@@ -1795,7 +1816,7 @@ void usn_ctx_destroy(usn_ctx *c) {
 int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
   if (!c || id >= USN_MAX_ENDPOINTS || kind < USN_EP_NIC || kind > USN_EP_UDS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   if (c->eps[id].used) return USN_EEXIST;
   if ((kind == USN_EP_NIC) != (for_nic < 0)) return USN_EINVAL;   // main.rs:157-159
   if (for_nic >= 0 && (for_nic >= USN_MAX_ENDPOINTS || !c->eps[for_nic].used ||
@@ -1815,7 +1836,7 @@ int usn_endpoint_add(usn_ctx *c, uint16_t id, int kind, int32_t for_nic) {
 int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
   if (!c || id >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   if (!c->eps[id].used) return USN_ENOENT;
   for (auto it = c->rules.begin(); it != c->rules.end();) {   // match_register.retain
     if (it->second.owner == id) {
@@ -1833,7 +1854,7 @@ int usn_endpoint_remove(usn_ctx *c, uint16_t id) {
 int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
   if (!c || !w || owner >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   Ep &e = c->eps[owner];
   if (!e.used) return USN_ENOENT;
   const WantKey k = canon(*w);
@@ -1850,7 +1871,7 @@ int usn_add_match(usn_ctx *c, const usn_want *w, uint16_t owner, int sticky) {
 int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
   if (!c || !w) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   const WantKey k = canon(*w);
   auto it = c->rules.find(k);
   if (it == c->rules.end()) return 0;
@@ -1863,14 +1884,14 @@ int usn_remove_match(usn_ctx *c, const usn_want *w, uint16_t requester) {
 int usn_rule_count(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   return (int)c->rules.size();
 }
 
 int usn_rules_get(usn_ctx *c, usn_want *w, uint16_t *owner, uint8_t *sticky, uint32_t cap) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   uint32_t n = 0;
   for (const auto &kv : c->rules) {
     if (n >= cap) break;
@@ -1894,7 +1915,7 @@ int usn_rules_get(usn_ctx *c, usn_want *w, uint16_t *owner, uint8_t *sticky, uin
 int usn_lookup(usn_ctx *c, const usn_want *w) {
   if (!c || !w) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   const int e = registry_get(c, canon(*w));
   return e < 0 ? USN_ENOENT : e;
 }
@@ -1902,7 +1923,7 @@ int usn_lookup(usn_ctx *c, const usn_want *w) {
 int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
   if (!c || !mac) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   c->bridge.push_back(mac48(mac));
   c->bridge_dirty = true;
   return USN_OK;
@@ -1911,7 +1932,7 @@ int usn_bridge_add(usn_ctx *c, const uint8_t mac[6]) {
 int usn_bridge_set(usn_ctx *c, const uint8_t (*macs)[6], uint32_t n) {
   if (!c || (n && !macs)) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   c->bridge.clear();
   for (uint32_t i = 0; i < n; ++i) c->bridge.push_back(mac48(macs[i]));
   c->bridge_dirty = true;
@@ -1921,7 +1942,7 @@ int usn_bridge_set(usn_ctx *c, const uint8_t (*macs)[6], uint32_t n) {
 int usn_table_build(usn_ctx *c, const usn_rule *rules, uint32_t n) {
   if (!c || (n && !rules)) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   for (uint32_t i = 0; i < n; ++i)
     if (rules[i].endpoint >= USN_MAX_ENDPOINTS || !c->eps[rules[i].endpoint].used)
       return USN_ENOENT;
@@ -1948,14 +1969,14 @@ int usn_table_build(usn_ctx *c, const usn_rule *rules, uint32_t n) {
 int usn_bridge_count(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   return (int)c->bridge.size();
 }
 
 int usn_frag_clear(usn_ctx *c) {
   if (!c) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   c->frags.clear();
   return USN_OK;
 }
@@ -2040,9 +2061,10 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
   std::lock_guard<std::mutex> g(c->mu);
   Replica &R = c->reps[c->sel];
   std::memset(out10, 0, 10 * sizeof(uint32_t));
-  if (R.counters) {
+  const uint32_t slot = c->txq.empty() ? (c->tx_next_slot ^ 1u) : c->txq.back().slot;   // the latest
+  if (R.txs[slot].counters) {
     HIPCHK(hipSetDevice(R.device));
-    HIPCHK(hipMemcpy(out10, R.counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out10, R.txs[slot].counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   out10[8] = R.epoch;
   return USN_OK;
@@ -2051,7 +2073,7 @@ int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
 int usn_cache_clear(usn_ctx *c, uint16_t ep) {
   if (!c || ep >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
+  if (!c->txq.empty()) return USN_EBUSY;
   cache_clear(c, ep);
   return USN_OK;
 }
@@ -2289,14 +2311,21 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
 
 /* device scratch of a tx batch of n frames on replica R; the epoch-tagged
  * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
-static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
-  if (n > T.learned_frames) {
-    if (T.learned) HIPCHK(hipFree(T.learned));
-    T.learned = nullptr;
-    HIPCHK(hipMalloc(&T.learned, n * 4 * sizeof(uint4)));   // <= 2 items of 2 x uint4 per frame
-    T.learned_frames = n;
-    T.learned_cap = (uint32_t)(2 * n);
+static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bool in_flight,
+                      hipStream_t s) {
+  Replica::TxSlot &X = T.txs[slot];
+  if (n > X.learned_frames) {
+    if (X.learned) HIPCHK(hipFree(X.learned));
+    X.learned = nullptr;
+    HIPCHK(hipMalloc(&X.learned, n * 4 * sizeof(uint4)));   // <= 2 items of 2 x uint4 per frame
+    X.learned_frames = n;
+    X.learned_cap = (uint32_t)(2 * n);
   }
+  // below, buffers the batch in flight uses are replaced or cleared: only
+  // after it has drained (rare: growth, or the 16-bit epoch wrapping)
+  const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
+  if (in_flight && (ntiles > T.aux_tiles || slots > T.set_slots || T.epoch + 1 > 0xFFFFu))
+    HIPCHK(hipDeviceSynchronize());
   if (ntiles > T.aux_tiles) {   // zeroed: no flag holds an epoch yet
     if (T.aux) HIPCHK(hipFree(T.aux));
     T.aux = nullptr;
@@ -2304,11 +2333,13 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
     HIPCHK(hipMemset(T.aux, 0, (size_t)ntiles * usn::TXA_WORDS_BYTES));
     T.aux_tiles = ntiles;
   }
-  if (!T.counters) {
-    HIPCHK(hipMalloc(&T.counters, 8 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(T.counters, 0, 8 * sizeof(uint32_t)));
+  if (!X.counters) {
+    HIPCHK(hipMalloc(&X.counters, 8 * sizeof(uint32_t)));
+    HIPCHK(hipMemset(X.counters, 0, 8 * sizeof(uint32_t)));
   }
-  const uint32_t slots = next_pow2((uint32_t)std::max<uint64_t>(1024, 2 * n));   // load <= 1/2
+  // the slot's timeout mark (counters[3], the epoch of a batch whose waits
+  // timed out): cleared for this batch (the slot's previous batch is final)
+  HIPCHK(hipMemsetAsync(X.counters + 3, 0, sizeof(uint32_t), s));
   bool clear = false;
   if (slots > T.set_slots) {
     if (T.macset) HIPCHK(hipFree(T.macset));
@@ -2324,7 +2355,6 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles) {
     HIPCHK(hipMemset(T.macset, 0, (size_t)T.set_slots * 2 * 8));
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
     HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
-    HIPCHK(hipMemset(T.counters + 3, 0, sizeof(uint32_t)));
     T.epoch = 1;
   }
   return USN_OK;
@@ -2396,7 +2426,6 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
   if (c->reps.empty()) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->tx.pending) return USN_EBUSY;
   bool tx = false;
   for (uint32_t k = 0; k < count; ++k) {
     int st = check_batch(c, &b[k], &r[k]);
@@ -2407,6 +2436,14 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   }
   if (tx && count != 1) return USN_EINVAL;   // a tx batch changes shared state: alone
   const uint32_t rep = c->sel;
+  /* while tx batches are in flight: only the next ring of the same source,
+   * on the same stream and replica, and at most two in flight */
+  if (!c->txq.empty()) {
+    const usn_ctx::Tx &p = c->txq.back();
+    if (!tx || c->txq.size() >= 2 || p.src != b[0].src_endpoint || p.replica != rep ||
+        p.stream != (hipStream_t)stream || p.decisions == r[0].decisions)
+      return USN_EBUSY;
+  }
   Replica &R = c->reps[rep];
   /* the table-version fence: this replica sees every registry and bridge
    * change made before this call */
@@ -2437,9 +2474,11 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     }
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
+  uint32_t slot = 0;
   if (tx) {
     const usn_batch &tb = b[0];
-    int st = tx_prepare(R, tb.n, m.b[0].ntiles);
+    slot = c->tx_next_slot;
+    int st = tx_prepare(R, tb.n, m.b[0].ntiles, slot, !c->txq.empty(), (hipStream_t)stream);
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
@@ -2451,19 +2490,24 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.ruleset = R.ruleset;
     t.macset_mask = t.ruleset_mask = R.set_slots - 1;
     t.epoch = R.epoch;
-    t.learned = R.learned;
-    t.counters = R.counters;
-    t.learned_cap = R.learned_cap;
+    t.learned = R.txs[slot].learned;
+    t.counters = R.txs[slot].counters;
+    t.learned_cap = R.txs[slot].learned_cap;
     t.bridge_set = R.d_bridge_set;
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
     t.next_dhcp_set = t.a.next_dhcp_set;
     if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
     else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
-    c->tx.pending = true;
-    c->tx.src = tb.src_endpoint;
-    c->tx.replica = rep;
-    c->tx.decisions = r[0].decisions;
+    usn_ctx::Tx p;
+    p.decisions = r[0].decisions;
+    p.src = tb.src_endpoint;
+    p.replica = rep;
+    p.slot = slot;
+    p.epoch = R.epoch;
+    p.stream = (hipStream_t)stream;
+    c->txq.push_back(p);
+    c->tx_next_slot ^= 1u;
   } else {
     /* a result whose lists are still being built on the side stream is not
      * overwritten before they are done */
@@ -2483,21 +2527,23 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     uint32_t *txs = nullptr;
     if (tx) {   // what usn_finalize reads first: written into host memory by the scatter's chunk 0
       if (!c->h_txstate) {
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), 64,
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_txstate), 2 * TXSTATE_BYTES,
                              hipHostMallocMapped | hipHostMallocCoherent));
-        c->h_txstate_cap = 64;
+        c->h_txstate_cap = 2 * TXSTATE_BYTES;
       }
       HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&txs), c->h_txstate, 0));
+      txs += slot * (TXSTATE_BYTES / 4);
       // word 11: set by any scatter chunk that finds inconsistent lists (the
-      // previous tx batch's kernels are done: its usn_finalize synchronised)
-      reinterpret_cast<volatile uint32_t *>(c->h_txstate)[11] = 0;
+      // slot's previous batch is final: its usn_finalize synchronised)
+      reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
     }
-    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.counters : nullptr);
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr);
     if (st) return st;
     if (tx) {
-      if (!R.txstate_ev) HIPCHK(hipEventCreateWithFlags(&R.txstate_ev, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(R.txstate_ev, (hipStream_t)stream));
-      c->txstate_for = r[0].decisions;
+      Replica::TxSlot &X = R.txs[slot];
+      if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(X.txstate_ev, (hipStream_t)stream));
+      c->txstate_for[slot] = r[0].decisions;
     }
   } else {
     // the scatter on the side stream, after this launch; the caller's stream
@@ -2752,31 +2798,71 @@ int fetch_host_lists(usn_ctx *c, const usn_result *r, const std::vector<usn_tile
 
 }  // namespace
 
+/* the cache a batch's device chain carries out: its last tile with a
+ * touching frame, else what it carried in (as resolve_carry / chain_to_host) */
+static void device_cout(const std::vector<usn_tile_hdr> &th, const usn_summary &sum, CacheState &cs) {
+  cs.valid = false;
+  cs.dst = 0;
+  std::memset(cs.info.w, 0, 16);
+  for (size_t t = th.size(); t > 0; --t) {
+    const usn_tile_hdr &h = th[t - 1];
+    if (!(h.last_state & USN_TS_HAS)) continue;
+    if ((h.last_state & USN_TS_RETAINED) && !(h.last_state & USN_TS_UNKNOWN)) {
+      cs.valid = true;
+      cs.dst = h.last_dst;
+      std::memcpy(cs.info.w, h.last_info, 16);
+    }
+    return;
+  }
+  cs.valid = sum.cin_state & USN_CS_VALID;
+  cs.dst = sum.cin_dst;
+  std::memcpy(cs.info.w, sum.cin_info, 16);
+}
+static bool same_cache(const CacheState &a, const CacheState &b) {
+  if (a.valid != b.valid) return false;
+  return !a.valid || (a.dst == b.dst && std::memcmp(a.info.w, b.info.w, 16) == 0);
+}
+
 /* Ordered host stage of a tx batch.  Frames before the first F_HOST frame h
  * are final on the device: apply what they learned in frame order (bridge
  * MACs, answer rules with the NIC cache reset, first fragments into the map).
  * From h on, find_forward runs sequentially on the host (endpoint.rs:172-296)
  * from the cache state just before h.  An overflow of the device sets
- * (counters[1]) makes h = 0. */
+ * (counters[1]) makes h = 0.  `redo`: the batch ran while the batch before
+ * it (pipelined, usn_ctx::txq) had not been finalized, and that finalize
+ * changed the state this batch started from: h = 0, from the carried cache
+ * usn_ctx::tx_cout when the batch before ran a host tail (else the one the
+ * device resolved).  *changed: this finalize changed the state a batch
+ * launched after this one started from (registry, bridge, DHCP steering, or
+ * a carried cache other than the device chain's). */
 static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_t s,
-                       usn_finalize_info *info) {
+                       usn_finalize_info *info, const usn_ctx::Tx &txp, bool redo, bool *changed) {
   StageClock clk("finalize_tx");
+  *changed = false;
+  // the previous batch's carried-out cache (its host tail), for a redo of this one
+  const bool cout_in = c->tx_cout_valid;
+  uint32_t cin_redo[6];
+  std::memcpy(cin_redo, c->tx_cout, sizeof cin_redo);
+  c->tx_cout_valid = false;
   const uint64_t n = b->n;
   const uint32_t ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
   const int src = b->src_endpoint;
   Ep &S = c->eps[src];
-  Replica &R = c->reps[c->tx.replica];
+  Replica &R = c->reps[txp.replica];
+  Replica::TxSlot &X = R.txs[txp.slot];
+  const int nd_src0 = S.next_dhcp, nd_nic0 = S.for_nic >= 0 ? c->eps[S.for_nic].next_dhcp : -1;
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[8];
-  if (c->txstate_for == r->decisions && R.txstate_ev) {   // gathered behind the launch
-    HIPCHK(hipEventSynchronize(R.txstate_ev));
-    c->txstate_for = nullptr;
-    const volatile uint32_t *q = reinterpret_cast<const volatile uint32_t *>(c->h_txstate);
+  if (c->txstate_for[txp.slot] == r->decisions && X.txstate_ev) {   // gathered behind the launch
+    HIPCHK(hipEventSynchronize(X.txstate_ev));
+    c->txstate_for[txp.slot] = nullptr;
+    const volatile uint32_t *q =
+        reinterpret_cast<const volatile uint32_t *>(c->h_txstate + txp.slot * TXSTATE_BYTES);
     uint32_t v[12];
     for (int k = 0; k < 12; ++k) v[k] = q[k];
     { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, n, c->n_ep + 3), s); if (e) return e; }
-    if (v[1] == 0 && v[2] == 0 && v[4] != R.epoch && v[5] == 0) {
+    if (!redo && v[1] == 0 && v[2] == 0 && v[4] != txp.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
       // results are final; class totals from bin_off (EP bins, NIC, FLOOD, DROP)
       usn_finalize_info fi;
@@ -2791,13 +2877,14 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     }
   }
   {
-    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, R.counters,
+    const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, X.counters,
                                     usn::scatter_diag(r->scratch, n, c->n_ep + 3));
     if (e) return e;
   }
-  // a tile wait of the kernel timed out (counters[3] = this epoch): the whole
-  // batch goes to the host stage
-  if (cnt[3] == R.epoch) cnt[1] |= 8u;
+  // a tile wait of the kernel timed out (counters[3] = this epoch), or the
+  // batch is redone: the whole batch goes to the host stage
+  if (cnt[3] == txp.epoch) cnt[1] |= 8u;
+  if (redo) cnt[1] |= 16u;
   clk.mark("state");
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
@@ -2823,7 +2910,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     for (uint32_t j : hosts)
       if (hv.dec[j] & USN_F_HOST) { h = j; break; }
   /* learned items and first fragments before h, in frame order */
-  const uint32_t nl = std::min(cnt[0], R.learned_cap);
+  const uint32_t nl = std::min(cnt[0], X.learned_cap);
   const uint4 *items = nullptr;   // the learned list, through pinned memory
   if (nl) {
     const size_t bytes = (size_t)nl * 2 * sizeof(uint4);
@@ -2835,7 +2922,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_items), cap, hipHostMallocDefault));
       c->h_items_cap = cap;
     }
-    HIPCHK(hipMemcpyAsync(c->h_items, R.learned, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_items, X.learned, bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     items = c->h_items;
   }
@@ -2969,6 +3056,11 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     cs.valid = sum.cin_state & USN_CS_VALID;
     cs.dst = sum.cin_dst;
     std::memcpy(cs.info.w, sum.cin_info, 16);
+    if (redo && cout_in) {   // h = 0: the previous batch's host tail left this cache
+      cs.valid = cin_redo[0] & USN_CS_VALID;
+      cs.dst = cin_redo[1];
+      std::memcpy(cs.info.w, cin_redo + 2, 16);
+    }
     if (walk_none) cs.valid = false;
     if (walk < n) {
       ParsedH p = host_parse(c, walk_bytes.data(), walk_len);
@@ -3006,7 +3098,18 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     HIPCHK(hipStreamSynchronize(s));
     st = lists_check(usn::scatter_diag(r->scratch, n, c->n_ep + 3), s);
     if (st) return st;
+    // what a batch launched after this one took as its carried cache: the
+    // device chain's (this batch's tile headers); the host tail's may differ
+    CacheState dev;
+    device_cout(th, sum, dev);
+    *changed = !same_cache(cs, dev);
+    c->tx_cout_valid = true;
+    c->tx_cout[0] = cs.valid ? USN_CS_VALID : 0u;
+    c->tx_cout[1] = cs.dst;
+    std::memcpy(c->tx_cout + 2, cs.info.w, 16);
   }
+  *changed = *changed || fi.n_learned > 0 || S.next_dhcp != nd_src0 ||
+             (S.for_nic >= 0 && c->eps[S.for_nic].next_dhcp != nd_nic0);
   if (info) *info = fi;
   return USN_OK;
 }
@@ -3016,16 +3119,20 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   if (!c || !b || !r || b->n == 0 || b->src_endpoint >= USN_MAX_ENDPOINTS) return USN_EINVAL;
   if (c->reps.empty()) return USN_ENODEV;
   std::lock_guard<std::mutex> g(c->mu);
-  const bool txb = c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions;
+  // the oldest tx batch in flight (finalized in order)
+  const bool txb = !c->txq.empty() && c->txq.front().src == b->src_endpoint &&
+                   c->txq.front().decisions == r->decisions;
   const auto br = c->batch_rep.find(r->decisions);
-  const uint32_t rep = txb ? c->tx.replica
+  const uint32_t rep = txb ? c->txq.front().replica
                      : br != c->batch_rep.end() ? br->second.rep : c->chains[b->src_endpoint].replica;
   // the bins the batch was classified with (an rx batch's endpoints may have
   // grown since; a tx batch blocks every registry change until it is final)
   const uint32_t nb0 = br != c->batch_rep.end() ? br->second.nbins : c->n_ep + 3;
   HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipStreamSynchronize(s));
+  // (a tx batch waits for its own launches only: the next ring may already
+  // be queued behind them on the stream)
+  if (!txb) HIPCHK(hipStreamSynchronize(s));
   {  // lists built on the side stream (usn_set_lists_async)
     auto it = c->lists_ev.find(r->decisions);
     if (it != c->lists_ev.end() && it->second.pending) {
@@ -3034,15 +3141,21 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
     }
   }
   if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
-    if (c->tx.pending && c->tx.src == b->src_endpoint && c->tx.decisions == r->decisions) {
-      const int st = finalize_tx(c, b, r, s, info);
+    if (txb) {
+      const usn_ctx::Tx p = c->txq.front();
+      bool changed = false;
+      const int st = finalize_tx(c, b, r, s, info, p, c->tx_redo_next, &changed);
       // refused before any side effect (a frame needs the frame reader and
       // none is set): the batch stays pending, so a call after
       // usn_set_frame_reader applies what it learned
-      if (st != USN_EAGAIN_READER) c->tx.pending = false;
-      return st == USN_EAGAIN_READER ? USN_EINVAL : st;
+      if (st == USN_EAGAIN_READER) return USN_EINVAL;
+      c->txq.pop_front();
+      // the next ring in flight started from the state before this finalize:
+      // decided again on the host when this one changed it (or failed)
+      c->tx_redo_next = !c->txq.empty() && (changed || st != USN_OK);
+      return st;
     }
-    if (c->tx.pending) return USN_EBUSY;
+    if (!c->txq.empty()) return USN_EBUSY;   // a later ring in flight (in order), or another source
     /* an already finalized tx batch: its results are final */
     const uint32_t nt = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
     std::vector<usn_tile_hdr> th(nt);
