@@ -54,7 +54,8 @@ case $S in
     # bench (c4tx pipelined + sequential), c3 PMC at the bench's launch shape
     bash tools/gpu.sh $S testsall || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
-    PMC_CFGS="c3" bash tools/gpu.sh $S pmc
+    PMC_CFGS="c3" bash tools/gpu.sh $S pmc || exit 1
+    SCB_CFGS="c5 c2" SCB_VARIANTS="base scnochk scwpe4" bash tools/gpu.sh $S scb
     ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -2886,6 +2886,10 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
 #ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
 #define USN_SC_GROUP 1
 #endif
+#ifndef USN_SC_CHECKS   /* A/B only: 0 = no empty-slot sentinel and no inconsistency report
+                           (the bounds clamps stay) */
+#define USN_SC_CHECKS 1
+#endif
 #ifndef USN_SCATTER_WPE   /* waves per SIMD the scatter is compiled for: 6 = 3 workgroups per CU
                              (80 VGPRs, a few spilled): c5 scan + scatter 57.5 vs 61.7 us per 16M
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
@@ -3004,7 +3008,7 @@ void scatter_kernel(ScatterArgs s) {
   }
   // every stage slot starts empty: a slot still empty at the write-out means
   // the count rows disagree with the decisions (reported, never hidden)
-  {
+  if (USN_SC_CHECKS) {
     uint4 *st4 = reinterpret_cast<uint4 *>(stage);
 #pragma unroll
     for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -3094,7 +3098,7 @@ void scatter_kernel(ScatterArgs s) {
     unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
   }
   STAMP(11);
-  if (USN_ABL_SC == 0 && __ballot(bad) && lane == 0) {   // rare: one report per wave
+  if (USN_ABL_SC == 0 && USN_SC_CHECKS && __ballot(bad) && lane == 0) {   // rare: one report per wave
     atomicOr(B.diag, USN_DIAG_LISTS);
     if (s.txs_out) s.txs_out[11] = USN_DIAG_LISTS;   // tx: beside chunk 0's copy of the scan's word
   }
