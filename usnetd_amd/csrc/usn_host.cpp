@@ -2311,8 +2311,7 @@ static int check_batch(usn_ctx *c, const usn_batch *b, const usn_result *r) {
 
 /* device scratch of a tx batch of n frames on replica R; the epoch-tagged
  * sets are cleared only when (re)allocated or when the 16-bit epoch wraps */
-static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bool in_flight,
-                      hipStream_t s) {
+static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bool in_flight) {
   Replica::TxSlot &X = T.txs[slot];
   if (n > X.learned_frames) {
     if (X.learned) HIPCHK(hipFree(X.learned));
@@ -2337,9 +2336,6 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bo
     HIPCHK(hipMalloc(&X.counters, 8 * sizeof(uint32_t)));
     HIPCHK(hipMemset(X.counters, 0, 8 * sizeof(uint32_t)));
   }
-  // the slot's timeout mark (counters[3], the epoch of a batch whose waits
-  // timed out): cleared for this batch (the slot's previous batch is final)
-  HIPCHK(hipMemsetAsync(X.counters + 3, 0, sizeof(uint32_t), s));
   bool clear = false;
   if (slots > T.set_slots) {
     if (T.macset) HIPCHK(hipFree(T.macset));
@@ -2355,6 +2351,10 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bo
     HIPCHK(hipMemset(T.macset, 0, (size_t)T.set_slots * 2 * 8));
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
     HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
+    // the slots' timeout marks (counters[3]: the epoch of a batch whose waits
+    // timed out) hold epochs of the cycle that ends here (the device drained)
+    for (auto &x : T.txs)
+      if (x.counters) HIPCHK(hipMemset(x.counters + 3, 0, sizeof(uint32_t)));
     T.epoch = 1;
   }
   return USN_OK;
@@ -2478,7 +2478,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
-    int st = tx_prepare(R, tb.n, m.b[0].ntiles, slot, !c->txq.empty(), (hipStream_t)stream);
+    int st = tx_prepare(R, tb.n, m.b[0].ntiles, slot, !c->txq.empty());
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
