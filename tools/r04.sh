@@ -57,6 +57,14 @@ case $S in
     PMC_CFGS="c3" bash tools/gpu.sh $S pmc || exit 1
     SCB_CFGS="c5 c2" SCB_VARIANTS="base scnochk scwpe4" bash tools/gpu.sh $S scb
     ;;
+  r04e)
+    # final-tree counters and kernel breakdown: rocprof of the bench (per
+    # kernel medians), PMC traffic of c5 / c2 / c4 and of the tx call
+    bash tools/gpu.sh $S rocprof || exit 1
+    PMC_CFGS="c5 c2 c4" bash tools/gpu.sh $S pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json > $O/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
