@@ -65,6 +65,14 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json > $O/pmct_c4tx.log 2>&1
     ;;
+  r04f)
+    # u8 count rows with per-tile exception rows: the suite, scan + scatter
+    # A/B against r04b's u16 rows, the bench, the kernel breakdown
+    bash tools/gpu.sh $S testsall || exit 1
+    SCB_CFGS="c5 c2" SCB_VARIANTS="base" bash tools/gpu.sh $S scb || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
