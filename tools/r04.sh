@@ -71,7 +71,17 @@ case $S in
     bash tools/gpu.sh $S testsall || exit 1
     SCB_CFGS="c5 c2" SCB_VARIANTS="base" bash tools/gpu.sh $S scb || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
-    bash tools/gpu.sh $S rocprof
+    bash tools/gpu.sh $S rocprof || exit 1
+    # small launches (1024 tiles: a tx ring, c3's calls): chunk length A/B
+    for tc in 1 2 4; do
+      for c in c4 c3; do
+        if [ $c = c4 ]; then A="--frames 1048576 --multi 1"; else A="--frames 262144 --multi 4"; fi
+        USN_SCATTER_TC=$tc timeout -k 10 300 python tools/scatter_bench.py --config $c $A --launches 100 \
+          > $O/scb_small_${c}_tc$tc.log 2>&1 || exit 1
+      done
+      USN_SCATTER_TC=$tc timeout -k 10 300 python tools/txbench.py 1048576 40 1 --rotate 6 \
+        > $O/txbench_tc$tc.log 2>&1 || exit 1
+    done
     ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
