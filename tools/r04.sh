@@ -83,6 +83,13 @@ case $S in
         > $O/txbench_tc$tc.log 2>&1 || exit 1
     done
     ;;
+  r04g)
+    # u8 rows + exception rows (HEAD) against u16 rows (f078668) in one
+    # process (tools/abl_commit.sh builds both): whole calls, then the lists
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="u8rows u16rows" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="u8rows u16rows" bash tools/gpu.sh $S abl || exit 1
+    SCB_CFGS="c5 c2" SCB_VARIANTS="u8rows u16rows" bash tools/gpu.sh $S scb
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
