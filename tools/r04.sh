@@ -90,6 +90,14 @@ case $S in
     ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="u8rows u16rows" bash tools/gpu.sh $S abl || exit 1
     SCB_CFGS="c5 c2" SCB_VARIANTS="u8rows u16rows" bash tools/gpu.sh $S scb
     ;;
+  r04h)
+    # u8 rows, branch-free loads: the scatter tests, then r04g's A/B
+    mkdir -p $O
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+      tests/test_gpu_scatter.py > $O/pytest_scatter.log 2>&1 || { tail -30 $O/pytest_scatter.log; exit 1; }
+    tail -2 $O/pytest_scatter.log
+    bash tools/r04.sh r04g
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
