@@ -98,6 +98,20 @@ case $S in
     tail -2 $O/pytest_scatter.log
     bash tools/r04.sh r04g
     ;;
+  r04i)
+    # tx lists on the side stream (USN_TX_LISTS_SIDE=1) against the caller's
+    # stream: the tx tests with the knob, then c4tx end to end, alternated
+    mkdir -p $O
+    USN_TX_LISTS_SIDE=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+      tests/test_gpu_tx.py > $O/pytest_tx_side.log 2>&1 || { tail -30 $O/pytest_tx_side.log; exit 1; }
+    tail -2 $O/pytest_tx_side.log
+    for rep in 1 2 3; do
+      for side in 0 1; do
+        USN_TX_LISTS_SIDE=$side timeout -k 10 300 python tools/txpipe.py > $O/txpipe_side${side}_$rep.log 2>&1 || exit 1
+        echo "side=$side $(tail -1 $O/txpipe_side${side}_$rep.log)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
