@@ -849,18 +849,6 @@ __device__ __forceinline__ uint32_t cnt_escaped(const uint16_t *xr, uint32_t b) 
   c = (e.w & 0xFFFFu) == b ? e.w >> 16 : c;
   return c;
 }
-/* a wave-uniform pointer pinned to SGPRs: a per-lane select between two of
- * them then selects values, where hipcc would otherwise select the two
- * fields' addresses and fetch the pointer with a vector load (and a wait) */
-__device__ __forceinline__ uint64_t sgpr_ptr(const void *p) {
-  uint64_t v = reinterpret_cast<uint64_t>(p);
-  asm volatile("" : "+s"(v));
-  return v;
-}
-/* a 4-byte global load at an integer address (global, not flat: the
- * address came through sgpr_ptr) */
-typedef const __attribute__((address_space(1))) uint32_t g_u32;
-__device__ __forceinline__ uint32_t gload_u32(uint64_t addr) { return *reinterpret_cast<g_u32 *>(addr); }
 /* bin b of tile t, synchronously (the scatter's rare paths) */
 __device__ __forceinline__ uint32_t cnt_get(const uint8_t *cnt, const uint16_t *cntx, uint32_t nbw,
                                             uint32_t n_ep, uint32_t t, uint32_t b) {
@@ -2843,64 +2831,46 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   const uint32_t b0 = bb * USN_SCAN_BLK + 4 * l;             // this thread's 4 bins
   const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
   const uint32_t c0 = r * 16 * CPT + rg * CPT;              // this thread's CPT chunks
-  // 1. u8 rows: 4 bins in one load; a thread whose bins lie in the class
-  // window reads their u16 counts from the tiles' exception rows instead
-  // (two loads: an address select, no branch -- the others load their row
-  // word twice).  A 255 byte below the window (an endpoint bin of 255+
-  // frames in a tile, rare) is fixed up after the sums, from its slot.
-  const uint32_t q = CNTX_WIN(s.n_ep);
-  const bool win = b0 - q < 8u;
-  const uint64_t src = win ? sgpr_ptr(B.cntx) + 2 * (b0 - q) : sgpr_ptr(B.cnt) + b0;
-  const uint32_t tstride = win ? CNTX_U16 * 2 : s.nbw;
-  uint32_t v[CPT][8], vh[CPT][8];
+  // 1. u8 rows; a thread whose 4 bins are in the class window reads them
+  // from the tiles' exception rows instead, and a 255 entry below it -- an
+  // endpoint bin of 255+ frames in a tile, rare -- its slot
+  const bool win = b0 - CNTX_WIN(s.n_ep) < 8u;
+  uint2 v[CPT][8];
 #pragma unroll
   for (uint32_t j = 0; j < CPT; ++j)
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) {
       const uint32_t t = (c0 + j) * s.tc + w;
       const bool ok = binok && w < s.tc && t < B.ntiles;
-      const uint64_t p = src + (uint64_t)t * tstride;
-      v[j][w] = ok ? gload_u32(p) : 0u;
-      vh[j][w] = ok ? gload_u32(win ? p + 4 : p) : 0u;
+      if (!ok) v[j][w] = make_uint2(0, 0);
+      else if (win) v[j][w] = *reinterpret_cast<const uint2 *>(B.cntx + (size_t)t * CNTX_U16 + (b0 - CNTX_WIN(s.n_ep)));
+      else v[j][w] = make_uint2(*reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw + b0), 0u);
     }
   uint32_t ex[CPT][4], tot[4] = {0, 0, 0, 0};
-  bool esc = false;
 #pragma unroll
   for (uint32_t j = 0; j < CPT; ++j) {
     uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) {
-      const uint32_t x = v[j][w], y = vh[j][w];
-      a[0] += win ? x & 0xFFFFu : x & 0xFFu;
-      a[1] += win ? x >> 16 : (x >> 8) & 0xFFu;
-      a[2] += win ? y & 0xFFFFu : (x >> 16) & 0xFFu;
-      a[3] += win ? y >> 16 : x >> 24;
-      esc |= !win && ((~x - 0x01010101u) & x & 0x80808080u) != 0;   // a 255 byte
+      const uint2 x = v[j][w];
+      if (win) {
+        a[0] += x.x & 0xFFFFu; a[1] += x.x >> 16;
+        a[2] += x.y & 0xFFFFu; a[3] += x.y >> 16;
+      } else {
+        a[0] += x.x & 0xFFu; a[1] += (x.x >> 8) & 0xFFu;
+        a[2] += (x.x >> 16) & 0xFFu; a[3] += x.x >> 24;
+        if (((~x.x - 0x01010101u) & x.x & 0x80808080u) != 0) {   // a 255 byte (rare)
+          const uint32_t t = (c0 + j) * s.tc + w;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i)
+            if (((x.x >> (8 * i)) & 0xFFu) == 255u)
+              a[i] += cnt_escaped(B.cntx + (size_t)t * CNTX_U16, b0 + i) - 255u;
+        }
+      }
     }
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) { ex[j][i] = tot[i]; tot[i] += a[i]; }
   }
-  if (esc) {   // rare: each 255 entry's count from its tile's slot
-    uint32_t run[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t j = 0; j < CPT; ++j) {
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) ex[j][i] += run[i];
-#pragma unroll
-      for (uint32_t w = 0; w < 8; ++w) {
-        const uint32_t t = (c0 + j) * s.tc + w;
-        if (!(binok && w < s.tc && t < B.ntiles)) continue;
-        const uint32_t x = v[j][w];
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i)
-          if (((x >> (8 * i)) & 0xFFu) == 255u)
-            run[i] += cnt_escaped(B.cntx + (size_t)t * CNTX_U16, b0 + i) - 255u;
-      }
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) tot[i] += run[i];
-  }
-
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) s_t[rg][4 * l + i] = tot[i];
   __syncthreads();
@@ -3046,20 +3016,15 @@ void scatter_kernel(ScatterArgs s) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
-  // u8 pairs: the row word that holds bins 2 tid, 2 tid + 1 (expanded below,
-  // once the decisions are in flight); a pair in the class window as u16
-  // from the tiles' exception rows (an address select, no branch)
-  const uint32_t q = CNTX_WIN(s.n_ep);
-  const bool win = 2 * tid - q < 8u;
-  {
-    const uint64_t src = win ? sgpr_ptr(B.cntx) + 2 * (2 * tid - q) : sgpr_ptr(B.cnt) + 4 * (tid >> 1);
-    const uint32_t tstride = win ? CNTX_U16 * 2 : s.nbw;
+  // u8 pairs (expanded below, once the decisions are in flight); a pair in
+  // the class window as u16 from the tiles' exception rows
+  const bool win = 2 * tid - CNTX_WIN(s.n_ep) < 8u;
 #pragma unroll
-    for (uint32_t w = 0; w < TC; ++w) {   // count rows of the chunk's tiles
-      const uint32_t t = t0 + min(w, ntc - 1);
-      rc[w] = mine ? gload_u32(src + (uint64_t)t * tstride) : 0u;
-      if (w >= ntc) rc[w] = 0;
-    }
+  for (uint32_t w = 0; w < TC; ++w) {
+    const uint32_t t = t0 + min(w, ntc - 1);
+    if (!mine) rc[w] = 0u;
+    else if (win) rc[w] = *reinterpret_cast<const uint32_t *>(B.cntx + (size_t)t * CNTX_U16 + (2 * tid - CNTX_WIN(s.n_ep)));
+    else rc[w] = reinterpret_cast<const uint16_t *>(B.cnt + (size_t)t * s.nbw)[tid];
   }
   // 1. this wave's tile (waves past the chunk's end re-read its last tile, unused)
   const uint32_t wt = min(wave, ntc - 1);
@@ -3070,24 +3035,21 @@ void scatter_kernel(ScatterArgs s) {
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
   // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
-    bool esc = false;
-#pragma unroll
-    for (uint32_t w = 0; w < TC; ++w) {   // u8 pair -> u16 pair
-      const uint32_t x = rc[w] >> (16u * (tid & 1u));
-      const uint32_t x0 = x & 0xFFu, x1 = (x >> 8) & 0xFFu;
-      esc |= !win && (x0 == 255u || x1 == 255u);
-      rc[w] = win ? rc[w] : x0 | (x1 << 16);
-    }
-    if (esc) {   // rare: an endpoint bin of 255+ frames in a tile, from its slot
+    if (!win) {
 #pragma unroll
       for (uint32_t w = 0; w < TC; ++w) {
-        const uint16_t *xr = B.cntx + (size_t)(t0 + min(w, ntc - 1)) * CNTX_U16;
-        uint32_t x0 = rc[w] & 0xFFFFu, x1 = rc[w] >> 16;
-        if (x0 == 255u) x0 = cnt_escaped(xr, 2 * tid);
-        if (x1 == 255u) x1 = cnt_escaped(xr, 2 * tid + 1);
+        uint32_t x0 = rc[w] & 0xFFu, x1 = (rc[w] >> 8) & 0xFFu;
+        if (x0 == 255u || x1 == 255u) {   // rare: an endpoint bin of 255+ frames in the tile
+          const uint16_t *xr = B.cntx + (size_t)(t0 + min(w, ntc - 1)) * CNTX_U16;
+          if (x0 == 255u) x0 = cnt_escaped(xr, 2 * tid);
+          if (x1 == 255u) x1 = cnt_escaped(xr, 2 * tid + 1);
+        }
         rc[w] = x0 | (x1 << 16);
       }
     }
+#pragma unroll
+    for (uint32_t w = 0; w < TC; ++w)
+      if (w >= ntc) rc[w] = 0;
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
