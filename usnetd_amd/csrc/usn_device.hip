@@ -680,12 +680,10 @@ struct Lds {
 __host__ __device__ inline uint32_t bin_words(uint32_t nbins) { return (nbins + 7u) & ~7u; }
 __host__ __device__ inline size_t hist_bytes(uint32_t nbins) { return (size_t)bin_words(nbins) * 2; }
 
-/* hist | scratch[20] | order[TILE] | table.  A kernel with a header stage
+/* hist | scratch[16] | order[TILE] | table.  A kernel with a header stage
  * (the GLDS classify) passes it as `stage`: its (unused) order row is then
- * the stage's, which leaves the dynamic LDS to the histogram and the image.
- * scratch[16]: hist_out's exception slots (hist_zero clears it). */
-#define LDS_ESC 16
-__host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) { return hist_bytes(nbins) + 20 * 4; }
+ * the stage's, which leaves the dynamic LDS to the histogram and the image. */
+__host__ __device__ inline size_t lds_head_bytes(uint32_t nbins) { return hist_bytes(nbins) + 16 * 4; }
 __host__ __device__ inline size_t lds_core_bytes(uint32_t nbins, bool own_stage = true) {
   return own_stage ? lds_head_bytes(nbins) + TILE * 2 : lds_head_bytes(nbins);
 }
@@ -789,74 +787,14 @@ __device__ __forceinline__ uint32_t byte_sum(uint32_t v) { return __builtin_amdg
 __device__ __forceinline__ uint32_t hist_get(const uint32_t *hist, uint32_t b) {
   return (hist[b >> 1] >> (16u * (b & 1u))) & 0xFFFFu;
 }
-/* after a barrier: the histogram as the tile's count row, u8 per bin (8-byte
- * stores), and its exception row xr (usn_kernels.h CNTX_*): the u16 counts of
- * the class window, and {bin, count} of an endpoint bin below it of 255
- * frames or more in a slot taken with an LDS atomic.  hist_zero cleared the
- * slot counter and emptied the slots, before a barrier. */
-__device__ __forceinline__ void hist_out(const uint32_t *hist, uint32_t nbw, uint32_t n_ep,
-                                         uint8_t *row, uint16_t *xr, uint32_t *scratch) {
+/* after a barrier: the histogram as the tile's count row (16-byte stores) */
+__device__ __forceinline__ void hist_out(const uint32_t *hist, uint32_t nbw, uint16_t *row) {
   const uint4 *h = reinterpret_cast<const uint4 *>(hist);
-  const uint32_t q = CNTX_WIN(n_ep);
-  for (uint32_t i = threadIdx.x; i < nbw / 8; i += NTHREADS) {
-    const uint4 v = h[i];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t o[2] = {0, 0};
-    bool big = false;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint32_t c0 = w[k] & 0xFFFFu, c1 = w[k] >> 16;
-      o[k >> 1] |= (min(c0, 255u) | (min(c1, 255u) << 8)) << (16u * (k & 1u));
-      big |= ((w[k] + 0x00010001u) & 0xFF00FF00u) != 0;   // a half >= 255 (halves <= TILE)
-    }
-    *reinterpret_cast<uint2 *>(row + 8 * i) = make_uint2(o[0], o[1]);
-    if (big && 8 * i < q) {   // rare below the window
-#pragma unroll
-      for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t b = 8 * i + j, c = (w[j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
-        if (c >= 255u && b < q) {
-          const uint32_t e = atomicAdd(&scratch[LDS_ESC], 1u);
-          if (e < CNTX_MAX_ESC) reinterpret_cast<uint32_t *>(xr)[4 + e] = b | (c << 16);
-        }
-      }
-    }
-  }
-  if (threadIdx.x == 0) {   // the window: bins q .. q+7 (0 past the row)
-    uint32_t x[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) x[k] = q / 2 + k < nbw / 2 ? hist[q / 2 + k] : 0u;
-    *reinterpret_cast<uint4 *>(xr) = make_uint4(x[0], x[1], x[2], x[3]);
-  }
+  uint4 *w = reinterpret_cast<uint4 *>(row);
+  for (uint32_t i = threadIdx.x; i < nbw / 8; i += NTHREADS) w[i] = h[i];
 }
-/* zero the LDS histogram; the exception row's slots empty, its slot counter
- * 0 -- a barrier follows before hist_out */
-__device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw, uint32_t *scratch, uint16_t *xr) {
+__device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw) {
   for (uint32_t i = threadIdx.x; i < nbw / 2; i += NTHREADS) hist[i] = 0;
-  if (threadIdx.x == NTHREADS - 1) {
-    scratch[LDS_ESC] = 0;
-    reinterpret_cast<uint4 *>(xr)[1] = make_uint4(~0u, ~0u, ~0u, ~0u);
-  }
-}
-/* the count of bin b (below the window) in a tile whose u8 entry is 255: its
- * exception slot (255 when none holds b: rows that disagree with the
- * decisions, which the scatter reports) */
-__device__ __forceinline__ uint32_t cnt_escaped(const uint16_t *xr, uint32_t b) {
-  const uint4 e = reinterpret_cast<const uint4 *>(xr)[1];
-  uint32_t c = 255u;
-  c = (e.x & 0xFFFFu) == b ? e.x >> 16 : c;
-  c = (e.y & 0xFFFFu) == b ? e.y >> 16 : c;
-  c = (e.z & 0xFFFFu) == b ? e.z >> 16 : c;
-  c = (e.w & 0xFFFFu) == b ? e.w >> 16 : c;
-  return c;
-}
-/* bin b of tile t, synchronously (the scatter's rare paths) */
-__device__ __forceinline__ uint32_t cnt_get(const uint8_t *cnt, const uint16_t *cntx, uint32_t nbw,
-                                            uint32_t n_ep, uint32_t t, uint32_t b) {
-  const uint16_t *xr = cntx + (size_t)t * CNTX_U16;
-  const uint32_t q = CNTX_WIN(n_ep);
-  if (b - q < 8u) return xr[b - q];
-  const uint32_t c = cnt[(size_t)t * nbw + b];
-  return c == 255u ? cnt_escaped(xr, b) : c;
 }
 
 /* --------------------------------------------------------------------------- */
@@ -1146,7 +1084,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     STAMP(1);
     // ---- while they fly: zero the bin histogram (the barrier also waits
     //      for every load: table and round 0 are in LDS / registers after it)
-    hist_zero(L.hist, a.nbw, L.scratch, a.cntx + (size_t)tile * CNTX_U16);
+    hist_zero(L.hist, a.nbw);
     if (tid < 8) s_misc[tid] = 0;
     __syncthreads();
     STAMP(2);
@@ -1497,8 +1435,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
 #endif
     __syncthreads();
     STAMP(10);
-    hist_out(L.hist, a.nbw, a.n_ep, a.cnt + (size_t)tile * a.nbw, a.cntx + (size_t)tile * CNTX_U16,
-             L.scratch);
+    hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
 
     // ---- tile header
     usn_tile_hdr *H = a.tiles + tile;
@@ -1539,7 +1476,7 @@ __global__ __launch_bounds__(NTHREADS) void recount_kernel(ClassifyArgs a, uint3
   const uint32_t tile = t0 + blockIdx.x;
   const uint64_t base = (uint64_t)tile * TILE;
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
-  hist_zero(L.hist, a.nbw, L.scratch, a.cntx + (size_t)tile * CNTX_U16);
+  hist_zero(L.hist, a.nbw);
   uint32_t bins[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -1550,8 +1487,7 @@ __global__ __launch_bounds__(NTHREADS) void recount_kernel(ClassifyArgs a, uint3
   __syncthreads();
   tile_hist(bins, nt, a.nbits, L.hist);
   __syncthreads();
-  hist_out(L.hist, a.nbw, a.n_ep, a.cnt + (size_t)tile * a.nbw, a.cntx + (size_t)tile * CNTX_U16,
-           L.scratch);
+  hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
   if (tid == 0) {
     usn_tile_hdr *H = a.tiles + tile;
     const uint32_t nic = hist_get(L.hist, a.n_ep), fl = hist_get(L.hist, a.n_ep + 1),
@@ -2020,7 +1956,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     s_early = 0; s_early_all = 0; s_slow = 0; s_dlearn = 0;
   }
   if (tid < 8) s_misc[tid] = 0;
-  hist_zero(L.hist, a.nbw, L.scratch, a.cntx + (size_t)blockIdx.x * CNTX_U16);
+  hist_zero(L.hist, a.nbw);
   __syncthreads();
   const uint32_t tile = blockIdx.x;
   STAMP_DECL
@@ -2599,8 +2535,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   tile_hist(bins, nt, a.nbits, L.hist);
   __syncthreads();
   STAMP(7);
-  hist_out(L.hist, a.nbw, a.n_ep, a.cnt + (size_t)tile * a.nbw, a.cntx + (size_t)tile * CNTX_U16,
-           L.scratch);
+  hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
   STAMP(10);
   usn_tile_hdr *H = a.tiles + tile;
   const uint32_t lastp = s_misc[0];
@@ -2774,7 +2709,7 @@ hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipSt
 /* ===========================================================================
  * Per-endpoint lists: the device-wide stable scatter (usn_kernels.h).
  * The classify / tx kernel leaves each tile's decisions and its count row
- * cnt[tile][bin] (u8, exceptions in cntx).  Two launches turn them into `index` (the batch's
+ * cnt[tile][bin] (u16).  Two launches turn them into `index` (the batch's
  * frame indices grouped by bin, frame order inside a bin) and bin_off:
  *   scan     (range of 64 chunks, block of 64 bins): agg[chunk][bin] = the
  *            bin's frames in the chunks before (exclusive scan over the
@@ -2831,10 +2766,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   const uint32_t b0 = bb * USN_SCAN_BLK + 4 * l;             // this thread's 4 bins
   const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
   const uint32_t c0 = r * 16 * CPT + rg * CPT;              // this thread's CPT chunks
-  // 1. u8 rows; a thread whose 4 bins are in the class window reads them
-  // from the tiles' exception rows instead, and a 255 entry below it -- an
-  // endpoint bin of 255+ frames in a tile, rare -- its slot
-  const bool win = b0 - CNTX_WIN(s.n_ep) < 8u;
+  // 1.
   uint2 v[CPT][8];
 #pragma unroll
   for (uint32_t j = 0; j < CPT; ++j)
@@ -2842,9 +2774,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
     for (uint32_t w = 0; w < 8; ++w) {
       const uint32_t t = (c0 + j) * s.tc + w;
       const bool ok = binok && w < s.tc && t < B.ntiles;
-      if (!ok) v[j][w] = make_uint2(0, 0);
-      else if (win) v[j][w] = *reinterpret_cast<const uint2 *>(B.cntx + (size_t)t * CNTX_U16 + (b0 - CNTX_WIN(s.n_ep)));
-      else v[j][w] = make_uint2(*reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw + b0), 0u);
+      v[j][w] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
     }
   uint32_t ex[CPT][4], tot[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -2852,21 +2782,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
     uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) {
-      const uint2 x = v[j][w];
-      if (win) {
-        a[0] += x.x & 0xFFFFu; a[1] += x.x >> 16;
-        a[2] += x.y & 0xFFFFu; a[3] += x.y >> 16;
-      } else {
-        a[0] += x.x & 0xFFu; a[1] += (x.x >> 8) & 0xFFu;
-        a[2] += (x.x >> 16) & 0xFFu; a[3] += x.x >> 24;
-        if (((~x.x - 0x01010101u) & x.x & 0x80808080u) != 0) {   // a 255 byte (rare)
-          const uint32_t t = (c0 + j) * s.tc + w;
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i)
-            if (((x.x >> (8 * i)) & 0xFFu) == 255u)
-              a[i] += cnt_escaped(B.cntx + (size_t)t * CNTX_U16, b0 + i) - 255u;
-        }
-      }
+      a[0] += v[j][w].x & 0xFFFFu; a[1] += v[j][w].x >> 16;
+      a[2] += v[j][w].y & 0xFFFFu; a[3] += v[j][w].y >> 16;
     }
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) { ex[j][i] = tot[i]; tot[i] += a[i]; }
@@ -3011,20 +2928,16 @@ void scatter_kernel(ScatterArgs s) {
   const bool mine = pair && 2 * tid < s.nbw;
   const bool noscan = (s.flags & USN_SCF_NOSCAN) != 0;   // one chunk per batch: its counts are the batch's
   uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
-  uint32_t rc[TC];   // bins 2 tid, 2 tid + 1 of the chunk's tiles: u16 pairs
+  uint32_t rc[TC];
   if (mine && !noscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
-  // u8 pairs (expanded below, once the decisions are in flight); a pair in
-  // the class window as u16 from the tiles' exception rows
-  const bool win = 2 * tid - CNTX_WIN(s.n_ep) < 8u;
 #pragma unroll
-  for (uint32_t w = 0; w < TC; ++w) {
+  for (uint32_t w = 0; w < TC; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
     const uint32_t t = t0 + min(w, ntc - 1);
-    if (!mine) rc[w] = 0u;
-    else if (win) rc[w] = *reinterpret_cast<const uint32_t *>(B.cntx + (size_t)t * CNTX_U16 + (2 * tid - CNTX_WIN(s.n_ep)));
-    else rc[w] = reinterpret_cast<const uint16_t *>(B.cnt + (size_t)t * s.nbw)[tid];
+    rc[w] = mine ? reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw)[tid] : 0u;
+    if (w >= ntc) rc[w] = 0;
   }
   // 1. this wave's tile (waves past the chunk's end re-read its last tile, unused)
   const uint32_t wt = min(wave, ntc - 1);
@@ -3035,21 +2948,6 @@ void scatter_kernel(ScatterArgs s) {
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
   // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
-    if (!win) {
-#pragma unroll
-      for (uint32_t w = 0; w < TC; ++w) {
-        uint32_t x0 = rc[w] & 0xFFu, x1 = (rc[w] >> 8) & 0xFFu;
-        if (x0 == 255u || x1 == 255u) {   // rare: an endpoint bin of 255+ frames in the tile
-          const uint16_t *xr = B.cntx + (size_t)(t0 + min(w, ntc - 1)) * CNTX_U16;
-          if (x0 == 255u) x0 = cnt_escaped(xr, 2 * tid);
-          if (x1 == 255u) x1 = cnt_escaped(xr, 2 * tid + 1);
-        }
-        rc[w] = x0 | (x1 << 16);
-      }
-    }
-#pragma unroll
-    for (uint32_t w = 0; w < TC; ++w)
-      if (w >= ntc) rc[w] = 0;
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
@@ -3084,7 +2982,7 @@ void scatter_kernel(ScatterArgs s) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
       uint32_t cb = 0;
-      for (uint32_t w = 0; w < ntc; ++w) cb += cnt_get(B.cnt, B.cntx, s.nbw, s.n_ep, t0 + w, b);
+      for (uint32_t w = 0; w < ntc; ++w) cb += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       sc += cb;
       st += noscan ? cb : B.tot[b];
     }
@@ -3098,13 +2996,13 @@ void scatter_kernel(ScatterArgs s) {
       if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
       if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
       if (noscan) {
-        for (uint32_t w = 0; w < ntc; ++w) pt += cnt_get(B.cnt, B.cntx, s.nbw, s.n_ep, t0 + w, b);
+        for (uint32_t w = 0; w < ntc; ++w) pt += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       } else {
         pt += B.tot[b];
       }
       for (uint32_t w = 0; w < TC; ++w) {
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
-        if (w < ntc) pc += cnt_get(B.cnt, B.cntx, s.nbw, s.n_ep, t0 + w, b);
+        if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       }
     }
   }
@@ -3210,8 +3108,8 @@ void scatter_kernel(ScatterArgs s) {
     // ballots segment by segment, the stage out again
     if (wave < ntc) {
       uint16_t *cw = cur + (size_t)wave * s.nbw;
-      for (uint32_t bb = lane; bb < s.nbw; bb += 64)
-        cw[bb] = (uint16_t)(cw[bb] - cnt_get(B.cnt, B.cntx, s.nbw, s.n_ep, t0 + wave, bb));
+      const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
+      for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
 #pragma unroll
       for (uint32_t k = 0; k < SEGS; ++k) {
         const uint32_t local = k * 64 + lane;

@@ -1637,13 +1637,12 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
 /* ========================================================================== */
 namespace usn {
 /* scratch of the per-endpoint scatter for one batch of n frames and nbins
- * bins: cnt[ntiles][nbw] u8 | cntx[ntiles][CNTX_U16] u16 (usn_kernels.h) |
- * agg[nchunks][nbw] u32 | tot[nbw] u32 |
+ * bins: cnt[ntiles][nbw] u16 | agg[nchunks][nbw] u32 | tot[nbw] u32 |
  * gran[nranges][nbw] u64 | diag u32.  agg and gran are sized
  * for one-tile chunks: a launch picks its chunk length (launch_scatter) */
 struct ScatterGeom {
   uint32_t nbw, ntiles;
-  size_t cnt, cntx, agg, tot, gran, diag, total;
+  size_t cnt, agg, tot, gran, diag, total;
 };
 static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   ScatterGeom g;
@@ -1652,8 +1651,7 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   const size_t ranges = (g.ntiles + USN_SCAN_RANGE_MIN - 1) / USN_SCAN_RANGE_MIN;
   size_t o = 0;
   auto a256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
-  g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw);
-  g.cntx = o; o = a256(o + (size_t)g.ntiles * CNTX_U16 * 2);
+  g.cnt = o; o = a256(o + (size_t)g.ntiles * g.nbw * 2);
   g.agg = o; o = a256(o + (size_t)g.ntiles * g.nbw * 4);
   g.tot = o; o = a256(o + (size_t)g.nbw * 4);
   g.gran = o; o = a256(o + ranges * g.nbw * 8);
@@ -1663,13 +1661,11 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
 }
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins) { return scatter_geom(n, nbins).total; }
 void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
-                   ScatterBatch &sb, uint8_t **cnt, uint16_t **cntx) {
+                   ScatterBatch &sb, uint16_t **cnt) {
   const ScatterGeom g = scatter_geom(n, nbins);
   uint8_t *p = static_cast<uint8_t *>(scratch);
-  *cnt = p + g.cnt;
-  *cntx = reinterpret_cast<uint16_t *>(p + g.cntx);
+  *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
   sb.cnt = *cnt;
-  sb.cntx = *cntx;
   sb.agg = reinterpret_cast<uint32_t *>(p + g.agg);
   sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
   sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
@@ -2147,7 +2143,7 @@ static void set_bins(const usn_result *r, uint64_t n, uint32_t nbins, usn::Class
   a.nbits = 1;
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, n, nbins, 1, 1, sb, &a.cnt, &a.cntx);
+  usn::scatter_carve(r->scratch, n, nbins, 1, 1, sb, &a.cnt);
   a.nbw = (nbins + 7u) & ~7u;
 }
 
@@ -2184,7 +2180,7 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   a.probe_mask = c->probe_mask;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, 1, sb, &a.cnt, &a.cntx);
+  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, 1, sb, &a.cnt);
   a.nbw = (a.nbins + 7u) & ~7u;
   return USN_OK;
 }
@@ -2256,9 +2252,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.epoch = c->scan_epoch;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
-    uint8_t *cnt;
-    uint16_t *cntx;
-    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, x.cpt, sb, &cnt, &cntx);
+    uint16_t *cnt;
+    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, x.cpt, sb, &cnt);
     sb.decisions = r[k].decisions;
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;
@@ -2278,14 +2273,14 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     }
   }
   // test hook (tests/test_gpu_scatter.py, read once per process):
-  // USN_DEBUG_CORRUPT=1 sets bin 0 of batch 0's first count row to 254, =2
+  // USN_DEBUG_CORRUPT=1 adds 257 to bin 0 of batch 0's first count row, =2
   // makes frame 0's decision name endpoint 0x0FF0 (past every batch's bins);
   // the scatter must report either (usn_finalize: USN_ELIST)
   static const int corrupt = [] {
     const char *e = std::getenv("USN_DEBUG_CORRUPT");
     return e ? std::atoi(e) : 0;
   }();
-  if (corrupt == 1) HIPCHK(hipMemsetAsync(const_cast<uint8_t *>(x.b[0].cnt), 0xFE, 1, s));
+  if (corrupt == 1) HIPCHK(hipMemsetAsync(const_cast<uint16_t *>(x.b[0].cnt), 0x01, 2, s));
   if (corrupt == 2) HIPCHK(hipMemsetD32Async(r[0].decisions, (int)((1u << 16) | 0x0FF0u), 1, s));
   HIPCHK(usn_t512::launch_scatter(x, s));
   return USN_OK;

@@ -15,21 +15,6 @@ namespace usn {
 
 enum CarryMode : uint32_t { CARRY_NONE = 0, CARRY_EXPLICIT = 1, CARRY_CHAIN = 2 };
 
-/* A tile's count row: u8 per bin (nbw bytes), and an exception row of
- * CNTX_U16 u16 for what a byte does not hold:
- *   [0..7]   the u16 counts of bins Q .. Q+7, Q = n_ep & ~3 (the class
- *            window: NIC, FLOOD and DROP with the bins beside them, so that
- *            a reader whose 2 or 4 bins lie there reads them from one load
- *            instead of the row); their u8 entries are unused
- *   [8..15]  4 slots {bin | count << 16} (empty: 0xFFFFFFFF) for endpoint
- *            bins below Q of 255 frames or more (at most 4 in 1024 frames);
- *            their u8 holds 255
- * Half the bytes of u16 rows for what the classify writes and the scan and
- * the scatter read per tile; the exception rows are 32 bytes a tile. */
-#define CNTX_U16 16u
-#define CNTX_MAX_ESC 4u
-#define CNTX_WIN(n_ep) ((n_ep) & ~3u)
-
 struct ClassifyArgs {
   /* batch */
   const uint8_t *frames;
@@ -41,9 +26,7 @@ struct ClassifyArgs {
   uint32_t window;          /* readable bytes at every frame start (usn_batch.window) */
   /* outputs */
   uint32_t *decisions;
-  uint8_t *cnt;             /* [ntiles][nbw] frames per bin of each tile (the scatter's input):
-                               u8 (CNTX_*) */
-  uint16_t *cntx;           /* [ntiles][CNTX_U16]: the class window's counts and the escapes */
+  uint16_t *cnt;            /* [ntiles][nbw] frames per bin of each tile (the scatter's input) */
   uint32_t nbw;             /* row length of cnt: nbins rounded up to 8 */
   usn_tile_hdr *tiles;
   usn_summary *summary;
@@ -142,7 +125,7 @@ hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t s
 
 /* ---- per-endpoint lists: the device-wide stable scatter ------------------
  * After the classify (or tx) kernel has written each tile's decisions and its
- * row of per-bin frame counts (cnt[tile][bin], u8 with u16 escapes), two launches:
+ * row of per-bin frame counts (cnt[tile][bin], u16), two launches:
  *   scan     (range of 16 x cpt chunks, block of USN_SCAN_BLK bins):
  *            agg[chunk][bin] = frames of the bin in the batch's chunks before
  *            (ranges hand their totals on through epoch-tagged granules),
@@ -156,8 +139,7 @@ hipError_t launch_patch(uint4 *table, const void *buf, uint32_t n, hipStream_t s
 #define USN_SCAN_BLK 64u     /* bins per scan workgroup */
 struct ScatterBatch {
   const uint32_t *decisions;
-  const uint8_t *cnt;       /* [ntiles][nbw] u8 count rows (ClassifyArgs::cnt) */
-  const uint16_t *cntx;     /* [ntiles][CNTX_U16] their exceptions (ClassifyArgs::cntx) */
+  const uint16_t *cnt;      /* [ntiles][nbw] */
   uint32_t *agg;            /* [nchunks][nbw]: frames per bin in the chunks before */
   uint32_t *tot;            /* [nbw]: frames per bin */
   unsigned long long *gran; /* [nranges][nbw]: {epoch, range total} */
@@ -210,7 +192,7 @@ inline uint32_t scatter_occupancy(size_t lds) {
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
 void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
-                   ScatterBatch &sb, uint8_t **cnt, uint16_t **cntx);
+                   ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
 
