@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     a = ap.parse_args()
     ctx = lib.Ctx(0)
+    a.no_cpu_baseline = True
     x = bench.measure_tx(ctx, a)
     keep = ("value", "sequential_mpps", "device_mpps", "ms_per_ring", "rings", "learned_in_timed_rings")
     print(json.dumps({k: x[k] for k in keep if k in x}))
