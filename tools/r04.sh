@@ -112,6 +112,21 @@ case $S in
       done
     done
     ;;
+  r04j)
+    # chunk length of small scatter launches (the knob now taken as is):
+    # lists alone (c4 1M, c3 4 x 256K) and c4tx end to end
+    mkdir -p $O
+    for tc in 0 1 2 4 8; do
+      for c in c4 c3; do
+        if [ $c = c4 ]; then A="--frames 1048576 --multi 1"; else A="--frames 262144 --multi 4"; fi
+        USN_SCATTER_TC=$tc timeout -k 10 300 python tools/scatter_bench.py --config $c $A --launches 100 \
+          > $O/scb_small_${c}_tc$tc.log 2>&1 || exit 1
+        echo "tc=$tc $c $(tail -1 $O/scb_small_${c}_tc$tc.log)"
+      done
+      USN_SCATTER_TC=$tc timeout -k 10 300 python tools/txpipe.py > $O/txpipe_tc$tc.log 2>&1 || exit 1
+      echo "tc=$tc c4tx $(tail -1 $O/txpipe_tc$tc.log)"
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

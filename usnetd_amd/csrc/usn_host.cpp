@@ -2225,7 +2225,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   // batches of at most one chunk each (a daemon's drained rings): no scan
   // launch, the scatter's one chunk per batch has the whole batch
   const bool noscan = max_tiles <= tc;
-  if (!noscan)
+  if (!noscan && !tc_knob)   // (the knob, an A/B, is taken as it is)
     while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
@@ -2537,27 +2537,12 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       // slot's previous batch is final: its usn_finalize synchronised)
       reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
     }
-    // A/B (USN_TX_LISTS_SIDE=1, read once): a tx ring's lists on the side
-    // stream, so that the next ring's tx kernel (queued behind this one on the
-    // caller's stream) overlaps them; usn_finalize waits for txstate_ev
-    static const bool tx_side = [] {
-      const char *e = std::getenv("USN_TX_LISTS_SIDE");
-      return e && std::atoi(e) == 1;
-    }();
-    hipStream_t ls = (hipStream_t)stream;
-    if (tx && tx_side) {
-      if (!R.side) HIPCHK(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
-      if (!R.classified) HIPCHK(hipEventCreateWithFlags(&R.classified, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(R.classified, (hipStream_t)stream));
-      HIPCHK(hipStreamWaitEvent(R.side, R.classified, 0));
-      ls = R.side;
-    }
-    int st = launch_scatter(c, m.b, r, count, ls, txs, tx ? R.txs[slot].counters : nullptr);
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr);
     if (st) return st;
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
       if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(X.txstate_ev, ls));
+      HIPCHK(hipEventRecord(X.txstate_ev, (hipStream_t)stream));
       c->txstate_for[slot] = r[0].decisions;
     }
   } else {
@@ -2869,9 +2854,6 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[8];
-  // the lists may have been built on the side stream (USN_TX_LISTS_SIDE):
-  // what this stage enqueues on s comes after them
-  if (X.txstate_ev) HIPCHK(hipStreamWaitEvent(s, X.txstate_ev, 0));
   if (c->txstate_for[txp.slot] == r->decisions && X.txstate_ev) {   // gathered behind the launch
     HIPCHK(hipEventSynchronize(X.txstate_ev));
     c->txstate_for[txp.slot] = nullptr;
