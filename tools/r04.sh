@@ -127,6 +127,11 @@ case $S in
       echo "tc=$tc c4tx $(tail -1 $O/txpipe_tc$tc.log)"
     done
     ;;
+  r04k)
+    # one chunk per CU for small scatter launches: the suite and the bench
+    bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -2195,7 +2195,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.count = count;
   x.nbins = as[0].nbins;
   x.nbw = as[0].nbw;
-    x.n_ep = as[0].n_ep;
+  x.n_ep = as[0].n_ep;
   x.nbits = as[0].nbits;
   /* chunk length: the shape's (long chunks: contiguous runs per bin), shorter
    * when the launch has too few tiles to give every CU its workgroups */
@@ -2214,7 +2214,6 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
         }
     }
   }
-  const uint32_t want = (uint32_t)std::max(cus, 1) * usn::scatter_occupancy(sh.lds);
   static const uint32_t tc_knob = [] {   // A/B: USN_SCATTER_TC=1|2|4|8 (at most the shape's)
     const char *e = std::getenv("USN_SCATTER_TC");
     const int v = e ? std::atoi(e) : 0;
@@ -2225,8 +2224,15 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   // batches of at most one chunk each (a daemon's drained rings): no scan
   // launch, the scatter's one chunk per batch has the whole batch
   const bool noscan = max_tiles <= tc;
-  if (!noscan && !tc_knob)   // (the knob, an A/B, is taken as it is)
-    while (tc > 1 && (launch_tiles + tc - 1) / tc < want) tc /= 2;
+  // about one chunk per CU: the longest chunk up to the shape's that still
+  // gives every CU one (A/B at 1024 tiles -- a tx ring, c3's call --
+  // profiles/r04/r04j: scan + scatter 21.3 / 16.7 / 16.1 / 17.6 us at chunks
+  // of 1 / 2 / 4 / 8 tiles, c4tx end to end 13.6 -> 14.6 Gpkt/s; c5 and c2
+  // keep 8).  The knob, an A/B, is taken as it is.
+  if (!noscan && !tc_knob) {
+    const uint32_t per = std::max(1u, launch_tiles / (uint32_t)std::max(cus, 1));
+    while (tc > 1 && tc > per) tc /= 2;
+  }
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
