@@ -132,6 +132,12 @@ case $S in
     bash tools/gpu.sh $S testsall || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
     ;;
+  r04l)
+    # both rounds' header DMA at the workgroup start (USN_EARLY_R1, 3
+    # workgroups per CU at c5's LDS) against the current build
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur early1" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur early1" bash tools/gpu.sh $S abl
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

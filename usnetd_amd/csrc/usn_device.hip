@@ -883,6 +883,13 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #endif
 #define GD USN_GLDS_DEPTH
 #define NWAVES (NTHREADS / 64)
+#ifndef USN_EARLY_R1   /* A/B: both rounds' header DMA at the workgroup's start (two 2 KiB
+                          stages per wave; the two-round batched paths of a global or
+                          displacement-LDS image), an LDS-only barrier before the parse */
+#define USN_EARLY_R1 0
+#endif
+#define STAGE_R_SLOTS (64u * GLDS_PARTS)   /* one round's parts per wave (USN_EARLY_R1) */
+static_assert(!USN_EARLY_R1 || USN_STAGE32, "USN_EARLY_R1: two-part stage");
 #ifndef GLDS_NT                  /* aux bits of the header glds: non-temporal */
 #define GLDS_NT 2
 #endif
@@ -1008,8 +1015,10 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   // both rounds' probes batched (two rounds per lane, global image)
   constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1 && USN_BATCH2 &&
                           !USN_ABL_LOADONLY && !USN_ABL_NOPROBE;
+  constexpr bool EARLY = BATCH2 && USN_EARLY_R1;
+  constexpr uint32_t WSTAGE = EARLY ? 2 * STAGE_R_SLOTS : GD * STAGE_ROUND_SLOTS;   // per wave
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ uint4 s_stage[GLDS ? NWAVES * GD * STAGE_ROUND_SLOTS : 1];
+  __shared__ uint4 s_stage[GLDS ? NWAVES * WSTAGE : 1];
   __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1017,7 +1026,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   // bins and table are shared by the batches.  GLDS: the order row and the
   // radix keys live in the header stage (carve)
   const Lds L = carve(smem, m.b[0].nbins, GLDS ? s_stage : nullptr);
-  uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);   // this wave's stage
+  uint4 *st = s_stage + (GLDS ? wave * WSTAGE : 0);   // this wave's stage
   const uint4 *T = m.b[0].table;
   const uint16_t *Dl = nullptr;
   if (TM != TM_GLOBAL) {   // image (or its displacements) -> LDS by glds, 64 units per instruction
@@ -1046,8 +1055,9 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     asm volatile("" : "+v"(tid));
     const uint32_t lane = tid & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint4 *st = s_stage + (GLDS ? wave * GD * STAGE_ROUND_SLOTS : 0);
+    uint4 *st = s_stage + (GLDS ? wave * WSTAGE : 0);
 #endif
+    uint4 *const st1 = EARLY ? st + STAGE_R_SLOTS : st;   // round 1's stage
     const uint32_t bi = batch_of(m, w);
     const ClassifyArgs &a = m.b[bi];
     const uint32_t tile = w - m.tile_base[bi];
@@ -1074,7 +1084,10 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
     uint4 q[ROUNDS][4];
-    if (GLDS) {
+    if (EARLY) {
+      glds_round(a, base, nt, 0, wave, lane, st);
+      glds_round(a, base, nt, 1, wave, lane, st1);
+    } else if (GLDS) {
 #pragma unroll
       for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
         glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
@@ -1086,7 +1099,14 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     //      for every load: table and round 0 are in LDS / registers after it)
     hist_zero(L.hist, a.nbw);
     if (tid < 8) s_misc[tid] = 0;
-    __syncthreads();
+    if (EARLY) {   // round 1's parts may still fly: an LDS-only barrier after this wave's image copy and round 0
+      vm_wait<GLDS_PARTS>();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    } else {
+      __syncthreads();
+    }
     STAMP(2);
 
     // ---- carried-in cache (block 0): stale check against the current table
@@ -1127,7 +1147,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t du0, du1;
       v4u32 su0, su1;
       stage_read_asm(sb, lane, q[0]);
-      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       const uint32_t e0 = u_key_e(pr[0]);
@@ -1137,7 +1157,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       asm_slot1(T, a.ph[2], n0, ku0, du0, su0);
       __builtin_amdgcn_sched_barrier(0);
       vm_wait<1>();                                               // round 1 landed (1 younger load)
-      stage_read_asm(sb, lane, q[1]);
+      stage_read_asm(st1, lane, q[1]);
       parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
       const uint32_t e1 = u_key_e(pr[1]);
       const PhKeyH ku1 = ph_hash(a.ph[2], pr[1].dst, 0u, e1, 0u);
@@ -1185,7 +1205,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
@@ -1194,7 +1214,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       asm_slot1(T, a.ph[0], n01, k0.k1, d01, s01);
       __builtin_amdgcn_sched_barrier(0);
       vm_wait<1>();                                               // round 1 landed (1 younger load)
-      stage_read_asm(sb, lane, q[1]);
+      stage_read_asm(st1, lane, q[1]);
       parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
       round_keys(a, pr[1], k1);
       lds_disp2(Dl, a, use1, use2, k1, d11, d12);
@@ -1222,7 +1242,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
@@ -1230,7 +1250,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       asm_slot2(T, a, use1, use2, k0, d01, d02, s01, s02);
       __builtin_amdgcn_sched_barrier(0);
       vm_wait<2>();                                               // round 1 landed (2 younger loads)
-      stage_read_asm(sb, lane, q[1]);
+      stage_read_asm(st1, lane, q[1]);
       parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
       round_keys(a, pr[1], k1);
       lds_disp2(Dl, a, use1, use2, k1, d11, d12);
@@ -1250,14 +1270,14 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
+      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
       asm_disp2(D, a, use1, use2, k0, d01, d02);
       __builtin_amdgcn_sched_barrier(0);
       vm_wait<2>();                                               // round 1 landed (2 younger loads)
-      stage_read_asm(sb, lane, q[1]);
+      stage_read_asm(st1, lane, q[1]);
       parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
       round_keys(a, pr[1], k1);
       asm_disp2(D, a, use1, use2, k1, d11, d12);
