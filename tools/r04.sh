@@ -138,6 +138,11 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur early1" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS="c4" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur early1" bash tools/gpu.sh $S abl
     ;;
+  r04m)
+    # c3's lane path: bytes 12..43 in two loads (cur) against 0..47 in three
+    ABL_CFGS=c3 ABL_ARGS="--frames 262144 --batches 16 --multi 4 --rounds 5 --launches 40" ABL_VARIANTS="cur lane48" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c3 ABL_ARGS="--frames 1048576 --batches 8 --multi 1 --rounds 5 --launches 40" ABL_VARIANTS="cur lane48" bash tools/gpu.sh $S abl
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
