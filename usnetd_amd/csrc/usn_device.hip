@@ -969,18 +969,10 @@ __device__ __forceinline__ void stage_read_asm(const uint4 *st, uint32_t lane, u
  * grows with its bytes: 4M frames in 89 / 108 / 140 us at 32 / 48 / 64 bytes
  * (tools/stride_floor.hip, profiles/r02f). */
 /* (Bytes 12..43 in two dword-aligned 16-byte loads instead, as the 32-byte
- * stage's DMA does: slower here, c3 1M frames 34.7 vs 33.4 us, profiles/r02bh.) */
-#ifndef USN_LANE32   /* the lane path reads bytes 12..43 (two 16-byte loads at 4-byte aligned
-                        addresses, as the STAGE32 glds do), else 0..47 */
-#define USN_LANE32 1
-#endif
+ * stage's DMA does: slower here, c3 1M frames 34.7 vs 33.4 us, profiles/r02bh;
+ * again in round 4, calls of 4 x 256K frames: 11.74 vs 11.56 us per ring,
+ * profiles/r04/r04m.) */
 __device__ __forceinline__ void lane_round(const uint8_t *fp, uint4 (&q)[4]) {
-  if (USN_LANE32) {
-    const uint4 a0 = ld_stream(reinterpret_cast<const uint4 *>(fp + 12));
-    const uint4 a1 = ld_stream(reinterpret_cast<const uint4 *>(fp + 28));
-    stage32_words(v4u32{a0.x, a0.y, a0.z, a0.w}, v4u32{a1.x, a1.y, a1.z, a1.w}, q);
-    return;
-  }
   const uint4 *w = reinterpret_cast<const uint4 *>(fp);
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) q[k] = ld_stream(w + k);
