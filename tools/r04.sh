@@ -143,6 +143,25 @@ case $S in
     ABL_CFGS=c3 ABL_ARGS="--frames 262144 --batches 16 --multi 4 --rounds 5 --launches 40" ABL_VARIANTS="cur lane48" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS=c3 ABL_ARGS="--frames 1048576 --batches 8 --multi 1 --rounds 5 --launches 40" ABL_VARIANTS="cur lane48" bash tools/gpu.sh $S abl
     ;;
+  r04n)
+    # small launches sum their count rows in the scatter (no scan launch):
+    # the scatter tests, then USN_SELFSCAN_KB 0 (off) / 256 / 1024 on the lists
+    # of c3's calls and a 1M c4 ring, and c4tx end to end
+    mkdir -p $O
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+      tests/test_gpu_scatter.py tests/test_gpu_tx.py > $O/pytest_sel.log 2>&1 || { tail -30 $O/pytest_sel.log; exit 1; }
+    tail -2 $O/pytest_sel.log
+    for kb in 0 256 1024; do
+      for c in c4 c3; do
+        if [ $c = c4 ]; then A="--frames 1048576 --multi 1"; else A="--frames 262144 --multi 4"; fi
+        USN_SELFSCAN_KB=$kb timeout -k 10 300 python tools/scatter_bench.py --config $c $A --launches 100 \
+          > $O/scb_small_${c}_kb$kb.log 2>&1 || exit 1
+        echo "kb=$kb $c $(tail -1 $O/scb_small_${c}_kb$kb.log)"
+      done
+      USN_SELFSCAN_KB=$kb timeout -k 10 300 python tools/txpipe.py > $O/txpipe_kb$kb.log 2>&1 || exit 1
+      echo "kb=$kb c4tx $(tail -1 $O/txpipe_kb$kb.log)"
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

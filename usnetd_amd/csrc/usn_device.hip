@@ -2917,7 +2917,7 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
 #endif
-template <int TC>
+template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SCATTER_WPE)))
 void scatter_kernel(ScatterArgs s) {
   static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
@@ -2949,9 +2949,10 @@ void scatter_kernel(ScatterArgs s) {
   const bool pair = s.nbw <= 2 * NTHREADS;
   const bool mine = pair && 2 * tid < s.nbw;
   const bool noscan = (s.flags & USN_SCF_NOSCAN) != 0;   // one chunk per batch: its counts are the batch's
+  const bool selfscan = SELF && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
   uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
-  if (mine && !noscan) {
+  if (mine && !noscan && !selfscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
@@ -2968,6 +2969,43 @@ void scatter_kernel(ScatterArgs s) {
   uint32_t d[SEGS];
 #pragma unroll
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
+  // 1b. (small launches) the scan's two sums for this chunk from the batch's
+  // count rows: thread (g, p) adds bin pair p of tiles g, g + G, ... into
+  // the totals and, for the tiles before the chunk, into its offsets
+  if (selfscan) {
+    uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals
+    uint32_t *sb = sa + s.nbw;                                                // [nbw] before the chunk
+    for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
+    __syncthreads();
+    const uint32_t np = s.nbw / 2, G = NTHREADS / np, pp = tid % np, g = tid / np;
+    if (g < G) {
+      const uint32_t *rows = reinterpret_cast<const uint32_t *>(B.cnt) + pp;   // row t: rows[t * np]
+      uint32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
+      for (uint32_t t = g; t < B.ntiles; t += 8 * G) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint32_t tt = t + k * G;
+          v[k] = tt < B.ntiles ? rows[(size_t)tt * np] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint32_t lo = v[k] & 0xFFFFu, hi = v[k] >> 16;
+          a0 += lo; a1 += hi;
+          if (t + k * G < t0) { e0 += lo; e1 += hi; }
+        }
+      }
+      if (a0) atomicAdd(&sa[2 * pp], a0);
+      if (a1) atomicAdd(&sa[2 * pp + 1], a1);
+      if (e0) atomicAdd(&sb[2 * pp], e0);
+      if (e1) atomicAdd(&sb[2 * pp + 1], e1);
+    }
+    __syncthreads();
+    if (mine) {
+      vt = make_uint2(sa[2 * tid], sa[2 * tid + 1]);
+      ve = make_uint2(sb[2 * tid], sb[2 * tid + 1]);
+    }
+  }
   // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
     uint32_t c0 = 0, c1 = 0;
@@ -3175,21 +3213,28 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  if (!(s.flags & USN_SCF_NOSCAN)) switch (s.cpt) {
+  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
     case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
     case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
     case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;
     default: return hipErrorInvalidValue;
   }
-  const size_t lds = scatter_lds(s.nbins, s.tc);
+  const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0);
   const dim3 g(chunks), b(NTHREADS);
+  const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
+#define USN_SC_LAUNCH(TC_)                                                              \
+  do {                                                                                  \
+    if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);    \
+    else hipLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, s);        \
+  } while (0)
   switch (s.tc) {
-    case 8: hipLaunchKernelGGL(scatter_kernel<8>, g, b, lds, stream, s); break;
-    case 4: hipLaunchKernelGGL(scatter_kernel<4>, g, b, lds, stream, s); break;
-    case 2: hipLaunchKernelGGL(scatter_kernel<2>, g, b, lds, stream, s); break;
-    case 1: hipLaunchKernelGGL(scatter_kernel<1>, g, b, lds, stream, s); break;
+    case 8: USN_SC_LAUNCH(8); break;
+    case 4: USN_SC_LAUNCH(4); break;
+    case 2: USN_SC_LAUNCH(2); break;
+    case 1: USN_SC_LAUNCH(1); break;
     default: return hipErrorInvalidValue;
   }
+#undef USN_SC_LAUNCH
   return hipGetLastError();
 }
 #endif  // USN_NTHREADS == 512

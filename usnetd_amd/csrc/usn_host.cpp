@@ -2235,7 +2235,19 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   }
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u);
+  // a launch whose chunks are all resident at once and whose batches' count
+  // rows are small: each chunk sums them itself (no scan launch)
+  static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (count-row KiB per batch; 0 off)
+    const char *e = std::getenv("USN_SELFSCAN_KB");
+    return e ? (uint32_t)std::atoi(e) : 256u;
+  }();
+  uint32_t chunks_all = 0;
+  for (uint32_t k = 0; k < count; ++k) chunks_all += (as[k].ntiles + tc - 1) / tc;
+  const bool selfscan = !noscan && x.nbw <= 2 * 512 && chunks_all <= (uint32_t)std::max(cus, 1) &&
+                        (size_t)max_tiles * x.nbw * 2 <= (size_t)selfscan_kb * 1024 &&
+                        usn::scatter_lds(x.nbins, tc, true) <= 64u * 1024u;
+  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u) |
+            (selfscan ? USN_SCF_SELFSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = std::getenv("USN_SCAN_CPT");

@@ -169,15 +169,19 @@ struct ScatterArgs {
 #define USN_DIAG_LISTS 2u       /* the scatter found count rows that disagree with the decisions */
 #define USN_SCF_NOSCAN 2u      /* every batch is one chunk: no scan launch; the chunk's own counts
                                   are the batch's (agg = 0, tot = the chunk's sums) */
+#define USN_SCF_SELFSCAN 4u    /* a small launch (every chunk resident at once, few count-row
+                                  bytes per batch): no scan launch; each chunk sums its batch's
+                                  count rows itself (the totals, and the tiles before it) */
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
  * bins: the longest chunk (contiguous runs per bin) whose LDS -- stage
- * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 -- fits 64 KiB. */
+ * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 (| self-scan sums
+ * nbw x 8) -- fits 64 KiB. */
 struct ScatterShape { uint32_t tc; size_t lds; };
-inline size_t scatter_lds(uint32_t nbins, uint32_t tc) {
+inline size_t scatter_lds(uint32_t nbins, uint32_t tc, bool selfscan = false) {
   const size_t nbw = (nbins + 7u) & ~7u;
-  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2;
+  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 + (selfscan ? nbw * 8 : 0);
 }
 inline ScatterShape scatter_shape(uint32_t nbins) {
   for (uint32_t tc : {8u, 4u, 2u})
