@@ -162,6 +162,11 @@ case $S in
       echo "kb=$kb c4tx $(tail -1 $O/txpipe_kb$kb.log)"
     done
     ;;
+  r04o)
+    # self-scan by bytes read: the suite and the bench
+    bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

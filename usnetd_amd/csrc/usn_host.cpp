@@ -2235,16 +2235,24 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   }
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  // a launch whose chunks are all resident at once and whose batches' count
-  // rows are small: each chunk sums them itself (no scan launch)
-  static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (count-row KiB per batch; 0 off)
+  // a launch whose chunks are all resident at once and whose chunks together
+  // read few count-row bytes (each reads its whole batch's rows): each chunk
+  // sums them itself, no scan launch (profiles/r04/r04n: c3's calls of 4 x
+  // 256K frames, 9.4 MB read, lists 15.1 -> 11.8 us; a 1M c4 ring, 138 MB
+  // read, 15.5 -> 33.7 us, so it keeps the scan)
+  static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (row KiB all chunks read; 0 off)
     const char *e = std::getenv("USN_SELFSCAN_KB");
-    return e ? (uint32_t)std::atoi(e) : 256u;
+    return e ? (uint32_t)std::atoi(e) : 16384u;
   }();
   uint32_t chunks_all = 0;
-  for (uint32_t k = 0; k < count; ++k) chunks_all += (as[k].ntiles + tc - 1) / tc;
+  size_t self_bytes = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const uint32_t ch = (as[k].ntiles + tc - 1) / tc;
+    chunks_all += ch;
+    self_bytes += (size_t)ch * as[k].ntiles * x.nbw * 2;
+  }
   const bool selfscan = !noscan && x.nbw <= 2 * 512 && chunks_all <= (uint32_t)std::max(cus, 1) &&
-                        (size_t)max_tiles * x.nbw * 2 <= (size_t)selfscan_kb * 1024 &&
+                        self_bytes <= (size_t)selfscan_kb * 1024 &&
                         usn::scatter_lds(x.nbins, tc, true) <= 64u * 1024u;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u) |
             (selfscan ? USN_SCF_SELFSCAN : 0u);
