@@ -167,6 +167,17 @@ case $S in
     bash tools/gpu.sh $S testsall || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench
     ;;
+  r04p)
+    # c3 under its bench key, self-scan off / on, alternated
+    mkdir -p $O
+    for rep in 1 2 3; do
+      for kb in 0 16384; do
+        USN_SELFSCAN_KB=$kb timeout -k 10 300 python bench.py --config c3 --queues 8 --no-extra --no-cpu-baseline \
+          --steps 200 --warmup 20 > $O/c3_kb${kb}_$rep.log 2>&1 || exit 1
+        echo "kb=$kb $(python3 tools/bench_summary.py $O/c3_kb${kb}_$rep.log | head -1)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
