@@ -339,7 +339,8 @@ def measure(run, args, dist, world):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": None,
-        "kernel": "classify_rx_kernel + per-endpoint scatter (scan_kernel, scatter_kernel)",
+        "kernel": "classify_rx_kernel + per-endpoint scatter (scan_kernel unless the launch "
+                  "self-scans, scatter_kernel)",
         "kernel_us_median": round(kern_ms * 1e3, 3) if kern_ms else None,
         "frames_per_launch": probe_frames,
         "algo_bytes_per_frame": ALGO_BYTES,
@@ -381,6 +382,7 @@ def measure(run, args, dist, world):
 # runs; 8 rings in calls of 4: 29.2, enqueue 0.043 of a 0.072 ms step
 # (profiles/r03/r03r)
 EXTRA_QUEUES = {"c3": 8}
+EXTRA_MIN_STEPS = {"c3": 200}   # c3's poll round is ~55 us: 200 rounds time ~11 ms, not ~2
 TX_ROTATE = 6              # c4tx: the ring in 6 device buffers (384 MiB > the 256 MiB Infinity Cache)
 TX_RINGS = 100             # c4tx: timed rings (and device event pairs) at least
 
@@ -576,7 +578,9 @@ def main(argv=None):
             else:
                 rx = Run(L, ctx, name, DEFAULT_FRAMES[name], 0, 1, EXTRA_QUEUES.get(name, 0),
                          args.streams, False)
-                x = measure(rx, args, None, 1)
+                xa = argparse.Namespace(**vars(args))
+                xa.steps = max(args.steps, EXTRA_MIN_STEPS.get(name, 0))
+                x = measure(rx, xa, None, 1)
                 x["workload"] = workload(rx, False)
                 if not args.no_cpu_baseline:
                     x["cpu_baseline"] = cpu_baseline(rx.cfg0, min(args.cpu_seconds, 3.0))

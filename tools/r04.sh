@@ -178,6 +178,27 @@ case $S in
       done
     done
     ;;
+  r04q)
+    # self-scan with 16-byte row loads (registers instead of occupancy): the
+    # scatter tests, c3 lists and bench key alternated with the scan, c3 PMC
+    mkdir -p $O
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+      tests/test_gpu_scatter.py > $O/pytest_sel.log 2>&1 || { tail -30 $O/pytest_sel.log; exit 1; }
+    tail -2 $O/pytest_sel.log
+    for kb in 0 16384; do
+      USN_SELFSCAN_KB=$kb timeout -k 10 300 python tools/scatter_bench.py --config c3 --frames 262144 --multi 4 \
+        --launches 100 > $O/scb_c3_kb$kb.log 2>&1 || exit 1
+      echo "kb=$kb c3 $(tail -1 $O/scb_c3_kb$kb.log)"
+    done
+    for rep in 1 2; do
+      for kb in 0 16384; do
+        USN_SELFSCAN_KB=$kb timeout -k 10 300 python bench.py --config c3 --queues 8 --no-extra --no-cpu-baseline \
+          --steps 200 --warmup 20 > $O/c3_kb${kb}_$rep.log 2>&1 || exit 1
+        echo "kb=$kb $(python3 tools/bench_summary.py $O/c3_kb${kb}_$rep.log | head -1)"
+      done
+    done
+    PMC_CFGS="c3" bash tools/gpu.sh $S pmc
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -2917,8 +2917,9 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
 #endif
-template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_SCATTER_WPE)))
+template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
+                               // registers for the row sums instead of occupancy)
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(SELF ? 2 : USN_SCATTER_WPE)))
 void scatter_kernel(ScatterArgs s) {
   static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
   constexpr uint32_t SEGS = TILE / 64;                               // 16 segments per tile
@@ -2970,35 +2971,42 @@ void scatter_kernel(ScatterArgs s) {
 #pragma unroll
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
   // 1b. (small launches) the scan's two sums for this chunk from the batch's
-  // count rows: thread (g, p) adds bin pair p of tiles g, g + G, ... into
-  // the totals and, for the tiles before the chunk, into its offsets
+  // count rows: thread (g, q) adds bins 8q..8q+7 (one 16-byte load) of tiles
+  // g, g + G, ... into the totals and, for the tiles before the chunk, into
+  // its offsets; up to 8 loads per thread in flight together
   if (selfscan) {
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals
     uint32_t *sb = sa + s.nbw;                                                // [nbw] before the chunk
     for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
     __syncthreads();
-    const uint32_t np = s.nbw / 2, G = NTHREADS / np, pp = tid % np, g = tid / np;
+    const uint32_t nq = s.nbw / 8, G = NTHREADS / nq, qq = tid % nq, g = tid / nq;
     if (g < G) {
-      const uint32_t *rows = reinterpret_cast<const uint32_t *>(B.cnt) + pp;   // row t: rows[t * np]
-      uint32_t a0 = 0, a1 = 0, e0 = 0, e1 = 0;
+      const uint4 *rows = reinterpret_cast<const uint4 *>(B.cnt) + qq;   // row t: rows[t * nq]
+      uint32_t at[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (uint32_t t = g; t < B.ntiles; t += 8 * G) {
-        uint32_t v[8];
+        uint4 v[8];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
           const uint32_t tt = t + k * G;
-          v[k] = tt < B.ntiles ? rows[(size_t)tt * np] : 0u;
+          v[k] = tt < B.ntiles ? rows[(size_t)tt * nq] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
-          const uint32_t lo = v[k] & 0xFFFFu, hi = v[k] >> 16;
-          a0 += lo; a1 += hi;
-          if (t + k * G < t0) { e0 += lo; e1 += hi; }
+          const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+          const bool before = t + k * G < t0;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
+            at[2 * j] += lo; at[2 * j + 1] += hi;
+            if (before) { ab[2 * j] += lo; ab[2 * j + 1] += hi; }
+          }
         }
       }
-      if (a0) atomicAdd(&sa[2 * pp], a0);
-      if (a1) atomicAdd(&sa[2 * pp + 1], a1);
-      if (e0) atomicAdd(&sb[2 * pp], e0);
-      if (e1) atomicAdd(&sb[2 * pp + 1], e1);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        if (at[j]) atomicAdd(&sa[8 * qq + j], at[j]);
+        if (ab[j]) atomicAdd(&sb[8 * qq + j], ab[j]);
+      }
     }
     __syncthreads();
     if (mine) {
