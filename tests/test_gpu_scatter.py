@@ -10,7 +10,8 @@ an unsorted chunk is ranked again by bit-sliced ballots.  These tests check
 that the optimistic path is the one taken (no chunk fell back) and that the
 ballot path, forced on every chunk (USN_SCATTER_SLOW_RANK=1, read once per
 process: a subprocess), gives the same lists -- both against the sequential
-oracle's decisions sorted stably by bin.
+oracle's decisions sorted stably by bin.  Small launches sum their count rows
+in the scatter itself (self-scan, no scan launch); both ways are checked.
 """
 import os
 import subprocess
@@ -75,6 +76,15 @@ def test_scatter_ballot_ranks_forced():
     out = _run({"USN_SCATTER_SLOW_RANK": "1"})
     assert out.strip().endswith("ok")
     assert all(not l.endswith(" 0") for l in out.splitlines()[:-1]), out
+
+
+@pytest.mark.parametrize("kb", ["0", "1048576"])
+def test_scatter_scan_or_self_scan(kb):
+    """The chunk offsets from the scan launch everywhere (USN_SELFSCAN_KB=0),
+    or summed by every launch whose chunks are all resident (self-scan even
+    at c5's 2 KiB rows and c4's 300K frames): the same lists."""
+    out = _run({"USN_SELFSCAN_KB": kb})
+    assert out.strip().endswith("ok")
 
 
 def _tile_plan(bins_of, rng, n_tiles):
