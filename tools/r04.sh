@@ -199,6 +199,15 @@ case $S in
     done
     PMC_CFGS="c3" bash tools/gpu.sh $S pmc
     ;;
+  r04r)
+    # the scatter tests (scan or self-scan), then nt decision reads in the
+    # scatter (index runs' partial lines merging in L2) against the current
+    mkdir -p $O
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+      tests/test_gpu_scatter.py > $O/pytest_scatter.log 2>&1 || { tail -30 $O/pytest_scatter.log; exit 1; }
+    tail -2 $O/pytest_scatter.log
+    SCB_CFGS="c5 c2" SCB_VARIANTS="cur scnt" bash tools/gpu.sh $S scb
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
