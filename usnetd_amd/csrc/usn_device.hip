@@ -2908,10 +2908,6 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
 #ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
 #define USN_SC_GROUP 1
 #endif
-#ifndef USN_SC_NT   /* A/B: the decisions read with the non-temporal hint (leave L2 to the
-                       index runs, whose partial lines then merge before write-back) */
-#define USN_SC_NT 0
-#endif
 #ifndef USN_SC_CHECKS   /* A/B only: 0 = no empty-slot sentinel and no inconsistency report
                            (the bounds clamps stay) */
 #define USN_SC_CHECKS 1
@@ -2973,10 +2969,7 @@ void scatter_kernel(ScatterArgs s) {
   const uint32_t tn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - tbase);
   uint32_t d[SEGS];
 #pragma unroll
-  for (uint32_t k = 0; k < SEGS; ++k) {
-    const uint32_t *dp = B.decisions + tbase + min(k * 64 + lane, tn - 1);
-    d[k] = USN_SC_NT ? __builtin_nontemporal_load(dp) : *dp;
-  }
+  for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
   // 1b. (small launches) the scan's two sums for this chunk from the batch's
   // count rows: thread (g, q) adds bins 8q..8q+7 (one 16-byte load) of tiles
   // g, g + G, ... into the totals and, for the tiles before the chunk, into
