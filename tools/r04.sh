@@ -208,6 +208,13 @@ case $S in
     tail -2 $O/pytest_scatter.log
     SCB_CFGS="c5 c2" SCB_VARIANTS="cur scnt" bash tools/gpu.sh $S scb
     ;;
+  r04s)
+    # phase stamps of the tx kernel and the c5 classify (diagnostic build)
+    STAMP_ARGS="c4tx 1048576" bash tools/gpu.sh $S stamps || exit 1
+    mv $O/stamps.log $O/stamps_c4tx.log
+    STAMP_ARGS="c5 8388608" bash tools/gpu.sh $S stamps
+    mv $O/stamps.log $O/stamps_c5.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
