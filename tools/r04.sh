@@ -215,6 +215,12 @@ case $S in
     STAMP_ARGS="c5 8388608" bash tools/gpu.sh $S stamps
     mv $O/stamps.log $O/stamps_c5.log
     ;;
+  r04t)
+    # persistent classify (resident workgroups loop over tiles; 64 VGPRs, 36 B
+    # spilled) against one workgroup per tile, c5 and c4
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur persist" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur persist" bash tools/gpu.sh $S abl
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
