@@ -11,8 +11,12 @@ per-endpoint scatter (scan_kernel, scatter_kernel): the
 counters of every dispatch of these kernels are summed per kernel name and
 divided by the number of classify / tx dispatches covering `frames` frames
 (every call of the run has that shape).
-usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json> [KERNEL=F ...]
-KERNEL=F: that kernel's FETCH_SIZE counted xF instead of x2.  c3's classify
+usage: pmc_traffic.py <fetch_dir> <write_dir> <frames_per_launch> <out.json> [KERNEL=F[+B] ...]
+KERNEL=F: that kernel's FETCH_SIZE counted xF instead of x2.  KERNEL=1+B: a
+kernel that mixes both kinds of read (the tx kernel: its header windows are
+coalesced 128-byte requests, its rule probes scattered 64-byte ones) counted
+x1 plus the B bytes per frame its coalesced reads' requests are short of
+(the tx kernel's 64-byte header line per frame, tallied at 32: tx_kernel=1+32).  c3's classify
 reads one window per 2048-byte slot inside the first 64-byte half of a line:
 a 64-byte EA request, which FETCH_SIZE (= TCC_EA0_RDREQ x 64 B) counts
 exactly, so c3 uses classify_rx_kernel=1 (calibration: tools/stride_floor.hip
@@ -48,15 +52,18 @@ def per_kernel(d, counter, frames):
 
 def main():
     fd, wd, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    factor = {}
+    factor, extra = {}, {}
     for kv in sys.argv[5:]:
         k, f = kv.split("=", 1)
+        f, _, b = f.partition("+")
         factor[k] = float(f)
+        if b:
+            extra[k] = float(b)
     fetch, nf = per_kernel(fd, "FETCH_SIZE", frames)
     write, nw = per_kernel(wd, "WRITE_SIZE", frames)
     if not nf or not nw:
         sys.exit("no classify dispatch of %d frames in %s / %s" % (frames, fd, wd))
-    rd = {k: factor.get(k, 2.0) * v * 1024 / nf for k, v in fetch.items()}
+    rd = {k: factor.get(k, 2.0) * v * 1024 / nf + extra.get(k, 0.0) * frames for k, v in fetch.items()}
     wr = {k: v * 1024 / nw for k, v in write.items()}
     read_algo = frames * (64 + 2)
     write_algo = frames * (4 + 4)
@@ -73,7 +80,8 @@ def main():
         "write_vs_algorithmic": round(sum(wr.values()) / write_algo, 4),
         "traffic_vs_algorithmic": round((sum(rd.values()) + sum(wr.values())) / (frames * 74), 4),
         "correction": "FETCH_SIZE x2 (gfx950, 128-B requests tallied at 64 B), WRITE_SIZE x1" +
-                      "".join("; %s FETCH_SIZE x%g" % (k, f) for k, f in sorted(factor.items())),
+                      "".join("; %s FETCH_SIZE x%g%s" % (k, f, " + %g B/frame" % extra[k] if k in extra else "")
+                              for k, f in sorted(factor.items())),
     }
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
