@@ -221,6 +221,17 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur persist" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur persist" bash tools/gpu.sh $S abl
     ;;
+  r04z)
+    # final tree: the suite, smoke, the bench as the driver runs it, rocprof
+    # of the bench, PMC of c5 / c2 / c4 and of the tx call (mixed requests)
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    PMC_CFGS="c5 c2 c4" bash tools/gpu.sh $S pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json tx_kernel=1+32 > $O/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
