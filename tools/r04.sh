@@ -232,6 +232,11 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 6" bash tools/gpu.sh $S txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 1048576 $O/pmc_c4tx.json tx_kernel=1+32 > $O/pmct_c4tx.log 2>&1
     ;;
+  r04u)
+    # the scatter at 8 waves per SIMD (64 VGPRs, spills): c2's and c4's 1024
+    # chunks in one generation of 4 workgroups per CU
+    SCB_CFGS="c2 c4 c5" SCB_VARIANTS="cur scwpe8" bash tools/gpu.sh $S scb
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
