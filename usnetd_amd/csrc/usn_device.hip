@@ -473,10 +473,13 @@ __device__ __forceinline__ void ph_disp_issue(const uint4 *T, const ClassifyArgs
 /* The slot reads of N keys whose displacements were read (ph_disp_issue;
  * keys [0, N1) in K1, the rest in K2), then the hits. */
 template <bool IN_LDS, int N, int N1>
-__device__ __forceinline__ void ph_slots_issue(const uint4 *T, const ClassifyArgs &a,
-                                               const PhKeyH (&k)[N], const uint32_t (&d)[N],
-                                               const bool (&on)[N], uint4 (&sl)[N]) {
+__device__ __forceinline__ void ph_slots_hit(const uint4 *T, const ClassifyArgs &a,
+                                             const uint32_t (&x)[N], const uint32_t (&y)[N],
+                                             const uint32_t (&z)[N], const uint32_t (&m)[N],
+                                             const PhKeyH (&k)[N], const uint32_t (&d)[N],
+                                             const bool (&on)[N], uint32_t (&w)[N]) {
   typedef __attribute__((address_space(3))) const v4u32 lds_v4;
+  uint4 sl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
@@ -488,15 +491,6 @@ __device__ __forceinline__ void ph_slots_issue(const uint4 *T, const ClassifyArg
       sl[i] = T[si];
     }
   }
-}
-template <bool IN_LDS, int N, int N1>
-__device__ __forceinline__ void ph_slots_hit(const uint4 *T, const ClassifyArgs &a,
-                                             const uint32_t (&x)[N], const uint32_t (&y)[N],
-                                             const uint32_t (&z)[N], const uint32_t (&m)[N],
-                                             const PhKeyH (&k)[N], const uint32_t (&d)[N],
-                                             const bool (&on)[N], uint32_t (&w)[N]) {
-  uint4 sl[N];
-  ph_slots_issue<IN_LDS, N, N1>(T, a, k, d, on, sl);
 #pragma unroll
   for (int i = 0; i < N; ++i) w[i] = on[i] ? ph_hit(sl[i], x[i], y[i], z[i], m[i]) : 0u;
 }
@@ -1706,50 +1700,6 @@ __device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t
   __syncthreads();
 }
 
-/* a workgroup barrier that orders LDS only (no wait for this wave's global
- * loads and stores in flight) */
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-/* tile_prefix_max with LDS-only barriers: the tx kernel's rule probes stay in
- * flight under it (USN_TX_EARLYPFX) */
-__device__ void tile_prefix_max_lds(const uint32_t v[ROUNDS], const Lds &L, uint32_t out[ROUNDS]) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) L.order[r * NTHREADS + tid] = (uint16_t)v[r];
-  lds_barrier();
-  const uint32_t p0 = tid * ROUNDS;
-  uint32_t e[ROUNDS], m = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) { e[k] = L.order[p0 + k]; m = max(m, e[k]); }
-  uint32_t inc = m;
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xA, 0xF, false));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xC, 0xF, false));
-  uint32_t exc = __shfl_up(inc, 1, 64);
-  if (lane == 0) exc = 0;
-  if (lane == 63) L.scratch[wave] = inc;
-  lds_barrier();
-  for (uint32_t w = 0; w < wave; ++w) exc = max(exc, L.scratch[w]);
-  uint32_t run = exc;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) {
-    const uint32_t x = e[k];
-    L.order[p0 + k] = (uint16_t)run;
-    run = max(run, x);
-  }
-  lds_barrier();
-#pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) out[r] = L.order[r * NTHREADS + tid];
-  lds_barrier();
-}
-
 #define TX_BRIDGE_LDS_SLOTS 2048u   /* bridge sets up to 16 KiB are staged in LDS */
 #define TX_LISTEN_LDS 64u           /* listening triples of the source staged in LDS */
 
@@ -2005,10 +1955,6 @@ __host__ __device__ inline size_t tx_lds_head(uint32_t nbins) {
 #ifndef USN_TX_PIPE   /* phase 1: probes of a round issued as it is parsed; LDS-only barrier */
 #define USN_TX_PIPE 1
 #endif
-#ifndef USN_TX_EARLYPFX   /* the records and the prefix max of touching frames while the rule
-                             probes' slot reads fly (LDS-only barriers); LEARNRULE after them */
-#define USN_TX_EARLYPFX 0
-#endif
 template <bool LDS>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(NTHREADS / 64)))
 void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames all resident)
@@ -2239,76 +2185,39 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   }
   uint32_t w1e[ROUNDS], w2e[ROUNDS];   // key1 / key2 results, valid where need[R + r]
   bool pre[ROUNDS];
-  uint32_t vt[ROUNDS], prev[ROUNDS];
-  if (USN_TX_EARLYPFX && USN_TX_PIPE) {
-    // the slot reads go out; the records and the prefix max of touching
-    // frames (parse only) are built while they fly, then LEARNRULE
-    uint4 sl[R3];
-    ph_slots_issue<LDS, R3, 2 * ROUNDS>(T, a, pk, pd, pon, sl);
-    STAMP(2);
-    lds_barrier();   // every wave is done with its header scratch before the records overwrite it
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local >= nt) rec[r] = make_uint4(0, 0, 0, 0);
-      srec[local] = rec[r];
-      vt[r] = (local < nt && tx_touch(rec[r])) ? local + 1 : 0u;
-      if (local < nt && (rec[r].x & TXR_LEARNMAC)) atomicOr(&s_early, 1u);
-    }
-    if (last) atomicMax(&s_last, last);
-    tile_prefix_max_lds(vt, L, prev);
+  {
     uint32_t w[R3];
-#pragma unroll
-    for (int i = 0; i < R3; ++i) w[i] = pon[i] ? ph_hit(sl[i], ax[i], ay[i], az[i], am[i]) : 0u;
-    bool lr = false;
+    if (USN_TX_PIPE) ph_slots_hit<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, pk, pd, pon, w);
+    else ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (need[r] && !w[r] && local < nt) {
-        rec[r].x |= TXR_LEARNRULE;
-        srec[local] = rec[r];
-        lr = true;
-      }
+      if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
       pre[r] = need[ROUNDS + r];
       w1e[r] = w[ROUNDS + r];
       w2e[r] = w[2 * ROUNDS + r];
     }
-    if (lr) atomicOr(&s_early, 2u);
-    lds_barrier();   // srec, s_last, s_early
-  } else {
-    {
-      uint32_t w[R3];
-      if (USN_TX_PIPE) ph_slots_hit<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, pk, pd, pon, w);
-      else ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
-#pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) {
-        if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
-        pre[r] = need[ROUNDS + r];
-        w1e[r] = w[ROUNDS + r];
-        w2e[r] = w[2 * ROUNDS + r];
-      }
-    }
-
-    STAMP(2);
-    // every wave is done with its header scratch before the records overwrite it
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    // ---- the tile's records in LDS; each frame's previous touching frame
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local >= nt) rec[r] = make_uint4(0, 0, 0, 0);
-      srec[local] = rec[r];
-      vt[r] = (local < nt && tx_touch(rec[r])) ? local + 1 : 0u;
-      if (local < nt && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE)))
-        atomicOr(&s_early, ((rec[r].x & TXR_LEARNMAC) ? 1u : 0u) | ((rec[r].x & TXR_LEARNRULE) ? 2u : 0u));
-    }
-    // (publishing LAST before the probes instead: 52.9 -> 61 us per 1M frames,
-    // the probes' compiler-placed vmcnt(0) then also waits for the sc1 stores)
-    if (last) atomicMax(&s_last, last);
-    tile_prefix_max(vt, L, prev);   // its barriers also publish srec, s_last and s_early
   }
+
+  STAMP(2);
+  // every wave is done with its header scratch before the records overwrite it
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  // ---- the tile's records in LDS; each frame's previous touching frame
+  uint32_t vt[ROUNDS], prev[ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    const uint32_t local = r * NTHREADS + tid;
+    if (local >= nt) rec[r] = make_uint4(0, 0, 0, 0);
+    srec[local] = rec[r];
+    vt[r] = (local < nt && tx_touch(rec[r])) ? local + 1 : 0u;
+    if (local < nt && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE)))
+      atomicOr(&s_early, ((rec[r].x & TXR_LEARNMAC) ? 1u : 0u) | ((rec[r].x & TXR_LEARNRULE) ? 2u : 0u));
+  }
+  // (publishing LAST before the probes instead: 52.9 -> 61 us per 1M frames,
+  // the probes' compiler-placed vmcnt(0) then also waits for the sc1 stores)
+  if (last) atomicMax(&s_last, last);
+  tile_prefix_max(vt, L, prev);   // its barriers also publish srec, s_last and s_early
   if (tid == 0) {
     const uint32_t lt = s_last;
     g_put4(aux + TXG_LREC, t.epoch, lt ? srec[lt - 1] : make_uint4(0, 0, 0, 0));
