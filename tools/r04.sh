@@ -237,6 +237,18 @@ case $S in
     # chunks in one generation of 4 workgroups per CU
     SCB_CFGS="c2 c4 c5" SCB_VARIANTS="cur scwpe8" bash tools/gpu.sh $S scb
     ;;
+  r04v)
+    # tx: records and prefix max under the rule probes' slot reads (txepfx,
+    # since reverted) against the current, alternated, device time per ring
+    mkdir -p $O
+    for rep in 1 2 3; do
+      for v in cur txepfx; do
+        timeout -k 10 300 python tools/txbench.py 1048576 40 1 build/abl/$v/libusn.so --rotate 6 \
+          > $O/txbench_${v}_$rep.log 2>&1 || exit 1
+        echo "$v $(tail -1 $O/txbench_${v}_$rep.log | cut -c1-200)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
