@@ -249,6 +249,19 @@ case $S in
       done
     done
     ;;
+  r04w)
+    # self-scan past one generation (USN_SELFSCAN_ANY=1): c2's 8 x 1M call
+    # (1024 chunks, 49 MB of rows read) with the row limit raised
+    mkdir -p $O
+    for rep in 1 2; do
+      for v in "0 16384" "1 65536"; do
+        set -- $v
+        USN_SELFSCAN_ANY=$1 USN_SELFSCAN_KB=$2 timeout -k 10 300 python tools/scatter_bench.py --config c2 \
+          --frames 1048576 --multi 8 --launches 100 > $O/scb_c2_any$1_$rep.log 2>&1 || exit 1
+        echo "any=$1 kb=$2 $(tail -1 $O/scb_c2_any$1_$rep.log)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
