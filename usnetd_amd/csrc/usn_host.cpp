@@ -2251,12 +2251,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     chunks_all += ch;
     self_bytes += (size_t)ch * as[k].ntiles * x.nbw * 2;
   }
-  static const bool selfscan_any = [] {   // A/B: USN_SELFSCAN_ANY=1 drops the residency condition
-    const char *e = std::getenv("USN_SELFSCAN_ANY");
-    return e && std::atoi(e) == 1;
-  }();
-  const bool selfscan = !noscan && x.nbw <= 2 * 512 &&
-                        (selfscan_any || chunks_all <= (uint32_t)std::max(cus, 1)) &&
+  const bool selfscan = !noscan && x.nbw <= 2 * 512 && chunks_all <= (uint32_t)std::max(cus, 1) &&
                         self_bytes <= (size_t)selfscan_kb * 1024 &&
                         usn::scatter_lds(x.nbins, tc, true) <= 64u * 1024u;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u) |
