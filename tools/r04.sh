@@ -262,6 +262,13 @@ case $S in
       done
     done
     ;;
+  r04x)
+    # the PCIe-inclusive loop on the final tree (hostio.py), c2 and c5
+    HOSTIO_ARGS="c2 1048576 8 4 6" bash tools/gpu.sh $S hostio || exit 1
+    mv $O/hostio.log $O/hostio_c2.log
+    HOSTIO_ARGS="c5 1048576 8 4 6" bash tools/gpu.sh $S hostio || exit 1
+    mv $O/hostio.log $O/hostio_c5.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
