@@ -269,6 +269,17 @@ case $S in
     HOSTIO_ARGS="c5 1048576 8 4 6" bash tools/gpu.sh $S hostio || exit 1
     mv $O/hostio.log $O/hostio_c5.log
     ;;
+  r04y)
+    # c2's PCIe-inclusive loop (1M rings on 4 streams): self-scan / scan /
+    # the old 1-tile chunks
+    mkdir -p $O
+    for v in "16384 0" "0 0" "0 1"; do
+      set -- $v
+      USN_SELFSCAN_KB=$1 USN_SCATTER_TC=$2 timeout -k 10 300 python tools/hostio.py c2 1048576 8 4 6 \
+        > $O/hostio_c2_kb$1_tc$2.log 2>&1 || exit 1
+      echo "kb=$1 tc=$2 $(head -c 160 $O/hostio_c2_kb$1_tc$2.log)"
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
