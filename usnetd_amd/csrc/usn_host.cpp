@@ -1680,6 +1680,55 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
   return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(n, nbins).diag);
 }
+/* How a launch's lists are built (launch_scatter): chunk length, scan
+ * threads' chunks, and whether the scan launch is skipped.
+ *  - chunk length: about one chunk per CU -- the longest chunk up to the LDS
+ *    shape's that still gives every CU one (A/B at 1024 tiles, a tx ring or
+ *    c3's call, profiles/r04/r04j: scan + scatter 21.3 / 16.7 / 16.1 / 17.6
+ *    us at chunks of 1 / 2 / 4 / 8 tiles; c5 and c2 keep 8).  tc_knob (A/B)
+ *    is taken as it is, at most the shape's;
+ *  - noscan: batches of at most one chunk each (a daemon's drained rings):
+ *    the scatter's one chunk per batch has the whole batch;
+ *  - selfscan: every chunk resident at once and all chunks together reading
+ *    at most selfscan_kb KiB of count rows (each reads its whole batch's):
+ *    each chunk sums them itself (profiles/r04/r04n: c3's calls, 9.4 MB,
+ *    lists 15.1 -> 11.8 us; a 1M c4 ring, 138 MB, 15.5 -> 33.7 us);
+ *  - cpt: 4 chunks per scan thread (a workgroup per 64 chunks) while that
+ *    gives >= 256 workgroups, else fewer (profiles/r03/r03i: c5 16M 56.6 /
+ *    57.3 / 60.3 us at 4 / 2 / 1; c2 8M 32.1 / 30.4 / 29.4). */
+ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb) {
+  ScatterPlan p{};
+  const ScatterShape sh = scatter_shape(nbins);
+  const uint32_t nbw = (nbins + 7u) & ~7u;
+  uint32_t launch_tiles = 0, max_tiles = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    launch_tiles += ntiles[k];
+    max_tiles = std::max(max_tiles, ntiles[k]);
+  }
+  uint32_t tc = tc_knob ? std::min(tc_knob, sh.tc) : sh.tc;
+  p.noscan = max_tiles <= tc;
+  if (!p.noscan && !tc_knob) {
+    const uint32_t per = std::max(1u, launch_tiles / std::max(cus, 1u));
+    while (tc > 1 && tc > per) tc /= 2;
+  }
+  p.tc = tc;
+  uint32_t chunks = 0;
+  size_t self_bytes = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const uint32_t ch = (ntiles[k] + tc - 1) / tc;
+    chunks += ch;
+    self_bytes += (size_t)ch * ntiles[k] * nbw * 2;
+  }
+  p.selfscan = !p.noscan && nbw <= 2 * 512 && chunks <= std::max(cus, 1u) &&
+               self_bytes <= (size_t)selfscan_kb * 1024 && scatter_lds(nbins, tc, true) <= 64u * 1024u;
+  const uint32_t nbb = (nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
+  uint32_t cpt = 4;
+  while (cpt > 1 && (chunks / (16 * cpt)) * nbb < 256) cpt /= 2;
+  p.cpt = cpt_knob ? cpt_knob : cpt;
+  return p;
+}
+
 /* the granule and diag part of a batch's scratch (zeroed on its first use
  * with this geometry) */
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes) {
@@ -2043,6 +2092,21 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
 /* Test hook: {full image builds, incremental updates, registry changes not
  * yet in the image, image version} -- after bringing the image up to date
  * when `refresh` is set */
+/* test hook (tests/test_scatter_plan.py, no GPU): the list plan of a launch
+ * of `count` batches of ntiles[k] tiles and nbins bins on `cus` CUs, with the
+ * default knobs: out4 = {chunk tiles, scan chunks per thread, noscan, selfscan} */
+int usn_debug_scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
+                           uint32_t *out4) {
+  if (!ntiles || !out4 || count == 0 || count > USN_MAX_MULTI || nbins == 0 || nbins > USN_MAX_BINS)
+    return USN_EINVAL;
+  const usn::ScatterPlan p = usn::scatter_plan(ntiles, count, nbins, cus, 0, 0, 16384);
+  out4[0] = p.tc;
+  out4[1] = p.cpt;
+  out4[2] = p.noscan ? 1u : 0u;
+  out4[3] = p.selfscan ? 1u : 0u;
+  return USN_OK;
+}
+
 int usn_debug_image_stats(usn_ctx *c, int refresh, uint64_t *out4) {
   if (!c || !out4) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -2197,11 +2261,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.nbw = as[0].nbw;
   x.n_ep = as[0].n_ep;
   x.nbits = as[0].nbits;
-  /* chunk length: the shape's (long chunks: contiguous runs per bin), shorter
-   * when the launch has too few tiles to give every CU its workgroups */
-  const usn::ScatterShape sh = usn::scatter_shape(x.nbins);
-  uint32_t launch_tiles = 0;
-  for (uint32_t k = 0; k < count; ++k) launch_tiles += as[k].ntiles;
+  uint32_t ntl[USN_MAX_MULTI];
+  for (uint32_t k = 0; k < count; ++k) ntl[k] = as[k].ntiles;
   int cus = 256;   // the replica's CUs, queried once
   {
     int dev = 0;
@@ -2219,58 +2280,24 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     const int v = e ? std::atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4 || v == 8) ? (uint32_t)v : 0u;
   }();
-  uint32_t tc = tc_knob ? std::min(tc_knob, sh.tc) : sh.tc, max_tiles = 0;
-  for (uint32_t k = 0; k < count; ++k) max_tiles = std::max(max_tiles, as[k].ntiles);
-  // batches of at most one chunk each (a daemon's drained rings): no scan
-  // launch, the scatter's one chunk per batch has the whole batch
-  const bool noscan = max_tiles <= tc;
-  // about one chunk per CU: the longest chunk up to the shape's that still
-  // gives every CU one (A/B at 1024 tiles -- a tx ring, c3's call --
-  // profiles/r04/r04j: scan + scatter 21.3 / 16.7 / 16.1 / 17.6 us at chunks
-  // of 1 / 2 / 4 / 8 tiles, c4tx end to end 13.6 -> 14.6 Gpkt/s; c5 and c2
-  // keep 8).  The knob, an A/B, is taken as it is.
-  if (!noscan && !tc_knob) {
-    const uint32_t per = std::max(1u, launch_tiles / (uint32_t)std::max(cus, 1));
-    while (tc > 1 && tc > per) tc /= 2;
-  }
-  x.tc = tc;
-  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
-  // a launch whose chunks are all resident at once and whose chunks together
-  // read few count-row bytes (each reads its whole batch's rows): each chunk
-  // sums them itself, no scan launch (profiles/r04/r04n: c3's calls of 4 x
-  // 256K frames, 9.4 MB read, lists 15.1 -> 11.8 us; a 1M c4 ring, 138 MB
-  // read, 15.5 -> 33.7 us, so it keeps the scan)
-  static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (row KiB all chunks read; 0 off)
-    const char *e = std::getenv("USN_SELFSCAN_KB");
-    return e ? (uint32_t)std::atoi(e) : 16384u;
-  }();
-  uint32_t chunks_all = 0;
-  size_t self_bytes = 0;
-  for (uint32_t k = 0; k < count; ++k) {
-    const uint32_t ch = (as[k].ntiles + tc - 1) / tc;
-    chunks_all += ch;
-    self_bytes += (size_t)ch * as[k].ntiles * x.nbw * 2;
-  }
-  const bool selfscan = !noscan && x.nbw <= 2 * 512 && chunks_all <= (uint32_t)std::max(cus, 1) &&
-                        self_bytes <= (size_t)selfscan_kb * 1024 &&
-                        usn::scatter_lds(x.nbins, tc, true) <= 64u * 1024u;
-  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (noscan ? USN_SCF_NOSCAN : 0u) |
-            (selfscan ? USN_SCF_SELFSCAN : 0u);
-  x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = std::getenv("USN_SCAN_CPT");
     const int v = e ? std::atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
   }();
-  // chunks per scan thread: 4 (a workgroup per 64 chunks) while that gives
-  // the launch >= 256 workgroups, else fewer (A/B, profiles/r03/r03i: c5 16M
-  // 56.6 / 57.3 / 60.3 us for scan + scatter at 4 / 2 / 1; c2 8M, 19 bins:
-  // 32.1 / 30.4 / 29.4)
-  uint32_t chunks = 0;
-  for (uint32_t k = 0; k < count; ++k) chunks += (as[k].ntiles + tc - 1) / tc;
-  uint32_t cpt = 4;
-  while (cpt > 1 && (chunks / (16 * cpt)) * x.nbb < 256) cpt /= 2;
-  x.cpt = cpt_knob ? cpt_knob : cpt;
+  static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (row KiB all chunks read; 0 off)
+    const char *e = std::getenv("USN_SELFSCAN_KB");
+    return e ? (uint32_t)std::atoi(e) : 16384u;
+  }();
+  const usn::ScatterPlan pl = usn::scatter_plan(ntl, count, x.nbins, (uint32_t)std::max(cus, 1), tc_knob,
+                                                cpt_knob, selfscan_kb);
+  const uint32_t tc = pl.tc;
+  x.tc = tc;
+  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
+  x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (pl.noscan ? USN_SCF_NOSCAN : 0u) |
+            (pl.selfscan ? USN_SCF_SELFSCAN : 0u);
+  x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
+  x.cpt = pl.cpt;
   x.txs_out = txs_out;
   x.txs_counters = txs_counters;
   x.txs_sum = r[0].summary;

@@ -192,6 +192,10 @@ inline uint32_t scatter_occupancy(size_t lds) {
   const uint32_t occ = (uint32_t)((160u * 1024u) / (lds ? lds : 1));
   return occ > 4 ? 4 : occ;
 }
+/* how a launch's lists are built (usn_host.cpp scatter_plan) */
+struct ScatterPlan { uint32_t tc, cpt; bool noscan, selfscan; };
+ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb);
 /* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
