@@ -2951,6 +2951,11 @@ void scatter_kernel(ScatterArgs s) {
   const bool mine = pair && 2 * tid < s.nbw;
   const bool noscan = (s.flags & USN_SCF_NOSCAN) != 0;   // one chunk per batch: its counts are the batch's
   const bool selfscan = SELF && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
+  if (selfscan) {   // the sums zeroed before any load is in flight (the barrier waits for none)
+    uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);
+    for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
+    __syncthreads();
+  }
   uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
   if (mine && !noscan && !selfscan) {
@@ -2975,10 +2980,8 @@ void scatter_kernel(ScatterArgs s) {
   // g, g + G, ... into the totals and, for the tiles before the chunk, into
   // its offsets; up to 8 loads per thread in flight together
   if (selfscan) {
-    uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals
+    uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals (zeroed above)
     uint32_t *sb = sa + s.nbw;                                                // [nbw] before the chunk
-    for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
-    __syncthreads();
     const uint32_t nq = s.nbw / 8, G = NTHREADS / nq, qq = tid % nq, g = tid / nq;
     if (g < G) {
       const uint4 *rows = reinterpret_cast<const uint4 *>(B.cnt) + qq;   // row t: rows[t * nq]
