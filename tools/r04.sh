@@ -280,6 +280,19 @@ case $S in
       echo "kb=$1 tc=$2 $(head -c 160 $O/hostio_c2_kb$1_tc$2.log)"
     done
     ;;
+  r04aa)
+    # the scatter_plan refactor and the earlier self-scan zeroing: scatter +
+    # tx tests, then c3's lists against the previous commit, alternated
+    mkdir -p $O
+    timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+      tests/test_gpu_scatter.py tests/test_gpu_tx.py > $O/pytest_sel.log 2>&1 || { tail -30 $O/pytest_sel.log; exit 1; }
+    tail -2 $O/pytest_sel.log
+    for rep in 1 2; do
+      timeout -k 10 300 python tools/scatter_bench.py --config c3 --frames 262144 --multi 4 --launches 100 \
+        cur selfold > $O/scb_c3_$rep.log 2>&1 || exit 1
+      grep scatter $O/scb_c3_$rep.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
