@@ -293,6 +293,17 @@ case $S in
       grep scatter $O/scb_c3_$rep.log
     done
     ;;
+  r04ab)
+    # c3 with self-scan at 8-tile chunks (128 chunks) against the plan's 4
+    mkdir -p $O
+    for rep in 1 2; do
+      for tc in 0 8; do
+        USN_SCATTER_TC=$tc timeout -k 10 300 python tools/scatter_bench.py --config c3 --frames 262144 --multi 4 \
+          --launches 100 > $O/scb_c3_tc${tc}_$rep.log 2>&1 || exit 1
+        echo "tc=$tc $(grep scatter $O/scb_c3_tc${tc}_$rep.log)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
