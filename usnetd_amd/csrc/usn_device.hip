@@ -21,7 +21,10 @@
  * scan_kernel + scatter_kernel: the device-wide per-endpoint lists (index,
  * bin_off) from the decisions and the count rows (§3.2): stable, frame order
  * inside each bin; a count row that disagrees with the decisions is reported
- * (diag USN_DIAG_LISTS -> usn_finalize USN_ELIST), never hidden.
+ * (diag USN_DIAG_LISTS -> usn_finalize USN_ELIST), never hidden.  About one
+ * chunk per CU; a launch whose chunks are all resident and whose rows are
+ * few skips the scan (each chunk sums its batch's rows: scatter_kernel<TC,
+ * true>; the plan is usn_host.cpp scatter_plan).
  * No MFMA: byte parsing and hash probing, bounded by HBM reads.
  *
  * Order-dependent state (fragment map, DHCP next endpoint, a stale carried
