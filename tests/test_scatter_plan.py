@@ -22,26 +22,24 @@ def plan(ntiles, nbins, cus=CUS):
     out = (ctypes.c_uint32 * 4)()
     rc = f(nt, len(ntiles), nbins, cus, out)
     assert rc == 0, rc
-    return {"tc": out[0], "cpt": out[1], "noscan": bool(out[2]), "selfscan": bool(out[3] & 1),
-            "fused": bool(out[3] & 2)}
+    return {"tc": out[0], "cpt": out[1], "noscan": bool(out[2]), "selfscan": bool(out[3])}
 
 
 @pytest.mark.parametrize("name,ntiles,nbins,want", [
     # c5: two 8M rings, 1005 bins -- 8-tile chunks, the scan at 4 chunks per thread
-    ("c5", [8192, 8192], 1005, {"tc": 8, "cpt": 4, "noscan": False, "selfscan": False, "fused": False}),
+    ("c5", [8192, 8192], 1005, {"tc": 8, "cpt": 4, "noscan": False, "selfscan": False}),
     # c2: eight 1M rings, 19 bins -- 1024 chunks, too many to self-scan
-    ("c2", [1024] * 8, 19, {"tc": 8, "cpt": 1, "noscan": False, "selfscan": False, "fused": False}),
+    ("c2", [1024] * 8, 19, {"tc": 8, "cpt": 1, "noscan": False, "selfscan": False}),
     # c4 rx: eight 1M rings, 259 bins
-    ("c4", [1024] * 8, 259, {"tc": 8, "cpt": 1, "noscan": False, "selfscan": False, "fused": False}),
+    ("c4", [1024] * 8, 259, {"tc": 8, "cpt": 1, "noscan": False, "selfscan": False}),
     # c3: four 256K rings, 67 bins -- a chunk per CU, 9.4 MB of rows: self-scan
-    ("c3", [256] * 4, 67, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": True, "fused": False}),
-    # a tx ring (c4tx): 1024 tiles, 261 bins -- 4-tile chunks, 138 MB of rows: no self-scan,
-    # but one batch whose 256 chunks are all resident: the scan inside the scatter
-    ("c4tx", [1024], 261, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": False, "fused": True}),
+    ("c3", [256] * 4, 67, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": True}),
+    # a tx ring (c4tx): 1024 tiles, 261 bins -- 4-tile chunks, 138 MB of rows: the scan
+    ("c4tx", [1024], 261, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": False}),
     # one 1M c2 ring (the daemon's): self-scan
-    ("c2ring", [1024], 19, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": True, "fused": False}),
+    ("c2ring", [1024], 19, {"tc": 4, "cpt": 1, "noscan": False, "selfscan": True}),
     # a drained ring of 8K frames: one chunk, no scan at all
-    ("small", [8], 19, {"tc": 8, "cpt": 1, "noscan": True, "selfscan": False, "fused": False}),
+    ("small", [8], 19, {"tc": 8, "cpt": 1, "noscan": True, "selfscan": False}),
 ])
 def test_plan_of_the_bench_shapes(name, ntiles, nbins, want):
     got = plan(ntiles, nbins)
@@ -60,17 +58,7 @@ def test_chunks_per_cu():
 
 def test_self_scan_needs_a_resident_launch_and_few_rows():
     assert plan([256] * 4, 67)["selfscan"]
-    assert plan([256] * 4, 67, cus=128) == {"tc": 8, "cpt": 1, "noscan": False, "selfscan": True,
-                                            "fused": False}
+    assert plan([256] * 4, 67, cus=128) == {"tc": 8, "cpt": 1, "noscan": False, "selfscan": True}
     assert not plan([300] * 4, 67)["selfscan"]                  # 4 x 75 chunks > 256 CUs
     assert not plan([1024], 1005)["selfscan"]                   # 2 KiB rows: 512 MB read
     assert not plan([2048] * 4, 67)["selfscan"]                 # 1024 chunks
-
-
-def test_fused_scan_needs_one_resident_batch():
-    """The scan done inside the scatter (two grid barriers) only for ONE batch
-    whose chunks (of two tiles or more) are all resident."""
-    assert plan([1024], 1005)["fused"]                     # a 1M c5 ring: 256 chunks of 4 tiles
-    assert not plan([1024, 1024], 261)["fused"]            # two batches
-    assert not plan([300], 261)["fused"]                   # 1-tile chunks: no room for the counts
-    assert not plan([8192], 261)["fused"]                  # 1024 chunks > 256 CUs

@@ -2920,41 +2920,9 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
 #endif
-__device__ __forceinline__ void vm_drain_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-/* USN_SCF_FUSED: thread 0 waits until `ctr` reaches `target` (every chunk
- * of the launch arrived; a chunk arrives after its sc1 stores landed), then
- * the workgroup goes on.  Bounded: after SCAN_SPIN_TICKS the batch's diag
- * gets USN_DIAG_TIMEOUT (usn_finalize: USN_EHIP) and the wait ends. */
-__device__ void grid_wait(const uint32_t *ctr, uint32_t target, uint32_t *diag) {
-  if (threadIdx.x == 0) {
-    uint64_t t0 = 0;
-    for (uint32_t it = 0;; ++it) {
-      const uint32_t v = __hip_atomic_load((__attribute__((address_space(1))) const uint32_t *)ctr,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((int32_t)(v - target) >= 0) break;
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (it == 0) t0 = now;
-      else if (now - t0 > SCAN_SPIN_TICKS) { atomicOr(diag, USN_DIAG_TIMEOUT); break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void st_sc1_u32(uint32_t *p, uint32_t v) {
-  __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)p, v, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t *p) {
-  return __hip_atomic_load((__attribute__((address_space(1))) const uint32_t *)p, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-/* MODE 0: the scan launch's sums; 1 (USN_SCF_SELFSCAN): the batch's rows
- * summed here (one workgroup per CU at most: registers for the row sums
- * instead of occupancy); 2 (USN_SCF_FUSED): the scan done across the
- * launch's chunks between two grid barriers */
-template <int TC, int MODE>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 2 : MODE == 2 ? 4 : USN_SCATTER_WPE)))
+template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
+                               // registers for the row sums instead of occupancy)
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(SELF ? 2 : USN_SCATTER_WPE)))
 void scatter_kernel(ScatterArgs s) {
   static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
   constexpr uint32_t SEGS = TILE / 64;                               // 16 segments per tile
@@ -2985,8 +2953,7 @@ void scatter_kernel(ScatterArgs s) {
   const bool pair = s.nbw <= 2 * NTHREADS;
   const bool mine = pair && 2 * tid < s.nbw;
   const bool noscan = (s.flags & USN_SCF_NOSCAN) != 0;   // one chunk per batch: its counts are the batch's
-  const bool selfscan = MODE == 1 && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
-  const bool fused = MODE == 2 && pair;      // the scan across the chunks here (USN_SCF_FUSED)
+  const bool selfscan = SELF && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
   if (selfscan) {   // the sums zeroed before any load is in flight (the barrier waits for none)
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);
     for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
@@ -2994,7 +2961,7 @@ void scatter_kernel(ScatterArgs s) {
   }
   uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
-  if (mine && !noscan && !selfscan && !fused) {
+  if (mine && !noscan && !selfscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
   }
@@ -3051,40 +3018,6 @@ void scatter_kernel(ScatterArgs s) {
     if (mine) {
       vt = make_uint2(sa[2 * tid], sa[2 * tid + 1]);
       ve = make_uint2(sb[2 * tid], sb[2 * tid + 1]);
-    }
-  }
-  // 1c. (one batch, every chunk resident) the scan across the chunks:
-  //   A. this chunk's counts out (sc1), then wait for every chunk's;
-  //   B. bins [c K, c K + K) of the batch: an exclusive scan over the chunks
-  //      (thread i = chunk i) -> agg[i][b], and the total -> tot[b]; wait;
-  //   C. this chunk's offsets and the totals, as the scan launch leaves them.
-  if (fused) {
-    uint32_t a0 = 0, a1 = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < TC; ++w) { a0 += rc[w] & 0xFFFFu; a1 += rc[w] >> 16; }
-    if (mine) {
-      st_sc1_u32(B.csum + (size_t)c * s.nbw + 2 * tid, a0);
-      st_sc1_u32(B.csum + (size_t)c * s.nbw + 2 * tid + 1, a1);
-    }
-    vm_drain_all();
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(B.gb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    grid_wait(B.gb, B.gb_target, B.diag);
-    const uint32_t K = (s.nbw + B.nchunks - 1) / B.nchunks;
-    for (uint32_t b = c * K; b < min(c * K + K, s.nbw); ++b) {
-      const uint32_t v = tid < B.nchunks ? ld_sc1_u32(B.csum + (size_t)tid * s.nbw + b) : 0u;
-      uint32_t total;
-      const uint32_t pre = block_excl_scan(v, s_scan, &total);
-      if (tid < B.nchunks) st_sc1_u32(B.agg + (size_t)tid * s.nbw + b, pre);
-      if (tid == 0) st_sc1_u32(B.tot + b, total);
-    }
-    vm_drain_all();
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(B.gb + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    grid_wait(B.gb + 1, B.gb_target, B.diag);
-    if (mine) {
-      vt = make_uint2(ld_sc1_u32(B.tot + 2 * tid), ld_sc1_u32(B.tot + 2 * tid + 1));
-      ve = make_uint2(ld_sc1_u32(ex + 2 * tid), ld_sc1_u32(ex + 2 * tid + 1));
     }
   }
   // 2. bases, the chunk's bin starts, the waves' cursors
@@ -3294,7 +3227,7 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN | USN_SCF_FUSED))) switch (s.cpt) {
+  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
     case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
     case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
     case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;
@@ -3302,12 +3235,11 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   }
   const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0);
   const dim3 g(chunks), b(NTHREADS);
-  const int mode = (s.flags & USN_SCF_SELFSCAN) ? 1 : (s.flags & USN_SCF_FUSED) ? 2 : 0;
+  const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
 #define USN_SC_LAUNCH(TC_)                                                              \
   do {                                                                                  \
-    if (mode == 1) hipLaunchKernelGGL((scatter_kernel<TC_, 1>), g, b, lds, stream, s);  \
-    else if (mode == 2) hipLaunchKernelGGL((scatter_kernel<TC_, 2>), g, b, lds, stream, s); \
-    else hipLaunchKernelGGL((scatter_kernel<TC_, 0>), g, b, lds, stream, s);            \
+    if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);    \
+    else hipLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, s);        \
   } while (0)
   switch (s.tc) {
     case 8: USN_SC_LAUNCH(8); break;

@@ -549,7 +549,7 @@ struct usn_ctx {
   uint32_t scan_epoch = (uint32_t)std::random_device{}();
   /* per scratch: the bind tag and geometry (frames, bins) its granules were
    * last zeroed for (one entry per scratch, not per geometry) */
-  struct Zeroed { uint32_t tag; uint64_t geo; uint32_t gb_base; };   // gb_base: fused arrivals so far
+  struct Zeroed { uint32_t tag; uint64_t geo; };
   std::unordered_map<const void *, Zeroed> scan_zeroed;
   uint64_t listen_gen = 0;   // Ep::listen_ver source
   /* a tx batch's summary flags, counters and class totals, written into
@@ -1670,14 +1670,11 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.tot = reinterpret_cast<uint32_t *>(p + g.tot);
   sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
   sb.diag = reinterpret_cast<uint32_t *>(p + g.diag);
-  sb.gb = sb.diag + 1;   // two arrival counters beside diag (the same 256-byte unit, zeroed with it)
   sb.n = (uint32_t)n;
   sb.ntiles = g.ntiles;
   sb.tc = tc;
   sb.nchunks = (g.ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
-  // agg is sized for one-tile chunks: at tc >= 2 its second half holds csum
-  sb.csum = sb.agg + (size_t)sb.nchunks * g.nbw;
 }
 /* the scan's diag word of a batch's scratch (bit 0: a wait timed out) */
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
@@ -1700,7 +1697,7 @@ uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
  *    gives >= 256 workgroups, else fewer (profiles/r03/r03i: c5 16M 56.6 /
  *    57.3 / 60.3 us at 4 / 2 / 1; c2 8M 32.1 / 30.4 / 29.4). */
 ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
-                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb, bool fused_ok) {
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb) {
   ScatterPlan p{};
   const ScatterShape sh = scatter_shape(nbins);
   const uint32_t nbw = (nbins + 7u) & ~7u;
@@ -1725,10 +1722,6 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
   }
   p.selfscan = !p.noscan && nbw <= 2 * 512 && chunks <= std::max(cus, 1u) &&
                self_bytes <= (size_t)selfscan_kb * 1024 && scatter_lds(nbins, tc, true) <= 64u * 1024u;
-  // fused: one batch, every chunk resident (its grid barriers), chunks of two
-  // tiles or more (csum in agg's second half), a bin pair per thread
-  p.fused = fused_ok && !p.noscan && !p.selfscan && count == 1 && tc >= 2 && nbw <= 2 * 512 &&
-            chunks <= std::max(cus, 1u) && chunks <= 512;
   const uint32_t nbb = (nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   uint32_t cpt = 4;
   while (cpt > 1 && (chunks / (16 * cpt)) * nbb < 256) cpt /= 2;
@@ -2101,17 +2094,16 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
  * when `refresh` is set */
 /* test hook (tests/test_scatter_plan.py, no GPU): the list plan of a launch
  * of `count` batches of ntiles[k] tiles and nbins bins on `cus` CUs, with the
- * default knobs: out4 = {chunk tiles, scan chunks per thread, noscan,
- * selfscan | fused << 1} */
+ * default knobs: out4 = {chunk tiles, scan chunks per thread, noscan, selfscan} */
 int usn_debug_scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
                            uint32_t *out4) {
   if (!ntiles || !out4 || count == 0 || count > USN_MAX_MULTI || nbins == 0 || nbins > USN_MAX_BINS)
     return USN_EINVAL;
-  const usn::ScatterPlan p = usn::scatter_plan(ntiles, count, nbins, cus, 0, 0, 16384, true);
+  const usn::ScatterPlan p = usn::scatter_plan(ntiles, count, nbins, cus, 0, 0, 16384);
   out4[0] = p.tc;
   out4[1] = p.cpt;
   out4[2] = p.noscan ? 1u : 0u;
-  out4[3] = (p.selfscan ? 1u : 0u) | (p.fused ? 2u : 0u);
+  out4[3] = p.selfscan ? 1u : 0u;
   return USN_OK;
 }
 
@@ -2297,17 +2289,13 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     const char *e = std::getenv("USN_SELFSCAN_KB");
     return e ? (uint32_t)std::atoi(e) : 16384u;
   }();
-  static const bool fused_ok = [] {   // A/B: USN_FUSED=0 keeps the scan launch
-    const char *e = std::getenv("USN_FUSED");
-    return !e || std::atoi(e) != 0;
-  }();
   const usn::ScatterPlan pl = usn::scatter_plan(ntl, count, x.nbins, (uint32_t)std::max(cus, 1), tc_knob,
-                                                cpt_knob, selfscan_kb, fused_ok);
+                                                cpt_knob, selfscan_kb);
   const uint32_t tc = pl.tc;
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (pl.noscan ? USN_SCF_NOSCAN : 0u) |
-            (pl.selfscan ? USN_SCF_SELFSCAN : 0u) | (pl.fused ? USN_SCF_FUSED : 0u);
+            (pl.selfscan ? USN_SCF_SELFSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   x.cpt = pl.cpt;
   x.txs_out = txs_out;
@@ -2330,16 +2318,11 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     const uint64_t geo = (as[k].n << 16) ^ x.nbins;
     auto zi = c->scan_zeroed.find(r[k].scratch);
     if (zi == c->scan_zeroed.end() || zi->second.tag != r[k].bind_tag || zi->second.geo != geo) {
-      c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo, 0u};
+      c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo};
       void *p;
       size_t bytes;
       usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
       HIPCHK(hipMemsetAsync(p, 0, bytes, s));
-    }
-    if (pl.fused) {   // both counters gain one arrival per chunk per launch
-      usn_ctx::Zeroed &z = c->scan_zeroed[r[k].scratch];
-      z.gb_base += sb.nchunks;
-      sb.gb_target = z.gb_base;
     }
   }
   // test hook (tests/test_gpu_scatter.py, read once per process):

@@ -146,9 +146,6 @@ struct ScatterBatch {
   uint32_t *diag;           /* USN_DIAG_*: the lists are wrong (usn_finalize reports it) */
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
-  uint32_t *csum;           /* USN_SCF_FUSED: [nchunks][nbw] each chunk's counts (in agg's space) */
-  uint32_t *gb;             /* USN_SCF_FUSED: 2 arrival counters (the scratch's tail) */
-  uint32_t gb_target;       /* USN_SCF_FUSED: both counters' value once every chunk arrived */
   uint32_t n, ntiles, tc, nchunks, nranges;
 };
 struct ScatterArgs {
@@ -175,9 +172,6 @@ struct ScatterArgs {
 #define USN_SCF_SELFSCAN 4u    /* a small launch (every chunk resident at once, few count-row
                                   bytes per batch): no scan launch; each chunk sums its batch's
                                   count rows itself (the totals, and the tiles before it) */
-#define USN_SCF_FUSED 8u       /* one batch whose chunks are all resident: no scan launch; the
-                                  scatter publishes its chunk counts, waits for every chunk, scans
-                                  a few bins across the chunks, waits again (two grid barriers) */
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
@@ -199,14 +193,14 @@ inline uint32_t scatter_occupancy(size_t lds) {
   return occ > 4 ? 4 : occ;
 }
 /* how a launch's lists are built (usn_host.cpp scatter_plan) */
-struct ScatterPlan { uint32_t tc, cpt; bool noscan, selfscan, fused; };
+struct ScatterPlan { uint32_t tc, cpt; bool noscan, selfscan; };
 ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
-                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb, bool fused_ok);
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb);
 /* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
 void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
-                   ScatterBatch &sb, uint16_t **cnt);   /* (csum / gb: USN_SCF_FUSED's, tc >= 2) */
+                   ScatterBatch &sb, uint16_t **cnt);
 void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
 uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
 
