@@ -304,6 +304,23 @@ case $S in
       done
     done
     ;;
+  r04ac)
+    # the scan inside the scatter for one resident batch (USN_SCF_FUSED, two
+    # grid barriers; since reverted): the suite, then fused / scan on a tx
+    # ring and 1M rings
+    bash tools/gpu.sh $S testsall || exit 1
+    for rep in 1 2; do
+      for f in 0 1; do
+        USN_FUSED=$f timeout -k 10 300 python tools/txpipe.py > $O/txpipe_f${f}_$rep.log 2>&1 || exit 1
+        echo "fused=$f c4tx $(tail -1 $O/txpipe_f${f}_$rep.log)"
+        for c in c4 c5; do
+          USN_FUSED=$f timeout -k 10 300 python tools/scatter_bench.py --config $c --frames 1048576 --multi 1 \
+            --launches 100 > $O/scb_${c}_f${f}_$rep.log 2>&1 || exit 1
+          echo "fused=$f $c $(grep scatter $O/scb_${c}_f${f}_$rep.log)"
+        done
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
