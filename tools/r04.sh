@@ -321,6 +321,14 @@ case $S in
       done
     done
     ;;
+  r04ad)
+    # the final tree again (after the reverted experiments): the suite, smoke,
+    # the bench with the driver's defaults, rocprof of the bench
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
