@@ -329,6 +329,12 @@ case $S in
     BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     bash tools/gpu.sh $S rocprof
     ;;
+  r04ae)
+    # the classify's first barrier LDS-only (each wave waits for its own
+    # round 0) against the current, c5 / c4 / c2
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur bar0" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur bar0" bash tools/gpu.sh $S abl
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
