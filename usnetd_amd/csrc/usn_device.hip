@@ -892,10 +892,6 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #define USN_EARLY_R1 0
 #endif
 #define STAGE_R_SLOTS (64u * GLDS_PARTS)   /* one round's parts per wave (USN_EARLY_R1) */
-#ifndef USN_LDS_BAR0   /* A/B: the tile's first barrier orders LDS only (after this wave's image
-                          copy); each wave then waits for its own round 0, not every wave's */
-#define USN_LDS_BAR0 0
-#endif
 static_assert(!USN_EARLY_R1 || USN_STAGE32, "USN_EARLY_R1: two-part stage");
 #ifndef GLDS_NT                  /* aux bits of the header glds: non-temporal */
 #define GLDS_NT 2
@@ -1113,11 +1109,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    } else if (USN_LDS_BAR0 && BATCH2) {   // round 0's parts may still fly
-      vm_wait<GLDS_PARTS>();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     } else {
       __syncthreads();
     }
@@ -1160,7 +1151,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint4 *sb = st;
       uint32_t du0, du1;
       v4u32 su0, su1;
-      if (USN_LDS_BAR0 && !EARLY) vm_wait<0>();                   // this wave's round 0
       stage_read_asm(sb, lane, q[0]);
       if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
@@ -1219,7 +1209,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       RoundKeys k0, k1;
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
-      if (USN_LDS_BAR0 && !EARLY) vm_wait<0>();                   // this wave's round 0
       stage_read_asm(sb, lane, q[0]);
       if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
@@ -1257,7 +1246,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       RoundKeys k0, k1;
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
-      if (USN_LDS_BAR0 && !EARLY) vm_wait<0>();                   // this wave's round 0
       stage_read_asm(sb, lane, q[0]);
       if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
@@ -1286,7 +1274,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       RoundKeys k0, k1;
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
-      if (USN_LDS_BAR0 && !EARLY) vm_wait<0>();                   // this wave's round 0
       stage_read_asm(sb, lane, q[0]);
       if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
