@@ -335,6 +335,26 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur bar0" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur bar0" bash tools/gpu.sh $S abl
     ;;
+  r04af)
+    # L2 hits and misses of the c5 call per kernel (are the U slot reads L2 hits?)
+    mkdir -p $O
+    rm -rf $O/l2
+    timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/l2 -o run -- \
+      python3 bench.py --config c5 --no-extra --steps 16 --warmup 4 --no-cpu-baseline --launch-probe 0 --ramp 0 \
+      > $O/l2.log 2>&1 || exit 1
+    python3 - $O/l2 <<'PY'
+import csv, glob, os, sys
+from collections import defaultdict
+tot = defaultdict(float); n = defaultdict(int)
+for f in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0][-40:]
+        tot[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+        if r["Counter_Name"] == "TCC_HIT_sum": n[k] += 1
+for (k, c), v in sorted(tot.items()):
+    print("%-42s %-14s %14.0f per dispatch %12.0f" % (k, c, v, v / max(1, n[k])))
+PY
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
