@@ -355,6 +355,11 @@ for (k, c), v in sorted(tot.items()):
     print("%-42s %-14s %14.0f per dispatch %12.0f" % (k, c, v, v / max(1, n[k])))
 PY
     ;;
+  r04ag)
+    # wave priority for the classify tile's tail (prio2) against the current
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur prio2" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur prio2" bash tools/gpu.sh $S abl
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
