@@ -1004,9 +1004,6 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 #ifndef USN_PERSIST
 #define USN_PERSIST 0
 #endif
-#ifndef USN_TAIL_PRIO   /* A/B: wave priority (s_setprio 1..3) from the decisions to the tile's end */
-#define USN_TAIL_PRIO 0
-#endif
 #ifndef USN_PERSIST_CAP
 #define USN_PERSIST_CAP 1
 #endif
@@ -1397,7 +1394,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
         differs |= 1u << r;        // later fragments also stop the device prefix
     }
     STAMP(5);
-    if (USN_TAIL_PRIO) __builtin_amdgcn_s_setprio(USN_TAIL_PRIO);   // A/B: the tile's tail ahead of other waves' parse
 
     // ---- stale carried cache: frames before the first break take the cached
     //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
@@ -1491,7 +1487,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     }
     STAMP(11);
     STAMP_FLUSH_AT(w);
-    if (USN_TAIL_PRIO) __builtin_amdgcn_s_setprio(0);
     if (!USN_PERSIST || w + gridDim.x >= ntiles_launch) break;
   }
 }
