@@ -360,6 +360,10 @@ PY
     ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --batches 4 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="cur prio2" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --batches 16 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="cur prio2" bash tools/gpu.sh $S abl
     ;;
+  r04ah)
+    # the driver's multi-GPU launch shape rehearsed on one GPU (two ranks)
+    bash tools/gpu.sh $S bench_n2
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
