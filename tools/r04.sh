@@ -364,6 +364,14 @@ PY
     # the driver's multi-GPU launch shape rehearsed on one GPU (two ranks)
     bash tools/gpu.sh $S bench_n2
     ;;
+  r04ai)
+    # c4tx timed without events in the pipelined loop (events in a second pass)
+    mkdir -p $O
+    for rep in 1 2 3; do
+      timeout -k 10 300 python tools/txpipe.py > $O/txpipe_$rep.log 2>&1 || exit 1
+      tail -1 $O/txpipe_$rep.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

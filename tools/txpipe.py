@@ -24,7 +24,8 @@ def main():
     ctx = lib.Ctx(0)
     a.no_cpu_baseline = True
     x = bench.measure_tx(ctx, a)
-    keep = ("value", "sequential_mpps", "device_mpps", "ms_per_ring", "rings", "learned_in_timed_rings")
+    keep = ("value", "pipelined_with_events_mpps", "sequential_mpps", "device_mpps", "ms_per_ring", "rings",
+            "learned_in_timed_rings")
     print(json.dumps({k: x[k] for k in keep if k in x}))
 
 
