@@ -372,6 +372,10 @@ PY
       tail -1 $O/txpipe_$rep.log
     done
     ;;
+  r04aj)
+    # the bench line with c4tx timed without events in its loop
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
