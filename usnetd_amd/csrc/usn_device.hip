@@ -2884,74 +2884,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
     B.tot[bb * USN_SCAN_BLK + tid] = s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid] + s_tot[tid];
 }
 
-/* USN_SCF_SCAN1 (small batches: a tx ring, 1M rx rings): ONE workgroup per
- * (batch, block of 64 bins) over all of the batch's chunks, so no workgroup
- * waits on another (the range scan's look-back over earlier ranges was most
- * of its 5.7 us on a 1M tx ring and 10.7 us on c4's 8 x 1M call):
- *  1. thread (segment sg of 32, lane l of 16) loads the count rows of its
- *     segment's tiles -- ceil(nchunks / 32) chunks, a contiguous run of at
- *     most SCAN1_ROWS rows, bins 4l..4l+3 -- every load in flight together;
- *  2. the 32 segments' totals are scanned in LDS (64 threads, a bin each),
- *     which also gives tot;
- *  3. each thread walks its rows again from registers and writes agg for
- *     its chunks (16-byte stores, 16 lanes = one 256-byte run of a row). */
-#define SCAN1_ROWS 32u
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void scan1_kernel(ScatterArgs s) {
-  static_assert(NTHREADS == 512, "scan1: 32 segments x 16 lanes");
-  __shared__ uint32_t s_t[32][USN_SCAN_BLK];
-  const uint32_t tid = threadIdx.x, l = tid & 15, sg = tid >> 4;
-  const uint32_t bi = blockIdx.x / s.nbb, bb = blockIdx.x - bi * s.nbb;
-  const ScatterBatch &B = s.b[bi];
-  const uint32_t b0 = bb * USN_SCAN_BLK + 4 * l;            // this thread's 4 bins
-  const bool binok = b0 < s.nbw;                           // nbw is a multiple of 8
-  const uint32_t tc = s.tc, lg = __builtin_ctz(tc);        // tc: 1, 2, 4 or 8
-  const uint32_t cps = (B.nchunks + 31) / 32;              // chunks per segment (cps * tc <= SCAN1_ROWS)
-  const uint32_t c0 = sg * cps, t0 = c0 * tc, tn = cps * tc;
-  // 1.
-  uint2 v[SCAN1_ROWS];
-#pragma unroll
-  for (uint32_t k = 0; k < SCAN1_ROWS; ++k) {
-    const uint32_t t = t0 + k;
-    const bool ok = binok && k < tn && t < B.ntiles;
-    v[k] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
-  }
-  uint32_t tot[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (uint32_t k = 0; k < SCAN1_ROWS; ++k) {
-    tot[0] += v[k].x & 0xFFFFu; tot[1] += v[k].x >> 16;
-    tot[2] += v[k].y & 0xFFFFu; tot[3] += v[k].y >> 16;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < 4; ++i) s_t[sg][4 * l + i] = tot[i];
-  __syncthreads();
-  // 2.
-  if (tid < USN_SCAN_BLK) {
-    uint32_t x[32];
-#pragma unroll
-    for (uint32_t k = 0; k < 32; ++k) x[k] = s_t[k][tid];
-    uint32_t run = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 32; ++k) { s_t[k][tid] = run; run += x[k]; }
-    if (bb * USN_SCAN_BLK + tid < s.nbw) B.tot[bb * USN_SCAN_BLK + tid] = run;
-  }
-  __syncthreads();
-  // 3.
-  if (binok) {
-    uint32_t run[4];
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) run[i] = s_t[sg][4 * l + i];
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN1_ROWS; ++k) {
-      const uint32_t c = c0 + (k >> lg);
-      if (k < tn && (k & (tc - 1)) == 0 && c < B.nchunks)
-        *reinterpret_cast<uint4 *>(B.agg + (size_t)c * s.nbw + b0) = make_uint4(run[0], run[1], run[2], run[3]);
-      run[0] += v[k].x & 0xFFFFu; run[1] += v[k].x >> 16;
-      run[2] += v[k].y & 0xFFFFu; run[3] += v[k].y >> 16;
-    }
-  }
-}
-
 /* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
  * of the chunk.
  *  1. each wave loads its tile's decisions at once (16 per lane: segment k
@@ -3295,12 +3227,7 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  if (s.flags & USN_SCF_SCAN1) {
-    if (s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN)) return hipErrorInvalidValue;
-    for (uint32_t k = 0; k < s.count; ++k)   // the plan's condition, checked where it is relied on
-      if (((s.b[k].nchunks + 31) / 32) * s.tc > SCAN1_ROWS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(scan1_kernel, dim3(s.count * s.nbb), dim3(NTHREADS), 0, stream, s);
-  } else if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
+  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
     case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
     case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
     case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;

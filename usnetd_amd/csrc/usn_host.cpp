@@ -1695,12 +1695,9 @@ uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
  *    lists 15.1 -> 11.8 us; a 1M c4 ring, 138 MB, 15.5 -> 33.7 us);
  *  - cpt: 4 chunks per scan thread (a workgroup per 64 chunks) while that
  *    gives >= 256 workgroups, else fewer (profiles/r03/r03i: c5 16M 56.6 /
- *    57.3 / 60.3 us at 4 / 2 / 1; c2 8M 32.1 / 30.4 / 29.4);
- *  - scan1: batches of at most 32 x 32 / tc chunks (1M-frame rings: a tx
- *    ring, c2's and c4's rx rings) take the scan as one workgroup per (batch,
- *    bin block), with no hand-offs between workgroups (scan1_kernel). */
+ *    57.3 / 60.3 us at 4 / 2 / 1; c2 8M 32.1 / 30.4 / 29.4). */
 ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
-                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb, bool scan1_ok) {
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb) {
   ScatterPlan p{};
   const ScatterShape sh = scatter_shape(nbins);
   const uint32_t nbw = (nbins + 7u) & ~7u;
@@ -1729,10 +1726,6 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
   uint32_t cpt = 4;
   while (cpt > 1 && (chunks / (16 * cpt)) * nbb < 256) cpt /= 2;
   p.cpt = cpt_knob ? cpt_knob : cpt;
-  // scan1: every batch's chunks fit 32 segments of at most 32 count rows
-  p.scan1 = scan1_ok && !p.noscan && !p.selfscan && !cpt_knob;
-  for (uint32_t k = 0; k < count && p.scan1; ++k)
-    p.scan1 = ((ntiles[k] + tc - 1) / tc + 31) / 32 * tc <= 32;
   return p;
 }
 
@@ -2101,18 +2094,16 @@ int usn_debug_image_info(usn_ctx *c, uint32_t *out6) {
  * when `refresh` is set */
 /* test hook (tests/test_scatter_plan.py, no GPU): the list plan of a launch
  * of `count` batches of ntiles[k] tiles and nbins bins on `cus` CUs, with the
- * default knobs: out5 = {chunk tiles, scan chunks per thread, noscan,
- * selfscan, scan1} */
+ * default knobs: out4 = {chunk tiles, scan chunks per thread, noscan, selfscan} */
 int usn_debug_scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
-                           uint32_t *out5) {
-  if (!ntiles || !out5 || count == 0 || count > USN_MAX_MULTI || nbins == 0 || nbins > USN_MAX_BINS)
+                           uint32_t *out4) {
+  if (!ntiles || !out4 || count == 0 || count > USN_MAX_MULTI || nbins == 0 || nbins > USN_MAX_BINS)
     return USN_EINVAL;
   const usn::ScatterPlan p = usn::scatter_plan(ntiles, count, nbins, cus, 0, 0, 16384);
-  out5[0] = p.tc;
-  out5[1] = p.cpt;
-  out5[2] = p.noscan ? 1u : 0u;
-  out5[3] = p.selfscan ? 1u : 0u;
-  out5[4] = p.scan1 ? 1u : 0u;
+  out4[0] = p.tc;
+  out4[1] = p.cpt;
+  out4[2] = p.noscan ? 1u : 0u;
+  out4[3] = p.selfscan ? 1u : 0u;
   return USN_OK;
 }
 
@@ -2298,17 +2289,13 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     const char *e = std::getenv("USN_SELFSCAN_KB");
     return e ? (uint32_t)std::atoi(e) : 16384u;
   }();
-  static const bool scan1_ok = [] {   // A/B: USN_SCAN1=0 keeps the range scan for small batches
-    const char *e = std::getenv("USN_SCAN1");
-    return !(e && std::atoi(e) == 0);
-  }();
   const usn::ScatterPlan pl = usn::scatter_plan(ntl, count, x.nbins, (uint32_t)std::max(cus, 1), tc_knob,
-                                                cpt_knob, selfscan_kb, scan1_ok);
+                                                cpt_knob, selfscan_kb);
   const uint32_t tc = pl.tc;
   x.tc = tc;
   static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (pl.noscan ? USN_SCF_NOSCAN : 0u) |
-            (pl.selfscan ? USN_SCF_SELFSCAN : 0u) | (pl.scan1 ? USN_SCF_SCAN1 : 0u);
+            (pl.selfscan ? USN_SCF_SELFSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   x.cpt = pl.cpt;
   x.txs_out = txs_out;

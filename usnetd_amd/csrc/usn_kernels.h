@@ -172,10 +172,7 @@ struct ScatterArgs {
 #define USN_SCF_SELFSCAN 4u    /* a small launch (every chunk resident at once, few count-row
                                   bytes per batch): no scan launch; each chunk sums its batch's
                                   count rows itself (the totals, and the tiles before it) */
-#define USN_SCF_SCAN1 8u       /* small batches (ceil(nchunks / 32) x tc <= 32 count rows per
-                                  segment of 32): the scan as one workgroup per (batch, bin
-                                  block) over all its chunks, no hand-offs (scan1_kernel) */
-#define USN_SCF_SLOW_RANK 1u  /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
+#define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
  * bins: the longest chunk (contiguous runs per bin) whose LDS -- stage
@@ -196,9 +193,9 @@ inline uint32_t scatter_occupancy(size_t lds) {
   return occ > 4 ? 4 : occ;
 }
 /* how a launch's lists are built (usn_host.cpp scatter_plan) */
-struct ScatterPlan { uint32_t tc, cpt; bool noscan, selfscan, scan1; };
+struct ScatterPlan { uint32_t tc, cpt; bool noscan, selfscan; };
 ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins, uint32_t cus,
-                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb, bool scan1_ok = true);
+                         uint32_t tc_knob, uint32_t cpt_knob, uint32_t selfscan_kb);
 /* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
