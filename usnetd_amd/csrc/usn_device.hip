@@ -737,24 +737,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
   return base + inc - v;
 }
 
-/* Two exclusive scans over the block at once (scratch[0..15]): one barrier
- * instead of two per scan.  No barrier after the scratch reads: the caller
- * passes one before scratch is written again. */
-__device__ __forceinline__ void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t *scratch,
-                                                 uint32_t &e0, uint32_t &e1) {
-  static_assert(NTHREADS / 64 <= 8, "scratch[0..15]");
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t i0 = wave_incl_scan(v0, lane), i1 = wave_incl_scan(v1, lane);
-  if (lane == 63) { scratch[wave] = i0; scratch[8 + wave] = i1; }
-  __syncthreads();
-  uint32_t b0 = 0, b1 = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < NTHREADS / 64; ++w)
-    if (w < wave) { b0 += scratch[w]; b1 += scratch[8 + w]; }
-  e0 = b0 + i0 - v0;
-  e1 = b1 + i1 - v1;
-}
-
 /* Largest r (0..ROUNDS-1) among the lanes with `valid`, via one ballot per round. */
 __device__ __forceinline__ uint32_t __reduce_max_rounds(uint32_t r, bool valid) {
   uint32_t m = 0;
@@ -2905,25 +2887,19 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
 /* (chunk of TC <= 8 tiles): one workgroup of 512 threads; wave w owns tile w
  * of the chunk.
  *  1. each wave loads its tile's decisions at once (16 per lane: segment k
- *     of 64 frames is lane + 64k), every wave in flight together, with the
- *     chunk's agg row and the totals;
- *  2. (USN_SC_HIST) each wave ranks its tile's frames with one LDS atomic
- *     each on its own zeroed counters (order: 3. below); the counters end as
- *     the tile's count row, so the scatter does not read the rows the
- *     classify wrote (c5: 33 MB per 16M frames) -- one barrier;
- *  3. per bin: off[b] = bin base (block scan of the totals) + the chunks
+ *     of 64 frames is lane + 64k), every wave in flight together;
+ *  2. per bin: off[b] = bin base (block scan of the totals) + the chunks
  *     before (agg) - b's start in the chunk (block scan of the chunk's
- *     counts, both scans in one), and each wave's cursor cur[w][b] = b's
- *     start in the chunk + b's frames in the chunk's tiles before w; the
- *     scan's sums are checked against the counts (agg of the next chunk =
- *     agg + the chunk's counts; the last chunk's: the totals) -- one barrier;
- *  4. each frame's stage slot = its wave's cursor + its rank: the chunk
- *     sorted by (bin, frame) in LDS -- one barrier;
- *  5. the stage is written out in order: index[off[bin] + q], contiguous
+ *     counts), and each
+ *     wave's cursor cur[w][b] = b's start in the chunk + b's frames in the
+ *     chunk's tiles before w (the classify kernel's count rows) -- one
+ *     barrier;
+ *  3. each wave ranks its tile's frames with one LDS atomic each on its own
+ *     cursors (below): the chunk sorted by (bin, frame) in LDS -- one
+ *     barrier;
+ *  4. the stage is written out in order: index[off[bin] + q], contiguous
  *     runs per bin (one L2 request per run instead of one per frame; c5,
  *     1005 bins: about 8 frames per run), and checked to be stably sorted.
- * (USN_SC_HIST=0: the count rows are loaded in 1., the cursors seeded from
- * them in 3., and the ranking atomics run on the seeded cursors in 4.)
  * Blocks are dealt round-robin over the 8 XCDs; USN_SCATTER_XCD remaps them
  * so that an XCD takes a contiguous run of chunks (cdna_hip_programming.md T1
  * swizzle, bijective). */
@@ -2943,10 +2919,6 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                              (80 VGPRs, a few spilled): c5 scan + scatter 57.5 vs 61.7 us per 16M
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
-#endif
-#ifndef USN_SC_HIST   /* 1: each wave counts its tile's frames per bin in LDS (the ranks come
-                         with the counts) instead of loading the count rows the classify wrote */
-#define USN_SC_HIST 1
 #endif
 template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
                                // registers for the row sums instead of occupancy)
@@ -2984,20 +2956,17 @@ void scatter_kernel(ScatterArgs s) {
   const bool selfscan = SELF && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
   if (selfscan) {   // the sums zeroed before any load is in flight (the barrier waits for none)
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);
-    for (uint32_t i = tid; i < (USN_SC_HIST ? 3u : 2u) * s.nbw; i += NTHREADS) sa[i] = 0;
+    for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
     __syncthreads();
   }
-  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0), vn = make_uint2(0, 0);
+  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
   if (mine && !noscan && !selfscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
-    // (HIST checks: the next chunk's offsets must be this chunk's plus its counts)
-    if (USN_SC_HIST && USN_SC_CHECKS && c + 1 < B.nchunks)
-      vn = *reinterpret_cast<const uint2 *>(ex + s.nbw + 2 * tid);
   }
 #pragma unroll
-  for (uint32_t w = 0; w < TC && !USN_SC_HIST; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
+  for (uint32_t w = 0; w < TC; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
     const uint32_t t = t0 + min(w, ntc - 1);
     rc[w] = mine ? reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw)[tid] : 0u;
     if (w >= ntc) rc[w] = 0;
@@ -3016,12 +2985,10 @@ void scatter_kernel(ScatterArgs s) {
   if (selfscan) {
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals (zeroed above)
     uint32_t *sb = sa + s.nbw;                                                // [nbw] before the chunk
-    uint32_t *so = sb + s.nbw;                     // [nbw] (HIST) the chunk's own tiles: checked
     const uint32_t nq = s.nbw / 8, G = NTHREADS / nq, qq = tid % nq, g = tid / nq;
     if (g < G) {
       const uint4 *rows = reinterpret_cast<const uint4 *>(B.cnt) + qq;   // row t: rows[t * nq]
       uint32_t at[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      uint32_t ao[USN_SC_HIST ? 8 : 1] = {0};
       for (uint32_t t = g; t < B.ntiles; t += 8 * G) {
         uint4 v[8];
 #pragma unroll
@@ -3032,13 +2999,12 @@ void scatter_kernel(ScatterArgs s) {
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
           const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const bool before = t + k * G < t0, own = !before && t + k * G < t0 + ntc;
+          const bool before = t + k * G < t0;
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
             at[2 * j] += lo; at[2 * j + 1] += hi;
             if (before) { ab[2 * j] += lo; ab[2 * j + 1] += hi; }
-            if (USN_SC_HIST && own) { ao[2 * j] += lo; ao[2 * j + 1] += hi; }
           }
         }
       }
@@ -3046,55 +3012,13 @@ void scatter_kernel(ScatterArgs s) {
       for (uint32_t j = 0; j < 8; ++j) {
         if (at[j]) atomicAdd(&sa[8 * qq + j], at[j]);
         if (ab[j]) atomicAdd(&sb[8 * qq + j], ab[j]);
-        if (USN_SC_HIST && ao[j]) atomicAdd(&so[8 * qq + j], ao[j]);
       }
     }
     __syncthreads();
     if (mine) {
       vt = make_uint2(sa[2 * tid], sa[2 * tid + 1]);
       ve = make_uint2(sb[2 * tid], sb[2 * tid + 1]);
-      vn = make_uint2(ve.x + so[2 * tid], ve.y + so[2 * tid + 1]);   // (HIST checks)
     }
-  }
-  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
-  // bad: a decision naming a bin past the batch's bins, a rank past the
-  // chunk, an empty stage slot or a list position past n -- the count rows
-  // and the decisions disagree.  Every access stays in bounds regardless, and
-  // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
-  bool bad = false;
-  // USN_SC_HIST: 1b'. each wave ranks its tile's frames on its own zeroed
-  // counters (one LDS atomic per frame, segment by segment, lanes in lane
-  // order -- see 3.): the returned value is the frame's rank among its tile's
-  // frames of its bin, and the counters end as the tile's count row
-  uint32_t pk[USN_SC_HIST ? SEGS : 1];   // bin << 16 | rank in the tile
-  if (USN_SC_HIST) {
-    uint4 *c4 = reinterpret_cast<uint4 *>(cur);
-    for (uint32_t q4 = tid; q4 < TC * s.nbw / 8; q4 += NTHREADS) c4[q4] = make_uint4(0, 0, 0, 0);
-    if (USN_SC_CHECKS) {   // every stage slot starts empty (checked at the write-out)
-      uint4 *st4 = reinterpret_cast<uint4 *>(stage);
-#pragma unroll
-      for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < SEGS; ++k) pk[k] = 0;
-    if (wave < ntc && USN_ABL_SC != 4) {
-      uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
-#pragma unroll
-      for (uint32_t k = 0; k < SEGS; ++k) {
-        const uint32_t raw = dec_bin(d[k], s.n_ep);
-        const uint32_t b = min(raw, s.nbins - 1u);
-        const uint32_t sh = 16u * (b & 1u);
-        const bool v = k * 64 + lane < tn;
-        const uint32_t r = v ? (atomicAdd(&cw[b >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
-        pk[k] = (b << 16) | r;
-        bad |= v && raw >= s.nbins;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t w = 0; w < TC; ++w)   // the tiles' counts (bins 2 tid, 2 tid + 1): their count rows
-      rc[w] = mine ? reinterpret_cast<const uint32_t *>(cur + (size_t)w * s.nbw)[tid] : 0u;
   }
   // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
@@ -3102,20 +3026,9 @@ void scatter_kernel(ScatterArgs s) {
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
     if (noscan) vt = make_uint2(c0, c1);
-    // HIST: the lists depend on the count rows only through the scan's sums;
-    // those must agree with the decisions (this chunk's counts, just taken)
-    if (USN_SC_HIST && USN_SC_CHECKS && mine && !noscan) {
-      const uint2 want = (selfscan || c + 1 < B.nchunks) ? vn : vt;
-      bad |= want.x != ve.x + c0 || want.y != ve.y + c1;
-    }
-    uint32_t pt, pc;
-    if (USN_SC_HIST) {
-      block_excl_scan2(vt.x + vt.y, c0 + c1, s_scan, pt, pc);   // (barrier 3. is the one after)
-    } else {
-      uint32_t total;
-      pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
-      pc = block_excl_scan(c0 + c1, s_scan, &total);
-    }
+    uint32_t total;
+    const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
+    const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
     if (mine) {
       const uint32_t b = 2 * tid;
       *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
@@ -3139,20 +3052,13 @@ void scatter_kernel(ScatterArgs s) {
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
     uint32_t st = 0, sc = 0;
-    // (HIST: cur holds the tiles' counts until this thread's bins get their seeds)
-    auto cnt_of = [&](uint32_t w, uint32_t b) -> uint32_t {
-      return USN_SC_HIST ? (uint32_t)cur[(size_t)w * s.nbw + b]
-                         : (w < ntc ? (uint32_t)B.cnt[(size_t)(t0 + w) * s.nbw + b] : 0u);
-    };
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
       uint32_t cb = 0;
-      for (uint32_t w = 0; w < ntc; ++w) cb += cnt_of(w, b);
+      for (uint32_t w = 0; w < ntc; ++w) cb += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       sc += cb;
       st += noscan ? cb : B.tot[b];
-      if (USN_SC_HIST && USN_SC_CHECKS && !noscan)
-        bad |= (c + 1 < B.nchunks ? ex[s.nbw + b] : B.tot[b]) != ex[b] + cb;
     }
     uint32_t total;
     uint32_t pt = block_excl_scan(st, s_scan, &total);
@@ -3164,20 +3070,19 @@ void scatter_kernel(ScatterArgs s) {
       if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
       if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
       if (noscan) {
-        for (uint32_t w = 0; w < ntc; ++w) pt += cnt_of(w, b);
+        for (uint32_t w = 0; w < ntc; ++w) pt += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       } else {
         pt += B.tot[b];
       }
       for (uint32_t w = 0; w < TC; ++w) {
-        const uint32_t cw_ = w < ntc ? cnt_of(w, b) : 0u;
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
-        pc += cw_;
+        if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       }
     }
   }
   // every stage slot starts empty: a slot still empty at the write-out means
   // the count rows disagree with the decisions (reported, never hidden)
-  if (USN_SC_CHECKS && !USN_SC_HIST) {
+  if (USN_SC_CHECKS) {
     uint4 *st4 = reinterpret_cast<uint4 *>(stage);
 #pragma unroll
     for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -3200,17 +3105,13 @@ void scatter_kernel(ScatterArgs s) {
   // out of order).  That is not an ISA guarantee, so step 4 verifies the
   // stage and a chunk that is not stably sorted is ranked again the
   // ballot way (5).
-  if (USN_SC_HIST && wave < ntc && USN_ABL_SC != 4) {
-    // the cursors now hold each wave's seeds: slot = seed + rank in the tile
-    const uint16_t *cw = cur + (size_t)wave * s.nbw;
-#pragma unroll
-    for (uint32_t k = 0; k < SEGS; ++k)
-      if (k * 64 + lane < tn) {
-        const uint32_t b = pk[k] >> 16, q = (uint32_t)cw[b] + (pk[k] & 0xFFFFu);
-        bad |= q >= nf;
-        stage[min(q, TC * TILE - 1u)] = (b << 16) | (wave * TILE + k * 64 + lane);
-      }
-  } else if (!USN_SC_HIST && wave < ntc && USN_ABL_SC != 4) {
+  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  // bad: a decision naming a bin past the batch's bins, a rank past the
+  // chunk, an empty stage slot or a list position past n -- the count rows
+  // and the decisions disagree.  Every access stays in bounds regardless, and
+  // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
+  bool bad = false;
+  if (wave < ntc && USN_ABL_SC != 4) {
     uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
     uint32_t at[SEGS];   // (the bins are recomputed below: 16 VGPRs fewer while the atomics fly)
 #pragma unroll
@@ -3282,8 +3183,7 @@ void scatter_kernel(ScatterArgs s) {
     if (wave < ntc) {
       uint16_t *cw = cur + (size_t)wave * s.nbw;
       const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
-      if (!USN_SC_HIST)   // (HIST: the cursors still hold the seeds)
-        for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
+      for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
 #pragma unroll
       for (uint32_t k = 0; k < SEGS; ++k) {
         const uint32_t local = k * 64 + lane;

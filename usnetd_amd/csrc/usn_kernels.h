@@ -177,11 +177,11 @@ struct ScatterArgs {
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
  * bins: the longest chunk (contiguous runs per bin) whose LDS -- stage
  * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 (| self-scan sums
- * nbw x 12: totals, the tiles before the chunk, the chunk's own) -- fits 64 KiB. */
+ * nbw x 8) -- fits 64 KiB. */
 struct ScatterShape { uint32_t tc; size_t lds; };
 inline size_t scatter_lds(uint32_t nbins, uint32_t tc, bool selfscan = false) {
   const size_t nbw = (nbins + 7u) & ~7u;
-  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 + (selfscan ? nbw * 12 : 0);
+  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 + (selfscan ? nbw * 8 : 0);
 }
 inline ScatterShape scatter_shape(uint32_t nbins) {
   for (uint32_t tc : {8u, 4u, 2u})
