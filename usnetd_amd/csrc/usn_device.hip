@@ -1007,16 +1007,6 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 #ifndef USN_PERSIST_CAP
 #define USN_PERSIST_CAP 1
 #endif
-/* USN_PF (A/B, with USN_PERSIST=1, fixed-stride LDS-DMA layouts): once a
- * tile's frames are decided, its workgroup already sends for its NEXT
- * tile's round-0 headers (into the wave's stage, which nothing reads any
- * more) and lengths, so that they fly under the decisions' stores, the
- * histogram, its barrier and the tile header instead of after them. */
-#ifndef USN_PF
-#define USN_PF 0
-#endif
-static_assert(!USN_PF || (USN_PERSIST == 1 && !USN_EARLY_R1 && USN_GLDS_DEPTH == 1),
-              "USN_PF: the persistent loop, one round of stage");
 #if USN_PERSIST && USN_PERSIST_CAP   /* the loop must not cost occupancy: 8 waves per SIMD (<= 64 VGPRs) */
 #define USN_RX_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 #else
@@ -1061,8 +1051,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
   // (one pass when USN_PERSIST is 0: no loop for hipcc to keep values live
   // across, 46 VGPRs instead of 115 at 512 threads)
   const uint32_t ntiles_launch = m.tile_base[m.count];
-  bool pf_done = false;                      // USN_PF: this tile's round 0 and lengths are on their way
-  uint32_t pf_len[USN_PF ? ROUNDS : 1];
   for (uint32_t w = blockIdx.x;; w += gridDim.x) {
     if (USN_PERSIST && w != blockIdx.x) __syncthreads();   // the previous tile is done with the stage and s_misc
 #if USN_PERSIST
@@ -1098,19 +1086,12 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       for (uint32_t r = 0; r < ROUNDS; ++r)
         fp[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
     }
-    if (USN_PF && GLDS && pf_done) {
 #pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = pf_len[USN_PF ? r : 0];
-    } else {
-#pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
-    }
+    for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
     uint4 q[ROUNDS][4];
     if (EARLY) {
       glds_round(a, base, nt, 0, wave, lane, st);
       glds_round(a, base, nt, 1, wave, lane, st1);
-    } else if (USN_PF && GLDS && pf_done) {
-      // round 0 was sent for at the end of the previous tile
     } else if (GLDS) {
 #pragma unroll
       for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
@@ -1444,24 +1425,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     if (tile == 0 && tid == 0) {
       a.summary->flags = s_carry[6];
       if (!(s_carry[6] & USN_S_STALE)) a.summary->first_break = 0xFFFFFFFFu;
-    }
-
-    // ---- USN_PF: the next tile's round 0 and lengths (the stage is read)
-    if (USN_PF && GLDS) {
-      const uint32_t wn = w + gridDim.x;
-      pf_done = wn < ntiles_launch;
-      if (pf_done) {
-        const uint32_t bn = batch_of(m, wn);
-        const ClassifyArgs &an = m.b[bn];
-        const uint64_t nbase = (uint64_t)(wn - m.tile_base[bn]) * TILE;
-        const uint32_t nnt = (uint32_t)min((uint64_t)TILE, an.n - nbase);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (uint32_t r = 0; r < ROUNDS; ++r)
-          pf_len[USN_PF ? r : 0] = an.lens[nbase + min(r * NTHREADS + tid, nnt - 1)];
-        glds_round(an, nbase, nnt, 0, wave, lane, st);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
 
     // ---- decisions out (coalesced), host list, last touching frame
