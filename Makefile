@@ -5,7 +5,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 CSRC := usnetd_amd/csrc
 LIB := usnetd_amd/libusn.so
-OBJS := build/usn_device.o build/usn_device512.o build/usn_device1024.o build/usn_host.o
+OBJS := build/usn_device.o build/usn_device512.o build/usn_host.o
 
 DAEMON := usnetd_amd/bin/usnetd
 
@@ -24,11 +24,6 @@ build/usn_device.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_ke
 build/usn_device512.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 -c -o $@ $<
-
-# (A/B: the classify at 1024 threads per tile, one round per lane; USN_T512=2)
-build/usn_device1024.o: $(CSRC)/usn_device.hip $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
-	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -DUSN_NTHREADS=1024 -DUSN_NS=usn_t1024 -c -o $@ $<
 
 build/usn_host.o: $(CSRC)/usn_host.cpp $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
 	@mkdir -p build
@@ -66,8 +61,7 @@ abl: build/usn_host.o
 	  mkdir -p build/abl/$$name; echo "variant $$name: $$flags"; \
 	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip & \
 	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 $$flags -c -o build/abl/$$name/dev512.o $(CSRC)/usn_device.hip & \
-	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 -DUSN_NTHREADS=1024 -DUSN_NS=usn_t1024 $$flags -c -o build/abl/$$name/dev1024.o $(CSRC)/usn_device.hip & \
 	  wait; \
-	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/abl/$$name/dev512.o build/abl/$$name/dev1024.o build/usn_host.o || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/abl/$$name/dev512.o build/usn_host.o || exit 1; \
 	done < tools/abl_variants.txt
 .PHONY: abl

@@ -287,10 +287,6 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #else
 #define USN_U_WAIT0 "1"   /* round 0's U slot read: round 1's is the one younger load */
 #endif
-#ifndef USN_XSPEC   /* U path: every frame's X slot read goes out with its U slot read (no
-                        second round trip for the projections with several K1 rules) */
-#define USN_XSPEC 0
-#endif
 #ifndef USN_X_BATCH   /* U path: both rounds' X probes in flight together */
 #define USN_X_BATCH 1
 #endif
@@ -1171,20 +1167,8 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       const bool n0 = pr[0].status == 1u;
       du0 = lds_disp1(Dl, a.ph[2], n0, ku0);
       asm_slot1(T, a.ph[2], n0, ku0, du0, su0);
-      // USN_XSPEC: key1 in X too, read with the U slot (X non-empty: uniform)
-      const bool xs = USN_XSPEC && a.ph[3].m != 0u;
-      uint32_t kx0[4], kx1[4];
-      v4u32 sx0, sx1;
-      if (USN_XSPEC) {
-        uint32_t t2[4];
-        rx_keys(pr[0], kx0[0], kx0[1], kx0[2], kx0[3], t2[0], t2[1], t2[2], t2[3]);
-        const PhKeyH kk = ph_hash(a.ph[3], kx0[0], kx0[1], kx0[2], kx0[3]);
-        const uint32_t dx = xs ? lds_disp1(Dl, a.ph[3], n0, kk) : 0u;
-        asm_slot1(T, a.ph[3 - (xs ? 0 : 1)], n0 && xs, kk, dx, sx0);
-      }
       __builtin_amdgcn_sched_barrier(0);
-      if (USN_XSPEC) vm_wait<2>();                                // round 1 landed (U, X younger)
-      else vm_wait<1>();                                          // round 1 landed (1 younger load)
+      vm_wait<1>();                                               // round 1 landed (1 younger load)
       stage_read_asm(st1, lane, q[1]);
       parse(q[1], NTHREADS + tid < nt ? len[1] : 0u, fp[1], a.window, pr[1]);
       const uint32_t e1 = u_key_e(pr[1]);
@@ -1192,36 +1176,16 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       const bool n1 = pr[1].status == 1u;
       du1 = lds_disp1(Dl, a.ph[2], n1, ku1);
       asm_slot1(T, a.ph[2], n1, ku1, du1, su1);
-      if (USN_XSPEC) {
-        uint32_t t2[4];
-        rx_keys(pr[1], kx1[0], kx1[1], kx1[2], kx1[3], t2[0], t2[1], t2[2], t2[3]);
-        const PhKeyH kk = ph_hash(a.ph[3], kx1[0], kx1[1], kx1[2], kx1[3]);
-        const uint32_t dx = xs ? lds_disp1(Dl, a.ph[3], n1, kk) : 0u;
-        asm_slot1(T, a.ph[3 - (xs ? 0 : 1)], n1 && xs, kk, dx, sx1);
-      }
 #if USN_ISA_PERTURB == 1   /* tests/test_isa_waits.py only: a load between issue and wait */
       uint32_t perturb;
       asm volatile("global_load_dword %0, %1, off" : "=v"(perturb) : "v"(a.lens + tid) : "memory");
 #endif
       uint32_t w01, w02, w11, w12;
       bool x0, x1;
-      if (USN_XSPEC) {   // issue order U0, X0, U1, X1
-        asm volatile("s_waitcnt vmcnt(3)" : "+v"(su0) :: "memory");
-        u_decode(su0, pr[0], e0, w01, w02, x0);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(sx0) :: "memory");
-        if (x0 && n0 && xs) w01 = ph_hitv(sx0, kx0[0], kx0[1], kx0[2], kx0[3]);
-        asm volatile("s_waitcnt vmcnt(1)" : "+v"(su1) :: "memory");
-        u_decode(su1, pr[1], e1, w11, w12, x1);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(sx1) :: "memory");
-        if (x1 && n1 && xs) w11 = ph_hitv(sx1, kx1[0], kx1[1], kx1[2], kx1[3]);
-        x0 = x0 && !xs;   // answered (an X-less image never sets MORE)
-        x1 = x1 && !xs;
-      } else {
-        asm volatile("s_waitcnt vmcnt(" USN_U_WAIT0 ")" : "+v"(su0) :: "memory");
-        u_decode(su0, pr[0], e0, w01, w02, x0);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(su1) :: "memory");
-        u_decode(su1, pr[1], e1, w11, w12, x1);
-      }
+      asm volatile("s_waitcnt vmcnt(" USN_U_WAIT0 ")" : "+v"(su0) :: "memory");
+      u_decode(su0, pr[0], e0, w01, w02, x0);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(su1) :: "memory");
+      u_decode(su1, pr[1], e1, w11, w12, x1);
 #if USN_ISA_PERTURB == 1
       if (perturb == 0xFFFFFFFFu) w01 = 0;
 #endif

@@ -455,7 +455,7 @@ constexpr size_t TXSTATE_BYTES = 64;   // a tx batch's gathered state (16 words)
 struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
   uint32_t sel = 0;      // selected replica (usn_replica_select)
-  int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always, 2 the 1024-thread classify
+  int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
   int tx512 = 1;   // USN_TX_T512 env (A/B): the tx kernel at 512 threads per tile (c4tx 1M:
                    // 51.2 vs 53.2 us at 256; two rounds per lane, 64 VGPRs, 4 workgroups per CU)
   double ph_load = USN_PH_LOAD;   // perfect-hash image geometry (env knobs)
@@ -1795,7 +1795,7 @@ int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
   if (!c) return USN_ENOMEM;
   c->reps.swap(reps);
   c->device = hip_devices[0];
-  if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) == 2 ? 2 : std::atoi(e) ? 1 : 0;
+  if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
   if (const char *e = std::getenv("USN_TX_T512")) c->tx512 = std::atoi(e) ? 1 : 0;
   c->ph_load = ph_load_knob();
   c->ph_group = ph_group_knob();
@@ -2571,9 +2571,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         it->second.pending = false;
       }
     }
-    if (c->t512 == 2)   // A/B: 1024 threads per tile
-      HIPCHK(usn_t1024::launch_classify(m, (hipStream_t)stream));
-    else if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
+    if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
       HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
     else
       HIPCHK(usn::launch_classify(m, (hipStream_t)stream));

@@ -206,12 +206,6 @@ uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
 
 }  // namespace usn
 
-/* A/B (USN_T512=2): the classify at 1024 threads per tile (one round per
- * lane), a third compilation of usn_device.hip */
-namespace usn_t1024 {
-hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
-}
-
 /* the same kernels at 512 threads per tile (a second compilation of
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
