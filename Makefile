@@ -9,7 +9,9 @@ OBJS := build/usn_device.o build/usn_device512.o build/usn_host.o
 
 DAEMON := usnetd_amd/bin/usnetd
 
-all: $(LIB) $(DAEMON) oracle
+TESTLIB := build/test/libusn.so
+
+all: $(LIB) $(TESTLIB) $(DAEMON) oracle
 
 # the daemon: plain C++ over the C ABI (links libusn.so; no HIP code of its own)
 $(DAEMON): usnetd_amd/daemon/usnetd.cpp usnetd_amd/daemon/messages.hpp usnetd_amd/daemon/json.hpp include/usn_classify.h $(LIB)
@@ -31,6 +33,16 @@ build/usn_host.o: $(CSRC)/usn_host.cpp $(CSRC)/usn_internal.h $(CSRC)/usn_kernel
 
 $(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+# the test build: the product's device code with a host object that reads the
+# A/B and test knobs of the environment (USN_TEST_HOOKS, usn_host.cpp).  Only
+# tests that force failures and tools/abl.py's variants load it.
+build/test/usn_host.o: $(CSRC)/usn_host.cpp $(CSRC)/usn_internal.h $(CSRC)/usn_kernels.h include/usn_classify.h
+	@mkdir -p build/test
+	$(HIPCC) $(HIPFLAGS) -DUSN_TEST_HOOKS=1 -x hip -c -o $@ $<
+
+$(TESTLIB): build/usn_device.o build/usn_device512.o build/test/usn_host.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -54,7 +66,7 @@ clean:
 # (USN_AB_BUILD=1: the A/B-only knobs that give wrong results are allowed
 # here and nowhere else, usn_device.hip)
 # (ABL_ONLY="v1 v2": only those)
-abl: build/usn_host.o
+abl: build/test/usn_host.o
 	@while read -r name flags; do \
 	  case "$$name" in ''|'#'*) continue;; esac; \
 	  case " $(ABL_ONLY) " in "  ") ;; *" $$name "*) ;; *) continue;; esac; \
@@ -62,6 +74,6 @@ abl: build/usn_host.o
 	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 $$flags -c -o build/abl/$$name/dev.o $(CSRC)/usn_device.hip & \
 	  $(HIPCC) $(HIPFLAGS) -DUSN_AB_BUILD=1 -DUSN_NTHREADS=512 -DUSN_NS=usn_t512 $$flags -c -o build/abl/$$name/dev512.o $(CSRC)/usn_device.hip & \
 	  wait; \
-	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/abl/$$name/dev512.o build/usn_host.o || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -shared -o build/abl/$$name/libusn.so build/abl/$$name/dev.o build/abl/$$name/dev512.o build/test/usn_host.o || exit 1; \
 	done < tools/abl_variants.txt
 .PHONY: abl

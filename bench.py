@@ -566,8 +566,11 @@ def main(argv=None):
     cfg0 = run.cfg0
     run.free()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg0, args.cpu_seconds)
-        out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, args.cpu_seconds)
+        # pinned like configs[0] (/root/reference/eval/Makefile:22
+        # runs the matcher under `taskset -c 6`): one spawned process on one
+        # CPU, and one pinned process per CPU of the job's share
+        out["cpu_baseline"] = cpu_pinned_1core(args.config, args.cpu_seconds, nshard=1 << 20)
+        out["cpu_baseline_ncores"] = cpu_baseline_ncores(args.config, args.cpu_seconds, pin=True)
     del cfg0
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_extra:
         # configs[0], the CPU-only config, in both traffic variants
@@ -593,7 +596,7 @@ def main(argv=None):
                 x = measure(rx, xa, None, 1)
                 x["workload"] = workload(rx, False)
                 if not args.no_cpu_baseline:
-                    x["cpu_baseline"] = cpu_baseline(rx.cfg0, min(args.cpu_seconds, 3.0))
+                    x["cpu_baseline"] = cpu_pinned_1core(name, min(args.cpu_seconds, 3.0))
                 rx.free()
             out[name] = x
     if rank == 0:

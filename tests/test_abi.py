@@ -74,3 +74,44 @@ def test_ab_only_knobs_refused_in_product_builds():
     ok = subprocess.run(base + ["-DUSN_ABL_NOPROBE=1", "-DUSN_AB_BUILD=1"], capture_output=True,
                         text=True)
     assert ok.returncode == 0, ok.stderr[-2000:]
+
+
+KNOBS = [b"USN_DEBUG_CORRUPT", b"USN_SCATTER_SLOW_RANK", b"USN_SCATTER_TC", b"USN_SCAN_CPT",
+         b"USN_SELFSCAN_KB", b"USN_NO_PROJ", b"USN_IMG_FULL", b"USN_PH_LOAD", b"USN_PH_GROUP",
+         b"USN_T512", b"USN_TX_T512", b"USN_PROFILE_HOST"]
+
+
+def test_product_library_reads_no_environment_knob():
+    """the test and A/B hooks (USN_DEBUG_CORRUPT corrupts count
+    rows or decisions; the others move the list plan or the image geometry)
+    are compiled only into the test build (build/test/libusn.so,
+    USN_TEST_HOOKS): the product library holds none of their names and does
+    not call getenv at all; the test build holds every one."""
+    import subprocess
+    from usnetd_amd import lib
+    prod = open(lib.LIB_PATH, "rb").read()
+    test = open(lib.TEST_LIB_PATH, "rb").read()
+    for k in KNOBS:
+        assert k not in prod, k
+        assert k in test, k
+    nm = subprocess.run(["nm", "-D", "--undefined-only", lib.LIB_PATH], capture_output=True, text=True)
+    if nm.returncode == 0:
+        assert not re.search(r"\bgetenv\b", nm.stdout), "the product library imports getenv"
+
+
+def test_result_release_without_gpu():
+    """usn_result_release on a registry-only context: the records of a result
+    are dropped (nothing to release is fine); a null result is refused."""
+    from usnetd_amd import lib
+    L = lib.load()
+    h = ctypes.c_void_p()
+    assert L.usn_ctx_create(-1, ctypes.byref(h)) == 0   # USN_HOST_ONLY
+    n = 4096
+    nbytes = L.usn_result_bytes(n)
+    buf = ctypes.create_string_buffer(nbytes + 256)
+    base = (ctypes.addressof(buf) + 255) & ~255
+    r = lib.Result()
+    assert L.usn_result_bind(base, nbytes, n, ctypes.byref(r)) == 0
+    assert L.usn_result_release(h, ctypes.byref(r)) == 0
+    assert L.usn_result_release(h, None) == -22
+    L.usn_ctx_destroy(h)

@@ -113,7 +113,7 @@ def _oracle_lists(d, n_ep):
     ("c5x", 1 << 20, None)])
 def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     from usnetd_amd import lib, traffic
-    if t512 is not None:   # USN_T512 (read at context creation): force one build
+    if t512 is not None:   # USN_T512 (test build, read at context creation): force one build
         monkeypatch.setenv("USN_T512", t512)
     kw = {}
     if name == "c5-4093":
@@ -122,7 +122,8 @@ def test_config_parity(name, n, t512, coracle_mod, monkeypatch):
     o = coracle_mod.Oracle()
     coracle_mod.install_oracle(o, cfg)
     want = o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
-    ctx = lib.Ctx(0)
+    # the forced build is a test knob: the test library reads it
+    ctx = lib.Ctx(0, libpath=lib.TEST_LIB_PATH) if t512 is not None else lib.Ctx(0)
     traffic.install_ctx(ctx, cfg)
     s = ctx.stream()
     b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)

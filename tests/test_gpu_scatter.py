@@ -9,7 +9,7 @@ order) and verifies that every bin's run of the chunk is in frame order;
 an unsorted chunk is ranked again by bit-sliced ballots.  These tests check
 that the optimistic path is the one taken (no chunk fell back) and that the
 ballot path, forced on every chunk (USN_SCATTER_SLOW_RANK=1, read once per
-process: a subprocess), gives the same lists -- both against the sequential
+process, in the test build: a subprocess), gives the same lists -- both against the sequential
 oracle's decisions sorted stably by bin.  Small launches sum their count rows
 in the scatter itself (self-scan, no scan launch); both ways are checked.
 """
@@ -34,7 +34,7 @@ for name, n in (("c5", 1 << 20), ("c2", 1 << 20), ("c4", 300000)):
     o = coracle.Oracle()
     coracle.install_oracle(o, cfg)
     want = o.forward_batch(cfg.src, cfg.frames, cfg.lens, stride=cfg.stride)
-    ctx = lib.Ctx(0)
+    ctx = lib.Ctx(0, libpath=lib.TEST_LIB_PATH)   # reads USN_SCATTER_SLOW_RANK
     traffic.install_ctx(ctx, cfg)
     s = ctx.stream()
     b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
@@ -168,7 +168,7 @@ sys.path[:0] = [%(root)r]
 from usnetd_amd import lib, traffic
 for name, n in (("c5", 1 << 20), ("c2", 1 << 16), ("c4tx", 1 << 16)):
     cfg = traffic.c4tx(n=n, seed=6) if name == "c4tx" else traffic.config(name, n=n, seed=4242)
-    ctx = lib.Ctx(0)
+    ctx = lib.Ctx(0, libpath=lib.TEST_LIB_PATH)   # the test build: USN_DEBUG_CORRUPT
     traffic.install_ctx(ctx, cfg)
     s = ctx.stream()
     b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)

@@ -115,3 +115,62 @@ def test_c5_full_bench_batch(coracle_mod):
     check_order_vec(r, want, max(e[0] for e in cfg.endpoints) + 1)
     assert ctx.scatter_fallbacks() == 0      # every chunk's optimistic ranks were stable
     ctx.close()
+
+
+def test_c5_headline_launch(coracle_mod):
+    """The bench's headline call itself: c5's two 8M-frame rx
+    rings of two distinct NIC sources, generated as bench.py generates them
+    (shard.queue_seed of queues 0 and 1), classified in ONE
+    usn_classify_multi call -- 16384 tiles, the scan at 512 workgroups (32
+    ranges of 64 chunks x 16 blocks of 64 bins), 2048 scatter chunks of 8
+    tiles that span the boundary between the two batches.  Two poll rounds
+    (the second from the device-carried caches of the first).  Every decision
+    and every per-endpoint list of each ring against the sequential oracle."""
+    import ctypes as C
+    from usnetd_amd import lib, shard, traffic
+    n = 1 << 23
+    cfg0 = traffic.config("c5", n=n, seed=shard.queue_seed(0, 0))
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg0)
+    nics = [cfg0.src] + traffic.extra_nics(cfg0, 1, ctx)
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, cfg0)
+    o.add_endpoint(nics[1], 0, -1)
+    n_ep = max(nics) + 1
+    # the launch shape rocprof shows for the bench (profiles/r04/r04as): the
+    # list plan of two 8192-tile batches at c5's bins
+    L = C.CDLL(lib.LIB_PATH)
+    f = L.usn_debug_scatter_plan
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+    nt = (C.c_uint32 * 2)(n >> 10, n >> 10)
+    out = (C.c_uint32 * 4)()
+    assert f(nt, 2, n_ep + 3, 256, out) == 0
+    tc, cpt = out[0], out[1]
+    assert (tc, cpt, out[2], out[3]) == (8, 4, 0, 0)
+    chunks = 2 * (n >> 10) // tc
+    assert chunks == 2048
+    assert (chunks // (16 * cpt)) * (((n_ep + 3 + 7) // 8 * 8 + 63) // 64) == 512
+    s = ctx.stream()
+    for rnd in range(2):
+        cfgs = [traffic.config("c5", n=n, seed=shard.queue_seed(q, rnd)) for q in range(2)]
+        bs = [lib.DeviceBatch(ctx, c.frames, c.lens, nics[q], stride=c.stride) for q, c in enumerate(cfgs)]
+        rs = [lib.DeviceResult(ctx, n) for _ in cfgs]
+        ba = (lib.Batch * 2)(*[b.desc for b in bs])
+        ra = (lib.Result * 2)(*[r.desc for r in rs])
+        lib.check(ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 2, s))
+        for q, c in enumerate(cfgs):
+            info = ctx.finalize(bs[q], rs[q], s)
+            want = o.forward_batch(nics[q], c.frames, c.lens, stride=c.stride)
+            got = rs[q].decisions()
+            mism = np.nonzero((got & katrun.PARITY_MASK) != (want & katrun.PARITY_MASK))[0]
+            assert mism.size == 0, "round %d ring %d: first mismatches %s" % (rnd, q, mism[:5])
+            assert info.n_host == 0
+            check_order_vec(rs[q], want, n_ep)
+        if rnd == 0:
+            keep = (bs, rs)          # the sources' device chains point at these results
+        else:
+            for x in keep[0] + keep[1]:
+                x.free()
+        del cfgs
+    assert ctx.scatter_fallbacks() == 0
+    ctx.close()

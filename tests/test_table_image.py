@@ -19,8 +19,8 @@ VALID = 1 << 11
 META_MASK = 0x0FFF
 
 
-def _ctx():
-    L = lib.load()
+def _ctx(test_build=False):
+    L = lib.load(lib.TEST_LIB_PATH) if test_build else lib.load()
     h = C.c_void_p()
     assert L.usn_ctx_create(-1, C.byref(h)) == 0
     L.usn_debug_image_probe.restype = C.c_int64
@@ -229,9 +229,10 @@ def test_projection_image_equals_k1_k2(seed):
 
 
 def test_projection_image_off(monkeypatch):
-    """USN_NO_PROJ (A/B): no U is built; the K1 / K2 path answers alone."""
+    """USN_NO_PROJ (A/B, the test build): no U is built; the K1 / K2 path
+    answers alone."""
     monkeypatch.setenv("USN_NO_PROJ", "1")
-    L, h = _ctx()
+    L, h = _ctx(test_build=True)
     L.usn_debug_image_probe_rx.argtypes = [C.c_void_p] + [C.c_uint32] * 6 + [C.c_void_p]
     assert L.usn_endpoint_add(h, 0, 0, -1) == 0
     assert L.usn_endpoint_add(h, 2, 2, 0) == 0

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-5 GPU sessions (each a sequence of tools/gpu.sh steps):
+#   bash tools/r05.sh <session>   output under gpurun_out/<session>/
+set -o pipefail
+S=${1:?session}
+O=gpurun_out/$S
+mkdir -p $O
+export TMPDIR=/tmp
+sq_pass() {   # sq_pass NAME "COUNTERS" CMD...: one rocprofv3 --pmc pass (<= 8 SQ counters)
+  local name=$1 ctr=$2; shift 2
+  rm -rf $O/$name
+  timeout -k 10 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $O/$name -o run -- "$@" \
+    > $O/$name.log 2>&1 || { echo "pmc pass $name failed rc=$?"; exit 1; }
+}
+case $S in
+  r05a)
+    # first session of the round: the whole GPU suite (with the headline
+    # launch's parity test), smoke, the driver's bench, and the c5
+    # classify's instruction mix and wave cycles (SQ counters, two passes)
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    timeout -k 10 60 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
+    sq_pass sq1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+      python3 tools/kbench.py c5 8388608 12
+    sq_pass sq2 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+      python3 tools/kbench.py c5 8388608 12
+    python3 tools/pmc_summary.py $O/sq1 $O/sq2 > $O/sq_summary.txt 2>&1 || true
+    ;;
+  *) echo "unknown session $S"; exit 2 ;;
+esac
+echo "== session $S done"

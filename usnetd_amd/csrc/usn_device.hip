@@ -122,10 +122,6 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #define USN_ABL_TXNOPROBE 0
 #endif
 
-#ifndef USN_LOAD_NT
-#define USN_LOAD_NT 0
-#endif
-
 #ifndef USN_ABL_NOPROBE   /* A/B only: no rule-table probes (wrong results) */
 #define USN_ABL_NOPROBE 0
 #endif
@@ -153,15 +149,9 @@ static_assert(USN_AB_BUILD || !(USN_ABL_NOTAGS || USN_ABL_TXNOPROBE || USN_ABL_N
                                 USN_ISA_PERTURB),
               "an A/B-only knob (wrong results) in a build without USN_AB_BUILD=1");
 
-/* 16-byte header load (`nt` streaming hint only when USN_LOAD_NT) */
-__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
-#if USN_LOAD_NT
-  const v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
-}
+/* 16-byte header load, default cache policy (the `nt` hint was slower on
+ * these per-lane loads: c3 and the tx kernel, profiles/r02cp, r04/r04at) */
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p) { return *p; }
 
 __device__ __forceinline__ uint32_t be16lo(uint32_t v) {  // bytes [0,1] of v as big-endian u16
   return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
@@ -274,9 +264,6 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #ifndef USN_LATE_DMA
 #define USN_LATE_DMA 1
 #endif
-#ifndef USN_BATCH2
-#define USN_BATCH2 1
-#endif
 /* tests/test_isa_waits.py builds perturbed variants to show its check fails:
  * 1 = an extra load between a slot read and its wait, 2 = a stale count */
 #ifndef USN_ISA_PERTURB
@@ -286,9 +273,6 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #define USN_U_WAIT0 "2"
 #else
 #define USN_U_WAIT0 "1"   /* round 0's U slot read: round 1's is the one younger load */
-#endif
-#ifndef USN_X_BATCH   /* U path: both rounds' X probes in flight together */
-#define USN_X_BATCH 1
 #endif
 #ifndef USN_SEQ_K2    /* key2's slot read only where key1 missed (get_endpoint's order) */
 #define USN_SEQ_K2 1
@@ -397,24 +381,12 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
 }
 
-#ifndef USN_SLOT_POLK   /* A/B only: cache-policy bits of the slot reads: 1 sc0, 2 nt, 3 sc1 */
-#define USN_SLOT_POLK 0
-#endif
-#if USN_SLOT_POLK == 1
-#define USN_SLOT_POL " sc0"
-#elif USN_SLOT_POLK == 2
-#define USN_SLOT_POL " nt"
-#elif USN_SLOT_POLK == 3
-#define USN_SLOT_POL " sc1"
-#else
-#define USN_SLOT_POL ""
-#endif
 /* one slot read of table t; a lane that does not need it reads the table's
  * first slot, which every such lane of the wave shares: one L2 request */
 __device__ __forceinline__ void asm_slot1(const uint4 *T, const usn_ph_table &t, bool need,
                                           const PhKeyH &k, uint32_t d, v4u32 &s) {
   const uint4 *p = T + t.slot_off + (need && !USN_ABL_ULINE ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
-  asm volatile("global_load_dwordx4 %0, %1, off" USN_SLOT_POL : "=&v"(s) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(s) : "v"(p) : "memory");
 }
 
 /* TM_DISPLDS: both displacements from the LDS copy (indexed like the image) */
@@ -893,13 +865,6 @@ __device__ __forceinline__ uint32_t stage_slot(uint32_t f, uint32_t j) {
 #endif
 #define GD USN_GLDS_DEPTH
 #define NWAVES (NTHREADS / 64)
-#ifndef USN_EARLY_R1   /* A/B: both rounds' header DMA at the workgroup's start (two 2 KiB
-                          stages per wave; the two-round batched paths of a global or
-                          displacement-LDS image), an LDS-only barrier before the parse */
-#define USN_EARLY_R1 0
-#endif
-#define STAGE_R_SLOTS (64u * GLDS_PARTS)   /* one round's parts per wave (USN_EARLY_R1) */
-static_assert(!USN_EARLY_R1 || USN_STAGE32, "USN_EARLY_R1: two-part stage");
 #ifndef GLDS_NT                  /* aux bits of the header glds: non-temporal */
 #define GLDS_NT 2
 #endif
@@ -1001,34 +966,20 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
 }
 
 /* The 1024-frame tiles of a launch (several batches = drained rx rings may
- * share one launch), one workgroup each.  USN_PERSIST=k > 1 (A/B only): k
- * tiles per workgroup, strided by the grid.  USN_PERSIST=1 (A/B only): the grid
- * is what the chip holds at once and each workgroup loops over tiles
- * blockIdx.x, + gridDim.x, ..., copying the rule image (or its displacements)
- * to LDS once instead of once per tile -- slower: c5 8M 185.5 vs 170.5 us, c4
- * 175.8 vs 160.9 (profiles/r02ah; the workgroups then run their phases in
- * step, the header streams of all of them at once). */
-#ifndef USN_PERSIST
-#define USN_PERSIST 0
-#endif
-#ifndef USN_PERSIST_CAP
-#define USN_PERSIST_CAP 1
-#endif
-#if USN_PERSIST && USN_PERSIST_CAP   /* the loop must not cost occupancy: 8 waves per SIMD (<= 64 VGPRs) */
-#define USN_RX_ATTR __attribute__((amdgpu_waves_per_eu(8)))
-#else
-#define USN_RX_ATTR
-#endif
+ * share one launch), one workgroup each.  (A persistent grid looping over
+ * tiles, copying the displacements once per workgroup, was slower in rounds
+ * 2 and 4: c5 8M 185.5 vs 170.5 us, profiles/r02ah; with the next tile's
+ * headers prefetched 175.4 vs 159.1, profiles/r04/r04ao.  Both rounds' header
+ * DMA at the workgroup's start was a wash, r04l.) */
 template <int TM, bool GLDS>
-__global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(MultiArgs m) {
+__global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
   constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
   // both rounds' probes batched (two rounds per lane, global image)
-  constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1 && USN_BATCH2 &&
+  constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1 &&
                           !USN_ABL_LOADONLY && !USN_ABL_NOPROBE;
-  constexpr bool EARLY = BATCH2 && USN_EARLY_R1;
-  constexpr uint32_t WSTAGE = EARLY ? 2 * STAGE_R_SLOTS : GD * STAGE_ROUND_SLOTS;   // per wave
+  constexpr uint32_t WSTAGE = GD * STAGE_ROUND_SLOTS;   // per wave
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * WSTAGE : 1];
   __shared__ uint32_t s_carry[8];
@@ -1054,22 +1005,10 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     if (TM == TM_LDS) T = L.table;
     else Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)u0 * 8;
   }
-  // (the first tile's barrier also waits for the image copy)
-  // (one pass when USN_PERSIST is 0: no loop for hipcc to keep values live
-  // across, 46 VGPRs instead of 115 at 512 threads)
-  const uint32_t ntiles_launch = m.tile_base[m.count];
-  for (uint32_t w = blockIdx.x;; w += gridDim.x) {
-    if (USN_PERSIST && w != blockIdx.x) __syncthreads();   // the previous tile is done with the stage and s_misc
-#if USN_PERSIST
-    // per-lane values recomputed for every tile (kept live across the loop
-    // they cost VGPRs: the lane, its stage and LDS addresses)
-    uint32_t tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));
-    const uint32_t lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint4 *st = s_stage + (GLDS ? wave * WSTAGE : 0);
-#endif
-    uint4 *const st1 = EARLY ? st + STAGE_R_SLOTS : st;   // round 1's stage
+  // (the tile's first barrier also waits for the image copy)
+  {
+    const uint32_t w = blockIdx.x;
+    uint4 *const st1 = st;   // round 1's stage: round 0's, once its reads are done
     const uint32_t bi = batch_of(m, w);
     const ClassifyArgs &a = m.b[bi];
     const uint32_t tile = w - m.tile_base[bi];
@@ -1096,10 +1035,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
     uint4 q[ROUNDS][4];
-    if (EARLY) {
-      glds_round(a, base, nt, 0, wave, lane, st);
-      glds_round(a, base, nt, 1, wave, lane, st1);
-    } else if (GLDS) {
+    if (GLDS) {
 #pragma unroll
       for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
         glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
@@ -1111,14 +1047,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     //      for every load: table and round 0 are in LDS / registers after it)
     hist_zero(L.hist, a.nbw);
     if (tid < 8) s_misc[tid] = 0;
-    if (EARLY) {   // round 1's parts may still fly: an LDS-only barrier after this wave's image copy and round 0
-      vm_wait<GLDS_PARTS>();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
     STAMP(2);
 
     // ---- carried-in cache (block 0): stale check against the current table
@@ -1159,7 +1088,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t du0, du1;
       v4u32 su0, su1;
       stage_read_asm(sb, lane, q[0]);
-      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       const uint32_t e0 = u_key_e(pr[0]);
@@ -1193,13 +1122,8 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       x1 = x1 && n1;
       STAMP(4);
       if (!USN_ABL_NOX && __ballot(x0 || x1)) {
-        uint32_t wx0, wx1;
-        if (USN_X_BATCH) {
-          x_probe2(T, Dl, a, pr[0], x0, pr[1], x1, wx0, wx1);
-        } else {   // A/B: one round after the other
-          wx0 = x_probe(T, Dl, a, pr[0], x0);
-          wx1 = x_probe(T, Dl, a, pr[1], x1);
-        }
+        uint32_t wx0, wx1;   // both rounds' X reads in flight together
+        x_probe2(T, Dl, a, pr[0], x0, pr[1], x1, wx0, wx1);
         if (x0) w01 = wx0;
         if (x1) w11 = wx1;
       }
@@ -1217,7 +1141,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
@@ -1254,7 +1178,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
@@ -1282,7 +1206,7 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
       uint32_t d01, d02, d11, d12;
       v4u32 s01, s02, s11, s12;
       stage_read_asm(sb, lane, q[0]);
-      if (!EARLY) glds_round(a, base, nt, 1, wave, lane, sb);     // round 1's headers
+      glds_round(a, base, nt, 1, wave, lane, sb);                 // round 1's headers
       __builtin_amdgcn_sched_barrier(0);
       parse(q[0], tid < nt ? len[0] : 0u, fp[0], a.window, pr[0]);
       round_keys(a, pr[0], k0);
@@ -1494,7 +1418,6 @@ __global__ __launch_bounds__(NTHREADS) USN_RX_ATTR void classify_rx_kernel(Multi
     }
     STAMP(11);
     STAMP_FLUSH_AT(w);
-    if (!USN_PERSIST || w + gridDim.x >= ntiles_launch) break;
   }
 }
 
@@ -2666,28 +2589,6 @@ static bool glds_layout(const MultiArgs &m) {
   return true;
 }
 
-/* USN_PERSIST: workgroups of kernel `fn` the device holds at once (its CUs x
- * the occupancy at `lds` bytes of dynamic LDS), cached per device and kernel */
-template <typename K>
-static uint32_t resident_grid(K fn, size_t lds) {
-  struct Entry { int dev; const void *fn; size_t lds; uint32_t blocks; };
-  thread_local Entry cache[16];
-  thread_local int used = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  for (int k = 0; k < used; ++k)
-    if (cache[k].dev == dev && cache[k].fn == reinterpret_cast<const void *>(fn) && cache[k].lds == lds)
-      return cache[k].blocks;
-  int cus = 0, per_cu = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHREADS, lds) != hipSuccess)
-    return 0;
-  const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 0) * (uint32_t)(per_cu > 0 ? per_cu : 0);
-  cache[used % 16] = Entry{dev, reinterpret_cast<const void *>(fn), lds, blocks};
-  if (used < 16) ++used;
-  return blocks;
-}
-
 hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
@@ -2698,18 +2599,8 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
                      (tm == TM_LDS ? table_lds_bytes(a.table_units)
                       : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
   const dim3 b(NTHREADS);
-  // a grid of at most what the chip holds (0 = the query failed: one per tile)
-#define USN_LAUNCH(T_, G_)                                                              \
-  do {                                                                                  \
-    uint32_t grid = tiles;                                                              \
-    if (USN_PERSIST == 1) {                                                             \
-      const uint32_t res = resident_grid(classify_rx_kernel<T_, G_>, lds);              \
-      if (res) grid = min(grid, res);                                                   \
-    } else if (USN_PERSIST > 1) {                                                       \
-      grid = (tiles + USN_PERSIST - 1) / USN_PERSIST;                                   \
-    }                                                                                   \
-    hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(grid), b, lds, stream, m);    \
-  } while (0)
+#define USN_LAUNCH(T_, G_) \
+  hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(tiles), b, lds, stream, m)
   if (tm == TM_LDS) { if (glds) USN_LAUNCH(TM_LDS, true); else USN_LAUNCH(TM_LDS, false); }
   else if (tm == TM_DISPLDS) { if (glds) USN_LAUNCH(TM_DISPLDS, true); else USN_LAUNCH(TM_DISPLDS, false); }
   else { if (glds) USN_LAUNCH(TM_GLOBAL, true); else USN_LAUNCH(TM_GLOBAL, false); }
@@ -2915,9 +2806,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
 #endif
 /* chunks that took step 5 (usn_debug_scatter_fallbacks) */
 __device__ uint32_t usn_scatter_fallbacks = 0;
-#ifndef USN_SC_GROUP   /* A/B: 0 = the write-out one entry per thread and pass */
-#define USN_SC_GROUP 1
-#endif
 #ifndef USN_SC_CHECKS   /* A/B only: 0 = no empty-slot sentinel and no inconsistency report
                            (the bounds clamps stay) */
 #define USN_SC_CHECKS 1
@@ -3145,7 +3033,7 @@ void scatter_kernel(ScatterArgs s) {
   // write past index), checking that each bin's run is in frame order
   bool unsorted = false;
   uint32_t q0 = 0;
-  if (USN_ABL_SC != 4 && USN_SC_GROUP) {
+  if (USN_ABL_SC != 4) {
     // groups of 8 entries per thread: every stage read of the group, then
     // every offset read, then the stores (the LDS round trips overlap)
     constexpr uint32_t G = 8;

@@ -385,6 +385,22 @@ struct Ep {
 };
 
 /* carried decision cache of one source endpoint */
+/* A/B and test knobs from the environment are read only by the test build
+ * (USN_TEST_HOOKS=1: build/test/libusn.so, which tools/abl.py's variants
+ * and the tests that force failures load).  The product library reads no
+ * environment variable: test_knob is nullptr there for every name. */
+#ifndef USN_TEST_HOOKS
+#define USN_TEST_HOOKS 0
+#endif
+static const char *test_knob(const char *name) {
+#if USN_TEST_HOOKS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 struct Chain {
   bool device_chain = false;        // previous result on the device is authoritative
   uint32_t replica = 0;             // where the source's last batch was classified
@@ -478,14 +494,14 @@ struct usn_ctx {
   uint32_t img_base = 0;       // units of the K1/K2 part; U and X follow
   uint32_t img_udisp = 0;      // first unit of U's and X's displacements
   uint32_t probe_mask = 0;   // tables holding rules (ClassifyArgs::probe_mask)
-  bool proj = std::getenv("USN_NO_PROJ") == nullptr;   // A/B: build U and X
+  bool proj = test_knob("USN_NO_PROJ") == nullptr;   // A/B: build U and X
   /* incremental image updates between full builds (AddMatch / RemoveMatch /
    * a few learned rules): the registry keys changed since the image was last
    * brought up to date, each table's displacement groups (slot indices from
    * the table's first slot; built on first use after a full build), its
    * keys, and the 16-byte units patched since the last full build, with the
    * image version that patched them (what a replica uploads) */
-  bool incremental = std::getenv("USN_IMG_FULL") == nullptr;   // A/B: every change rebuilds
+  bool incremental = test_knob("USN_IMG_FULL") == nullptr;   // A/B: every change rebuilds
   std::vector<WantKey> img_delta;
   bool img_groups_ok = false;
   std::vector<std::vector<uint32_t>> img_groups[4];
@@ -599,9 +615,9 @@ void rule_insert(usn_ctx *c, const WantKey &k, Rule r) {
   note_change(c, k);
 }
 
-/* USN_PROFILE_HOST=1: per-stage wall times of the host stages on stderr */
+/* USN_PROFILE_HOST=1 (test build): per-stage wall times of the host stages on stderr */
 struct StageClock {
-  bool on = std::getenv("USN_PROFILE_HOST") != nullptr;
+  bool on = test_knob("USN_PROFILE_HOST") != nullptr;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   const char *name;
   explicit StageClock(const char *n) : name(n) {}
@@ -625,12 +641,12 @@ void prefetch_rule(const usn_ctx *c, const WantKey &k) { c->rules.prefetch(k); }
 /* A/B knobs, read at context creation: USN_PH_LOAD (slot load), USN_PH_GROUP
  * (keys per displacement) */
 double ph_load_knob() {
-  const char *e = std::getenv("USN_PH_LOAD");
+  const char *e = test_knob("USN_PH_LOAD");
   const double v = e ? std::atof(e) : USN_PH_LOAD;
   return v > 0.05 && v < 0.99 ? v : USN_PH_LOAD;
 }
 uint32_t ph_group_knob() {
-  const char *e = std::getenv("USN_PH_GROUP");
+  const char *e = test_knob("USN_PH_GROUP");
   const int v = e ? std::atoi(e) : USN_PH_GROUP;
   return v >= 1 && v <= 32 ? (uint32_t)v : USN_PH_GROUP;
 }
@@ -1316,7 +1332,7 @@ int refresh_image(usn_ctx *c) {
       c->img_patches.size() > IMG_MAX_PATCHES)
     return build_image(c);
   if (!c->img_groups_ok) img_groups_build(c);
-  static const bool verbose = std::getenv("USN_PROFILE_HOST") != nullptr;
+  static const bool verbose = test_knob("USN_PROFILE_HOST") != nullptr;
   for (const WantKey &k : c->img_delta)
     if (!img_apply_key(c, k)) {
       if (verbose)
@@ -1660,9 +1676,13 @@ static ScatterGeom scatter_geom(uint64_t n, uint32_t nbins) {
   return g;
 }
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins) { return scatter_geom(n, nbins).total; }
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
+/* the scratch's layout follows the result's capacity (cap = usn_result.n),
+ * not the batch's frames: a result keeps one geometry per bin count however
+ * its batches vary (the granules are zeroed once per bind and bin count) */
+void scatter_carve(void *scratch, uint64_t cap, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
                    ScatterBatch &sb, uint16_t **cnt) {
-  const ScatterGeom g = scatter_geom(n, nbins);
+  const ScatterGeom g = scatter_geom(cap, nbins);
+  const uint32_t ntiles = (uint32_t)((n + USN_TILE - 1) / USN_TILE);
   uint8_t *p = static_cast<uint8_t *>(scratch);
   *cnt = reinterpret_cast<uint16_t *>(p + g.cnt);
   sb.cnt = *cnt;
@@ -1671,14 +1691,14 @@ void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint3
   sb.gran = reinterpret_cast<unsigned long long *>(p + g.gran);
   sb.diag = reinterpret_cast<uint32_t *>(p + g.diag);
   sb.n = (uint32_t)n;
-  sb.ntiles = g.ntiles;
+  sb.ntiles = ntiles;
   sb.tc = tc;
-  sb.nchunks = (g.ntiles + tc - 1) / tc;
+  sb.nchunks = (ntiles + tc - 1) / tc;
   sb.nranges = (sb.nchunks + 16 * cpt - 1) / (16 * cpt);
 }
 /* the scan's diag word of a batch's scratch (bit 0: a wait timed out) */
-uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins) {
-  return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(n, nbins).diag);
+uint32_t *scatter_diag(void *scratch, uint64_t cap, uint32_t nbins) {
+  return reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + scatter_geom(cap, nbins).diag);
 }
 /* How a launch's lists are built (launch_scatter): chunk length, scan
  * threads' chunks, and whether the scan launch is skipped.
@@ -1731,8 +1751,8 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
 
 /* the granule and diag part of a batch's scratch (zeroed on its first use
  * with this geometry) */
-void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes) {
-  const ScatterGeom g = scatter_geom(n, nbins);
+void scatter_tail(void *scratch, uint64_t cap, uint32_t nbins, void **p, size_t *bytes) {
+  const ScatterGeom g = scatter_geom(cap, nbins);
   *p = static_cast<uint8_t *>(scratch) + g.gran;
   *bytes = g.total - g.gran;
 }
@@ -1795,8 +1815,8 @@ int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
   if (!c) return USN_ENOMEM;
   c->reps.swap(reps);
   c->device = hip_devices[0];
-  if (const char *e = std::getenv("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
-  if (const char *e = std::getenv("USN_TX_T512")) c->tx512 = std::atoi(e) ? 1 : 0;
+  if (const char *e = test_knob("USN_T512")) c->t512 = std::atoi(e) ? 1 : 0;
+  if (const char *e = test_knob("USN_TX_T512")) c->tx512 = std::atoi(e) ? 1 : 0;
   c->ph_load = ph_load_knob();
   c->ph_group = ph_group_knob();
   *out = c;
@@ -2207,7 +2227,7 @@ static void set_bins(const usn_result *r, uint64_t n, uint32_t nbins, usn::Class
   a.nbits = 1;
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, n, nbins, 1, 1, sb, &a.cnt);
+  usn::scatter_carve(r->scratch, r->n, n, nbins, 1, 1, sb, &a.cnt);
   a.nbw = (nbins + 7u) & ~7u;
 }
 
@@ -2244,7 +2264,7 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
   while ((1u << a.nbits) < a.nbins) ++a.nbits;
   a.probe_mask = c->probe_mask;
   usn::ScatterBatch sb;
-  usn::scatter_carve(r->scratch, b->n, a.nbins, 1, 1, sb, &a.cnt);
+  usn::scatter_carve(r->scratch, r->n, b->n, a.nbins, 1, 1, sb, &a.cnt);
   a.nbw = (a.nbins + 7u) & ~7u;
   return USN_OK;
 }
@@ -2276,24 +2296,24 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     }
   }
   static const uint32_t tc_knob = [] {   // A/B: USN_SCATTER_TC=1|2|4|8 (at most the shape's)
-    const char *e = std::getenv("USN_SCATTER_TC");
+    const char *e = test_knob("USN_SCATTER_TC");
     const int v = e ? std::atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4 || v == 8) ? (uint32_t)v : 0u;
   }();
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
-    const char *e = std::getenv("USN_SCAN_CPT");
+    const char *e = test_knob("USN_SCAN_CPT");
     const int v = e ? std::atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4) ? (uint32_t)v : 0u;
   }();
   static const uint32_t selfscan_kb = [] {   // A/B: USN_SELFSCAN_KB (row KiB all chunks read; 0 off)
-    const char *e = std::getenv("USN_SELFSCAN_KB");
+    const char *e = test_knob("USN_SELFSCAN_KB");
     return e ? (uint32_t)std::atoi(e) : 16384u;
   }();
   const usn::ScatterPlan pl = usn::scatter_plan(ntl, count, x.nbins, (uint32_t)std::max(cus, 1), tc_knob,
                                                 cpt_knob, selfscan_kb);
   const uint32_t tc = pl.tc;
   x.tc = tc;
-  static const bool slow_rank = std::getenv("USN_SCATTER_SLOW_RANK") != nullptr;
+  static const bool slow_rank = test_knob("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (pl.noscan ? USN_SCF_NOSCAN : 0u) |
             (pl.selfscan ? USN_SCF_SELFSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
@@ -2306,7 +2326,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
-    usn::scatter_carve(r[k].scratch, as[k].n, x.nbins, tc, x.cpt, sb, &cnt);
+    usn::scatter_carve(r[k].scratch, r[k].n, as[k].n, x.nbins, tc, x.cpt, sb, &cnt);
     sb.decisions = r[k].decisions;
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;
@@ -2314,27 +2334,29 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     x.range_base[k + 1] = x.range_base[k] + sb.nranges;
     // granules of a scratch never used before may hold anything: zero them
     // after every bind, and again when the geometry moves them (their place
-    // depends on the batch's frames and bins)
-    const uint64_t geo = (as[k].n << 16) ^ x.nbins;
+    // depends on the result's capacity and the bins)
+    const uint64_t geo = (r[k].n << 16) ^ x.nbins;
     auto zi = c->scan_zeroed.find(r[k].scratch);
     if (zi == c->scan_zeroed.end() || zi->second.tag != r[k].bind_tag || zi->second.geo != geo) {
       c->scan_zeroed[r[k].scratch] = usn_ctx::Zeroed{r[k].bind_tag, geo};
       void *p;
       size_t bytes;
-      usn::scatter_tail(r[k].scratch, as[k].n, x.nbins, &p, &bytes);
+      usn::scatter_tail(r[k].scratch, r[k].n, x.nbins, &p, &bytes);
       HIPCHK(hipMemsetAsync(p, 0, bytes, s));
     }
   }
-  // test hook (tests/test_gpu_scatter.py, read once per process):
-  // USN_DEBUG_CORRUPT=1 adds 257 to bin 0 of batch 0's first count row, =2
-  // makes frame 0's decision name endpoint 0x0FF0 (past every batch's bins);
-  // the scatter must report either (usn_finalize: USN_ELIST)
+#if USN_TEST_HOOKS
+  // test hook (tests/test_gpu_scatter.py, the test build only, read once per
+  // process): USN_DEBUG_CORRUPT=1 sets bin 0 of batch 0's first count row to
+  // 257, =2 makes frame 0's decision name endpoint 0x0FF0 (past every
+  // batch's bins); the scatter must report either (usn_finalize: USN_ELIST)
   static const int corrupt = [] {
-    const char *e = std::getenv("USN_DEBUG_CORRUPT");
+    const char *e = test_knob("USN_DEBUG_CORRUPT");
     return e ? std::atoi(e) : 0;
   }();
   if (corrupt == 1) HIPCHK(hipMemsetAsync(const_cast<uint16_t *>(x.b[0].cnt), 0x01, 2, s));
   if (corrupt == 2) HIPCHK(hipMemsetD32Async(r[0].decisions, (int)((1u << 16) | 0x0FF0u), 1, s));
+#endif
   HIPCHK(usn_t512::launch_scatter(x, s));
   return USN_OK;
 }
@@ -2471,6 +2493,32 @@ static int chain_to_host(usn_ctx *c, Chain &ch) {
   ch.state = st;
   ch.dst = dst;
   std::memcpy(ch.info, info, 16);
+  return USN_OK;
+}
+
+int usn_result_release(usn_ctx *c, const usn_result *r) {
+  if (!c || !r || !r->decisions) return USN_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  for (const usn_ctx::Tx &t : c->txq)
+    if (t.decisions == r->decisions) return USN_EBUSY;
+  for (Chain &ch : c->chains)   // a carried cache read from this result's tile headers
+    if (ch.device_chain && ch.summary == r->summary) {
+      const int s = chain_to_host(c, ch);
+      if (s) return s;
+    }
+  c->batch_rep.erase(r->decisions);
+  const auto le = c->lists_ev.find(r->decisions);
+  if (le != c->lists_ev.end()) {
+    if (le->second.ev) {
+      HIPCHK(hipSetDevice(le->second.device));
+      HIPCHK(hipEventSynchronize(le->second.ev));   // the lists may still be built into r
+      HIPCHK(hipEventDestroy(le->second.ev));
+    }
+    c->lists_ev.erase(le);
+  }
+  c->scan_zeroed.erase(r->scratch);
+  for (const void *&t : c->txstate_for)
+    if (t == r->decisions) t = nullptr;
   return USN_OK;
 }
 
@@ -2892,7 +2940,9 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
                        usn_finalize_info *info, const usn_ctx::Tx &txp, bool redo, bool *changed) {
   StageClock clk("finalize_tx");
   *changed = false;
-  // the previous batch's carried-out cache (its host tail), for a redo of this one
+  // the previous batch's carried-out cache (its host tail), for a redo of this
+  // one.  Consumed here: every return below pops the batch (usn_finalize),
+  // except USN_EAGAIN_READER, which puts it back
   const bool cout_in = c->tx_cout_valid;
   uint32_t cin_redo[6];
   std::memcpy(cin_redo, c->tx_cout, sizeof cin_redo);
@@ -2914,7 +2964,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
         reinterpret_cast<const volatile uint32_t *>(c->h_txstate + txp.slot * TXSTATE_BYTES);
     uint32_t v[12];
     for (int k = 0; k < 12; ++k) v[k] = q[k];
-    { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, n, c->n_ep + 3), s); if (e) return e; }
+    { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, r->n, c->n_ep + 3), s); if (e) return e; }
     if (!redo && v[1] == 0 && v[2] == 0 && v[4] != txp.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
       // results are final; class totals from bin_off (EP bins, NIC, FLOOD, DROP)
@@ -2931,7 +2981,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   }
   {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, cnt, X.counters,
-                                    usn::scatter_diag(r->scratch, n, c->n_ep + 3));
+                                    usn::scatter_diag(r->scratch, r->n, c->n_ep + 3));
     if (e) return e;
   }
   // a tile wait of the kernel timed out (counters[3] = this epoch), or the
@@ -2955,7 +3005,10 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   HostView hv{c, b, r, s, {}, {}, false, false};
   st = hv.fetch_dec();
   if (st) return st;
-  if (!c->reader && needs_reader(hv.dec, hosts)) return USN_EAGAIN_READER;   // before any side effect
+  if (!c->reader && needs_reader(hv.dec, hosts)) {   // before any side effect: the batch stays
+    c->tx_cout_valid = cout_in;                      // pending, and its retry redoes it from
+    return USN_EAGAIN_READER;                        // the same carried cache
+  }
   clk.mark("decisions");
   uint64_t h = n;
   if (cnt[1]) h = 0;
@@ -3149,7 +3202,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     std::memcpy(o.cout_info, cs.info.w, 16);
     HIPCHK(hipMemcpy(r->summary, &o, sizeof o, hipMemcpyHostToDevice));
     HIPCHK(hipStreamSynchronize(s));
-    st = lists_check(usn::scatter_diag(r->scratch, n, c->n_ep + 3), s);
+    st = lists_check(usn::scatter_diag(r->scratch, r->n, c->n_ep + 3), s);
     if (st) return st;
     // what a batch launched after this one took as its carried cache: the
     // device chain's (this batch's tile headers); the host tail's may differ
@@ -3225,7 +3278,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   std::vector<usn_tile_hdr> th;
   {
     const int e = fetch_batch_state(c, r, ntiles, s, sum, th, nullptr, nullptr,
-                                    usn::scatter_diag(r->scratch, b->n, nb0));
+                                    usn::scatter_diag(r->scratch, r->n, nb0));
     if (e) return e;
   }
   usn_finalize_info fi;
@@ -3365,7 +3418,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HIPCHK(hipMemcpy(r->summary, &out, sizeof out, hipMemcpyHostToDevice));
   HIPCHK(hipStreamSynchronize(s));
   if (any) {
-    st = lists_check(usn::scatter_diag(r->scratch, b->n, nb), s);
+    st = lists_check(usn::scatter_diag(r->scratch, r->n, nb), s);
     if (st) return st;
   }
   if (info) *info = fi;

@@ -199,10 +199,10 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
 /* scratch bytes of one batch (cnt | agg | tot | gran | diag; agg and gran
  * sized for one-tile chunks) and its carve for chunks of tc tiles */
 size_t scatter_scratch_bytes(uint64_t n, uint32_t nbins);
-void scatter_carve(void *scratch, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
+void scatter_carve(void *scratch, uint64_t cap, uint64_t n, uint32_t nbins, uint32_t tc, uint32_t cpt,
                    ScatterBatch &sb, uint16_t **cnt);
-void scatter_tail(void *scratch, uint64_t n, uint32_t nbins, void **p, size_t *bytes);
-uint32_t *scatter_diag(void *scratch, uint64_t n, uint32_t nbins);
+void scatter_tail(void *scratch, uint64_t cap, uint32_t nbins, void **p, size_t *bytes);
+uint32_t *scatter_diag(void *scratch, uint64_t cap, uint32_t nbins);
 
 }  // namespace usn
 

@@ -142,6 +142,7 @@ struct Dev {
   uint32_t rep = 0;           // the device replica its rings are classified on
   /* two result buffers per source: the carried cache reads the previous one */
   void *res[2] = {nullptr, nullptr};
+  usn_result rb[2] = {};      // bound once per allocation (a bind per round re-zeroes scratch)
   int cur = 0;
   uint64_t frames_in = 0, frames_out = 0;
 };
@@ -694,7 +695,11 @@ void Daemon::remove_dev(const DevP &d) {
                       pipe_monitor_.end());
   if (d->res[0] || d->res[1]) {
     select(d->rep);
-    for (void *r : d->res) if (r) usn_dev_free(ctx_, r);
+    for (int k = 0; k < 2; ++k)
+      if (d->res[k]) {
+        usn_result_release(ctx_, &d->rb[k]);
+        usn_dev_free(ctx_, d->res[k]);
+      }
   }
   if (d->fd >= 0) close(d->fd);
   if (d->txfd >= 0) close(d->txfd);
@@ -921,8 +926,9 @@ void Daemon::forward_round(const std::vector<DevP> &ready) {
         end_ = true;
         return;
       }
+      usn_result_bind(d.res[d.cur], usn_result_bytes(max_batch_), max_batch_, &d.rb[d.cur]);
     }
-    usn_result_bind(d.res[d.cur], usn_result_bytes(max_batch_), max_batch_, &s.res);
+    s.res = d.rb[d.cur];
   }
   /* 4. classify in device order.  A run of consecutive NIC rings changes no
    *    shared state: its rings go to their replicas' GPUs at once (up to 8

@@ -13,6 +13,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libusn.so")
+# the test build (Makefile: the product's device code, a host object that
+# reads the A/B and test knobs of the environment); only tests that force
+# failures and A/B tools load it -- the product library reads no environment
+TEST_LIB_PATH = os.path.join(os.path.dirname(HERE), "build", "test", "libusn.so")
 
 USN_TILE = 1024
 USN_WINDOW = 64
@@ -108,6 +112,7 @@ def load(path: str | None = None):
         "usn_frag_clear": ([P], I), "usn_cache_clear": ([P, U16], I),
         "usn_result_bytes": ([U64], SZ), "usn_result_bytes_ep": ([U64, U32], SZ),
         "usn_result_bind": ([P, SZ, U64, C.POINTER(Result)], I),
+        "usn_result_release": ([P, C.POINTER(Result)], I),
         "usn_classify": ([P, C.POINTER(Batch), C.POINTER(Result), P], I),
         "usn_finalize": ([P, C.POINTER(Batch), C.POINTER(Result), P, C.POINTER(FinalizeInfo)], I),
         "usn_dev_alloc": ([P, SZ, C.POINTER(P)], I), "usn_dev_free": ([P, P], I),
@@ -129,7 +134,7 @@ def load(path: str | None = None):
     }
     optional = {"usn_set_frame_reader", "usn_ctx_create_group", "usn_ctx_replicas",
                 "usn_replica_select", "usn_replica_device", "usn_result_bytes_ep",
-                "usn_set_lists_async", "usn_lists_wait"}   # A/B builds of older ABI versions lack these
+                "usn_set_lists_async", "usn_lists_wait", "usn_result_release"}   # A/B builds of older ABI versions lack these
     for name, (args, res) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -151,7 +156,7 @@ EXPORTED = ["usn_abi_version", "usn_strerror", "usn_last_hip_error", "usn_ctx_cr
             "usn_event_elapsed_ms", "usn_stream_wait_event", "usn_classify_multi",
             "usn_bridge_set", "usn_table_build", "usn_set_frame_reader", "usn_ctx_create_group",
             "usn_ctx_replicas", "usn_replica_select", "usn_replica_device", "usn_set_lists_async",
-            "usn_lists_wait"]
+            "usn_lists_wait", "usn_result_release"]
 
 
 def check(rc, what=""):
@@ -482,7 +487,13 @@ class DeviceResult:
         return raw.view(SUMMARY_DTYPE)[0]
 
     def free(self):
+        """usn_result_release (the context's records of this result), then the memory"""
+        if self.buf is None:
+            return
+        if hasattr(self.ctx.L, "usn_result_release") and self.ctx.h:
+            check(self.ctx.L.usn_result_release(self.ctx.h, C.byref(self.desc)), "usn_result_release")
         self.buf.free()
+        self.buf = None
 
 
 def dec_bin(dec: np.ndarray, n_ep: int) -> np.ndarray:
