@@ -24,7 +24,9 @@ It reports
     i.e. the hand count no longer equals the instructions actually issued in
     between (the wait is then stricter than intended: slower, and a sign the
     count is stale).  vmcnt(0) is a drain and names no count to go stale.
-LDS-DMA loads (global_load_lds, builtins) have no register destination and
+A path through an instruction marked `; usn_rare` in its asm (a rare path's
+extra store, which only makes the waits after it stricter) reports no loose
+wait.  LDS-DMA loads (global_load_lds, builtins) have no register destination and
 are only counted as issued instructions here.
 """
 from __future__ import annotations
@@ -46,6 +48,7 @@ class Insn:
     args: str
     in_asm: bool
     block: int = -1    # inline-asm block index (-1: compiler code)
+    rare: bool = False # an inline-asm instruction marked `; usn_rare` (a rare path's extra store)
 
 
 @dataclass
@@ -102,6 +105,7 @@ def parse(asm_text: str) -> list:
         if s.startswith(".Lfunc_end"):
             cur = None
             continue
+        rare = "usn_rare" in s
         s = s.split(";", 1)[0].strip()
         if not s:
             continue
@@ -112,7 +116,7 @@ def parse(asm_text: str) -> list:
         if s.startswith("."):
             continue
         op, _, args = s.partition(" ")
-        cur.insns.append(Insn(ln, s, op, args.strip(), in_asm, nblock if in_asm else -1))
+        cur.insns.append(Insn(ln, s, op, args.strip(), in_asm, nblock if in_asm else -1, rare))
     return funcs
 
 
@@ -149,14 +153,15 @@ def check_load(f: Func, i: int, tight: bool, max_steps=20000) -> list:
     load = f.insns[i]
     dest = vmem_dest(load)
     out = []
-    stack = [(j, 0) for j in successors(f, i)]
+    # (instruction, issued since the load, a rare instruction on the path)
+    stack = [(j, 0, False) for j in successors(f, i)]
     seen = set()
     steps = 0
     while stack and steps < max_steps:
-        j, y = stack.pop()
-        if (j, y) in seen:
+        j, y, rare = stack.pop()
+        if (j, y, rare) in seen:
             continue
-        seen.add((j, y))
+        seen.add((j, y, rare))
         steps += 1
         ins = f.insns[j]
         if ins.op == "s_waitcnt":
@@ -165,7 +170,7 @@ def check_load(f: Func, i: int, tight: bool, max_steps=20000) -> list:
             if n is None and ins.args.strip() == "0":
                 n = 0
             if n is not None and n <= y:
-                if tight and ins.in_asm and 0 < n < y:
+                if tight and ins.in_asm and 0 < n < y and not rare:
                     out.append(Finding(f.name, "loose", load.line, load.text, ins.line, ins.text,
                                        "%d vector-memory instructions issued after the load, "
                                        "wait counts %d" % (y, n)))
@@ -177,8 +182,9 @@ def check_load(f: Func, i: int, tight: bool, max_steps=20000) -> list:
             continue
         if is_vmem(ins.op):
             y = min(y + 1, 63)
+        rare = rare or ins.rare
         for k in successors(f, j):
-            stack.append((k, y))
+            stack.append((k, y, rare))
     return out
 
 

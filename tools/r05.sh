@@ -27,6 +27,18 @@ case $S in
       python3 tools/kbench.py c5 8388608 12
     python3 tools/pmc_summary.py $O/sq1 $O/sq2 > $O/sq_summary.txt 2>&1 || true
     ;;
+  r05b)
+    # classify_chunk_kernel (pipelined wave-per-tile classify, one count row
+    # per chunk) + the self-counting scatter: the GPU suite, A/B against the
+    # one-tile-per-workgroup classify in one process (c5 2 x 8M, c4 8 x 1M),
+    # the driver's bench
+    bash tools/gpu.sh $S testsall || exit 1
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --rounds 5 --launches 40" ABL_VARIANTS="base nochunk" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="--frames 1048576 --multi 8 --rounds 5 --launches 40" ABL_VARIANTS="base nochunk" \
+      bash tools/gpu.sh $S abl || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
