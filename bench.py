@@ -247,6 +247,57 @@ class Run:
             dist.barrier()
         return t1 - t0, ctx.elapsed_ms(self.ev0, self.ev1)
 
+    def finalize_round(self, i, times=None):
+        """usn_finalize of every ring of poll round i, on the stream its call
+        ran on (the ordered host stage, /root/reference/src/endpoint.rs:128-169:
+        the reference decides and delivers every frame of a drain before the
+        next); `times` collects each call's wall time"""
+        rnd = i % self.R
+        for s, qs in self.launches:
+            st = self.streams[s]
+            for j in qs:
+                k = rnd * self.Q + j
+                t = time.perf_counter()
+                self.ctx.finalize(self.batches[k], self.results[k], st)
+                if times is not None:
+                    times.append(time.perf_counter() - t)
+
+    def end_to_end(self, steps, dist):
+        """Poll rounds with the ordered host stage in the timed loop: round i's
+        calls, then usn_finalize of every ring of round i - 1 (a daemon
+        finalizes and delivers round i - 1 while round i runs on the GPU),
+        the last round finalized before the clock stops.  Returns (wall s,
+        finalize call times)."""
+        ctx = self.ctx
+        for x in self.streams:
+            ctx.sync(x)
+        if dist:
+            dist.barrier()
+        times = []
+        t0 = time.perf_counter()
+        for i in range(steps):
+            self.step(i)
+            if i:
+                self.finalize_round(i - 1, times)
+        self.finalize_round(steps - 1, times)
+        for x in self.streams:
+            ctx.sync(x)
+        wall = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        return wall, times
+
+    def finalize_host_us(self, rounds=3):
+        """usn_finalize's own host time per ring: the rounds' GPU work done
+        first, so the call waits for nothing"""
+        times = []
+        for i in range(rounds):
+            self.step(i)
+            for x in self.streams:
+                self.ctx.sync(x)
+            self.finalize_round(i, times)
+        return float(np.median(times)) * 1e6
+
     def lists_wait(self, ra, cnt, stream):
         """the stream waits for the lists of one launch (side-stream mode)"""
         for j in range(cnt):
@@ -330,6 +381,11 @@ def measure(run, args, dist, world):
     wall, ev_ms = run.timed(args.steps, dist)
     elapsed = shard.max_over_ranks(wall, dist)
     host_frames, flags, cls = run.finalize_all()
+    # the same poll rounds with usn_finalize of every ring in the timed loop
+    # (what the reference does per drain)
+    e2e_wall, fin_times = run.end_to_end(args.steps, dist)
+    e2e_elapsed = shard.max_over_ranks(e2e_wall, dist)
+    fin_host_us = run.finalize_host_us()
     frames = world * args.steps * run.frames_per_step()
     achieved = ALGO_BYTES * probe_frames / (kern_ms * 1e-3) / 1e9 if kern_ms else None
     roof = {
@@ -364,6 +420,15 @@ def measure(run, args, dist, world):
             pass
     return {
         "value": round(frames / elapsed / 1e6, 2),
+        "end_to_end_mpps": round(frames / e2e_elapsed / 1e6, 2),
+        "end_to_end": {
+            "basis": "poll rounds with usn_finalize of every ring in the timed loop (round i-1's "
+                     "rings finalized after round i's calls are enqueued), wall clock, max over ranks",
+            "ms_per_step": round(e2e_elapsed * 1e3 / args.steps, 5),
+            "finalize_call_us_per_ring_median": round(float(np.median(fin_times)) * 1e6, 2),
+            "finalize_host_us_per_ring": round(fin_host_us, 2),
+            "rings_per_step": run.Q,
+        },
         "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
         "event_ms_per_step": round(ev_ms / args.steps, 5),
         # the host's own time to enqueue a step's calls (close to ms_per_step: host-bound)
@@ -408,9 +473,16 @@ def measure_tx(ctx, args):
     bufs = [lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
             for _ in range(TX_ROTATE)]
     res = [lib.DeviceResult(ctx, n) for _ in range(2)]
+    learn_us, learn_n, next_us = None, 0, None
     for k in range(TX_ROTATE + args.warmup):          # learning pass + warm-up
+        ctx.sync()
+        t = time.perf_counter()
         ctx.classify(bufs[k % TX_ROTATE], res[k % 2], s)
-        ctx.finalize(bufs[k % TX_ROTATE], res[k % 2], s)
+        nl = ctx.finalize(bufs[k % TX_ROTATE], res[k % 2], s).n_learned
+        if k == 0:   # the first ring learns every flow's answer rule (and the bridge MACs)
+            learn_us, learn_n = (time.perf_counter() - t) * 1e6, nl
+        elif k == 1:   # its classify brings the rule image up to date with what ring 0 learned
+            next_us = (time.perf_counter() - t) * 1e6
     # >= 100 rings (about 8 ms) and as many event pairs for the device median
     # (the anti-cache rule of BASELINE.md: >= 100 launches)
     K = max(args.steps, TX_RINGS)
@@ -472,6 +544,12 @@ def measure_tx(ctx, args):
          "device_mpps": round(n / (dev_ms * 1e-3) / 1e6, 2), "ms_per_ring": round(wall * 1e3 / K, 4),
          "pipelined_with_events_mpps": round(K * n / wall_ev / 1e6, 2),
          "rings": K, "learned_in_timed_rings": int(learned),
+         "learning_ring_us": round(learn_us, 1), "learning_ring_learned": int(learn_n),
+         "after_learning_ring_us": round(next_us, 1),
+         "learning_ring_basis": "wall time of the first ring (classify call + usn_finalize, "
+                                "which applies what it learned: answer rules into the registry, "
+                                "the rule image brought up to date by the next ring's classify: "
+                                "after_learning_ring_us)",
          "workload": "c4tx: %d x 64B frames per ring sent by the host endpoint, %d rules after "
                      "learning, ADD_MACS bridge; ring in %d rotating buffers (%d MiB)"
                      % (n, ctx.rule_count(), TX_ROTATE, TX_ROTATE * n * cfg.stride >> 20),
