@@ -611,6 +611,8 @@ def main(argv=None):
         "metric": METRIC,
         "value": res["value"],
         "unit": "Mpkts/s",
+        "end_to_end_mpps": res["end_to_end_mpps"],
+        "end_to_end": res["end_to_end"],
         "n_gpus": len(joined),
         "steps": args.steps,
         "warmup": args.warmup,

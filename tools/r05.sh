@@ -39,6 +39,20 @@ case $S in
       bash tools/gpu.sh $S abl || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05c)
+    # where the chunk kernel's call time goes: rocprof kernel stats of the
+    # A/B (base: classify_chunk_kernel + chunk-row scan + counting scatter;
+    # nochunk: round 4's three kernels), c5 2 x 8M and c4 8 x 1M
+    rm -rf $O/prof5 $O/prof4
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof5 -o run -- \
+      python3 tools/abl.py --config c5 --frames 8388608 --multi 2 --batches 4 --rounds 3 --launches 30 \
+      --json $O/abl_c5.json base nochunk > $O/abl_c5.log 2>&1 || exit 1
+    python3 tools/trace_summary.py $O/prof5/run_kernel_trace.csv > $O/trace_c5.log 2>&1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof4 -o run -- \
+      python3 tools/abl.py --config c4 --frames 1048576 --multi 8 --batches 8 --rounds 3 --launches 30 \
+      --json $O/abl_c4.json base nochunk > $O/abl_c4.log 2>&1 || exit 1
+    python3 tools/trace_summary.py $O/prof4/run_kernel_trace.csv > $O/trace_c4.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
