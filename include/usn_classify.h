@@ -148,7 +148,9 @@ typedef struct {
   uint32_t n_ep;           /* endpoint bins of usn_result.index: bins 0..n_ep-1 are endpoint ids,
                               n_ep = NIC, n_ep+1 = FLOOD, n_ep+2 = DROP */
   uint32_t n_bins;         /* n_ep + 3: usn_result.bin_off has n_bins + 1 entries */
-  uint32_t _pad[2];
+  uint32_t host_epoch;     /* internal: the launch tag of the last classify whose tiles listed
+                              frames for the ordered host stage */
+  uint32_t _pad;
 } usn_summary;             /* 80 bytes */
 #define USN_S_STALE 1u         /* carried cache entry disagrees with the current table */
 #define USN_S_STALE_EXTENDS 2u /* stale prefix may continue past tile 0 */

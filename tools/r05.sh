@@ -53,6 +53,30 @@ case $S in
       --json $O/abl_c4.json base nochunk > $O/abl_c4.log 2>&1 || exit 1
     python3 tools/trace_summary.py $O/prof4/run_kernel_trace.csv > $O/trace_c4.log 2>&1
     ;;
+  r05d)
+    # instruction mix of classify_chunk_kernel against classify_rx_kernel
+    # (SQ counters, two passes over the A/B harness, c5 2 x 8M)
+    A="tools/abl.py --config c5 --frames 8388608 --multi 2 --batches 4 --rounds 1 --launches 6 base nochunk"
+    sq_pass sq1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" python3 $A
+    sq_pass sq2 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_SALU" python3 $A
+    python3 tools/pmc_summary.py $O/sq1 $O/sq2 > $O/sq_summary.txt 2>&1 || true
+    ;;
+  r05e)
+    # classify_chunk_kernel variants (steady steps as a loop over pairs at 64
+    # VGPRs, the same at 80, the 16-step unroll) against round 4's classify:
+    # rocprof kernel stats of the A/B harness, c5 2 x 8M and c4 8 x 1M; then the
+    # volume parity tests on the default build
+    for c in c5 c4; do
+      if [ $c = c5 ]; then A="--frames 8388608 --multi 2 --batches 4"; else A="--frames 1048576 --multi 8 --batches 8"; fi
+      rm -rf $O/prof_$c
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o run -- \
+        python3 tools/abl.py --config $c $A --rounds 3 --launches 30 --json $O/abl_$c.json \
+        base ckloop ckwpe6 nochunk > $O/abl_$c.log 2>&1 || exit 1
+      python3 tools/trace_summary.py $O/prof_$c/run_kernel_trace.csv > $O/trace_$c.log 2>&1
+    done
+    bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -1406,6 +1406,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     if (tid == 0) {
       const uint32_t nic = hist_get(L.hist, a.n_ep), fl = hist_get(L.hist, a.n_ep + 1),
                      dr = hist_get(L.hist, a.n_ep + 2);
+      if (s_misc[1]) a.summary->host_epoch = a.epoch;   // (usn_finalize's rx state)
       H->n_frames = (uint16_t)nt;
       H->_r0 = 0;
       H->n_host = (uint16_t)s_misc[1];
@@ -2621,6 +2622,9 @@ static bool glds_layout(const MultiArgs &m) {
  * stricter.  A batch's partial last tile runs the same steps with every wait
  * a drain (ck_tail).
  * =========================================================================== */
+#ifndef USN_CK_UNROLL   /* A/B: 1 = the 16 steps of a tile fully unrolled */
+#define USN_CK_UNROLL 1
+#endif
 #ifndef USN_CHUNK_KERNEL   /* A/B: 0 = classify_rx_kernel for every launch */
 #define USN_CHUNK_KERNEL 1
 #endif
@@ -2629,23 +2633,24 @@ static bool glds_layout(const MultiArgs &m) {
 static_assert(CK_SEGS == 16 && NWAVES == 8, "classify_chunk_kernel: 8 waves x 16 segments");
 
 struct CkSeg {            // a segment between its U slot read and its decision: what the
-                          // decision needs of Parsed, packed (9 VGPRs held across a step)
-  uint32_t w0;            // status | frag_first << 3
-  uint32_t i0, src, dst, ports;
+                          // decision needs of Parsed, packed (8 VGPRs held across a step)
+  uint32_t w0;            // status | frag_first << 3 | i0 << 8 (i0: 17 bits)
+  uint32_t src, dst, ports;
   v4u32 s;                // the U slot (in flight until the decision's wait)
 };
 __device__ __forceinline__ void ck_unpack(const CkSeg &g, Parsed &p) {
   p.status = g.w0 & 7u;
-  p.frag_first = g.w0 >> 3;
-  p.i0 = g.i0; p.src = g.src; p.dst = g.dst; p.ports = g.ports;
-  p.proto = (g.i0 >> 8) & 0xFFu;          // (IPv4 frames: the only ones whose decision reads
-  p.has_ports = (g.i0 >> 16) & 1u;        //  proto, has_ports and the ports)
+  p.frag_first = (g.w0 >> 3) & 1u;
+  p.i0 = g.w0 >> 8;
+  p.src = g.src; p.dst = g.dst; p.ports = g.ports;
+  p.proto = (p.i0 >> 8) & 0xFFu;          // (IPv4 frames: the only ones whose decision reads
+  p.has_ports = (p.i0 >> 16) & 1u;        //  proto, has_ports and the ports)
   p.sport = g.ports & 0xFFFFu;
   p.dport = g.ports >> 16;
 }
 struct CkTile {           // what a wave keeps of its tile
-  uint32_t my_last;       // per lane: 1 + its last touching frame | touch << 16
-  uint32_t my_dec, my_info[4];
+  uint32_t my_last;       // per lane: 1 + its last touching frame | touch << 16 (the frame's
+                          // info and decision are read again at the tile's end)
   uint32_t n_nic, n_flood, n_drop, n_host;          // wave-uniform
   uint32_t stale_on, first_break;                   // wave-uniform (tile 0 of a stale batch)
 };
@@ -2735,10 +2740,7 @@ __device__ __forceinline__ void ck_decide(const ClassifyArgs &a, const uint4 *T,
                     (uint32_t)(base + local));
     t.n_host += (uint32_t)__popcll(hm);
   }
-  if (touch) {
-    t.my_last = (local + 1) | (touch << 16); t.my_dec = dec;
-    t.my_info[0] = p.i0; t.my_info[1] = p.src; t.my_info[2] = p.dst; t.my_info[3] = p.ports;
-  }
+  if (touch) t.my_last = (local + 1) | (touch << 16);
 }
 
 /* segment k's parse and U slot read (its headers and length have landed in
@@ -2752,8 +2754,8 @@ __device__ __forceinline__ void ck_probe(const ClassifyArgs &a, const uint4 *T, 
   const bool need = p.status == 1u;
   const uint32_t du = lds_disp1(Dl, a.ph[2], need, ku);
   asm_slot1(T, a.ph[2], need, ku, du, g.s);
-  g.w0 = p.status | (p.frag_first << 3);
-  g.i0 = p.i0; g.src = p.src; g.dst = p.dst; g.ports = p.ports;
+  g.w0 = p.status | (p.frag_first << 3) | (p.i0 << 8);
+  g.src = p.src; g.dst = p.dst; g.ports = p.ports;
 }
 
 /* one pipeline step of a full tile: WA = the vector-memory instructions
@@ -2763,7 +2765,7 @@ template <int WA, int WE, bool NEXT, bool PREV>
 __device__ __forceinline__ void ck_step(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
                                         uint32_t *hist, const uint32_t *carry, uint64_t base,
                                         uint32_t tile, uint32_t k, uint32_t lane, uint4 *st,
-                                        uint32_t &len, CkSeg &prev, CkTile &t) {
+                                        uint32_t &len, CkSeg &cur, CkSeg &prev, CkTile &t) {
   asm volatile("s_waitcnt vmcnt(%1)" : "+v"(len) : "n"(WA) : "memory");   // segment k landed
   uint4 q[4];
   stage_read_asm(st, lane, q);                        // (waits for its LDS reads)
@@ -2773,14 +2775,12 @@ __device__ __forceinline__ void ck_step(const ClassifyArgs &a, const uint4 *T, c
     len = ck_len(a.lens + base + (k + 1) * 64 + lane);
   }
   __builtin_amdgcn_sched_barrier(0);
-  CkSeg cur;
   ck_probe(a, T, Dl, q, lk, a.frames + (base + k * 64 + lane) * a.stride, cur);
   __builtin_amdgcn_sched_barrier(0);
   if (PREV) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(prev.s) : "n"(WE) : "memory");   // slot k - 1 landed
     ck_decide<true>(a, T, Dl, hist, carry, base, tile, k - 1, TILE, lane, prev, t);
   }
-  prev = cur;
 }
 
 template <int K>
@@ -2792,8 +2792,10 @@ __device__ __forceinline__ void ck_steps(const ClassifyArgs &a, const uint4 *T, 
   constexpr int NX = 1 + GLDS_PARTS;
   constexpr int WA = K == 0 ? 0 : K == 1 ? 1 : 2;                     // slot k-1 (+ store k-2)
   constexpr int WE = (K >= 2 ? 1 : 0) + (K + 1 < CK_SEGS ? NX : 0) + 1;   // store k-2, next, slot k
+  CkSeg cur;
   ck_step<WA, WE, (K + 1 < CK_SEGS), (K > 0)>(a, T, Dl, hist, carry, base, tile, K, lane, st, len,
-                                               prev, t);
+                                               cur, prev, t);
+  prev = cur;
   if constexpr (K + 1 < CK_SEGS)
     ck_steps<K + 1>(a, T, Dl, hist, carry, base, tile, lane, st, len, prev, t);
 }
@@ -2835,7 +2837,10 @@ __device__ __forceinline__ uint32_t ck_batch(const MultiArgs &m, uint32_t g, uin
   return bi;
 }
 
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef USN_CK_WPE   /* waves per SIMD classify_chunk_kernel is compiled for (8: 64 VGPRs) */
+#define USN_CK_WPE 8
+#endif
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_CK_WPE)))
 void classify_chunk_kernel(MultiArgs m) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[NWAVES * CK_STAGE];
@@ -2890,17 +2895,37 @@ void classify_chunk_kernel(MultiArgs m) {
   }
   const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
   CkTile t;
-  t.my_last = 0; t.my_dec = 0;
-  for (int k = 0; k < 4; ++k) t.my_info[k] = 0;
+  t.my_last = 0;
   t.n_nic = t.n_flood = t.n_drop = t.n_host = 0;
   t.stale_on = stale ? 1u : 0u;
   t.first_break = TILE;
   const uint32_t *carry = s_carry;   // (read in the rare stale steps only)
   if (full) {
     CkSeg prev;
+#if USN_CK_UNROLL
     ck_steps<0>(a, T, Dl, L.hist, carry, base, tile, lane, st, len, prev, t);
+#else
+    // steps 0 and 1, the steady steps 2..13 as a loop over pairs (the two
+    // segments' states alternate between x0 and x1: nothing in flight is
+    // copied at the back edge; a 16-fold unroll hoisted addresses and spilled
+    // 84 SGPRs), steps 14 and 15
+    constexpr int NX = 1 + GLDS_PARTS;
+    CkSeg x1;
+    ck_step<0, 0, true, false>(a, T, Dl, L.hist, carry, base, tile, 0, lane, st, len, prev, x1, t);
+    ck_step<1, NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, 1, lane, st, len, x1, prev, t);
+    for (uint32_t k = 2; k + 2 < CK_SEGS; k += 2) {
+      ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, k, lane, st, len, prev, x1, t);
+      ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, k + 1, lane, st, len, x1, prev, t);
+    }
+    ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 2, lane, st, len, prev, x1, t);
+    ck_step<2, 2, false, true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, lane, st, len, x1, prev, t);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(x1.s) :: "memory");   // slot 15 (store 14 after it)
+    ck_decide<true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, TILE, lane, x1, t);
+#endif
+#if USN_CK_UNROLL
     asm volatile("s_waitcnt vmcnt(1)" : "+v"(prev.s) :: "memory");   // slot 15 (store 14 after it)
     ck_decide<true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, TILE, lane, prev, t);
+#endif
   } else if (mine) {
     ck_tail(a, T, Dl, L.hist, carry, base, tile, nt, lane, st, t);
   }
@@ -2910,14 +2935,22 @@ void classify_chunk_kernel(MultiArgs m) {
 #pragma unroll
     for (uint32_t d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
     usn_tile_hdr *H = a.tiles + tile;
-    if (mx && my == mx) {
+    if (mx && my == mx) {   // one lane: its frame's info parsed again, its decision read back
+      const uint64_t f = base + mx - 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the decision stores have landed)
+      const uint8_t *fp = a.frames + f * a.stride;
+      uint4 q[4];
+      lane_round(fp, q);
+      Parsed p;
+      parse(q, a.lens[f], fp, a.window, p);
       H->last_state = USN_TS_HAS | (my_touch == 1u ? USN_TS_RETAINED : 0u) |
                       (my_touch == 3u ? USN_TS_UNKNOWN : 0u);
-      H->last_dst = t.my_dec & USN_PARITY_MASK;
-      for (int k = 0; k < 4; ++k) H->last_info[k] = t.my_info[k];
-      H->last_idx = (uint32_t)(base + mx - 1);
+      H->last_dst = a.decisions[f] & USN_PARITY_MASK;
+      H->last_info[0] = p.i0; H->last_info[1] = p.src; H->last_info[2] = p.dst; H->last_info[3] = p.ports;
+      H->last_idx = (uint32_t)f;
     }
     if (lane == 0) {
+      if (t.n_host) a.summary->host_epoch = a.epoch;   // (usn_finalize's rx state)
       H->n_frames = (uint16_t)nt;
       H->_r0 = 0;
       H->n_host = (uint16_t)t.n_host;
@@ -3374,6 +3407,10 @@ void scatter_kernel(ScatterArgs s) {
           if (b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
           if (b + 1 >= s.n_ep && b + 1 < s.n_ep + 3) s.txs_out[7 + b - s.n_ep] = pt + vt.x;
         }
+        if (B.rx_state) {             // rx: the same into the batch's state
+          if (b >= s.n_ep && b < s.n_ep + 3) B.rx_state[4 + b - s.n_ep] = pt;
+          if (b + 1 >= s.n_ep && b + 1 < s.n_ep + 3) B.rx_state[5 + b - s.n_ep] = pt + vt.x;
+        }
       }
     }
   } else {   // more bins: per-thread contiguous runs of bins, the same sums
@@ -3404,6 +3441,7 @@ void scatter_kernel(ScatterArgs s) {
       off[b] = pt + (noscan ? 0u : ex[b]) - pc;
       if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
       if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
+      if (c == 0 && B.rx_state && b >= s.n_ep && b < s.n_ep + 3) B.rx_state[4 + b - s.n_ep] = pt;
       if (noscan) {
         for (uint32_t w = 0; w < ntc; ++w) pt += cnt_of(w, b);
       } else {
@@ -3424,6 +3462,12 @@ void scatter_kernel(ScatterArgs s) {
     for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
   }
   if (c == 0 && tid == 0) B.bin_off[s.nbins] = B.n;
+  if (c == 0 && B.rx_state && tid == 0) {   // rx: what usn_finalize reads first (host memory)
+    B.rx_state[1] = B.summary->flags;
+    B.rx_state[3] = B.summary->host_epoch == s.epoch ? 1u : 0u;
+    B.rx_state[7] = *B.diag;
+    B.rx_state[0] = s.epoch;
+  }
   if (c == 0 && bi == 0 && s.txs_out && tid < 6) {   // tx: summary flags, counters[0..4], n
     uint32_t v = tid == 0 ? s.txs_sum->flags
                           : __hip_atomic_load(s.txs_counters + tid - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3515,6 +3559,7 @@ void scatter_kernel(ScatterArgs s) {
   if (USN_ABL_SC == 0 && USN_SC_CHECKS && __ballot(bad) && lane == 0) {   // rare: one report per wave
     atomicOr(B.diag, USN_DIAG_LISTS);
     if (s.txs_out) s.txs_out[11] = USN_DIAG_LISTS;   // tx: beside chunk 0's copy of the scan's word
+    if (B.rx_state) B.rx_state[2] = USN_DIAG_LISTS;
   }
   if (USN_ABL_SC == 0 && __syncthreads_or(unsorted || (s.flags & USN_SCF_SLOW_RANK))) {
     // 5. (not taken on gfx950 so far) the wave's cursors back to their

@@ -552,8 +552,11 @@ struct usn_ctx {
   /* per classified batch (by its decisions): the replica it ran on and its
    * bin count (endpoints can be added before its usn_finalize: the batch's
    * scratch, count rows and lists keep the bins it was classified with) */
-  struct BatchRec { uint32_t rep, nbins; bool chunk_rows; };   // chunk_rows: one count row per
-                                                                 // chunk (classify_chunk_kernel)
+  struct BatchRec {
+    uint32_t rep, nbins;
+    bool chunk_rows;        // one count row per chunk (classify_chunk_kernel)
+    uint32_t slot, epoch;   // its rx state slot (RX_SLOTS: none) and launch tag
+  };
   std::unordered_map<const void *, BatchRec> batch_rep;
   /* usn_set_lists_async: lists built on the replica's side stream; each
    * result's `lists done` event (keyed by its decisions array, created on
@@ -575,6 +578,12 @@ struct usn_ctx {
   uint8_t *h_txstate = nullptr;      // 2 slots x TXSTATE_BYTES
   size_t h_txstate_cap = 0;
   const void *txstate_for[2] = {nullptr, nullptr};   // the result (decisions) each slot holds
+  /* an rx batch's state for usn_finalize (ScatterBatch::rx_state), written
+   * by its scatter into host-mapped memory: RX_SLOTS slots of 8 words, dealt
+   * round-robin to the batches of each classify call (BatchRec::slot) */
+  static constexpr uint32_t RX_SLOTS = 1024;
+  uint32_t *h_rxstate = nullptr;
+  uint32_t rx_next_slot = 0;
 };
 
 namespace {
@@ -1878,6 +1887,7 @@ void usn_ctx_destroy(usn_ctx *c) {
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_patch) (void)hipHostFree(c->h_patch);
   if (c->h_txstate) (void)hipHostFree(c->h_txstate);
+  if (c->h_rxstate) (void)hipHostFree(c->h_rxstate);
   if (c->h_lists) (void)hipHostFree(c->h_lists);
   if (c->h_items) (void)hipHostFree(c->h_items);
   delete c;
@@ -2272,6 +2282,13 @@ static int fill_args(usn_ctx *c, const Replica &R, const usn_batch *b, const usn
 
 /* the per-endpoint scatter of `count` classified batches (after their
  * classify / tx launch, or after finalize recounted patched tiles) */
+/* a launch's tag: the scan's granules and a batch's rx state carry it (0 is
+ * what zeroed granules hold) */
+static uint32_t next_epoch(usn_ctx *c) {
+  if (++c->scan_epoch == 0) c->scan_epoch = 1;
+  return c->scan_epoch;
+}
+
 /* the lists' plan of a launch (usn::scatter_plan, with the A/B knobs of the
  * test build) */
 static usn::ScatterPlan plan_lists(usn_ctx *c, const usn::ClassifyArgs *as, uint32_t count) {
@@ -2312,7 +2329,8 @@ static usn::ScatterPlan plan_lists(usn_ctx *c, const usn::ClassifyArgs *as, uint
  * chunk_rows: the classify wrote one count row per chunk of 8 tiles */
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
                           uint32_t count, hipStream_t s, uint32_t *txs_out = nullptr,
-                          const uint32_t *txs_counters = nullptr, bool chunk_rows = false) {
+                          const uint32_t *txs_counters = nullptr, bool chunk_rows = false,
+                          uint32_t epoch = 0, uint32_t *const *rx_state = nullptr) {
   usn::ScatterArgs x;
   std::memset(&x, 0, sizeof x);
   x.count = count;
@@ -2332,8 +2350,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.txs_out = txs_out;
   x.txs_counters = txs_counters;
   x.txs_sum = r[0].summary;
-  if (++c->scan_epoch == 0) c->scan_epoch = 1;   // 0 is what zeroed granules hold
-  x.epoch = c->scan_epoch;
+  if (!epoch) epoch = next_epoch(c);   // (the classify of this launch took one already)
+  x.epoch = epoch;
   for (uint32_t k = 0; k < count; ++k) {
     usn::ScatterBatch &sb = x.b[k];
     uint16_t *cnt;
@@ -2341,6 +2359,8 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
     sb.decisions = r[k].decisions;
     sb.index = r[k].index;
     sb.bin_off = r[k].bin_off;
+    sb.rx_state = rx_state ? rx_state[k] : nullptr;
+    sb.summary = r[k].summary;
     x.chunk_base[k + 1] = x.chunk_base[k] + sb.nchunks;
     x.range_base[k + 1] = x.range_base[k] + sb.nranges;
     // granules of a scratch never used before may hold anything: zero them
@@ -2588,6 +2608,9 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   }
   uint32_t slot = 0;
   bool chunk_rows = false;   // the classify wrote one count row per chunk of 8 tiles
+  uint32_t epoch = 0;        // rx: the launch tag (classify and lists)
+  uint32_t rx_slot[USN_MAX_MULTI];
+  uint32_t *rx_state[USN_MAX_MULTI];
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
@@ -2631,6 +2654,22 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         it->second.pending = false;
       }
     }
+    /* the batches' state for usn_finalize: a slot of host-mapped memory each,
+     * written by the scatter (ScatterBatch::rx_state) */
+    if (!c->h_rxstate)
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_rxstate), usn_ctx::RX_SLOTS * 32,
+                           hipHostMallocMapped | hipHostMallocCoherent));
+    uint32_t *d_rx = nullptr;
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_rx), c->h_rxstate, 0));
+    epoch = next_epoch(c);
+    for (uint32_t k = 0; k < count; ++k) {
+      rx_slot[k] = c->rx_next_slot++ % usn_ctx::RX_SLOTS;
+      volatile uint32_t *h = c->h_rxstate + rx_slot[k] * 8;
+      h[0] = 0;   // (the tag, until the scatter writes it)
+      h[2] = 0;   // (set by any scatter chunk that finds inconsistent lists)
+      rx_state[k] = d_rx + rx_slot[k] * 8;
+      m.b[k].epoch = epoch;
+    }
     // chunks of 8 tiles for the lists let the classify write a row per chunk
     const usn::ScatterPlan pl = plan_lists(c, m.b, count);
     m.chunk_tc = (pl.tc == 8 && (!pl.selfscan || usn::scatter_lds(m.b[0].nbins, 8, true, true) <= 64u * 1024u))
@@ -2655,7 +2694,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
     }
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
-                            chunk_rows);
+                            chunk_rows, epoch, tx ? nullptr : rx_state);
     if (st) return st;
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
@@ -2670,7 +2709,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (!R.classified) HIPCHK(hipEventCreateWithFlags(&R.classified, hipEventDisableTiming));
     HIPCHK(hipEventRecord(R.classified, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(R.side, R.classified, 0));
-    int st = launch_scatter(c, m.b, r, count, R.side, nullptr, nullptr, chunk_rows);
+    int st = launch_scatter(c, m.b, r, count, R.side, nullptr, nullptr, chunk_rows, epoch, rx_state);
     if (st) return st;
     for (uint32_t k = 0; k < count; ++k) {
       usn_ctx::ListsEv &le = c->lists_ev[r[k].decisions];
@@ -2699,7 +2738,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       if (!ch.done[rep]) HIPCHK(hipEventCreateWithFlags(&ch.done[rep], hipEventDisableTiming));
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
-    c->batch_rep[r[k].decisions] = usn_ctx::BatchRec{rep, m.b[k].nbins, chunk_rows};
+    c->batch_rep[r[k].decisions] =
+        usn_ctx::BatchRec{rep, m.b[k].nbins, chunk_rows, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch};
   }
   return USN_OK;
 }
@@ -3289,6 +3329,28 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
       for (int k = 0; k < 4; ++k) fi.class_count[k] += th[t].class_count[k];
     if (info) *info = fi;
     return USN_OK;
+  }
+  /* NIC batch: its scatter left the batch's state in host-mapped memory
+   * (summary flags, whether any tile listed frames for the host stage, the
+   * class totals, the lists' diag word).  With nothing for the host stage the
+   * device results are final: no copy of the summary and the tile headers
+   * (37 us per 1M-frame ring, profiles/r05/r05b) */
+  if (br != c->batch_rep.end() && br->second.slot < usn_ctx::RX_SLOTS) {
+    const volatile uint32_t *h = c->h_rxstate + br->second.slot * 8;
+    if (h[0] == br->second.epoch) {
+      const uint32_t lists = h[2] | h[7];
+      if (lists) return lists_failed(lists, usn::scatter_diag(r->scratch, r->n, nb0), s);
+      if (h[1] == 0 && h[3] == 0) {
+        usn_finalize_info fi;
+        std::memset(&fi, 0, sizeof fi);
+        fi.class_count[USN_CLS_EP] = h[4];
+        fi.class_count[USN_CLS_NIC] = h[5] - h[4];
+        fi.class_count[USN_CLS_FLOOD] = h[6] - h[5];
+        fi.class_count[USN_CLS_DROP] = (uint32_t)b->n - h[6];
+        if (info) *info = fi;
+        return USN_OK;   // device results are final; the device chain carries the cache
+      }
+    }
   }
   const uint32_t ntiles = (uint32_t)((b->n + USN_TILE - 1) / USN_TILE);
   usn_summary sum;

@@ -24,6 +24,8 @@ struct ClassifyArgs {
   uint64_t n;
   uint32_t ntiles;
   uint32_t window;          /* readable bytes at every frame start (usn_batch.window) */
+  uint32_t epoch;           /* the launch tag (ScatterArgs::epoch): a tile that lists frames for
+                               the host stage stores it in summary->host_epoch */
   /* outputs */
   uint32_t *decisions;
   uint16_t *cnt;            /* [ntiles][nbw] frames per bin of each tile (the scatter's input) */
@@ -152,6 +154,13 @@ struct ScatterBatch {
   uint32_t *index;          /* [n] */
   uint32_t *bin_off;        /* [nbins + 1] */
   uint32_t n, ntiles, tc, nchunks, nranges;
+  /* an rx batch's state for usn_finalize, in host-mapped memory (or null):
+   * [0] the launch tag, [1] summary flags, [2] USN_DIAG_LISTS when a chunk
+   * found inconsistent lists, [3] 1 when a tile listed frames for the host
+   * stage, [4..6] bin_off at the NIC, FLOOD and DROP bins, [7] the scan's
+   * diag word.  Written by the scatter (chunk 0; [2] by any chunk). */
+  uint32_t *rx_state;
+  const usn_summary *summary;
 };
 struct ScatterArgs {
   ScatterBatch b[USN_MAX_MULTI];

@@ -77,7 +77,7 @@ SUMMARY_DTYPE = np.dtype([("flags", "<u4"), ("first_break", "<u4"), ("n_frames",
                           ("n_tiles", "<u4"), ("cin_state", "<u4"), ("cin_dst", "<u4"),
                           ("cin_info", "<u4", (4,)), ("cout_state", "<u4"), ("cout_dst", "<u4"),
                           ("cout_info", "<u4", (4,)), ("n_ep", "<u4"), ("n_bins", "<u4"),
-                          ("_pad", "<u4", (2,))])
+                          ("host_epoch", "<u4"), ("_pad", "<u4")])
 RULE_DTYPE = np.dtype([("dst_addr", "<u4"), ("src_addr", "<u4"), ("dst_port", "<u2"),
                        ("src_port", "<u2"), ("protocol", "u1"), ("present", "u1"),
                        ("endpoint", "<u2")])
