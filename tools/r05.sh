@@ -77,6 +77,15 @@ case $S in
     bash tools/gpu.sh $S testsall || exit 1
     BENCH_ARGS="--steps 20 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05f)
+    # A/B: the chunk kernel with interleaved segments (a workgroup's waves
+    # read 512 consecutive frames at a time) against its tile-per-wave order
+    # and round 4's classify
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base ckinter nochunk" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="--frames 1048576 --multi 8 --batches 8 --rounds 5 --launches 30" ABL_VARIANTS="base ckinter nochunk" \
+      bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -2590,415 +2590,12 @@ static bool glds_layout(const MultiArgs &m) {
   return true;
 }
 
-#if USN_NTHREADS == 512
-/* ===========================================================================
- * classify_chunk_kernel: the rx classify of launches whose per-endpoint
- * lists take chunks of 8 tiles (c5's 2 x 8M rings, c4's 8 x 1M) and whose
- * rule image is read through the projection table U with U's and X's
- * displacements in LDS.  One workgroup per chunk of 8 tiles (the scatter's
- * chunk); wave w classifies tile w of the chunk ALONE, as 16 segments of 64
- * frames in a software pipeline:
- *   - segment k + 1's header DMA and lengths are issued before segment k is
- *     parsed, so they land under segment k's work;
- *   - segment k's U slot read flies while segment k - 1 is decided;
- * so in steady state a wave waits neither for a header nor for a probe
- * round trip, and no barrier separates its segments (classify_rx_kernel,
- * one tile per workgroup, waits for both once per tile and holds its slot
- * through two barriers: DESIGN §9, the U round trip was 17.5 of the probes'
- * 22 us per 16M frames).  The displacements are copied to LDS once per 8
- * tiles instead of once per tile.
- * The chunk's frames per bin are ONE LDS histogram, written out as one count
- * row per chunk (cnt[chunk][bin], u16): c5 writes 4.1 MB of rows per 16M
- * frames instead of 33, and the scan reads that much (scan_kernel with
- * rows_per_chunk = 1); the scatter ranks each tile itself
- * (scatter_kernel<8, false, true>).  Everything else is classify_rx_kernel's
- * output: decisions, tile headers, the summary, host lists (in frame order
- * within a tile here).
- * Waits: every vector-memory instruction of the pipeline is inline asm
- * (header DMA by builtin: no register result), issued unconditionally in a
- * fixed order per segment, so each `s_waitcnt vmcnt(N)` is a hand count
- * (checked on the ISA by tests/test_isa_waits.py); rare extra instructions
- * (host-list stores, X probes, IHL != 5 port reloads) only make a wait
- * stricter.  A batch's partial last tile runs the same steps with every wait
- * a drain (ck_tail).
- * =========================================================================== */
-#ifndef USN_CK_UNROLL   /* A/B: 1 = the 16 steps of a tile fully unrolled */
-#define USN_CK_UNROLL 1
-#endif
-#ifndef USN_CHUNK_KERNEL   /* A/B: 0 = classify_rx_kernel for every launch */
-#define USN_CHUNK_KERNEL 1
-#endif
-#define CK_SEGS (TILE / 64)
-#define CK_STAGE (64u * GLDS_PARTS)   /* 16-byte stage slots per wave: one segment */
-static_assert(CK_SEGS == 16 && NWAVES == 8, "classify_chunk_kernel: 8 waves x 16 segments");
-
-struct CkSeg {            // a segment between its U slot read and its decision: what the
-                          // decision needs of Parsed, packed (8 VGPRs held across a step)
-  uint32_t w0;            // status | frag_first << 3 | i0 << 8 (i0: 17 bits)
-  uint32_t src, dst, ports;
-  v4u32 s;                // the U slot (in flight until the decision's wait)
-};
-__device__ __forceinline__ void ck_unpack(const CkSeg &g, Parsed &p) {
-  p.status = g.w0 & 7u;
-  p.frag_first = (g.w0 >> 3) & 1u;
-  p.i0 = g.w0 >> 8;
-  p.src = g.src; p.dst = g.dst; p.ports = g.ports;
-  p.proto = (p.i0 >> 8) & 0xFFu;          // (IPv4 frames: the only ones whose decision reads
-  p.has_ports = (p.i0 >> 16) & 1u;        //  proto, has_ports and the ports)
-  p.sport = g.ports & 0xFFFFu;
-  p.dport = g.ports >> 16;
-}
-struct CkTile {           // what a wave keeps of its tile
-  uint32_t my_last;       // per lane: 1 + its last touching frame | touch << 16 (the frame's
-                          // info and decision are read again at the tile's end)
-  uint32_t n_nic, n_flood, n_drop, n_host;          // wave-uniform
-  uint32_t stale_on, first_break;                   // wave-uniform (tile 0 of a stale batch)
-};
-
-/* frames f0 .. f0+63 of the batch into this wave's stage (nv valid; lanes
- * past them re-read the last valid frame), the layout stage_read_asm reads */
-__device__ __forceinline__ void ck_glds(const ClassifyArgs &a, uint64_t f0, uint32_t nv, uint32_t lane,
-                                        uint4 *st) {
-#pragma unroll
-  for (uint32_t k = 0; k < GLDS_PARTS; ++k) {
-    const uint32_t u = 64 * k + lane;
-    const uint32_t f = u / GLDS_PARTS, p = u - GLDS_PARTS * f;
-    const uint32_t fl = f < nv ? f : nv - 1;
-    const uint8_t *src = a.frames + (f0 + fl) * a.stride + GLDS_OFF + p * 16;
-    __builtin_amdgcn_global_load_lds(src, (lds_void_t *)(st + 64 * k), 16, 0, GLDS_NT);
-  }
-}
-__device__ __forceinline__ uint32_t ck_len(const uint16_t *p) {   // one frame's length, in flight
-  uint32_t v;
-  asm volatile("global_load_ushort %0, %1, off" : "=&v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ void ck_store(uint32_t *p, uint32_t v) {
-  asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void ck_store_rare(uint32_t *p, uint32_t v) {   // isa_check: a rare path
-  asm volatile("global_store_dword %0, %1, off ; usn_rare" ::"v"(p), "v"(v) : "memory");
-}
-
-/* segment j's decision (its U slot has landed) and what follows from it:
- * the stale prefix of tile 0, the decision store, the chunk histogram, the
- * tile's class counts, host list and last touching frame */
-template <bool FULL>
-__device__ __forceinline__ void ck_decide(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
-                                          uint32_t *hist, const uint32_t *carry, uint64_t base,
-                                          uint32_t tile, uint32_t j, uint32_t nt, uint32_t lane,
-                                          const CkSeg &g, CkTile &t) {
-  const uint32_t local = j * 64 + lane;
-  const bool v = FULL || local < nt;
-  Parsed p;
-  ck_unpack(g, p);
-  uint32_t w1, w2;
-  bool x;
-  u_decode(g.s, p, u_key_e(p), w1, w2, x);
-  x = x && p.status == 1u;
-  if (!USN_ABL_NOX && __ballot(x)) {   // rare: the projection's further K1 rules (drains vmcnt)
-    const uint32_t wx = x_probe(T, Dl, a, p, x);
-    if (x) w1 = wx;
-  }
-  uint32_t dec = decide_rx_w(a, p, w1, w2);
-  // cache touch: 0 none (parse failure), 1 retains Some(info), 2 leaves None, 3 unknown
-  uint32_t touch = p.status == 0u ? 0u : p.status >= 4u ? 3u
-                 : (p.status == 1u && (p.dst >> 24) != 127u) ? 1u : 2u;
-  if (!v) touch = 0;
-  if (t.stale_on) {   // tile 0 of a batch whose carried cache went stale (wave-uniform, rare):
-    // frames before the first touching frame whose info differs take the
-    // cached decision (endpoint.rs:186-191; later fragments end it too)
-    const bool diff = touch && !(touch == 1u && p.i0 == carry[2] && p.src == carry[3] &&
-                                 p.dst == carry[4] && p.ports == carry[5]);
-    const uint64_t m = __ballot(diff);
-    const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-    if (v && lane < first && USN_DEC_REASON(dec) != USN_R_PARSE)
-      dec = (carry[1] & USN_PARITY_MASK) | USN_F_CACHE | (dec & (USN_F_HOST | USN_F_FRAG1 | USN_F_DHCP));
-    if (m) {
-      t.stale_on = 0;
-      t.first_break = j * 64 + first;
-    }
-  }
-  if (v) ck_store(a.decisions + base + local, dec);
-  const uint32_t b = dec_bin(dec, a.n_ep);
-  if (a.nbits <= 6) {   // few bins: one LDS add per distinct bin of the wave
-    const uint64_t same = match_bin(b, __ballot(v), a.nbits);
-    if (v && (same & lanemask_lt(lane)) == 0)
-      atomicAdd(&hist[b >> 1], (uint32_t)__popcll(same) << (16u * (b & 1u)));
-  } else if (v) {
-    atomicAdd(&hist[b >> 1], 1u << (16u * (b & 1u)));
-  }
-  const uint32_t c = USN_DEC_CLASS(dec);
-  t.n_nic += (uint32_t)__popcll(__ballot(v && c == USN_CLS_NIC));
-  t.n_flood += (uint32_t)__popcll(__ballot(v && c == USN_CLS_FLOOD));
-  t.n_drop += (uint32_t)__popcll(__ballot(v && c == USN_CLS_DROP));
-  const bool host = v && (dec & USN_F_HOST);
-  const uint64_t hm = __ballot(host);
-  if (hm) {   // rare: frames for the ordered host stage, in frame order
-    if (host)
-      ck_store_rare(a.host_list + (size_t)tile * TILE + t.n_host + (uint32_t)__popcll(hm & lanemask_lt(lane)),
-                    (uint32_t)(base + local));
-    t.n_host += (uint32_t)__popcll(hm);
-  }
-  if (touch) t.my_last = (local + 1) | (touch << 16);
-}
-
-/* segment k's parse and U slot read (its headers and length have landed in
- * the stage / `len`) */
-__device__ __forceinline__ void ck_probe(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
-                                         const uint4 (&q)[4], uint32_t len, const uint8_t *fp, CkSeg &g) {
-  Parsed p;
-  parse(q, len, fp, a.window, p);
-  const uint32_t e = u_key_e(p);
-  const PhKeyH ku = ph_hash(a.ph[2], p.dst, 0u, e, 0u);
-  const bool need = p.status == 1u;
-  const uint32_t du = lds_disp1(Dl, a.ph[2], need, ku);
-  asm_slot1(T, a.ph[2], need, ku, du, g.s);
-  g.w0 = p.status | (p.frag_first << 3) | (p.i0 << 8);
-  g.src = p.src; g.dst = p.dst; g.ports = p.ports;
-}
-
-/* one pipeline step of a full tile: WA = the vector-memory instructions
- * issued after segment k's headers and length (still in flight when they are
- * waited for), WE = those issued after segment k - 1's slot read */
-template <int WA, int WE, bool NEXT, bool PREV>
-__device__ __forceinline__ void ck_step(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
-                                        uint32_t *hist, const uint32_t *carry, uint64_t base,
-                                        uint32_t tile, uint32_t k, uint32_t lane, uint4 *st,
-                                        uint32_t &len, CkSeg &cur, CkSeg &prev, CkTile &t) {
-  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(len) : "n"(WA) : "memory");   // segment k landed
-  uint4 q[4];
-  stage_read_asm(st, lane, q);                        // (waits for its LDS reads)
-  const uint32_t lk = len;
-  if (NEXT) {                                         // segment k + 1: headers, length
-    ck_glds(a, base + (k + 1) * 64, 64, lane, st);
-    len = ck_len(a.lens + base + (k + 1) * 64 + lane);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  ck_probe(a, T, Dl, q, lk, a.frames + (base + k * 64 + lane) * a.stride, cur);
-  __builtin_amdgcn_sched_barrier(0);
-  if (PREV) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(prev.s) : "n"(WE) : "memory");   // slot k - 1 landed
-    ck_decide<true>(a, T, Dl, hist, carry, base, tile, k - 1, TILE, lane, prev, t);
-  }
-}
-
-template <int K>
-__device__ __forceinline__ void ck_steps(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
-                                         uint32_t *hist, const uint32_t *carry, uint64_t base,
-                                         uint32_t tile, uint32_t lane, uint4 *st, uint32_t &len,
-                                         CkSeg &prev, CkTile &t) {
-  // issued per step: [DMA k+1 (GLDS_PARTS), len k+1] [slot k] [store k-1]
-  constexpr int NX = 1 + GLDS_PARTS;
-  constexpr int WA = K == 0 ? 0 : K == 1 ? 1 : 2;                     // slot k-1 (+ store k-2)
-  constexpr int WE = (K >= 2 ? 1 : 0) + (K + 1 < CK_SEGS ? NX : 0) + 1;   // store k-2, next, slot k
-  CkSeg cur;
-  ck_step<WA, WE, (K + 1 < CK_SEGS), (K > 0)>(a, T, Dl, hist, carry, base, tile, K, lane, st, len,
-                                               cur, prev, t);
-  prev = cur;
-  if constexpr (K + 1 < CK_SEGS)
-    ck_steps<K + 1>(a, T, Dl, hist, carry, base, tile, lane, st, len, prev, t);
-}
-
-/* a batch's partial last tile: the same steps, every wait a drain */
-__device__ __forceinline__ void ck_tail(const ClassifyArgs &a, const uint4 *T, const uint16_t *Dl,
-                                     uint32_t *hist, const uint32_t *carry, uint64_t base,
-                                     uint32_t tile, uint32_t nt, uint32_t lane, uint4 *st, CkTile &t) {
-  const uint32_t nseg = (nt + 63) / 64;
-  for (uint32_t k = 0; k < nseg; ++k) {
-    const uint32_t nv = min(64u, nt - k * 64);
-    uint32_t len = ck_len(a.lens + base + k * 64 + min(lane, nv - 1));
-    ck_glds(a, base + k * 64, nv, lane, st);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(len) :: "memory");
-    uint4 q[4];
-    stage_read_asm(st, lane, q);
-    CkSeg g;
-    const uint32_t local = k * 64 + lane;
-    ck_probe(a, T, Dl, q, local < nt ? len : 0u,
-             a.frames + (base + min(local, nt - 1)) * a.stride, g);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(g.s) :: "memory");
-    ck_decide<false>(a, T, Dl, hist, carry, base, tile, k, nt, lane, g, t);
-  }
-}
-
-/* which batch chunk g belongs to (chunks of 8 tiles per batch) */
-__device__ __forceinline__ uint32_t ck_batch(const MultiArgs &m, uint32_t g, uint32_t &c) {
-  uint32_t bi = 0, cb = 0;
-  bool found = false;
-#pragma unroll
-  for (uint32_t k = 0; k < USN_MAX_MULTI; ++k) {
-    if (k < m.count && !found) {
-      const uint32_t nch = (m.tile_base[k + 1] - m.tile_base[k] + NWAVES - 1) / NWAVES;
-      if (g < cb + nch) { bi = k; found = true; }
-      else cb += nch;
-    }
-  }
-  c = g - cb;
-  return bi;
-}
-
-#ifndef USN_CK_WPE   /* waves per SIMD classify_chunk_kernel is compiled for (8: 64 VGPRs) */
-#define USN_CK_WPE 8
-#endif
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(USN_CK_WPE)))
-void classify_chunk_kernel(MultiArgs m) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ uint4 s_stage[NWAVES * CK_STAGE];
-  __shared__ uint32_t s_carry[8];
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Lds L = carve(smem, m.b[0].nbins, s_stage);
-  uint4 *st = s_stage + wave * CK_STAGE;
-  const uint4 *T = m.b[0].table;
-  // U's and X's displacements -> LDS (once per chunk of 8 tiles)
-  {
-    const uint32_t u0 = m.b[0].u_disp_unit, units = m.b[0].u_end_unit - u0;
-    for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
-      const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
-      __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
-    }
-  }
-  const uint16_t *Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)m.b[0].u_disp_unit * 8;
-  uint32_t chunk;
-  const uint32_t bi = ck_batch(m, blockIdx.x, chunk);
-  const ClassifyArgs &a = m.b[bi];
-  const uint32_t tile = chunk * NWAVES + wave;
-  const bool mine = tile < a.ntiles;
-  const uint64_t base = (uint64_t)tile * TILE;
-  const uint32_t nt = mine ? (uint32_t)min((uint64_t)TILE, a.n - base) : 0u;
-  const bool full = nt == TILE;
-  // segment 0 of a full tile in flight before the barrier
-  uint32_t len = 0;
-  if (full) {
-    ck_glds(a, base, 64, lane, st);
-    len = ck_len(a.lens + base + lane);
-  }
-  hist_zero(L.hist, a.nbw);
-  __syncthreads();   // the displacements, the zeroed histogram (and segment 0) have landed
-  // carried-in cache of the batch (its chunk 0, every thread): the stale check
-  if (chunk == 0) {
-    resolve_carry(a, s_carry, L.scratch);
-    if (tid == 0) {
-      const uint32_t cst = s_carry[0], dst = s_carry[1];
-      uint32_t flags = 0;
-      if ((cst & USN_CS_VALID) &&
-          ((decide_info_rx<TM_DISPLDS>(T, Dl, a, s_carry + 2) ^ dst) & USN_PARITY_MASK))
-        flags |= USN_S_STALE;
-      s_carry[6] = flags;
-      usn_summary *S = a.summary;
-      S->cin_state = cst; S->cin_dst = dst;
-      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
-      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
-      S->n_ep = a.n_ep; S->n_bins = a.nbins;
-    }
-    __syncthreads();
-  }
-  const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
-  CkTile t;
-  t.my_last = 0;
-  t.n_nic = t.n_flood = t.n_drop = t.n_host = 0;
-  t.stale_on = stale ? 1u : 0u;
-  t.first_break = TILE;
-  const uint32_t *carry = s_carry;   // (read in the rare stale steps only)
-  if (full) {
-    CkSeg prev;
-#if USN_CK_UNROLL
-    ck_steps<0>(a, T, Dl, L.hist, carry, base, tile, lane, st, len, prev, t);
-#else
-    // steps 0 and 1, the steady steps 2..13 as a loop over pairs (the two
-    // segments' states alternate between x0 and x1: nothing in flight is
-    // copied at the back edge; a 16-fold unroll hoisted addresses and spilled
-    // 84 SGPRs), steps 14 and 15
-    constexpr int NX = 1 + GLDS_PARTS;
-    CkSeg x1;
-    ck_step<0, 0, true, false>(a, T, Dl, L.hist, carry, base, tile, 0, lane, st, len, prev, x1, t);
-    ck_step<1, NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, 1, lane, st, len, x1, prev, t);
-    for (uint32_t k = 2; k + 2 < CK_SEGS; k += 2) {
-      ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, k, lane, st, len, prev, x1, t);
-      ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, k + 1, lane, st, len, x1, prev, t);
-    }
-    ck_step<2, 1 + NX + 1, true, true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 2, lane, st, len, prev, x1, t);
-    ck_step<2, 2, false, true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, lane, st, len, x1, prev, t);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(x1.s) :: "memory");   // slot 15 (store 14 after it)
-    ck_decide<true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, TILE, lane, x1, t);
-#endif
-#if USN_CK_UNROLL
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(prev.s) :: "memory");   // slot 15 (store 14 after it)
-    ck_decide<true>(a, T, Dl, L.hist, carry, base, tile, CK_SEGS - 1, TILE, lane, prev, t);
-#endif
-  } else if (mine) {
-    ck_tail(a, T, Dl, L.hist, carry, base, tile, nt, lane, st, t);
-  }
-  if (mine) {   // the tile header
-    const uint32_t my = t.my_last & 0xFFFFu, my_touch = t.my_last >> 16;
-    uint32_t mx = my;
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-    usn_tile_hdr *H = a.tiles + tile;
-    if (mx && my == mx) {   // one lane: its frame's info parsed again, its decision read back
-      const uint64_t f = base + mx - 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the decision stores have landed)
-      const uint8_t *fp = a.frames + f * a.stride;
-      uint4 q[4];
-      lane_round(fp, q);
-      Parsed p;
-      parse(q, a.lens[f], fp, a.window, p);
-      H->last_state = USN_TS_HAS | (my_touch == 1u ? USN_TS_RETAINED : 0u) |
-                      (my_touch == 3u ? USN_TS_UNKNOWN : 0u);
-      H->last_dst = a.decisions[f] & USN_PARITY_MASK;
-      H->last_info[0] = p.i0; H->last_info[1] = p.src; H->last_info[2] = p.dst; H->last_info[3] = p.ports;
-      H->last_idx = (uint32_t)f;
-    }
-    if (lane == 0) {
-      if (t.n_host) a.summary->host_epoch = a.epoch;   // (usn_finalize's rx state)
-      H->n_frames = (uint16_t)nt;
-      H->_r0 = 0;
-      H->n_host = (uint16_t)t.n_host;
-      H->bin_nic = (uint16_t)a.n_ep;
-      H->class_count[0] = (uint16_t)t.n_drop;
-      H->class_count[2] = (uint16_t)t.n_nic;
-      H->class_count[3] = (uint16_t)t.n_flood;
-      H->class_count[1] = (uint16_t)(nt - t.n_nic - t.n_flood - t.n_drop);
-      if (!mx) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
-      if (tile == 0) {
-        uint32_t f = s_carry[6];
-        if (stale) {
-          const uint32_t first = t.stale_on ? TILE : t.first_break;
-          if (first >= nt && a.n > TILE) f |= USN_S_STALE_EXTENDS;
-          a.summary->first_break = first;
-        } else {
-          a.summary->first_break = 0xFFFFFFFFu;
-        }
-        a.summary->flags = f;
-      }
-    }
-  }
-  __syncthreads();   // every wave's histogram adds
-  hist_out(L.hist, a.nbw, a.cnt + (size_t)chunk * a.nbw);   // the chunk's count row
-}
-#endif  // USN_NTHREADS == 512
-
-hipError_t launch_classify(const MultiArgs &m, hipStream_t stream, bool *chunk_rows) {
-  if (chunk_rows) *chunk_rows = false;
+hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
   const uint32_t tiles = m.tile_base[m.count];
   if (tiles == 0) return hipSuccess;
   const ClassifyArgs &a = m.b[0];   // table and bins are shared by every batch
   const int tm = table_mode(a);
   const bool glds = USN_GLDS_ENABLE && glds_layout(m);
-#if USN_NTHREADS == 512
-  // the pipelined chunk kernel: lists in chunks of 8 tiles, the image read
-  // through U with U's and X's displacements in LDS, dense slots
-  if (m.chunk_tc == NWAVES && chunk_rows && glds && tm == TM_DISPLDS && (a.probe_mask & 4u) &&
-      USN_CHUNK_KERNEL) {
-    uint32_t chunks = 0;
-    for (uint32_t k = 0; k < m.count; ++k)
-      chunks += (m.tile_base[k + 1] - m.tile_base[k] + NWAVES - 1) / NWAVES;
-    const size_t lds = lds_core_bytes(a.nbins, false) + table_lds_bytes(disp_lds_units(a));
-    hipLaunchKernelGGL(classify_chunk_kernel, dim3(chunks), dim3(NTHREADS), lds, stream, m);
-    *chunk_rows = true;
-    return hipGetLastError();
-  }
-#endif
   const size_t lds = lds_core_bytes(a.nbins, !glds) +
                      (tm == TM_LDS ? table_lds_bytes(a.table_units)
                       : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
@@ -3080,9 +2677,7 @@ __device__ __forceinline__ void scan_put(unsigned long long *g, uint32_t epoch, 
  *     writes tot.  (Bin bases here too, handed on between bin blocks, cost
  *     the scan's last ranges one more round trip: 15.4 against 13.9 us for
  *     c5, more than the scatter's block scan they saved, profiles/r03.) */
-template <int CPT, int RPC>   // chunks per thread: a range is 16 * CPT chunks; count rows per
-                              // chunk: up to 8 (a row per tile) or 1 (classify_chunk_kernel's
-                              // row per chunk)
+template <int CPT>   // chunks per thread: a range is 16 * CPT chunks
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   __shared__ uint32_t s_t[16][USN_SCAN_BLK];
   __shared__ uint32_t s_c[4][USN_SCAN_BLK];
@@ -3096,14 +2691,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
   const uint32_t c0 = r * 16 * CPT + rg * CPT;              // this thread's CPT chunks
   // 1.
-  uint2 v[CPT][RPC];
-  const uint32_t rpc = RPC == 1 ? 1u : s.tc, nrows = RPC == 1 ? B.nchunks : B.ntiles;
+  uint2 v[CPT][8];
 #pragma unroll
   for (uint32_t j = 0; j < CPT; ++j)
 #pragma unroll
-    for (uint32_t w = 0; w < RPC; ++w) {
-      const uint32_t t = (c0 + j) * rpc + w;
-      const bool ok = binok && w < rpc && t < nrows;
+    for (uint32_t w = 0; w < 8; ++w) {
+      const uint32_t t = (c0 + j) * s.tc + w;
+      const bool ok = binok && w < s.tc && t < B.ntiles;
       v[j][w] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
     }
   uint32_t ex[CPT][4], tot[4] = {0, 0, 0, 0};
@@ -3111,7 +2705,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   for (uint32_t j = 0; j < CPT; ++j) {
     uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t w = 0; w < RPC; ++w) {
+    for (uint32_t w = 0; w < 8; ++w) {
       a[0] += v[j][w].x & 0xFFFFu; a[1] += v[j][w].x >> 16;
       a[2] += v[j][w].y & 0xFFFFu; a[3] += v[j][w].y >> 16;
     }
@@ -3222,11 +2816,8 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                              frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
 #define USN_SCATTER_WPE 6
 #endif
-template <int TC, bool SELF, bool HIST>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU
-                                          // at most: registers for the row sums instead of
-                                          // occupancy).  HIST: the count rows are per chunk
-                                          // (classify_chunk_kernel): each wave counts its own
-                                          // tile's frames per bin first (1c)
+template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
+                               // registers for the row sums instead of occupancy)
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(SELF ? 2 : USN_SCATTER_WPE)))
 void scatter_kernel(ScatterArgs s) {
   static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
@@ -3261,20 +2852,17 @@ void scatter_kernel(ScatterArgs s) {
   const bool selfscan = SELF && pair;   // the scan's sums done here (USN_SCF_SELFSCAN)
   if (selfscan) {   // the sums zeroed before any load is in flight (the barrier waits for none)
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);
-    for (uint32_t i = tid; i < (HIST ? 3u : 2u) * s.nbw; i += NTHREADS) sa[i] = 0;
+    for (uint32_t i = tid; i < 2 * s.nbw; i += NTHREADS) sa[i] = 0;
     __syncthreads();
   }
-  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0), vn = make_uint2(0, 0);
+  uint2 vt = make_uint2(0, 0), ve = make_uint2(0, 0);
   uint32_t rc[TC];
   if (mine && !noscan && !selfscan) {
     vt = *reinterpret_cast<const uint2 *>(B.tot + 2 * tid);
     ve = *reinterpret_cast<const uint2 *>(ex + 2 * tid);
-    // (HIST checks: the next chunk's offsets must be this chunk's plus its counts)
-    if (HIST && USN_SC_CHECKS && c + 1 < B.nchunks)
-      vn = *reinterpret_cast<const uint2 *>(ex + s.nbw + 2 * tid);
   }
 #pragma unroll
-  for (uint32_t w = 0; w < TC && !HIST; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
+  for (uint32_t w = 0; w < TC; ++w) {   // count rows of the chunk's tiles (bins 2 tid, 2 tid + 1)
     const uint32_t t = t0 + min(w, ntc - 1);
     rc[w] = mine ? reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw)[tid] : 0u;
     if (w >= ntc) rc[w] = 0;
@@ -3293,31 +2881,26 @@ void scatter_kernel(ScatterArgs s) {
   if (selfscan) {
     uint32_t *sa = reinterpret_cast<uint32_t *>(cur + (size_t)TC * s.nbw);   // [nbw] totals (zeroed above)
     uint32_t *sb = sa + s.nbw;                                                // [nbw] before the chunk
-    uint32_t *so = sb + s.nbw;                     // [nbw] (HIST) the chunk's own row: checked
-    // the batch's rows: per tile, or (HIST) per chunk
-    const uint32_t nrows = HIST ? B.nchunks : B.ntiles, r0 = HIST ? c : t0, r1 = HIST ? c + 1 : t0 + ntc;
     const uint32_t nq = s.nbw / 8, G = NTHREADS / nq, qq = tid % nq, g = tid / nq;
     if (g < G) {
       const uint4 *rows = reinterpret_cast<const uint4 *>(B.cnt) + qq;   // row t: rows[t * nq]
       uint32_t at[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      uint32_t ao[HIST ? 8 : 1] = {0};
-      for (uint32_t t = g; t < nrows; t += 8 * G) {
+      for (uint32_t t = g; t < B.ntiles; t += 8 * G) {
         uint4 v[8];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
           const uint32_t tt = t + k * G;
-          v[k] = tt < nrows ? rows[(size_t)tt * nq] : make_uint4(0, 0, 0, 0);
+          v[k] = tt < B.ntiles ? rows[(size_t)tt * nq] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
           const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const bool before = t + k * G < r0, own = !before && t + k * G < r1;
+          const bool before = t + k * G < t0;
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
             at[2 * j] += lo; at[2 * j + 1] += hi;
             if (before) { ab[2 * j] += lo; ab[2 * j + 1] += hi; }
-            if (HIST && own) { ao[2 * j] += lo; ao[2 * j + 1] += hi; }
           }
         }
       }
@@ -3325,55 +2908,13 @@ void scatter_kernel(ScatterArgs s) {
       for (uint32_t j = 0; j < 8; ++j) {
         if (at[j]) atomicAdd(&sa[8 * qq + j], at[j]);
         if (ab[j]) atomicAdd(&sb[8 * qq + j], ab[j]);
-        if (HIST && ao[j]) atomicAdd(&so[8 * qq + j], ao[j]);
       }
     }
     __syncthreads();
     if (mine) {
       vt = make_uint2(sa[2 * tid], sa[2 * tid + 1]);
       ve = make_uint2(sb[2 * tid], sb[2 * tid + 1]);
-      if (HIST) vn = make_uint2(ve.x + so[2 * tid], ve.y + so[2 * tid + 1]);   // (HIST checks)
     }
-  }
-  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
-  // bad: a decision naming a bin past the batch's bins, a rank past the
-  // chunk, an empty stage slot or a list position past n -- the count rows
-  // and the decisions disagree.  Every access stays in bounds regardless, and
-  // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
-  bool bad = false;
-  // 1c. (HIST) each wave ranks its tile's frames on its own zeroed counters
-  // (one LDS atomic per frame, segment by segment, lanes in lane order -- see
-  // 3.): the returned value is the frame's rank among its tile's frames of
-  // its bin, and the counters end as the tile's count row
-  uint32_t pk[HIST ? SEGS : 1];   // bin << 16 | rank in the tile
-  if (HIST) {
-    uint4 *c4 = reinterpret_cast<uint4 *>(cur);
-    for (uint32_t q4 = tid; q4 < TC * s.nbw / 8; q4 += NTHREADS) c4[q4] = make_uint4(0, 0, 0, 0);
-    if (USN_SC_CHECKS) {   // every stage slot starts empty (checked at the write-out)
-      uint4 *st4 = reinterpret_cast<uint4 *>(stage);
-#pragma unroll
-      for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < SEGS; ++k) pk[k] = 0;
-    if (wave < ntc && USN_ABL_SC != 4) {
-      uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
-#pragma unroll
-      for (uint32_t k = 0; k < SEGS; ++k) {
-        const uint32_t raw = dec_bin(d[k], s.n_ep);
-        const uint32_t b = min(raw, s.nbins - 1u);
-        const uint32_t sh = 16u * (b & 1u);
-        const bool v = k * 64 + lane < tn;
-        const uint32_t r = v ? (atomicAdd(&cw[b >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
-        pk[k] = (b << 16) | r;
-        bad |= v && raw >= s.nbins;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t w = 0; w < TC; ++w)   // the tiles' counts (bins 2 tid, 2 tid + 1)
-      rc[w] = mine ? reinterpret_cast<const uint32_t *>(cur + (size_t)w * s.nbw)[tid] : 0u;
   }
   // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
@@ -3381,12 +2922,6 @@ void scatter_kernel(ScatterArgs s) {
 #pragma unroll
     for (uint32_t w = 0; w < TC; ++w) { c0 += rc[w] & 0xFFFFu; c1 += rc[w] >> 16; }
     if (noscan) vt = make_uint2(c0, c1);
-    // HIST: the lists depend on the count rows only through the scan's sums;
-    // those must agree with the decisions (this chunk's counts, just taken)
-    if (HIST && USN_SC_CHECKS && mine && !noscan) {
-      const uint2 want = (selfscan || c + 1 < B.nchunks) ? vn : vt;
-      bad |= want.x != ve.x + c0 || want.y != ve.y + c1;
-    }
     uint32_t total;
     const uint32_t pt = block_excl_scan(vt.x + vt.y, s_scan, &total);
     const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
@@ -3417,20 +2952,13 @@ void scatter_kernel(ScatterArgs s) {
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
     uint32_t st = 0, sc = 0;
-    // (HIST: cur holds the tiles' counts until this thread's bins get their seeds)
-    auto cnt_of = [&](uint32_t w, uint32_t b) -> uint32_t {
-      return HIST ? (uint32_t)cur[(size_t)w * s.nbw + b]
-                  : (w < ntc ? (uint32_t)B.cnt[(size_t)(t0 + w) * s.nbw + b] : 0u);
-    };
     for (uint32_t k = 0; k < per; ++k) {
       const uint32_t b = b0 + k;
       if (b >= s.nbw) break;
       uint32_t cb = 0;
-      for (uint32_t w = 0; w < ntc; ++w) cb += cnt_of(w, b);
+      for (uint32_t w = 0; w < ntc; ++w) cb += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       sc += cb;
       st += noscan ? cb : B.tot[b];
-      if (HIST && USN_SC_CHECKS && !noscan && !selfscan)
-        bad |= (c + 1 < B.nchunks ? ex[s.nbw + b] : B.tot[b]) != ex[b] + cb;
     }
     uint32_t total;
     uint32_t pt = block_excl_scan(st, s_scan, &total);
@@ -3443,20 +2971,19 @@ void scatter_kernel(ScatterArgs s) {
       if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
       if (c == 0 && B.rx_state && b >= s.n_ep && b < s.n_ep + 3) B.rx_state[4 + b - s.n_ep] = pt;
       if (noscan) {
-        for (uint32_t w = 0; w < ntc; ++w) pt += cnt_of(w, b);
+        for (uint32_t w = 0; w < ntc; ++w) pt += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       } else {
         pt += B.tot[b];
       }
       for (uint32_t w = 0; w < TC; ++w) {
-        const uint32_t cw_ = w < ntc ? cnt_of(w, b) : 0u;
         cur[(size_t)w * s.nbw + b] = (uint16_t)pc;
-        pc += cw_;
+        if (w < ntc) pc += B.cnt[(size_t)(t0 + w) * s.nbw + b];
       }
     }
   }
   // every stage slot starts empty: a slot still empty at the write-out means
   // the count rows disagree with the decisions (reported, never hidden)
-  if (USN_SC_CHECKS && !HIST) {
+  if (USN_SC_CHECKS) {
     uint4 *st4 = reinterpret_cast<uint4 *>(stage);
 #pragma unroll
     for (uint32_t q4 = tid; q4 < TC * TILE / 4; q4 += NTHREADS) st4[q4] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -3485,17 +3012,13 @@ void scatter_kernel(ScatterArgs s) {
   // out of order).  That is not an ISA guarantee, so step 4 verifies the
   // stage and a chunk that is not stably sorted is ranked again the
   // ballot way (5).
-  if (HIST && wave < ntc && USN_ABL_SC != 4) {
-    // the cursors now hold each wave's seeds: slot = seed + rank in the tile
-    const uint16_t *cw = cur + (size_t)wave * s.nbw;
-#pragma unroll
-    for (uint32_t k = 0; k < SEGS; ++k)
-      if (k * 64 + lane < tn) {
-        const uint32_t b = pk[k] >> 16, q = (uint32_t)cw[b] + (pk[k] & 0xFFFFu);
-        bad |= q >= nf;
-        stage[min(q, TC * TILE - 1u)] = (b << 16) | (wave * TILE + k * 64 + lane);
-      }
-  } else if (!HIST && wave < ntc && USN_ABL_SC != 4) {
+  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  // bad: a decision naming a bin past the batch's bins, a rank past the
+  // chunk, an empty stage slot or a list position past n -- the count rows
+  // and the decisions disagree.  Every access stays in bounds regardless, and
+  // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
+  bool bad = false;
+  if (wave < ntc && USN_ABL_SC != 4) {
     uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
     uint32_t at[SEGS];   // (the bins are recomputed below: 16 VGPRs fewer while the atomics fly)
 #pragma unroll
@@ -3567,10 +3090,8 @@ void scatter_kernel(ScatterArgs s) {
     // ballots segment by segment, the stage out again
     if (wave < ntc) {
       uint16_t *cw = cur + (size_t)wave * s.nbw;
-      if (!HIST) {   // (HIST: the cursors were never advanced, they are the seeds)
-        const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
-        for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
-      }
+      const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
+      for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
 #pragma unroll
       for (uint32_t k = 0; k < SEGS; ++k) {
         const uint32_t local = k * 64 + lane;
@@ -3614,30 +3135,20 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  const bool hist = (s.flags & USN_SCF_CHUNKROWS) != 0;   // rows per chunk: the scatter counts tiles
-  if (hist && s.tc != NWAVES) return hipErrorInvalidValue;   // classify_chunk_kernel's chunks
-  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch ((int)s.cpt * (hist ? -1 : 1)) {
-    case 4: hipLaunchKernelGGL((scan_kernel<4, 8>), sg, sb, 0, stream, s); break;
-    case 2: hipLaunchKernelGGL((scan_kernel<2, 8>), sg, sb, 0, stream, s); break;
-    case 1: hipLaunchKernelGGL((scan_kernel<1, 8>), sg, sb, 0, stream, s); break;
-    case -4: hipLaunchKernelGGL((scan_kernel<4, 1>), sg, sb, 0, stream, s); break;
-    case -2: hipLaunchKernelGGL((scan_kernel<2, 1>), sg, sb, 0, stream, s); break;
-    case -1: hipLaunchKernelGGL((scan_kernel<1, 1>), sg, sb, 0, stream, s); break;
+  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
+    case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
+    case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
+    case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;
     default: return hipErrorInvalidValue;
   }
-  const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0, hist);
+  const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0);
   const dim3 g(chunks), b(NTHREADS);
   const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
 #define USN_SC_LAUNCH(TC_)                                                              \
   do {                                                                                  \
-    if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true, false>), g, b, lds, stream, s);  \
-    else hipLaunchKernelGGL((scatter_kernel<TC_, false, false>), g, b, lds, stream, s);      \
+    if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);    \
+    else hipLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, s);        \
   } while (0)
-  if (hist) {
-    if (self) hipLaunchKernelGGL((scatter_kernel<NWAVES, true, true>), g, b, lds, stream, s);
-    else hipLaunchKernelGGL((scatter_kernel<NWAVES, false, true>), g, b, lds, stream, s);
-    return hipGetLastError();
-  }
   switch (s.tc) {
     case 8: USN_SC_LAUNCH(8); break;
     case 4: USN_SC_LAUNCH(4); break;

@@ -554,7 +554,6 @@ struct usn_ctx {
    * scratch, count rows and lists keep the bins it was classified with) */
   struct BatchRec {
     uint32_t rep, nbins;
-    bool chunk_rows;        // one count row per chunk (classify_chunk_kernel)
     uint32_t slot, epoch;   // its rx state slot (RX_SLOTS: none) and launch tag
   };
   std::unordered_map<const void *, BatchRec> batch_rep;
@@ -2325,12 +2324,13 @@ static usn::ScatterPlan plan_lists(usn_ctx *c, const usn::ClassifyArgs *as, uint
 }
 
 /* the per-endpoint scatter of `count` classified batches (after their
- * classify / tx launch, or after finalize recounted patched tiles);
- * chunk_rows: the classify wrote one count row per chunk of 8 tiles */
+ * classify / tx launch, or after finalize recounted patched tiles); epoch:
+ * the launch's tag when its classify took one; rx_state: the batches' state
+ * slots for usn_finalize (host-mapped) */
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
                           uint32_t count, hipStream_t s, uint32_t *txs_out = nullptr,
-                          const uint32_t *txs_counters = nullptr, bool chunk_rows = false,
-                          uint32_t epoch = 0, uint32_t *const *rx_state = nullptr) {
+                          const uint32_t *txs_counters = nullptr, uint32_t epoch = 0,
+                          uint32_t *const *rx_state = nullptr) {
   usn::ScatterArgs x;
   std::memset(&x, 0, sizeof x);
   x.count = count;
@@ -2340,11 +2340,10 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.nbits = as[0].nbits;
   const usn::ScatterPlan pl = plan_lists(c, as, count);
   const uint32_t tc = pl.tc;
-  if (chunk_rows && tc != 8) return USN_EINVAL;   // (the classify took its chunks from this plan)
   x.tc = tc;
   static const bool slow_rank = test_knob("USN_SCATTER_SLOW_RANK") != nullptr;
   x.flags = (slow_rank ? USN_SCF_SLOW_RANK : 0u) | (pl.noscan ? USN_SCF_NOSCAN : 0u) |
-            (pl.selfscan ? USN_SCF_SELFSCAN : 0u) | (chunk_rows ? USN_SCF_CHUNKROWS : 0u);
+            (pl.selfscan ? USN_SCF_SELFSCAN : 0u);
   x.nbb = (x.nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   x.cpt = pl.cpt;
   x.txs_out = txs_out;
@@ -2607,7 +2606,6 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
   uint32_t slot = 0;
-  bool chunk_rows = false;   // the classify wrote one count row per chunk of 8 tiles
   uint32_t epoch = 0;        // rx: the launch tag (classify and lists)
   uint32_t rx_slot[USN_MAX_MULTI];
   uint32_t *rx_state[USN_MAX_MULTI];
@@ -2670,14 +2668,10 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       rx_state[k] = d_rx + rx_slot[k] * 8;
       m.b[k].epoch = epoch;
     }
-    // chunks of 8 tiles for the lists let the classify write a row per chunk
-    const usn::ScatterPlan pl = plan_lists(c, m.b, count);
-    m.chunk_tc = (pl.tc == 8 && (!pl.selfscan || usn::scatter_lds(m.b[0].nbins, 8, true, true) <= 64u * 1024u))
-                     ? 8u : 0u;
     if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
-      HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream, &chunk_rows));   // large table in L2
+      HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
     else
-      HIPCHK(usn::launch_classify(m, (hipStream_t)stream, &chunk_rows));
+      HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
   }
   if (tx || !c->lists_async) {
     uint32_t *txs = nullptr;
@@ -2694,7 +2688,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
     }
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
-                            chunk_rows, epoch, tx ? nullptr : rx_state);
+                            epoch, tx ? nullptr : rx_state);
     if (st) return st;
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
@@ -2709,7 +2703,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (!R.classified) HIPCHK(hipEventCreateWithFlags(&R.classified, hipEventDisableTiming));
     HIPCHK(hipEventRecord(R.classified, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(R.side, R.classified, 0));
-    int st = launch_scatter(c, m.b, r, count, R.side, nullptr, nullptr, chunk_rows, epoch, rx_state);
+    int st = launch_scatter(c, m.b, r, count, R.side, nullptr, nullptr, epoch, rx_state);
     if (st) return st;
     for (uint32_t k = 0; k < count; ++k) {
       usn_ctx::ListsEv &le = c->lists_ev[r[k].decisions];
@@ -2739,7 +2733,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
     c->batch_rep[r[k].decisions] =
-        usn_ctx::BatchRec{rep, m.b[k].nbins, chunk_rows, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch};
+        usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch};
   }
   return USN_OK;
 }
@@ -3468,11 +3462,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
    * bins the batch was classified with -- unless a decision of the host stage
    * names an endpoint added since (then every tile, with today's bins) */
   const uint32_t nb = new_ep ? c->n_ep + 3 : nb0;   // <= max_bins: checked before any side effect
-  // a batch classified with a count row per chunk gets a row per tile again:
-  // every tile is recounted once any is (the relaunch's scan reads tile rows)
-  const bool chunk_rows = br != c->batch_rep.end() && br->second.chunk_rows;
-  if (nb != nb0 || (chunk_rows && std::find(dirty.begin(), dirty.end(), 1) != dirty.end()))
-    std::fill(dirty.begin(), dirty.end(), 1);
+  if (nb != nb0) std::fill(dirty.begin(), dirty.end(), 1);
   ClassifyArgs a;
   fill_args(c, c->reps[rep], b, r, a);
   set_bins(r, b->n, nb, a);
@@ -3494,7 +3484,6 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   out.n_ep = nb - 3;
   out.n_bins = nb;
   if (nb != nb0) c->batch_rep[r->decisions].nbins = nb;
-  if (any) c->batch_rep[r->decisions].chunk_rows = false;
   out.flags |= USN_S_COUT;
   out.cout_state = cs.valid ? USN_CS_VALID : 0u;
   out.cout_dst = cs.dst;
@@ -3519,9 +3508,7 @@ int usn_debug_scatter(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t co
   HIPCHK(hipSetDevice(R.device));
   usn::ClassifyArgs as[USN_MAX_MULTI];
   for (uint32_t k = 0; k < count; ++k) fill_args(c, R, &b[k], &r[k], as[k]);
-  const auto br = c->batch_rep.find(r[0].decisions);   // the rows the classify left
-  const bool chunk_rows = br != c->batch_rep.end() && br->second.chunk_rows;
-  return launch_scatter(c, as, r, count, (hipStream_t)stream, nullptr, nullptr, chunk_rows);
+  return launch_scatter(c, as, r, count, (hipStream_t)stream);
 }
 
 /* diagnostics: scatter chunks on the selected replica's device whose

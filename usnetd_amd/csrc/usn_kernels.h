@@ -68,8 +68,6 @@ struct MultiArgs {
   ClassifyArgs b[USN_MAX_MULTI];
   uint32_t tile_base[USN_MAX_MULTI + 1];
   uint32_t count;
-  uint32_t chunk_tc;   /* the lists' chunk length for this launch (scatter_plan): 8 lets the
-                          launch write one count row per chunk (classify_chunk_kernel) */
 };
 static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 
@@ -120,10 +118,7 @@ hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 size_t classify_lds_bytes(uint32_t nbins, uint32_t table_units, bool table_in_lds, bool glds);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
 
-/* *chunk_rows (when not null): the launch wrote one count row per chunk of 8
- * tiles (classify_chunk_kernel; m.chunk_tc == 8 asks for it), else one per
- * tile */
-hipError_t launch_classify(const MultiArgs &m, hipStream_t stream, bool *chunk_rows = nullptr);
+hipError_t launch_classify(const MultiArgs &m, hipStream_t stream);
 /* Recount the bin rows and class counts of tiles [t0, t1) from the (patched)
  * decisions (the scatter then runs again). */
 hipError_t launch_recount(const ClassifyArgs &a, uint32_t t0, uint32_t t1, hipStream_t stream);
@@ -186,9 +181,6 @@ struct ScatterArgs {
 #define USN_SCF_SELFSCAN 4u    /* a small launch (every chunk resident at once, few count-row
                                   bytes per batch): no scan launch; each chunk sums its batch's
                                   count rows itself (the totals, and the tiles before it) */
-#define USN_SCF_CHUNKROWS 8u   /* the count rows are one per chunk of 8 tiles (classify_chunk_kernel):
-                                  the scan reads a row per chunk, the scatter counts each tile's
-                                  frames per bin itself */
 #define USN_SCF_SLOW_RANK 1u   /* test hook (USN_SCATTER_SLOW_RANK=1): every chunk also ranks the
                                   ballot way and writes its stage out again */
 /* The scatter kernel's chunk length (tc tiles, one wave each) for nbins
@@ -196,10 +188,9 @@ struct ScatterArgs {
  * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 (| self-scan sums
  * nbw x 8) -- fits 64 KiB. */
 struct ScatterShape { uint32_t tc; size_t lds; };
-inline size_t scatter_lds(uint32_t nbins, uint32_t tc, bool selfscan = false, bool chunk_rows = false) {
+inline size_t scatter_lds(uint32_t nbins, uint32_t tc, bool selfscan = false) {
   const size_t nbw = (nbins + 7u) & ~7u;
-  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 +
-         (selfscan ? nbw * (chunk_rows ? 12 : 8) : 0);
+  return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 + (selfscan ? nbw * 8 : 0);
 }
 inline ScatterShape scatter_shape(uint32_t nbins) {
   for (uint32_t tc : {8u, 4u, 2u})
@@ -227,7 +218,7 @@ uint32_t *scatter_diag(void *scratch, uint64_t cap, uint32_t nbins);
 /* the same kernels at 512 threads per tile (a second compilation of
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
-hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream, bool *chunk_rows = nullptr);
+hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
 hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream);
 uint32_t scatter_fallbacks();   /* chunks the scatter ranked again (current device) */
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
