@@ -329,7 +329,11 @@ int usn_set_lists_async(usn_ctx *ctx, int on);
 int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
 
 /* Ordered host stage for one classified batch (synchronises the stream; for
- * a tx batch, waits for that batch's own launches only).
+ * a tx batch, waits for that batch's own launches only, and `hip_stream` must
+ * be the stream the batch was classified on: else USN_EINVAL).  A NIC batch
+ * with nothing for the host stage (no stale carried cache, no frame listed)
+ * reads only the few words its scatter left in host-mapped memory: about one
+ * microsecond of host time.
  * Resolves fragments, DHCP steering, stale cache prefixes and tx learning in
  * frame order and patches decisions and the per-endpoint lists on the device.  Must be called
  * before the next usn_classify of the same source whenever the summary has
@@ -343,7 +347,12 @@ int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
  * (summary n_bins) when endpoints were added since; only a host-stage
  * decision naming such an endpoint rebuilds its lists with today's bins
  * (summary n_ep / n_bins updated).  USN_ERANGE, before any side effect: the
- * batch needs the host stage and today's bins exceed the result's max_bins. */
+ * batch needs the host stage and today's bins exceed the result's max_bins
+ * (a result sized by usn_result_bytes_ep for fewer endpoints than the context
+ * has by then).  This is decided before the host stage runs, so it holds even
+ * when no resolved decision would name a new endpoint; the batch cannot be
+ * finalized into that result -- classify the ring again into a result sized
+ * by usn_result_bytes (any endpoint count never gets USN_ERANGE). */
 int usn_finalize(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream,
                  usn_finalize_info *info);
 

@@ -3300,6 +3300,8 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   if (c->eps[b->src_endpoint].used && c->eps[b->src_endpoint].kind != USN_EP_NIC) {
     if (txb) {
       const usn_ctx::Tx p = c->txq.front();
+      // its state is copied on `s`: the stream the batch's launches are on
+      if (p.stream != s) return USN_EINVAL;
       bool changed = false;
       const int st = finalize_tx(c, b, r, s, info, p, c->tx_redo_next, &changed);
       // refused before any side effect (a frame needs the frame reader and
