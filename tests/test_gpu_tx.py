@@ -324,3 +324,165 @@ def test_tx_pipeline_order_and_busy(coracle_mod):
     ctx.classify(b, r2, s)
     ctx.finalize(b, r2, s)
     ctx.close()
+
+
+def _ring_launches(rings, coracle_mod, pipelined=False, src=None):
+    """Rings of one sending endpoint, two consecutive rings per
+    usn_classify_multi launch (one tx grid: ring 2's tiles order after ring
+    1's); with `pipelined`, launch j + 1 is enqueued before
+    launch j's rings are finalized.  Every ring's decisions and lists, and
+    the registry and bridge at the end, against the sequential oracle."""
+    from usnetd_amd import lib, traffic
+    src = rings[0].src if src is None else src
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, rings[0])
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, rings[0])
+    s = ctx.stream()
+    bs = [lib.DeviceBatch(ctx, c.frames, c.lens, src, stride=c.stride) for c in rings]
+    rs = [lib.DeviceResult(ctx, c.n) for c in rings]
+    pairs = [list(range(k, min(k + 2, len(rings)))) for k in range(0, len(rings), 2)]
+    infos = [None] * len(rings)
+
+    def launch(p):
+        ctx.classify_multi([bs[k] for k in p], [rs[k] for k in p], s)
+
+    def fin(k):
+        infos[k] = ctx.finalize(bs[k], rs[k], s)
+        c = rings[k]
+        want = o.forward_batch(src, c.frames, c.lens, stride=c.stride)
+        got = rs[k].decisions()
+        bad = np.nonzero((got & katrun.PARITY_MASK) != (want & katrun.PARITY_MASK))[0]
+        assert bad.size == 0, "ring %d: %d mismatches, first %d: got %#x want %#x" % (
+            k, bad.size, bad[0], got[bad[0]], want[bad[0]])
+        check_order(rs[k], got)
+        cls = np.bincount((want >> 16) & 0xF, minlength=4)
+        assert list(infos[k].class_count) == [int(x) for x in cls], k
+
+    if pipelined:
+        launch(pairs[0])
+        for j, p in enumerate(pairs):
+            if j + 1 < len(pairs):
+                launch(pairs[j + 1])
+            for k in p:
+                fin(k)
+    else:
+        for p in pairs:
+            launch(p)
+            for k in p:
+                fin(k)
+    assert sorted(o.rules()) == _registry_gpu(ctx)
+    assert o.bridge_count() == ctx.bridge_count()
+    ctx.close()
+    return infos
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_tx_two_rings_one_launch(n, coracle_mod):
+    """Ring 1 learns; ring 2 (the same frames) saw that learning inside the
+    grid, so it is final on the device: no host stage, nothing left to learn."""
+    from usnetd_amd import traffic
+    cfg = traffic.config("c4tx", n=n)
+    infos = _ring_launches([cfg] * 4, coracle_mod)
+    assert infos[0].n_learned > 0
+    assert infos[1].n_learned == 0
+    assert [i.n_host for i in infos] == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_tx_two_ring_launches_pipelined(n, coracle_mod):
+    """Launch 1 enqueued before launch 0's rings are finalized: launch 0
+    learned, so both of launch 1's rings are decided again on the host;
+    launch 2 was enqueued after launch 0's finalizes and is final on the
+    device."""
+    from usnetd_amd import traffic
+    cfg = traffic.config("c4tx", n=n)
+    infos = _ring_launches([cfg] * 8, coracle_mod, pipelined=True)
+    assert infos[0].n_learned > 0
+    assert infos[1].n_host == 0
+    assert [i.n_host for i in infos[2:4]] == [n, n]
+    assert [i.n_host for i in infos[4:]] == [0, 0, 0, 0]
+
+
+def test_tx_two_rings_all_learn(coracle_mod):
+    """Every ring brings new flows: ring 2 learns its own on the device, with
+    ring 1's already visible to it (first learners across the ring boundary)."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=1 << 16, seed=30 + k) for k in range(4)]
+    infos = _ring_launches(rings, coracle_mod)
+    assert all(i.n_learned > 0 for i in infos)
+    assert [i.n_host for i in infos] == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_tx_two_rings_host_tail(first, coracle_mod):
+    """A DHCP request sends the rest of its ring through the ordered host
+    stage.  In ring 1, ring 2 is then decided again on the host (it ran
+    behind ring 1's device results); in ring 2, ring 1 stays final."""
+    from usnetd_amd import traffic
+    a = traffic.c4tx(n=5000, host_at=[2500], seed=40)
+    b = traffic.c4tx(n=5000, seed=41)
+    rings = [a, b] if first else [b, a]
+    infos = _ring_launches(rings, coracle_mod)
+    if first:
+        assert [i.n_host for i in infos] == [2500, 5000]
+    else:
+        assert [i.n_host for i in infos] == [0, 2500]
+
+
+def test_tx_two_rings_cache_across(coracle_mod):
+    """The carried cache across the ring boundary inside a grid: ragged
+    rings, ring 2 opening with ring 1's last flow (cache hits on ring 1's
+    frames), a ring without any cache-touching frame as ring 1 (ring 2 then
+    compares with the cache carried into the launch) and as ring 2 (the next
+    launch takes ring 1's cache through ring 2's summary)."""
+    from usnetd_amd import traffic
+    r1 = traffic.c4tx(n=3000, seed=50)
+    r2 = traffic.c4tx(n=1025, seed=51)
+    g = traffic.c4tx(n=2100, seed=52)
+    st = r1.stride
+    V1 = r1.frames[:r1.n * st].reshape(r1.n, st)
+    V2 = r2.frames[:r2.n * st].reshape(r2.n, st)
+    G = g.frames[:g.n * st].reshape(g.n, st)
+    ip = np.nonzero((V1[:, 12] == 8) & (V1[:, 13] == 0))[0]
+    V1[2990:3000] = V1[ip[5]]
+    V2[0:50] = V1[ip[5]]
+    G[:, 12:14] = 0x12                          # no parse: no frame touches the cache
+    infos = _ring_launches([r1, r2, g, r1, r1, g, r2], coracle_mod)
+    assert [i.n_host for i in infos] == [0] * 7
+
+
+def test_tx_two_ring_launch_rules(coracle_mod):
+    """Two rings per tx launch: of one source, distinct results; at most two
+    launches in flight; rings finalized in order."""
+    import ctypes as C
+    from usnetd_amd import lib, traffic
+    cfg = traffic.config("c4tx", n=4096)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s = ctx.stream()
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+    b2 = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, 2, stride=cfg.stride)
+    rs = [lib.DeviceResult(ctx, cfg.n) for _ in range(6)]
+
+    def multi(bb, rr):
+        ba = (lib.Batch * len(bb))(*[x.desc for x in bb])
+        ra = (lib.Result * len(rr))(*[x.desc for x in rr])
+        return ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(bb), s)
+
+    assert multi([b, b2], rs[:2]) == lib.USN_EINVAL          # two sources
+    assert multi([b, b, b], rs[:3]) == lib.USN_EINVAL        # three rings
+    assert multi([b, b], [rs[0], rs[0]]) == lib.USN_EINVAL   # one result twice
+    assert multi([b, b], rs[:2]) == 0
+    assert multi([b], [rs[1]]) == lib.USN_EBUSY              # a result in flight
+    assert multi([b, b], rs[2:4]) == 0                       # the second launch
+    assert multi([b], [rs[4]]) == lib.USN_EBUSY              # a third
+    info = lib.FinalizeInfo()
+    assert ctx.L.usn_finalize(ctx.h, C.byref(b.desc), C.byref(rs[1].desc), s, C.byref(info)) == lib.USN_EBUSY
+    ctx.finalize(b, rs[0], s)
+    assert multi([b], [rs[4]]) == lib.USN_EBUSY              # launch 0's ring 2 still in flight
+    ctx.finalize(b, rs[1], s)
+    assert multi([b], [rs[4]]) == 0
+    for r in rs[2:5]:
+        ctx.finalize(b, r, s)
+    ctx.close()

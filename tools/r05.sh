@@ -86,6 +86,20 @@ case $S in
     ABL_CFGS=c4 ABL_ARGS="--frames 1048576 --multi 8 --batches 8 --rounds 5 --launches 30" ABL_VARIANTS="base ckinter nochunk" \
       bash tools/gpu.sh $S abl || exit 1
     ;;
+  r05g)
+    # two consecutive rings per tx launch (one grid): the tx GPU tests, the
+    # bench's c4tx line (one ring per launch and two, pipelined)
+    TESTS=tests/test_gpu_tx.py bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 10 --warmup 3 --extras c4tx --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
+  r05h)
+    # two rings per tx launch, round 2: the tx GPU tests, the c4tx line, the
+    # kernel times and HBM traffic of a two-ring launch (6 rotating buffers)
+    TESTS=tests/test_gpu_tx.py bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 10 --warmup 3 --extras c4tx --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6 --rings 2" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 2097152 $O/pmc_c4tx2.json tx_kernel=1+32 > $O/pmct_c4tx2.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -1893,8 +1893,13 @@ template <bool LDS>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(NTHREADS / 64)))
 void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames all resident)
   extern __shared__ __align__(16) uint8_t smem[];
-  const ClassifyArgs &a = t.a;
-  const Lds L = carve(smem, a.nbins);
+  /* tile: this workgroup's tile in the launch (the protocol's); rt: in its
+     ring (rings = 2: ring 2's tiles follow ring 1's, TxArgs) */
+  const uint32_t tile = blockIdx.x;
+  const bool ring2 = tile >= t.a.ntiles;
+  const ClassifyArgs &a = ring2 ? t.a2 : t.a;
+  const uint32_t rt = ring2 ? tile - t.a.ntiles : tile;
+  const Lds L = carve(smem, t.a.nbins);
   uint4 *srec = reinterpret_cast<uint4 *>(smem + lds_core_bytes(a.nbins));   // the tile's records
   uint32_t *sdec = reinterpret_cast<uint32_t *>(srec + TILE);               // its decisions
   uint4 *stab = reinterpret_cast<uint4 *>(smem + tx_lds_head(a.nbins));
@@ -1914,10 +1919,10 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (tid < 8) s_misc[tid] = 0;
   hist_zero(L.hist, a.nbw);
   __syncthreads();
-  const uint32_t tile = blockIdx.x;
   STAMP_DECL
   STAMP(0);   // tickets out of step with the host: the waits time out
-  const uint64_t base = (uint64_t)tile * TILE;
+  const uint64_t base = (uint64_t)rt * TILE;      // the tile's first frame in its ring
+  const uint32_t vbase = tile * TILE;             // ... in the launch
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
   unsigned long long *aux = t.aux + (size_t)tile * TXA_GRANULES;
   const uint4 *T = a.table;
@@ -1926,7 +1931,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     T = stab;
   }
   if (tile == 0) {   // carried-in cache of this source; counters for phase 2 (all wait for tile 0)
-    if (tid < 5 && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
+    if (tid < 7 && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
       __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
@@ -2171,7 +2176,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   int deferred = -1;   // the round of this lane's first touching frame (touch 1, prev 0)
   auto hit_claim = [&](uint32_t r, bool hit) {
     const uint32_t local = r * NTHREADS + tid;
-    const uint64_t i = base + local;
+    const uint32_t i = vbase + local;
     uint32_t fl = rec[r].x;
     if (hit) fl |= TXR_HIT;
     rec[r].x = fl;
@@ -2179,10 +2184,10 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     if (hit || (fl & TXR_HOST)) return;
     if (fl & (TXR_LEARNMAC | TXR_LEARNRULE)) {
       if (fl & TXR_LEARNMAC) {
-        const uint64_t m = rec_smac(frame_head(a, i));
+        const uint64_t m = rec_smac(frame_head(a, base + local));
         unsigned long long *slot = set_claim(t.macset, t.macset_mask, 2, t.epoch, m,
                                              usn_mac_hash(m), &s_ovf);
-        if (slot) first_index_update(slot + 1, t.epoch, (uint32_t)i);
+        if (slot) first_index_update(slot + 1, t.epoch, i);
         ins |= 1u;
       }
       if (fl & TXR_LEARNRULE) {
@@ -2194,7 +2199,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
         if (slot) {
           st_sc1(slot + 2, ((unsigned long long)y << 32) | x);   // full key: collision check below
           st_sc1(slot + 3, ((unsigned long long)meta << 32) | z);
-          first_index_update(slot + 1, t.epoch, (uint32_t)i);
+          first_index_update(slot + 1, t.epoch, i);
         }
         ins |= 2u;
       }
@@ -2312,7 +2317,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (tid == 0) {   // this tile's prefixes, for the tiles TX_LOOKBACK + 1 and more after it
     const uint32_t own = s_lastnh;
     g_put(aux + TXG_PINS, t.epoch, s_insall | s_ins);
-    g_put(aux + TXG_PHEAD, t.epoch, own ? (uint32_t)base + own : s_hidx);
+    g_put(aux + TXG_PHEAD, t.epoch, own ? vbase + own : s_hidx);
     g_put(aux + TXG_PEARLY, t.epoch, s_early_all | s_early);
   }
   const uint32_t insall = __builtin_amdgcn_readfirstlane(s_insall | s_ins);
@@ -2357,7 +2362,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       d = usn_mkdec(USN_CLS_FLOOD, USN_R_NONE, 0xFFFFu);
     } else if (touch == 2u) {
       d = usn_mkdec(USN_CLS_DROP, USN_R_LOOPBACK, 0xFFFFu);
-    } else if (!tx_dmac_in(t, fl, r1[r], (uint32_t)(base + local), ins_d)) {
+    } else if (!tx_dmac_in(t, fl, r1[r], vbase + local, ins_d)) {
       d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
     } else {
       d = usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);  // (the A/B no-probe build keeps it)
@@ -2387,12 +2392,12 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     const uint32_t local = r * NTHREADS + tid;
     v[r] = 0;
     if (local >= nt) { dec[r] = 0; continue; }
-    const uint64_t i = base + local;
+    const uint32_t i = vbase + local;
     const uint32_t fl = rec[r].x, touch = tx_touch(rec[r]);
     uint32_t d = dec[r];
     if (use[r]) {   // key1, then a key1 learned by a frame <= i, then key2 (endpoint.rs:317-327)
       uint32_t wr = w[r];
-      if (!wr && (ins_d & 2u)) wr = tx_learned_key1(t, kx[r], ky[r], kz[r], km[r], (uint32_t)i);
+      if (!wr && (ins_d & 2u)) wr = tx_learned_key1(t, kx[r], ky[r], kz[r], km[r], i);
       if (!wr) wr = w[ROUNDS + r];
       d = tx_lookup_dec(a, fl, wr);
     }
@@ -2402,11 +2407,11 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       bool learned = false;
       if (fl & TXR_LEARNMAC) {
         const uint64_t m = rec_smac(r1[r]);
-        if (slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, m, usn_mac_hash(m)), t.epoch) ==
-            (uint32_t)i) {
+        if (slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, m, usn_mac_hash(m)), t.epoch) == i) {
           const uint32_t pos = atomicAdd(t.counters, 1u);
+          if (ring2) atomicAdd(t.counters + 6, 1u);
           if (pos < t.learned_cap) {
-            t.learned[2 * pos] = make_uint4((uint32_t)i, 0u, 0u, 0u);
+            t.learned[2 * pos] = make_uint4(i, 0u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, 0u);
           } else {
             atomicOr(t.counters + 1, 4u);
@@ -2420,13 +2425,14 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
         const unsigned long long *slot = set_find(t.ruleset, t.ruleset_mask, 4, t.epoch,
                                                   usn_key_fp48(x, y, z, meta),
                                                   usn_key_hash(x, y, z, meta));
-        if (slot_first(slot, t.epoch) == (uint32_t)i) {
+        if (slot_first(slot, t.epoch) == i) {
           if (ld_sc1(slot + 2) != (((unsigned long long)y << 32) | x) ||
               ld_sc1(slot + 3) != (((unsigned long long)meta << 32) | z))
             atomicOr(t.counters + 1, 2u);
           const uint32_t pos = atomicAdd(t.counters, 1u);
+          if (ring2) atomicAdd(t.counters + 6, 1u);
           if (pos < t.learned_cap) {
-            t.learned[2 * pos] = make_uint4((uint32_t)i, 1u, 0u, 0u);
+            t.learned[2 * pos] = make_uint4(i, 1u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4(x, y, z, meta);
           } else {
             atomicOr(t.counters + 1, 4u);
@@ -2455,12 +2461,28 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       if (g_getn<1>(t.aux + (size_t)((hx - 1) / TILE) * TXA_GRANULES + TXG_HDEC, t, hv)) hd = hv[0];
     }
     s_head = hd;
+    if (ring2 && rt == 0) {   // ring 2's summary: the cache ring 1 hands on (state after its last frame)
+      usn_summary *S = a.summary;
+      const uint32_t st = s_before ? (tx_touch(s_brec) == 1u && !(s_brec.x & TXR_HOST) ? USN_CS_VALID : 0u)
+                                   : s_cin[0];
+      S->cin_state = st;
+      S->cin_dst = (hx ? hd : s_cin[1]) & USN_PARITY_MASK;
+      if (s_before) {
+        S->cin_info[0] = s_brec.x & TXR_I0_MASK; S->cin_info[1] = s_brec.y;
+        S->cin_info[2] = s_brec.z; S->cin_info[3] = s_brec.w;
+      } else {
+        for (int k = 0; k < 4; ++k) S->cin_info[k] = s_cin[2 + k];
+      }
+      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      S->n_ep = a.n_ep; S->n_bins = a.nbins;
+      S->flags = 0; S->first_break = 0xFFFFFFFFu;
+    }
   }
   STAMP(6);
   tile_prefix_max(v, L, head);   // its barriers also publish sdec and s_head
   uint32_t my_last = 0, my_touch = 0, my_dec = 0, my_host = 0;
   uint4 my_info = make_uint4(0, 0, 0, 0);
-  uint32_t *hl = a.host_list + (size_t)tile * TILE;
+  uint32_t *hl = a.host_list + (size_t)rt * TILE;
   uint32_t bins[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -2491,9 +2513,9 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   tile_hist(bins, nt, a.nbits, L.hist);
   __syncthreads();
   STAMP(7);
-  hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
+  hist_out(L.hist, a.nbw, a.cnt + (size_t)rt * a.nbw);
   STAMP(10);
-  usn_tile_hdr *H = a.tiles + tile;
+  usn_tile_hdr *H = a.tiles + rt;
   const uint32_t lastp = s_misc[0];
   if (lastp && my_last == lastp) {
     H->last_state = USN_TS_HAS | (my_touch == 1u && !my_host ? USN_TS_RETAINED : 0u) |
@@ -2515,7 +2537,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     H->class_count[3] = (uint16_t)fl;
     H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
-    if (s_misc[1]) atomicAdd(t.counters + 4, s_misc[1]);   // after phase 2: tile 0 zeroed it
+    if (s_misc[1]) atomicAdd(t.counters + (ring2 ? 5 : 4), s_misc[1]);   // after phase 2: tile 0 zeroed it
   }
   STAMP(11);
   STAMP_FLUSH_AT(tile);
@@ -2526,8 +2548,9 @@ static inline size_t table_lds_bytes(uint32_t table_units);
 
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
   const ClassifyArgs &a = t.a;
-  if (a.ntiles == 0) return hipSuccess;
-  const dim3 g(a.ntiles), b(NTHREADS);
+  const uint32_t ntiles = a.ntiles + (t.rings == 2 ? t.a2.ntiles : 0u);
+  if (ntiles == 0) return hipSuccess;
+  const dim3 g(ntiles), b(NTHREADS);
   const size_t head = tx_lds_head(a.nbins);
   const size_t bridge = t.bridge_mask < TX_BRIDGE_LDS_SLOTS ? (size_t)(t.bridge_mask + 1) * 8 : 0;
   const size_t with_table = head + table_lds_bytes(a.table_units) + bridge;
@@ -2938,9 +2961,10 @@ void scatter_kernel(ScatterArgs s) {
       if (c == 0) {
         if (b <= s.nbins) B.bin_off[b] = pt;                   // pad bins past nbins are empty
         if (b + 1 <= s.nbins) B.bin_off[b + 1] = pt + vt.x;
-        if (s.txs_out && bi == 0) {   // tx: the class totals for usn_finalize (host memory)
-          if (b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
-          if (b + 1 >= s.n_ep && b + 1 < s.n_ep + 3) s.txs_out[7 + b - s.n_ep] = pt + vt.x;
+        if (s.txs_out) {   // tx: the ring's class totals for usn_finalize (host memory)
+          uint32_t *to = s.txs_out + USN_TXS_WORDS * bi;
+          if (b >= s.n_ep && b < s.n_ep + 3) to[6 + b - s.n_ep] = pt;
+          if (b + 1 >= s.n_ep && b + 1 < s.n_ep + 3) to[7 + b - s.n_ep] = pt + vt.x;
         }
         if (B.rx_state) {             // rx: the same into the batch's state
           if (b >= s.n_ep && b < s.n_ep + 3) B.rx_state[4 + b - s.n_ep] = pt;
@@ -2968,7 +2992,7 @@ void scatter_kernel(ScatterArgs s) {
       if (b >= s.nbw) break;
       off[b] = pt + (noscan ? 0u : ex[b]) - pc;
       if (c == 0 && b <= s.nbins) B.bin_off[b] = pt;
-      if (c == 0 && s.txs_out && bi == 0 && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[6 + b - s.n_ep] = pt;
+      if (c == 0 && s.txs_out && b >= s.n_ep && b < s.n_ep + 3) s.txs_out[USN_TXS_WORDS * bi + 6 + b - s.n_ep] = pt;
       if (c == 0 && B.rx_state && b >= s.n_ep && b < s.n_ep + 3) B.rx_state[4 + b - s.n_ep] = pt;
       if (noscan) {
         for (uint32_t w = 0; w < ntc; ++w) pt += B.cnt[(size_t)(t0 + w) * s.nbw + b];
@@ -2995,11 +3019,18 @@ void scatter_kernel(ScatterArgs s) {
     B.rx_state[7] = *B.diag;
     B.rx_state[0] = s.epoch;
   }
-  if (c == 0 && bi == 0 && s.txs_out && tid < 6) {   // tx: summary flags, counters[0..4], n
-    uint32_t v = tid == 0 ? s.txs_sum->flags
-                          : __hip_atomic_load(s.txs_counters + tid - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s.txs_out[tid] = v;
-    if (tid == 0) { s.txs_out[9] = B.n; s.txs_out[10] = *B.diag; }
+  if (c == 0 && s.txs_out && tid < 6) {   // tx, per ring: summary flags, counters, n, diag
+    auto ctr = [&](uint32_t k) {
+      return __hip_atomic_load(s.txs_counters + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    uint32_t v;
+    if (tid == 0) v = B.summary->flags;
+    else if (tid == 1) v = bi == 0 ? ctr(0) - ctr(6) : ctr(6);   // the ring's learned items
+    else if (tid == 5) v = ctr(4 + bi);                           // ... frames for the host stage
+    else v = ctr(tid - 1);                                        // flags, sets, timeout epoch
+    uint32_t *to = s.txs_out + USN_TXS_WORDS * bi;
+    to[tid] = v;
+    if (tid == 0) { to[9] = B.n; to[10] = *B.diag; }
   }
   __syncthreads();
   STAMP(1);

@@ -466,7 +466,7 @@ struct Replica {
   hipEvent_t classified = nullptr;
 };
 
-constexpr size_t TXSTATE_BYTES = 64;   // a tx batch's gathered state (16 words) per slot
+constexpr size_t TXSTATE_BYTES = 2 * USN_TXS_WORDS * 4;   // a tx launch's gathered state per slot
 
 struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
@@ -515,20 +515,29 @@ struct usn_ctx {
   std::vector<unsigned long long> bridge_set;
   uint32_t bridge_mask = 0;
   /* tx batches in flight: classified, not finalized, so the registry is not
-   * final (every registry call returns USN_EBUSY).  At most two, of one
-   * source, on one stream and replica: ring k + 1 may be enqueued before ring
-   * k's usn_finalize (the device is not left idle while the host finalizes).
-   * Ring k + 1 ran against the state ring k started from; when ring k's
-   * finalize changed that state (it learned, or ran a host tail), ring k + 1
-   * is decided again on the host from its first frame (tx_redo_next). */
+   * final (every registry call returns USN_EBUSY).  At most two launches
+   * (each one ring, or two consecutive rings in one grid), of one source, on
+   * one stream and replica: launch k + 1 may be enqueued before launch k's
+   * rings are finalized (the device is not left idle while the host
+   * finalizes).  Launch k + 1 ran against the state launch k started from;
+   * when a finalize of launch k's rings changed that state (it learned, or
+   * ran a host tail), launch k + 1's first ring is decided again on the host
+   * from its first frame (tx_redo_next).  Ring 2 of a launch saw ring 1's
+   * learning on the device: it is redone only after ring 1 ran a host tail. */
   struct Tx {
     const uint32_t *decisions = nullptr;
+    const void *launch_dec = nullptr;   // ring 1's decisions (usn_ctx::txstate_for)
     int src = -1;
     uint32_t replica = 0, slot = 0, epoch = 0;
+    uint32_t ring = 0, rings = 1;       // this ring of the launch's
+    uint32_t voff = 0;                  // the launch's frame index of the ring's frame 0
+    uint64_t launch = 0;
     hipStream_t stream = nullptr;
   };
   std::deque<Tx> txq;
   uint32_t tx_next_slot = 0;
+  uint64_t tx_launches = 0;
+  bool tx_chg = false;           // a finalize changed the state since the latest tx launch
   bool tx_redo_next = false;     // the next batch in txq is redone on the host from frame 0
   bool tx_cout_valid = false;    // ... from this carried cache (the previous batch's host tail)
   uint32_t tx_cout[6] = {0, 0, 0, 0, 0, 0};   // {state, dst, info[4]}
@@ -543,6 +552,7 @@ struct usn_ctx {
   size_t h_lists_cap = 0;
   uint4 *h_items = nullptr;      // pinned: a tx batch's learned list
   size_t h_items_cap = 0;
+  uint64_t h_items_for = 0;      // the launch whose list h_items holds (both rings read it)
   /* host frame reader: frames whose ports lie past the batch window */
   usn_frame_reader reader = nullptr;
   void *reader_user = nullptr;
@@ -2348,7 +2358,6 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   x.cpt = pl.cpt;
   x.txs_out = txs_out;
   x.txs_counters = txs_counters;
-  x.txs_sum = r[0].summary;
   if (!epoch) epoch = next_epoch(c);   // (the classify of this launch took one already)
   x.epoch = epoch;
   for (uint32_t k = 0; k < count; ++k) {
@@ -2562,18 +2571,32 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     int st = check_batch(c, &b[k], &r[k]);
     if (st) return st;
     tx |= c->eps[b[k].src_endpoint].kind != USN_EP_NIC;
-    for (uint32_t j = 0; j < k; ++j)
-      if (b[j].src_endpoint == b[k].src_endpoint) return USN_EINVAL;   // one batch per source
   }
-  if (tx && count != 1) return USN_EINVAL;   // a tx batch changes shared state: alone
+  if (tx) {   // a tx launch changes shared state: one ring of a source, or two consecutive rings
+    if (count > 2) return USN_EINVAL;
+    if (count == 2) {
+      if (b[1].src_endpoint != b[0].src_endpoint || r[1].decisions == r[0].decisions ||
+          r[1].scratch == r[0].scratch)
+        return USN_EINVAL;
+      // the launch's frame index (ring 2 after ring 1's tiles) stays below 2^32 - 1
+      if ((b[0].n + USN_TILE - 1) / USN_TILE * USN_TILE + b[1].n >= 0xFFFFFFFFull) return USN_ERANGE;
+    }
+  } else {
+    for (uint32_t k = 0; k < count; ++k)
+      for (uint32_t j = 0; j < k; ++j)
+        if (b[j].src_endpoint == b[k].src_endpoint) return USN_EINVAL;   // one batch per source
+  }
   const uint32_t rep = c->sel;
-  /* while tx batches are in flight: only the next ring of the same source,
-   * on the same stream and replica, and at most two in flight */
+  /* while tx batches are in flight: only the next ring(s) of the same source,
+   * on the same stream and replica, and at most two launches in flight */
   if (!c->txq.empty()) {
     const usn_ctx::Tx &p = c->txq.back();
-    if (!tx || c->txq.size() >= 2 || p.src != b[0].src_endpoint || p.replica != rep ||
-        p.stream != (hipStream_t)stream || p.decisions == r[0].decisions)
+    if (!tx || c->txq.front().launch != p.launch || p.src != b[0].src_endpoint || p.replica != rep ||
+        p.stream != (hipStream_t)stream)
       return USN_EBUSY;
+    for (const usn_ctx::Tx &q : c->txq)
+      for (uint32_t k = 0; k < count; ++k)
+        if (q.decisions == r[k].decisions) return USN_EBUSY;
   }
   Replica &R = c->reps[rep];
   /* the table-version fence: this replica sees every registry and bridge
@@ -2612,11 +2635,14 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
-    int st = tx_prepare(R, tb.n, m.b[0].ntiles, slot, !c->txq.empty());
+    const uint64_t n_all = tb.n + (count == 2 ? b[1].n : 0);
+    int st = tx_prepare(R, n_all, m.tile_base[count], slot, !c->txq.empty());
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
     t.a = m.b[0];
+    t.rings = count;
+    if (count == 2) t.a2 = m.b[1];
     st = tx_listen(R, tb.src_endpoint, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
     t.aux = R.aux;
@@ -2633,14 +2659,23 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.next_dhcp_set = t.a.next_dhcp_set;
     if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
     else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
-    usn_ctx::Tx p;
-    p.decisions = r[0].decisions;
-    p.src = tb.src_endpoint;
-    p.replica = rep;
-    p.slot = slot;
-    p.epoch = R.epoch;
-    p.stream = (hipStream_t)stream;
-    c->txq.push_back(p);
+    const uint64_t launch = ++c->tx_launches;
+    for (uint32_t k = 0; k < count; ++k) {
+      usn_ctx::Tx p;
+      p.decisions = r[k].decisions;
+      p.launch_dec = r[0].decisions;
+      p.src = tb.src_endpoint;
+      p.replica = rep;
+      p.slot = slot;
+      p.epoch = R.epoch;
+      p.ring = k;
+      p.rings = count;
+      p.voff = k ? m.b[0].ntiles * USN_TILE : 0u;
+      p.launch = launch;
+      p.stream = (hipStream_t)stream;
+      c->txq.push_back(p);
+    }
+    c->tx_chg = false;
     c->tx_next_slot ^= 1u;
   } else {
     /* a result whose lists are still being built on the side stream is not
@@ -2988,9 +3023,11 @@ static bool same_cache(const CacheState &a, const CacheState &b) {
  * launched after this one started from (registry, bridge, DHCP steering, or
  * a carried cache other than the device chain's). */
 static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_t s,
-                       usn_finalize_info *info, const usn_ctx::Tx &txp, bool redo, bool *changed) {
+                       usn_finalize_info *info, const usn_ctx::Tx &txp, bool redo, bool *changed,
+                       bool *tail) {
   StageClock clk("finalize_tx");
   *changed = false;
+  *tail = redo;
   // the previous batch's carried-out cache (its host tail), for a redo of this
   // one.  Consumed here: every return below pops the batch (usn_finalize),
   // except USN_EAGAIN_READER, which puts it back
@@ -3008,13 +3045,14 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
   uint32_t cnt[8];
-  if (c->txstate_for[txp.slot] == r->decisions && X.txstate_ev) {   // gathered behind the launch
+  if (c->txstate_for[txp.slot] == txp.launch_dec && X.txstate_ev) {   // gathered behind the launch
     HIPCHK(hipEventSynchronize(X.txstate_ev));
-    c->txstate_for[txp.slot] = nullptr;
+    if (txp.ring + 1 == txp.rings) c->txstate_for[txp.slot] = nullptr;
     const volatile uint32_t *q =
         reinterpret_cast<const volatile uint32_t *>(c->h_txstate + txp.slot * TXSTATE_BYTES);
     uint32_t v[12];
-    for (int k = 0; k < 12; ++k) v[k] = q[k];
+    for (int k = 0; k < 11; ++k) v[k] = q[USN_TXS_WORDS * txp.ring + k];
+    v[11] = q[11];   // (ring 1's block: any chunk of the launch)
     { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, r->n, c->n_ep + 3), s); if (e) return e; }
     if (!redo && v[1] == 0 && v[2] == 0 && v[4] != txp.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
@@ -3039,6 +3077,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   // batch is redone: the whole batch goes to the host stage
   if (cnt[3] == txp.epoch) cnt[1] |= 8u;
   if (redo) cnt[1] |= 16u;
+  const uint32_t items_here = txp.ring ? cnt[6] : cnt[0] - cnt[6];   // learned by this ring's frames
   clk.mark("state");
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
@@ -3049,7 +3088,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   int st = fetch_host_lists(c, r, th, hosts, s);
   if (st) return st;
   clk.mark("summary");
-  if (hosts.empty() && cnt[0] == 0 && cnt[1] == 0) {   // nothing learned, nothing ordered
+  if (hosts.empty() && items_here == 0 && cnt[1] == 0) {   // nothing learned, nothing ordered
     if (info) *info = fi;
     return USN_OK;
   }
@@ -3067,9 +3106,12 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     for (uint32_t j : hosts)
       if (hv.dec[j] & USN_F_HOST) { h = j; break; }
   /* learned items and first fragments before h, in frame order */
-  const uint32_t nl = std::min(cnt[0], X.learned_cap);
-  const uint4 *items = nullptr;   // the learned list, through pinned memory
-  if (nl) {
+  const uint32_t nl = items_here ? std::min(cnt[0], X.learned_cap) : 0u;
+  const uint4 *items = nullptr;   // the learned list (the launch's), through pinned memory
+  if (nl && c->h_items_for == txp.launch) {
+    items = c->h_items;           // ring 1 of this launch fetched it
+  } else if (nl) {
+    c->h_items_for = 0;
     const size_t bytes = (size_t)nl * 2 * sizeof(uint4);
     if (bytes > c->h_items_cap) {
       if (c->h_items) HIPCHK(hipHostFree(c->h_items));
@@ -3082,6 +3124,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
     HIPCHK(hipMemcpyAsync(c->h_items, X.learned, bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     items = c->h_items;
+    c->h_items_for = txp.launch;
   }
   clk.mark("items");
   struct Ev { uint64_t idx; uint32_t kind; uint4 key; };   // kind 0 mac, 1 rule, 2 frag1
@@ -3089,8 +3132,10 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   evs.reserve(nl + hosts.size());
   c->rules.reserve(c->rules.size() + nl);
   clk.mark("reserve");
-  for (uint32_t k = 0; k < nl; ++k)
-    if (items[2 * k].x < h) evs.push_back(Ev{items[2 * k].x, items[2 * k].y, items[2 * k + 1]});
+  for (uint32_t k = 0; k < nl; ++k) {   // (launch frame index -> this ring's)
+    const uint32_t x = items[2 * k].x;
+    if (x >= txp.voff && x - txp.voff < h) evs.push_back(Ev{x - txp.voff, items[2 * k].y, items[2 * k + 1]});
+  }
   for (uint32_t j : hosts)
     if (j < h && (hv.dec[j] & USN_F_FRAG1)) evs.push_back(Ev{j, 2, make_uint4(0, 0, 0, 0)});
   /* frame order; within a frame the fragment map first (kind 2, 1, 0).
@@ -3238,6 +3283,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
       out[j - h] = d;
     }
     fi.n_host = (uint32_t)(n - h);
+    *tail = true;
     /* the registry is final from here on; a HIP failure below leaves this
      * batch's device results unpatched (reported, not retried) */
     HIPCHK(hipMemcpy(r->decisions + h, out.data(), out.size() * 4, hipMemcpyHostToDevice));
@@ -3302,16 +3348,21 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
       const usn_ctx::Tx p = c->txq.front();
       // its state is copied on `s`: the stream the batch's launches are on
       if (p.stream != s) return USN_EINVAL;
-      bool changed = false;
-      const int st = finalize_tx(c, b, r, s, info, p, c->tx_redo_next, &changed);
+      bool changed = false, tail = false;
+      const int st = finalize_tx(c, b, r, s, info, p, c->tx_redo_next, &changed, &tail);
       // refused before any side effect (a frame needs the frame reader and
       // none is set): the batch stays pending, so a call after
       // usn_set_frame_reader applies what it learned
       if (st == USN_EAGAIN_READER) return USN_EINVAL;
       c->txq.pop_front();
-      // the next ring in flight started from the state before this finalize:
-      // decided again on the host when this one changed it (or failed)
-      c->tx_redo_next = !c->txq.empty() && (changed || st != USN_OK);
+      c->tx_chg = c->tx_chg || changed || st != USN_OK;
+      // the next ring in flight: ring 2 of this launch saw this ring's device
+      // results (redone when the host decided part of this ring, or it
+      // failed); a later launch started from the state before the finalizes
+      // since it was enqueued (redone when one of them changed it)
+      if (c->txq.empty()) c->tx_redo_next = false;
+      else if (c->txq.front().launch == p.launch) c->tx_redo_next = tail || st != USN_OK;
+      else c->tx_redo_next = c->tx_chg;
       return st;
     }
     if (!c->txq.empty()) return USN_EBUSY;   // a later ring in flight (in order), or another source

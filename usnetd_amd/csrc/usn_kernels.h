@@ -90,8 +90,16 @@ static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 #define TXR_WINDOW (1u << 30)    /* L4 ports lie past the batch window: the host reads the frame */
 #define TXR_I0_MASK 0x1FFFFu
 
+/* A tx launch takes one ring of the source, or two consecutive rings (a2,
+ * rings = 2): workgroups [0, a.ntiles) take ring 1's tiles, the rest ring
+ * 2's.  The cross-tile protocol (aux granules, the learning sets' first
+ * learners, learned items) runs over the launch's frame index: ring 2's
+ * frame j is a.ntiles * USN_TILE + j; decisions, host lists, count rows and
+ * tile headers are each ring's own. */
 struct TxArgs {
   ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
+  ClassifyArgs a2;            /* rings = 2: the second ring (same source; carry_mode unused) */
+  uint32_t rings;
   unsigned long long *aux;    /* per tile x TXA_GRANULES {epoch, value}: what crosses a tile boundary */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
@@ -101,7 +109,8 @@ struct TxArgs {
                                  {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
   uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with
                                  items, [3] epoch of a batch whose tile waits timed out, [4] frames
-                                 listed for the host stage */
+                                 of ring 1 listed for the host stage, [5] ring 2's, [6] learned
+                                 items of ring 2's frames */
   uint32_t learned_cap;
   const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
   uint32_t bridge_mask;
@@ -112,6 +121,7 @@ struct TxArgs {
 
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
+static_assert(sizeof(TxArgs) <= 4096, "kernel argument block");
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */
@@ -167,13 +177,16 @@ struct ScatterArgs {
   uint32_t flags;                           /* USN_SCF_* */
   uint32_t epoch;                           /* this launch's granule tag (never 0) */
   uint32_t cpt;                             /* scan: chunks per thread (1, 2, 4) */
-  /* tx: chunk 0 of batch 0 also writes {summary flags, counters[0..4],
-   * bin_off[n_ep .. n_ep + 3], the scan's diag} into host-mapped memory
-   * (usn_finalize) */
+  /* tx: chunk 0 of each batch (ring) also writes its state into host-mapped
+   * memory for usn_finalize, USN_TXS_WORDS per ring: [0] summary flags,
+   * [1] the ring's learned items, [2] counters[1] (flags), [3] counters[2],
+   * [4] counters[3] (timeout epoch), [5] the ring's host-stage frames,
+   * [6..8] bin_off[n_ep .. n_ep + 2], [9] n, [10] the scan's diag; word 11 of
+   * ring 1's set by any chunk that finds inconsistent lists */
   uint32_t *txs_out;
   const uint32_t *txs_counters;
-  const usn_summary *txs_sum;
 };
+#define USN_TXS_WORDS 16u
 #define USN_DIAG_TIMEOUT 1u     /* a scan wait timed out (200 ms; never observed) */
 #define USN_DIAG_LISTS 2u       /* the scatter found count rows that disagree with the decisions */
 #define USN_SCF_NOSCAN 2u      /* every batch is one chunk: no scan launch; the chunk's own counts

@@ -33,6 +33,7 @@ S_STALE, S_STALE_EXTENDS, S_COUT = 1, 2, 8
 STATUS = {0: "ok", -22: "EINVAL", -12: "ENOMEM", -17: "EEXIST", -2: "ENOENT", -1: "EPERM",
           -5: "EHIP", -19: "ENODEV", -34: "ERANGE", -16: "EBUSY", -74: "ELIST"}
 USN_EBUSY = -16
+USN_EINVAL = -22
 USN_ELIST = -74
 
 
@@ -373,6 +374,16 @@ class Ctx:
     def classify(self, batch: "DeviceBatch", result: "DeviceResult", stream=None):
         check(self.L.usn_classify(self.h, C.byref(batch.desc), C.byref(result.desc), stream),
               "usn_classify")
+
+    def classify_multi(self, batches, results, stream=None):
+        """One launch over several batches (usn_classify_multi): rx rings of
+        distinct NIC sources, or one or two consecutive rings of a sending
+        endpoint (the two in one tx grid)."""
+        n = len(batches)
+        ba = (Batch * n)(*[b.desc for b in batches])
+        ra = (Result * n)(*[r.desc for r in results])
+        check(self.L.usn_classify_multi(self.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), n,
+                                        stream), "usn_classify_multi")
 
     def set_lists_async(self, on=True):
         """Build the per-endpoint lists on a side stream (usn_set_lists_async)."""
