@@ -574,6 +574,8 @@ def measure_tx(ctx, args):
                 pm = json.load(fh)
             if int(pm.get("frames_per_launch", -1)) == F2:
                 roof["traffic"] = pm.get("hbm_bytes_per_launch")
+                roof["traffic_x2"] = pm.get("hbm_bytes_per_launch_x2")   # the guide's x2 throughout
+                roof["traffic_model"] = pm.get("correction")
                 roof["traffic_source"] = os.path.relpath(pmc, ROOT)
         except (OSError, ValueError):
             pass

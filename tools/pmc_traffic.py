@@ -16,7 +16,13 @@ KERNEL=F: that kernel's FETCH_SIZE counted xF instead of x2.  KERNEL=1+B: a
 kernel that mixes both kinds of read (the tx kernel: its header windows are
 coalesced 128-byte requests, its rule probes scattered 64-byte ones) counted
 x1 plus the B bytes per frame its coalesced reads' requests are short of
-(the tx kernel's 64-byte header line per frame, tallied at 32: tx_kernel=1+32).  c3's classify
+(the tx kernel's 64-byte header line and 2-byte length per frame, tallied at
+32 and 1: tx_kernel=1+33; calibration: tools/tx_pmc_cal.hip under the TCC
+request counters, profiles/r05/r05i/pmc_cal.json -- the header pattern 0.50
+requests per frame tallied at 32 B, the lengths at 1 B, a scattered 16-byte
+probe one request tallied at 64 B, a kernel mixing the three within 3 % of
+its parts; the guide's x2 for the whole kernel is reported beside it as
+hbm_bytes_per_launch_x2).  c3's classify
 reads one window per 2048-byte slot inside the first 64-byte half of a line:
 a 64-byte EA request, which FETCH_SIZE (= TCC_EA0_RDREQ x 64 B) counts
 exactly, so c3 uses classify_rx_kernel=1 (calibration: tools/stride_floor.hip
@@ -79,6 +85,8 @@ def main():
         "fetch_vs_algorithmic": round(sum(rd.values()) / read_algo, 4),
         "write_vs_algorithmic": round(sum(wr.values()) / write_algo, 4),
         "traffic_vs_algorithmic": round((sum(rd.values()) + sum(wr.values())) / (frames * 74), 4),
+        # every kernel's FETCH_SIZE x2 (the guide's streaming correction), beside the model
+        "hbm_bytes_per_launch_x2": int(sum(2.0 * v * 1024 / nf for v in fetch.values()) + sum(wr.values())),
         "correction": "FETCH_SIZE x2 (gfx950, 128-B requests tallied at 64 B), WRITE_SIZE x1" +
                       "".join("; %s FETCH_SIZE x%g%s" % (k, f, " + %g B/frame" % extra[k] if k in extra else "")
                               for k, f in sorted(factor.items())),

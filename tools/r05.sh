@@ -100,6 +100,22 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 6 --rings 2" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 2097152 $O/pmc_c4tx2.json tx_kernel=1+32 > $O/pmct_c4tx2.log 2>&1
     ;;
+  r05i)
+    # the tx PMC model's calibration: TCC request counters
+    # of tools/tx_pmc_cal.hip's kernels (one request type each, known units)
+    # and of a two-ring tx call, three passes each
+    TX="tools/txbench.py 1048576 12 1 --rotate 6 --rings 2"
+    P1="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum"
+    P2="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"
+    timeout -k 10 120 build/tx_pmc_cal > $O/cal_time.log 2>&1 || exit 1
+    sq_pass calr "$P1" build/tx_pmc_cal
+    sq_pass calw "$P2" build/tx_pmc_cal
+    sq_pass calf FETCH_SIZE build/tx_pmc_cal
+    sq_pass txr "$P1" python3 $TX
+    sq_pass txw "$P2" python3 $TX
+    sq_pass txf FETCH_SIZE python3 $TX
+    python3 tools/pmc_cal_summary.py 2097152 $O/pmc_cal.json $O/calr $O/calw $O/calf $O/txr $O/txw $O/txf > $O/pmc_cal.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
