@@ -116,6 +116,16 @@ case $S in
     sq_pass txf FETCH_SIZE python3 $TX
     python3 tools/pmc_cal_summary.py 2097152 $O/pmc_cal.json $O/calr $O/calw $O/calf $O/txr $O/txw $O/txf > $O/pmc_cal.log 2>&1
     ;;
+  r05j)
+    # the scatter deriving its per-tile counts from the decisions in LDS (no
+    # count-row reads; the scan's sums checked against them) against the
+    # row-reading scatter (HEAD, build/abl/scrows): scatter tests, scan +
+    # scatter device time, whole calls
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py" bash tools/gpu.sh $S testsall || exit 1
+    SCB_CFGS="c5 c2 c4" SCB_VARIANTS="base scrows" bash tools/gpu.sh $S scb || exit 1
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base scrows" \
+      bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
