@@ -486,3 +486,24 @@ def test_tx_two_ring_launch_rules(coracle_mod):
     for r in rs[2:5]:
         ctx.finalize(b, r, s)
     ctx.close()
+
+
+def test_tx_finalize_on_another_stream_is_refused(coracle_mod):
+    """a tx batch's state is copied on the stream its
+    launches are on; usn_finalize on another stream returns USN_EINVAL and
+    leaves the batch pending."""
+    import ctypes as C
+    from usnetd_amd import lib, traffic
+    cfg = traffic.config("c4tx", n=4096)
+    ctx = lib.Ctx(0)
+    traffic.install_ctx(ctx, cfg)
+    s, s2 = ctx.stream(), ctx.stream()
+    b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
+    r = lib.DeviceResult(ctx, cfg.n)
+    ctx.classify(b, r, s)
+    info = lib.FinalizeInfo()
+    assert ctx.L.usn_finalize(ctx.h, C.byref(b.desc), C.byref(r.desc), s2, C.byref(info)) == lib.USN_EINVAL
+    assert ctx.L.usn_rule_count(ctx.h) == lib.USN_EBUSY
+    ctx.finalize(b, r, s)
+    assert ctx.rule_count() > len(cfg.rules)
+    ctx.close()

@@ -220,3 +220,55 @@ def test_window_validation():
     b = lib.DeviceBatch(ctx, win, lens, 0, stride=64, window=64)
     ctx.classify(b, r, None)
     ctx.close()
+
+
+def test_tx_redo_after_refused_finalize_keeps_host_tail_cache(coracle_mod):
+    """ring k's finalize runs a host tail that leaves a
+    carried cache the device chain does not (its last frame's ports lie past
+    the window: UNKNOWN on the device, retained on the host); ring k + 1,
+    enqueued before it, is redone from that cache.  A finalize of ring k + 1
+    refused for want of a frame reader must not lose it: ring k + 1's first
+    frame repeats ring k's last PacketInfo with a dmac outside the bridge, so
+    only the host tail's cache (a hit: ring k's last decision) gives the
+    oracle's decision; the device chain's would send it to the NIC."""
+    from usnetd_amd import lib, traffic
+    n = 2048
+    fa, la, ihl = _frames(n, 61)
+    fb, lb, _ = _frames(n, 62)
+    # an IHL 15 UDP frame to an even pipe port (7000 + k, k even: a UDP rule of pipe 2 + k)
+    dp = fa[:, 76].astype(np.int64) * 256 + fa[:, 77]
+    j = int(np.nonzero((ihl == 15) & (fa[:, 23] == 17) & (dp >= 7000) & (dp < 7016) & (dp % 2 == 0))[0][0])
+    fa[n - 1], la[n - 1] = fa[j], la[j]
+    fa[n - 1, 0:6] = np.frombuffer(traffic.REMMAC, np.uint8)     # in the bridge: get_endpoint
+    fb[0], lb[0] = fa[n - 1], la[n - 1]
+    fb[0, 0:6] = np.frombuffer(traffic.NICMAC, np.uint8)         # not in the bridge
+    eps, rules = _setup()
+    ctx = lib.Ctx(0)
+    o = coracle_mod.Oracle()
+    _install(ctx, o, eps, rules)
+    want_a = o.forward_batch(1, fa.reshape(-1), la, stride=FULL)
+    want_b = o.forward_batch(1, fb.reshape(-1), lb, stride=FULL)
+    assert (want_b[0] >> 16) & 0xF == lib.CLS_EP          # the cache hit on ring k's last frame
+    s = ctx.stream()
+    ba = lib.DeviceBatch(ctx, np.ascontiguousarray(fa[:, :64]).reshape(-1), la, 1, stride=64)
+    bb = lib.DeviceBatch(ctx, np.ascontiguousarray(fb[:, :64]).reshape(-1), lb, 1, stride=64)
+    ra, rb = lib.DeviceResult(ctx, n), lib.DeviceResult(ctx, n)
+    ctx.classify(ba, ra, s)
+    ctx.classify(bb, rb, s)                              # before ring k's finalize
+    cur = {"f": fa, "l": la}
+    ctx.set_frame_reader(lambda s_, i: cur["f"][i, :int(cur["l"][i])].tobytes())
+    ctx.finalize(ba, ra, s)
+    assert np.array_equal(ra.decisions() & katrun.PARITY_MASK, want_a & katrun.PARITY_MASK)
+    ctx.set_frame_reader(None)
+    with pytest.raises(lib.UsnError, match="EINVAL"):
+        ctx.finalize(bb, rb, s)                          # refused: ring k + 1 stays pending
+    cur.update(f=fb, l=lb)
+    ctx.set_frame_reader(lambda s_, i: cur["f"][i, :int(cur["l"][i])].tobytes())
+    info = ctx.finalize(bb, rb, s)
+    assert info.n_host == n                              # redone from its first frame
+    got = rb.decisions()
+    mism = np.nonzero((got & katrun.PARITY_MASK) != (want_b & katrun.PARITY_MASK))[0]
+    assert mism.size == 0, "first mismatches %s: got %s want %s" % (
+        mism[:5], [hex(x) for x in got[mism[:5]]], [hex(x) for x in want_b[mism[:5]]])
+    assert ctx.rule_count() == o.rule_count()
+    ctx.close()

@@ -126,6 +126,11 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base scrows" \
       bash tools/gpu.sh $S abl || exit 1
     ;;
+  r05k)
+    # the ADVICE r04 regression tests (the host tail's carried cache across a
+    # refused finalize; a tx finalize on another stream) with the tx suite
+    TESTS="tests/test_gpu_window.py tests/test_gpu_tx.py" bash tools/gpu.sh $S testsall || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
