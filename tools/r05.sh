@@ -131,6 +131,17 @@ case $S in
     # refused finalize; a tx finalize on another stream) with the tx suite
     TESTS="tests/test_gpu_window.py tests/test_gpu_tx.py" bash tools/gpu.sh $S testsall || exit 1
     ;;
+  r05z)
+    # final tree: the suite, smoke, the bench as the driver runs it, rocprof
+    # of the bench, PMC of c5 / c2 / c3 / c4 and of the two-ring tx call
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    PMC_CFGS="c5 c2 c3 c4" bash tools/gpu.sh $S pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 6 --rings 2" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 2097152 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
