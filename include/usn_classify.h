@@ -301,17 +301,26 @@ int usn_result_release(usn_ctx *ctx, const usn_result *r);
  * A batch sent by a non-NIC endpoint (tx: find_forward with incoming ==
  * false) learns bridge MACs and answer rules; until its usn_finalize every
  * other call that reads or changes the registry returns USN_EBUSY, except
- * the source's next tx ring on the same stream: at most two tx batches are
- * in flight and they are finalized in order (a later one first: USN_EBUSY).
- * The second ran against the state the first started from; when the first's
- * usn_finalize changed that state (it learned, or ran a host tail that left
- * another carried cache or DHCP steering), the second's usn_finalize decides
- * it again on the host from its first frame. */
+ * the source's next tx ring(s) on the same stream: at most two tx launches
+ * (each one ring, or two rings through usn_classify_multi) are in flight,
+ * and their rings are finalized in order (a later one first: USN_EBUSY).
+ * A launch ran against the state the launch before it started from; when a
+ * usn_finalize of the earlier launch's rings changed that state (it learned,
+ * or ran a host tail that left another carried cache or DHCP steering), the
+ * later launch's rings are decided again on the host from their first
+ * frame. */
 int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stream);
 /* Several drained rings of DISTINCT sources (e.g. the rx queues of the NICs
  * polled in one poll() round, main.rs:1029-1046) in one launch: b[k] -> r[k],
- * count <= 8.  Same semantics as `count` usn_classify calls.  A tx batch
- * must be classified alone (count == 1). */
+ * count <= 8.  Same semantics as `count` usn_classify calls.
+ * A sending endpoint's (tx) rings: one ring, or two CONSECUTIVE rings of the
+ * same source (count == 2, distinct results) in one grid, ring 2's frames
+ * following ring 1's: the same decisions, learning and carried cache as two
+ * usn_classify calls finalized in turn (ring 2 sees what ring 1 learned on the
+ * device, and is decided again on the host only when ring 1's usn_finalize
+ * ran a host tail).  Finalize ring 1, then ring 2.  Two tx rings of different
+ * sources, or more than two: USN_EINVAL; ring 1's tiles * USN_TILE + ring 2's
+ * frames must stay below 2^32 - 1 (else USN_ERANGE). */
 int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
                        void *hip_stream);
 
