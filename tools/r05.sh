@@ -142,6 +142,10 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 6 --rings 2" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 2097152 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
     ;;
+  r05l)
+    # the bench's end-to-end loops with their ctypes arguments built once
+    BENCH_ARGS="--steps 20 --warmup 3 --extras c2,c3,c4tx --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
