@@ -337,9 +337,12 @@ int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t
 int usn_set_lists_async(usn_ctx *ctx, int on);
 int usn_lists_wait(usn_ctx *ctx, const usn_result *r, void *hip_stream);
 
-/* Ordered host stage for one classified batch (synchronises the stream; for
- * a tx batch, waits for that batch's own launches only, and `hip_stream` must
- * be the stream the batch was classified on: else USN_EINVAL).  A NIC batch
+/* Ordered host stage for one classified batch.  Waits for the batch's own
+ * launches, not for work queued behind them on the stream (a NIC batch whose
+ * lists are built on the side stream: for the stream and its lists); for a
+ * tx batch `hip_stream` must be the stream the batch was classified on (else
+ * USN_EINVAL).  When the batch needs the host stage, its copies and patches
+ * are ordered on `hip_stream` and the call returns after them.  A NIC batch
  * with nothing for the host stage (no stale carried cache, no frame listed)
  * reads only the few words its scatter left in host-mapped memory: about one
  * microsecond of host time.

@@ -146,6 +146,12 @@ case $S in
     # the bench's end-to-end loops with their ctypes arguments built once
     BENCH_ARGS="--steps 20 --warmup 3 --extras c2,c3,c4tx --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05m)
+    # an rx usn_finalize waits for its own launch's event, not the stream:
+    # the suite, then the end-to-end loops
+    bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 20 --warmup 3 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

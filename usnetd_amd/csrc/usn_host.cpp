@@ -464,6 +464,13 @@ struct Replica {
    * launch by the `classified` event */
   hipStream_t side = nullptr;
   hipEvent_t classified = nullptr;
+  /* rx launches' completion (recorded after their scatter on the caller's
+   * stream): usn_finalize of an rx batch waits for its own launch, not for
+   * the later batches queued behind it.  A ring of events: a slot reused by
+   * a later launch only makes that wait longer */
+  static constexpr uint32_t RX_EVS = 64;
+  hipEvent_t rx_ev[RX_EVS] = {};
+  uint32_t rx_ev_next = 0;
 };
 
 constexpr size_t TXSTATE_BYTES = 2 * USN_TXS_WORDS * 4;   // a tx launch's gathered state per slot
@@ -565,6 +572,7 @@ struct usn_ctx {
   struct BatchRec {
     uint32_t rep, nbins;
     uint32_t slot, epoch;   // its rx state slot (RX_SLOTS: none) and launch tag
+    hipEvent_t done;        // rx: recorded after its launch's scatter (Replica::rx_ev), or null
   };
   std::unordered_map<const void *, BatchRec> batch_rep;
   /* usn_set_lists_async: lists built on the replica's side stream; each
@@ -1883,6 +1891,8 @@ void usn_ctx_destroy(usn_ctx *c) {
   for (Replica &R : c->reps) {
     (void)hipSetDevice(R.device);
     if (R.classified) (void)hipEventDestroy(R.classified);
+    for (hipEvent_t e : R.rx_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto &x : R.txs)
       if (x.txstate_ev) (void)hipEventDestroy(x.txstate_ev);
     if (R.side) (void)hipStreamDestroy(R.side);
@@ -2632,6 +2642,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   uint32_t epoch = 0;        // rx: the launch tag (classify and lists)
   uint32_t rx_slot[USN_MAX_MULTI];
   uint32_t *rx_state[USN_MAX_MULTI];
+  hipEvent_t rx_done = nullptr;   // rx, lists on the caller's stream: the launch's completion
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
@@ -2725,6 +2736,12 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
                             epoch, tx ? nullptr : rx_state);
     if (st) return st;
+    if (!tx) {
+      hipEvent_t &e = R.rx_ev[R.rx_ev_next++ % Replica::RX_EVS];
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(e, (hipStream_t)stream));
+      rx_done = e;
+    }
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
       if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, hipEventDisableTiming));
@@ -2768,7 +2785,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
     c->batch_rep[r[k].decisions] =
-        usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch};
+        usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch, rx_done};
   }
   return USN_OK;
 }
@@ -3334,8 +3351,13 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   HIPCHK(hipSetDevice(c->reps[rep].device));
   hipStream_t s = (hipStream_t)stream;
   // (a tx batch waits for its own launches only: the next ring may already
-  // be queued behind them on the stream)
-  if (!txb) HIPCHK(hipStreamSynchronize(s));
+  // be queued behind them on the stream; so does an rx batch whose launch
+  // recorded its completion, and the host-stage path below orders its copies
+  // on the stream itself)
+  if (!txb) {
+    if (br != c->batch_rep.end() && br->second.done) HIPCHK(hipEventSynchronize(br->second.done));
+    else HIPCHK(hipStreamSynchronize(s));
+  }
   {  // lists built on the side stream (usn_set_lists_async)
     auto it = c->lists_ev.find(r->decisions);
     if (it != c->lists_ev.end() && it->second.pending) {
