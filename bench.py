@@ -194,18 +194,27 @@ class Run:
                 self.results.append(_result(ctx, n))
                 del cfg
         self.R = R
+        # results are double-buffered even when one round's batches cover the
+        # rotation: the end-to-end loop finalizes round i - 1 after round i's
+        # calls, so round i must not write into round i - 1's results (a
+        # daemon keeps two per source, daemon/usnetd.cpp)
+        self.RR = max(R, 2)
+        for _ in range(self.RR - R):
+            for j in range(Q):
+                self.results.append(_result(ctx, n))
         self.cfg0 = cfg0
         self.rotating_bytes = int(R * Q * (frame_bytes + 2 * n))
         self.streams = [ctx.stream() for _ in range(S)]
         self.joins = [ctx.event() for _ in range(S)]
         self.ev0, self.ev1 = ctx.event(), ctx.event()
         self.groups = []                                  # per round, per launch: (stream, ptrs)
-        for rnd in range(R):
+        for rnd in range(self.RR):
             gl = []
             for s, qs in self.launches:
-                ks = [rnd * Q + j for j in qs]
-                ba = (_lib().Batch * len(ks))(*[self.batches[k].desc for k in ks])
-                ra = (_lib().Result * len(ks))(*[self.results[k].desc for k in ks])
+                kb = [(rnd % R) * Q + j for j in qs]
+                kr = [rnd * Q + j for j in qs]
+                ba = (_lib().Batch * len(kb))(*[self.batches[k].desc for k in kb])
+                ra = (_lib().Result * len(kr))(*[self.results[k].desc for k in kr])
                 gl.append((s, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(ks), ba, ra))
             self.groups.append(gl)
         self.h = ctx.h
@@ -215,7 +224,7 @@ class Run:
 
     def step(self, i, stream_override=None):
         multi = self.L.usn_classify_multi
-        for s, ba, ra, cnt, _, _ in self.groups[i % self.R]:
+        for s, ba, ra, cnt, _, _ in self.groups[i % self.RR]:
             st = self.streams[s] if stream_override is None else stream_override
             rc = multi(self.h, ba, ra, cnt, st)
             if rc:
@@ -256,11 +265,11 @@ class Run:
             from usnetd_amd import lib as _l
             self._fin_info = _l.FinalizeInfo()
             ib = C.byref(self._fin_info)
-            self._fin_args = [[(self.h, C.byref(self.batches[r * self.Q + j].desc),
+            self._fin_args = [[(self.h, C.byref(self.batches[(r % self.R) * self.Q + j].desc),
                                 C.byref(self.results[r * self.Q + j].desc), self.streams[s], ib)
-                               for s, qs in self.launches for j in qs] for r in range(self.R)]
+                               for s, qs in self.launches for j in qs] for r in range(self.RR)]
         fin = self.L.usn_finalize
-        for a in self._fin_args[i % self.R]:
+        for a in self._fin_args[i % self.RR]:
             t = time.perf_counter()
             rc = fin(*a)
             if rc:
@@ -281,17 +290,22 @@ class Run:
             dist.barrier()
         times = []
         t0 = time.perf_counter()
+        t1 = None
         for i in range(steps):
             self.step(i)
             if i:
                 self.finalize_round(i - 1, times)
+                if i == 1:
+                    t1 = time.perf_counter()   # round 0 out: the pipeline is full
         self.finalize_round(steps - 1, times)
         for x in self.streams:
             ctx.sync(x)
-        wall = time.perf_counter() - t0
+        t2 = time.perf_counter()
         if dist:
             dist.barrier()
-        return wall, times
+        # (wall of all rounds; and rounds 1.. after round 0's finalize, without
+        # the pipeline's fill)
+        return t2 - t0, times, (t2 - t1 if t1 is not None else t2 - t0)
 
     def finalize_host_us(self, rounds=3):
         """usn_finalize's own host time per ring: the rounds' GPU work done
@@ -321,7 +335,7 @@ class Run:
         for x in self.streams:
             ctx.sync(x)
         for i, (ea, eb) in enumerate(evs):
-            _, ba, ra, cnt, _, ral = self.groups[i % self.R][0]
+            _, ba, ra, cnt, _, ral = self.groups[i % self.RR][0]
             ctx.record(ea, st)
             rc = self.L.usn_classify_multi(self.h, ba, ra, cnt, st)
             if rc:
@@ -340,8 +354,8 @@ class Run:
         host_frames, flags, cls = 0, 0, [0, 0, 0, 0]
         for x in self.streams:
             self.ctx.sync(x)
-        for k in range(len(self.batches)):
-            info = self.ctx.finalize(self.batches[k], self.results[k], self.streams[0])
+        for k in range(len(self.results)):
+            info = self.ctx.finalize(self.batches[k % len(self.batches)], self.results[k], self.streams[0])
             host_frames += info.n_host
             flags |= info.flags
             cls = [x + y for x, y in zip(cls, info.class_count)]
@@ -389,8 +403,9 @@ def measure(run, args, dist, world):
     host_frames, flags, cls = run.finalize_all()
     # the same poll rounds with usn_finalize of every ring in the timed loop
     # (what the reference does per drain)
-    e2e_wall, fin_times = run.end_to_end(args.steps, dist)
+    e2e_wall, fin_times, e2e_steady = run.end_to_end(args.steps, dist)
     e2e_elapsed = shard.max_over_ranks(e2e_wall, dist)
+    e2e_steady = shard.max_over_ranks(e2e_steady, dist)
     fin_host_us = run.finalize_host_us()
     frames = world * args.steps * run.frames_per_step()
     achieved = ALGO_BYTES * probe_frames / (kern_ms * 1e-3) / 1e9 if kern_ms else None
@@ -431,6 +446,9 @@ def measure(run, args, dist, world):
             "basis": "poll rounds with usn_finalize of every ring in the timed loop (round i-1's "
                      "rings finalized after round i's calls are enqueued), wall clock, max over ranks",
             "ms_per_step": round(e2e_elapsed * 1e3 / args.steps, 5),
+            # rounds 1..K-1 after round 0's usn_finalize returned (the pipeline full)
+            "steady_mpps": round(frames * (args.steps - 1) / args.steps / e2e_steady / 1e6, 2)
+            if args.steps > 1 else None,
             "finalize_call_us_per_ring_median": round(float(np.median(fin_times)) * 1e6, 2),
             "finalize_host_us_per_ring": round(fin_host_us, 2),
             "rings_per_step": run.Q,

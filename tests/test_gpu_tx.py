@@ -507,3 +507,15 @@ def test_tx_finalize_on_another_stream_is_refused(coracle_mod):
     ctx.finalize(b, r, s)
     assert ctx.rule_count() > len(cfg.rules)
     ctx.close()
+
+
+@pytest.mark.parametrize("n1,n2", [(1, 1), (1, 5000), (1023, 1), (1024, 1025), (2047, 2049)])
+def test_tx_two_rings_tile_edges(n1, n2, coracle_mod):
+    """Two rings in one grid at tile edges: single-frame rings, a ring 1
+    that ends inside its last tile (ring 2 starts on a fresh tile of the
+    grid), full tiles, and a ring 2 of one frame; every ring twice."""
+    from usnetd_amd import traffic
+    r1 = traffic.c4tx(n=n1, seed=70)
+    r2 = traffic.c4tx(n=n2, seed=71)
+    infos = _ring_launches([r1, r2, r1, r2], coracle_mod)
+    assert [i.n_host for i in infos] == [0, 0, 0, 0]

@@ -152,6 +152,26 @@ case $S in
     bash tools/gpu.sh $S testsall || exit 1
     BENCH_ARGS="--steps 20 --warmup 3 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05n)
+    # the two-ring tile-edge tests; the end-to-end loops' steady state
+    TESTS=tests/test_gpu_tx.py TEST_K=tile_edges bash tools/gpu.sh $S testsall || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5 --extras c3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
+  r05o)
+    # where the end-to-end loop's host time goes (c3, c2, c5)
+    for c in c3 c2 c5; do
+      timeout -k 10 240 python3 tools/e2e_trace.py $c 200 > $O/e2e_$c.log 2>&1 || exit 1
+    done
+    ;;
+  r05p)
+    # results double-buffered in the bench: the end-to-end loop's host time,
+    # then the bench line
+    for c in c3 c2 c5; do
+      timeout -k 10 240 python3 tools/e2e_trace.py $c 200 > $O/e2e_$c.log 2>&1 || exit 1
+    done
+    BENCH_ARGS="--steps 40 --warmup 5 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    TESTS=tests/test_gpu_bench.py bash tools/gpu.sh $S testsall || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
