@@ -215,7 +215,7 @@ class Run:
                 kr = [rnd * Q + j for j in qs]
                 ba = (_lib().Batch * len(kb))(*[self.batches[k].desc for k in kb])
                 ra = (_lib().Result * len(kr))(*[self.results[k].desc for k in kr])
-                gl.append((s, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(ks), ba, ra))
+                gl.append((s, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(kb), ba, ra))
             self.groups.append(gl)
         self.h = ctx.h
 
