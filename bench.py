@@ -99,6 +99,9 @@ def parse_args(argv=None):
     ap.add_argument("--lists-async", type=int, default=0,
                     help="1: per-endpoint lists on the library's side stream (usn_set_lists_async): "
                          "a round's scatter overlaps the next round's classify")
+    ap.add_argument("--result-rounds", type=int, default=2,
+                    help="rounds of result buffers (>= 2: the end-to-end loop finalizes round i - 1 "
+                         "while round i is queued)")
     ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
     ap.add_argument("--launch-check", action="store_true",
@@ -145,7 +148,7 @@ class Run:
     of one poll round."""
 
     def __init__(self, L, ctx, name, n, rank, world, queues, streams, strong, rings_per_launch=0,
-                 rotate_bytes=ROTATE_BYTES):
+                 rotate_bytes=ROTATE_BYTES, result_rounds=2):
         from usnetd_amd import shard, traffic
         self.L, self.ctx, self.name, self.n = L, ctx, name, n
         P = rings_per_launch or max(1, min(8, LAUNCH_FRAMES // n))   # rings per launch
@@ -194,11 +197,14 @@ class Run:
                 self.results.append(_result(ctx, n))
                 del cfg
         self.R = R
-        # results are double-buffered even when one round's batches cover the
-        # rotation: the end-to-end loop finalizes round i - 1 after round i's
-        # calls, so round i must not write into round i - 1's results (a
-        # daemon keeps two per source, daemon/usnetd.cpp)
-        self.RR = max(R, 2)
+        # results: the device-throughput loop (the value) writes round i into
+        # the same results as round i - R, as a round's results are consumed
+        # before the next round; the end-to-end loop finalizes round i - 1 after
+        # round i's calls, so it double-buffers them (as the daemon keeps two
+        # per source, daemon/usnetd.cpp).  Double-buffered outputs no longer
+        # stay in the Infinity Cache between rounds: the value loop would run
+        # 6-7 % slower with them (profiles/r05/r05q)
+        self.RR = max(R, result_rounds)
         for _ in range(self.RR - R):
             for j in range(Q):
                 self.results.append(_result(ctx, n))
@@ -222,9 +228,9 @@ class Run:
     def frames_per_step(self):
         return self.Q * self.n
 
-    def step(self, i, stream_override=None):
+    def step(self, i, stream_override=None, e2e=False):
         multi = self.L.usn_classify_multi
-        for s, ba, ra, cnt, _, _ in self.groups[i % self.RR]:
+        for s, ba, ra, cnt, _, _ in self.groups[i % (self.RR if e2e else self.R)]:
             st = self.streams[s] if stream_override is None else stream_override
             rc = multi(self.h, ba, ra, cnt, st)
             if rc:
@@ -292,7 +298,7 @@ class Run:
         t0 = time.perf_counter()
         t1 = None
         for i in range(steps):
-            self.step(i)
+            self.step(i, e2e=True)
             if i:
                 self.finalize_round(i - 1, times)
                 if i == 1:
@@ -312,7 +318,7 @@ class Run:
         first, so the call waits for nothing"""
         times = []
         for i in range(rounds):
-            self.step(i)
+            self.step(i, e2e=True)
             for x in self.streams:
                 self.ctx.sync(x)
             self.finalize_round(i, times)
@@ -335,7 +341,7 @@ class Run:
         for x in self.streams:
             ctx.sync(x)
         for i, (ea, eb) in enumerate(evs):
-            _, ba, ra, cnt, _, ral = self.groups[i % self.RR][0]
+            _, ba, ra, cnt, _, ral = self.groups[i % self.R][0]
             ctx.record(ea, st)
             rc = self.L.usn_classify_multi(self.h, ba, ra, cnt, st)
             if rc:
@@ -354,8 +360,8 @@ class Run:
         host_frames, flags, cls = 0, 0, [0, 0, 0, 0]
         for x in self.streams:
             self.ctx.sync(x)
-        for k in range(len(self.results)):
-            info = self.ctx.finalize(self.batches[k % len(self.batches)], self.results[k], self.streams[0])
+        for k in range(len(self.batches)):   # the value loop's results (rounds 0 .. R - 1)
+            info = self.ctx.finalize(self.batches[k], self.results[k], self.streams[0])
             host_frames += info.n_host
             flags |= info.flags
             cls = [x + y for x, y in zip(cls, info.class_count)]
@@ -699,7 +705,7 @@ def main(argv=None):
     joined = joined_ranks(dist, rank, device)   # every rank is in the group, on its device
     n = args.frames or DEFAULT_FRAMES[args.config]
     run = Run(L, ctx, args.config, n, rank, world, args.queues, args.streams, args.strong,
-              args.rings_per_launch, args.rotate_mib << 20)
+              args.rings_per_launch, args.rotate_mib << 20, args.result_rounds)
     res = measure(run, args, dist, world)
     out = {
         "metric": METRIC,
@@ -764,7 +770,7 @@ def main(argv=None):
                 x = measure_tx(ctx, args)
             else:
                 rx = Run(L, ctx, name, DEFAULT_FRAMES[name], 0, 1, EXTRA_QUEUES.get(name, 0),
-                         args.streams, False)
+                         args.streams, False, result_rounds=args.result_rounds)
                 xa = argparse.Namespace(**vars(args))
                 xa.steps = max(args.steps, EXTRA_MIN_STEPS.get(name, 0))
                 x = measure(rx, xa, None, 1)

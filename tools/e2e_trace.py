@@ -26,7 +26,7 @@ enq, fins, steps = [], [], []
 t_prev = None
 for i in range(K):
     t0 = time.perf_counter()
-    run.step(i)
+    run.step(i, e2e=True)
     t1 = time.perf_counter()
     enq.append(t1 - t0)
     if i:

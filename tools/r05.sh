@@ -172,6 +172,20 @@ case $S in
     BENCH_ARGS="--steps 40 --warmup 5 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     TESTS=tests/test_gpu_bench.py bash tools/gpu.sh $S testsall || exit 1
     ;;
+  r05q)
+    # A/B in turn on one box: result buffers of one round against two (the
+    # value loop's outputs stay MALL-resident when every round rewrites the same)
+    for rr in 1 2 1 2; do
+      timeout -k 10 300 python bench.py --steps 40 --warmup 5 --extras c2,c3 --no-cpu-baseline \
+        --result-rounds $rr > $O/bench_rr$rr.log 2>&1 || exit 1
+      python3 -c "import json,sys; d=json.loads([l for l in open('$O/bench_rr$rr.log') if l.startswith('{')][-1]); print('rr=$rr', d['value'], d['end_to_end_mpps'], d['c2']['value'], d['c3']['value'])"
+    done
+    ;;
+  r05r)
+    # the value loop on one round's results, the end-to-end loop on two
+    BENCH_ARGS="--steps 40 --warmup 5 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    TESTS=tests/test_gpu_bench.py bash tools/gpu.sh $S testsall || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
