@@ -186,6 +186,21 @@ case $S in
     BENCH_ARGS="--steps 40 --warmup 5 --extras c2,c3,c4 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     TESTS=tests/test_gpu_bench.py bash tools/gpu.sh $S testsall || exit 1
     ;;
+  r05s)
+    # the c5 scan's chunks per thread (product: 4, 512 workgroups) against 2
+    # and 1 (the test build's USN_SCAN_CPT knob), scan + scatter device time
+    for cpt in 2 1; do
+      USN_SCAN_CPT=$cpt timeout -k 10 300 python tools/scatter_bench.py --config c5 --frames 8388608 --multi 2 \
+        --json $O/scb_cpt$cpt.json base testlib > $O/scb_cpt$cpt.log 2>&1 || exit 1
+      cat $O/scb_cpt$cpt.log | grep scatter
+    done
+    ;;
+  r05t)
+    # the scan with 16-byte row loads (scan16_kernel) against 8-byte
+    # (build/abl/scan8 = HEAD): the lists' tests, scan + scatter device time
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py" bash tools/gpu.sh $S testsall || exit 1
+    SCB_CFGS="c5 c2 c4" SCB_VARIANTS="base scan8 base scan8" bash tools/gpu.sh $S scb || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
