@@ -201,6 +201,44 @@ case $S in
     TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py" bash tools/gpu.sh $S testsall || exit 1
     SCB_CFGS="c5 c2 c4" SCB_VARIANTS="base scan8 base scan8" bash tools/gpu.sh $S scb || exit 1
     ;;
+  r05y)
+    # final tree (after the rx finalize event and the bench's result
+    # buffering): the suite, smoke, the bench as the driver runs it, rocprof
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    ;;
+  r05u)
+    # what the rx launch's completion event costs: the product library against
+    # the commit before it (build/abl/noev), whole calls in the bench's shapes
+    ABL_CFGS=c3 ABL_ARGS="--frames 262144 --multi 4 --batches 16 --streams 2 --rounds 5 --launches 60" ABL_VARIANTS="base noev" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="--frames 1048576 --multi 8 --batches 16 --streams 2 --rounds 5 --launches 40" ABL_VARIANTS="base noev" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base noev" \
+      bash tools/gpu.sh $S abl || exit 1
+    ;;
+  r05v)
+    # the rx completion event's flags: default (system fence), device-scope
+    # release, no system fence, against no event (build/abl/noev), c5 and c2
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base noev evdev evnofence" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="--frames 1048576 --multi 8 --batches 16 --rounds 5 --launches 40" ABL_VARIANTS="base noev evdev evnofence" \
+      bash tools/gpu.sh $S abl || exit 1
+    ;;
+  r05w)
+    # completion events without the system fence (rx and tx): the suite,
+    # smoke, the A/B against the fenced events (build/abl/sysfence), the
+    # c4tx pipeline (txpipe), the bench
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30" ABL_VARIANTS="base sysfence noev" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="--frames 1048576 --multi 8 --batches 16 --rounds 5 --launches 40" ABL_VARIANTS="base sysfence noev" \
+      bash tools/gpu.sh $S abl || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

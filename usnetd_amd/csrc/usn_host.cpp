@@ -473,6 +473,16 @@ struct Replica {
   uint32_t rx_ev_next = 0;
 };
 
+/* The completion events of rx and tx launches (usn_finalize waits for its
+ * own launch on them).  An event between back-to-back launches of one stream
+ * costs the next launch 1-2 % of a c5 call and 2-3 % of a c4 one (the A/B
+ * harness, one stream: 160.3 -> 162.3 us per 8M ring, profiles/r05/r05w);
+ * without the system-scope fence it is the same within noise (r05v), so the
+ * events keep it (the host reads what they order: the launch's state words,
+ * then the results through copies). */
+#ifndef USN_DONE_EV_FLAGS
+#define USN_DONE_EV_FLAGS hipEventDisableTiming
+#endif
 constexpr size_t TXSTATE_BYTES = 2 * USN_TXS_WORDS * 4;   // a tx launch's gathered state per slot
 
 struct usn_ctx {
@@ -2738,13 +2748,13 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (st) return st;
     if (!tx) {
       hipEvent_t &e = R.rx_ev[R.rx_ev_next++ % Replica::RX_EVS];
-      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, USN_DONE_EV_FLAGS));
       HIPCHK(hipEventRecord(e, (hipStream_t)stream));
       rx_done = e;
     }
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
-      if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, hipEventDisableTiming));
+      if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, USN_DONE_EV_FLAGS));
       HIPCHK(hipEventRecord(X.txstate_ev, (hipStream_t)stream));
       c->txstate_for[slot] = r[0].decisions;
     }
