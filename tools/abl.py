@@ -44,7 +44,10 @@ def main():
         # "build@ENV=VAL,ENV2=VAL": the build's library with context knobs set
         # while its context is created (USN_PH_GROUP, USN_PH_LOAD, USN_T512)
         build, _, knobs = nm.partition("@")
-        path = os.path.join(ROOT, "build", "abl", build, "libusn.so")
+        # "product": the in-tree library (usnetd_amd/libusn.so, always the tree
+        # under test); other names: build/abl/<name>, built by `make abl` or
+        # tools/abl_commit.sh (rebuild them with the tree they are to match)
+        path = None if build == "product" else os.path.join(ROOT, "build", "abl", build, "libusn.so")
         saved = {}
         for kv in filter(None, knobs.split(",")):
             k, v = kv.split("=", 1)
