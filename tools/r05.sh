@@ -239,6 +239,17 @@ case $S in
       bash tools/gpu.sh $S abl || exit 1
     BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05x)
+    # the classify's header stage at the two parts it loads (16 KiB: c5 at 4
+    # workgroups per CU) against 3 parts (build/abl/stage192 = HEAD)
+    TESTS="tests/test_gpu_volume.py tests/test_gpu_parity.py" bash tools/gpu.sh $S testsall || exit 1
+    ABL_CFGS=c5 ABL_ARGS="--frames 8388608 --multi 2 --batches 4 --rounds 8 --launches 30" ABL_VARIANTS="product stage192" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS="c4 c2" ABL_ARGS="--frames 1048576 --multi 8 --batches 16 --rounds 5 --launches 40" ABL_VARIANTS="product stage192" \
+      bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c3 ABL_ARGS="--frames 262144 --multi 4 --batches 16 --streams 2 --rounds 5 --launches 60" ABL_VARIANTS="product stage192" \
+      bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

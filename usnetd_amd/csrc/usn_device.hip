@@ -59,8 +59,12 @@ using namespace ::usn;
 #endif
 #define GLDS_PARTS (USN_STAGE32 ? 2u : 3u)       /* 16-byte LDS-DMA parts per frame and round */
 #define GLDS_OFF (USN_STAGE32 ? 12u : 0u)        /* first byte of a frame in the stage */
-#define STAGE_ROUND_SLOTS (64u * 3u)             /* 16-byte slots per wave and round (the sort
-                                                    also counts in the stage: 24 KiB at 512 threads) */
+#ifndef USN_STAGE_SLOTS   /* A/B: 16-byte slots per wave and round (round 4: 192, a sort's counts
+                             shared the stage; nothing else uses it since the device-wide lists) */
+#define USN_STAGE_SLOTS (64u * GLDS_PARTS)
+#endif
+#define STAGE_ROUND_SLOTS (USN_STAGE_SLOTS)      /* 16 KiB at 512 threads and 2 parts: with c5's 16 KiB
+                                                    of displacements, 4 workgroups per CU instead of 3 */
 #define MAX_NBITS 13   /* nbins <= USN_MAX_ENDPOINTS + 3 <= 8192 */
 #define LDS_TABLE_MAX_BYTES (32u * 1024u)   /* rule images up to 32 KiB live in LDS */
 /* the LDS copy of the image, rounded up to whole 64-unit glds chunks */
