@@ -129,3 +129,66 @@ def test_control_plane_changes_and_moving_sources(coracle_mod):
         _same(r.decisions(), want, "step %d on replica %d" % (step, rep))
         keep.append((b, r))
     ctx.close()
+
+
+def test_two_ring_tx_launch_hands_its_cache_to_another_replica(coracle_mod):
+    """Two tx rings in one grid on replica 1, the second without any
+    cache-touching frame: the source's next ring, on replica 0, takes its
+    carried cache from the launch's ring-2 summary (written inside the grid:
+    the state ring 1 hands on) through the host.  Ring B's first frame repeats
+    its last frame's PacketInfo with the gateway's dmac, so only the carried
+    cache (a hit: the last frame's lookup) gives the oracle's decision."""
+    from usnetd_amd import lib, traffic
+    a = traffic.c4tx(n=5000, seed=81)
+    b = traffic.c4tx(n=3000, seed=82)
+    g = traffic.c4tx(n=2100, seed=83)
+    st = b.stride
+    B = b.frames[:b.n * st].reshape(b.n, st)
+    ip = np.nonzero((B[:, 12] == 8) & (B[:, 13] == 0) & (B[:, 23] == 17))[0]
+    B[b.n - 1] = B[ip[3]]
+    B[b.n - 1, 0:6] = [0x02, 0, 0, 0, 0xB0, 0x07]            # a bridged MAC: get_endpoint
+    B[0] = B[b.n - 1]
+    B[0, 0:6] = np.frombuffer(traffic.NICMAC, np.uint8)       # not bridged: NIC unless cached
+    G = g.frames[:g.n * st].reshape(g.n, st)
+    G[:, 12:14] = 0x12                                        # no parse: nothing touches the cache
+    ctx = lib.Ctx(devices=[0, 0])
+    traffic.install_ctx(ctx, a)
+    o = coracle_mod.Oracle()
+    coracle_mod.install_oracle(o, a)
+    streams = []
+    for rep in (0, 1):
+        ctx.select(rep)
+        streams.append(ctx.stream())
+    bufs = {}
+    for name, cfg in (("a", a), ("b", b), ("g", g)):
+        for rep in (0, 1):
+            ctx.select(rep)
+            bufs[name, rep] = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, a.src, stride=st)
+    keep = []
+
+    def check(cfg, r, what):
+        want = o.forward_batch(a.src, cfg.frames, cfg.lens, stride=st)
+        _same(r.decisions(), want, what)
+        return want
+
+    ctx.select(0)
+    ra = lib.DeviceResult(ctx, a.n)
+    ctx.classify(bufs["a", 0], ra, streams[0])
+    ctx.finalize(bufs["a", 0], ra, streams[0])
+    check(a, ra, "ring a, replica 0")
+    ctx.select(1)
+    rb, rg = lib.DeviceResult(ctx, b.n), lib.DeviceResult(ctx, g.n)
+    ctx.classify_multi([bufs["b", 1], bufs["g", 1]], [rb, rg], streams[1])
+    ctx.finalize(bufs["b", 1], rb, streams[1])
+    check(b, rb, "ring b (ring 1 of the grid), replica 1")
+    ctx.finalize(bufs["g", 1], rg, streams[1])
+    check(g, rg, "ring g (ring 2 of the grid), replica 1")
+    ctx.select(0)
+    rb2 = lib.DeviceResult(ctx, b.n)
+    ctx.classify(bufs["b", 0], rb2, streams[0])
+    ctx.finalize(bufs["b", 0], rb2, streams[0])
+    want = check(b, rb2, "ring b again, replica 0")
+    assert (want[0] >> 16) & 0xF != lib.CLS_NIC                # decided by the carried cache
+    assert ctx.rule_count() == o.rule_count()
+    keep += [ra, rb, rg, rb2]
+    ctx.close()

@@ -250,6 +250,10 @@ case $S in
     ABL_CFGS=c3 ABL_ARGS="--frames 262144 --multi 4 --batches 16 --streams 2 --rounds 5 --launches 60" ABL_VARIANTS="product stage192" \
       bash tools/gpu.sh $S abl || exit 1
     ;;
+  r05aa)
+    # a two-ring tx grid handing its carried cache to another replica
+    TESTS="tests/test_gpu_group.py tests/test_gpu_tx.py" bash tools/gpu.sh $S testsall || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
