@@ -254,6 +254,13 @@ case $S in
     # a two-ring tx grid handing its carried cache to another replica
     TESTS="tests/test_gpu_group.py tests/test_gpu_tx.py" bash tools/gpu.sh $S testsall || exit 1
     ;;
+  r05ab)
+    # flake check: the whole GPU suite twice, then smoke
+    TAILN=3 bash tools/gpu.sh $S testsall || exit 1
+    mv $O/pytest_gpu.log $O/pytest_gpu_1.log
+    TAILN=3 bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
