@@ -33,7 +33,9 @@
 extern "C" {
 #endif
 
-#define USN_ABI_VERSION 3
+/* 4: usn_result_release; two consecutive tx rings per usn_classify_multi;
+ *    usn_finalize waits for the batch's own launch, not the stream */
+#define USN_ABI_VERSION 4
 #define USN_WINDOW 64     /* default readable header bytes at every frame start (usn_batch.window) */
 #define USN_WINDOW_MAX 80 /* the most extract_pkt_info ever reads: L4 ports of IHL 15 end at byte 78 */
 #define USN_TILE 1024     /* frames per tile (one classify workgroup; tile headers) */

@@ -31,7 +31,7 @@ def _gpu():
 def test_library_is_native_and_gfx950():
     from usnetd_amd import lib
     ctx = lib.Ctx(0)
-    assert lib.load().usn_abi_version() == 3
+    assert lib.load().usn_abi_version() == 4
     ctx.close()
 
 
