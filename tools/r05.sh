@@ -261,6 +261,18 @@ case $S in
     TAILN=3 bash tools/gpu.sh $S testsall || exit 1
     bash tools/gpu.sh $S smoke || exit 1
     ;;
+  r05ac)
+    # the scatter ranking few-bin launches by bit-sliced match (one atomic per
+    # distinct bin of a segment; c2's 19 bins) against atomics per frame
+    # (build/abl/scold = HEAD), and with the threshold at 2^7 bins (c3's 69)
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_parity.py" bash tools/gpu.sh $S testsall || exit 1
+    SCB_CFGS="c2 c5" SCB_VARIANTS="base scold scmatch7" bash tools/gpu.sh $S scb || exit 1
+    for c in c3 c1; do
+      timeout -k 10 300 python tools/scatter_bench.py --config $c --frames 262144 --multi 4 \
+        --json $O/scb_$c.json base scold scmatch7 > $O/scb_$c.log 2>&1 || exit 1
+      grep scatter $O/scb_$c.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
