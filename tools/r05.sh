@@ -273,6 +273,18 @@ case $S in
       grep scatter $O/scb_$c.log
     done
     ;;
+  r05ad)
+    # the scatter's chunk length for c2 / c4 (8 x 1M per call; product: 8
+    # tiles, 1024 chunks in one generation) at 4 and 2 (the test build's
+    # USN_SCATTER_TC knob)
+    for tc in 4 2; do
+      for c in c2 c4; do
+        USN_SCATTER_TC=$tc timeout -k 10 300 python tools/scatter_bench.py --config $c --frames 1048576 --multi 8 \
+          base testlib > $O/scb_${c}_tc$tc.log 2>&1 || exit 1
+        echo "tc=$tc $c"; grep scatter $O/scb_${c}_tc$tc.log
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
