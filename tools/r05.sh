@@ -285,6 +285,16 @@ case $S in
       done
     done
     ;;
+  r05ae)
+    # a two-ring tx launch's lists at 4-tile chunks (512 chunks: two per CU)
+    # against the plan's 8 (256, one per CU): the test build's USN_SCATTER_TC
+    for rep in 1 2; do
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 6 --rings 2 > $O/txb_prod_$rep.log 2>&1 || exit 1
+      USN_SCATTER_TC=4 timeout -k 10 200 python tools/txbench.py 1048576 24 1 build/test/libusn.so --rotate 6 --rings 2 \
+        > $O/txb_tc4_$rep.log 2>&1 || exit 1
+      tail -1 $O/txb_prod_$rep.log; tail -1 $O/txb_tc4_$rep.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
