@@ -14,11 +14,18 @@ SLOT = 128
 
 
 class GpuBackend:
-    def __init__(self, ctx: lib.Ctx | None = None, check_order=True):
+    def __init__(self, ctx: lib.Ctx | None = None, check_order=True, split_tx_seed=None):
+        """split_tx_seed: a sending endpoint's run of frames goes to the
+        device as TWO consecutive rings in one usn_classify_multi launch (one
+        tx grid), split at a seeded random frame"""
         self.ctx = ctx or lib.Ctx(0)
         self.check_order = check_order
         self.stream = self.ctx.stream()
         self.kinds = {}
+        self.split_rng = None
+        if split_tx_seed is not None:
+            import random
+            self.split_rng = random.Random(split_tx_seed)
 
     def add_endpoint(self, eid, kind, for_nic):
         self.kinds[eid] = kind
@@ -39,7 +46,7 @@ class GpuBackend:
     def frag_clear(self):
         self.ctx.frag_clear()
 
-    def forward_run(self, src, frames):
+    def _batch(self, src, frames):
         n = len(frames)
         buf = np.zeros(n * SLOT, dtype=np.uint8)
         lens = np.zeros(n, dtype=np.uint16)
@@ -47,8 +54,26 @@ class GpuBackend:
             f = f[:SLOT]
             buf[i * SLOT:i * SLOT + len(f)] = np.frombuffer(f, np.uint8)
             lens[i] = len(f)
-        b = lib.DeviceBatch(self.ctx, buf, lens, src, stride=SLOT)
-        r = lib.DeviceResult(self.ctx, n)
+        return lib.DeviceBatch(self.ctx, buf, lens, src, stride=SLOT), lib.DeviceResult(self.ctx, n)
+
+    def forward_run(self, src, frames):
+        n = len(frames)
+        if self.split_rng is not None and self.kinds.get(src) != lib.EP_NIC and n >= 2:
+            k = self.split_rng.randrange(1, n)
+            parts = [self._batch(src, frames[:k]), self._batch(src, frames[k:])]
+            try:
+                self.ctx.classify_multi([p[0] for p in parts], [p[1] for p in parts], self.stream)
+                out = []
+                for b, r in parts:
+                    self.ctx.finalize(b, r, self.stream)
+                    d = r.decisions()
+                    if self.check_order:
+                        check_order(r, d)
+                    out += [int(x) for x in d]
+            finally:
+                self._keep = parts
+            return out
+        b, r = self._batch(src, frames)
         try:
             self.ctx.classify(b, r, self.stream)
             self.ctx.finalize(b, r, self.stream)

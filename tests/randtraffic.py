@@ -76,9 +76,12 @@ def rand_want(rng):
     return w
 
 
-def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, n_rules=None):
+def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, n_rules=None,
+                switch_p: float = 0.15, ops_p: float = 0.02):
     """Returns a fixture-shaped dict {endpoints, bridge, steps} without expectations.
-    n_rules: how many initial rules (default 3..11)."""
+    n_rules: how many initial rules (default 3..11); switch_p: chance per
+    frame of a new source (runs of about 1/switch_p frames); ops_p: chance
+    per event of a control op (each also ends the run)."""
     rng = random.Random(seed)
     endpoints = [[0, 0, -1], [1, 1, 0], [2, 2, 0], [3, 2, 0], [4, 3, 0], [5, 0, -1], [6, 2, 5]]
     live = {1, 2, 3, 4, 6}
@@ -96,7 +99,7 @@ def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, 
                 bytes([0x45, 0, 0, 48, 0, 9, 0x40, 0, 64, 17, 0, 0]) + ipb("10.0.0.1") +
                 ipb("255.255.255.255") + struct.pack(">HHHH", 67, 68, 28, 0) + bytes(20))
     for _ in range(n_events):
-        if ops and rng.random() < 0.02:
+        if ops and rng.random() < ops_p:
             k = rng.random()
             if k < 0.5:
                 steps.append({"op": "add_match", "want": rand_want(rng),
@@ -113,7 +116,7 @@ def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, 
                 if src == victim:
                     src = 0
             continue
-        if rng.random() < 0.15:  # switch source endpoint (new batch)
+        if rng.random() < switch_p:  # switch source endpoint (new batch)
             if rng.random() < tx_frac:
                 src = rng.choice(sorted(live))
             else:

@@ -55,6 +55,25 @@ def test_random_streams_gpu(seed, tx_frac, coracle_mod):
             assert (x & katrun.PARITY_MASK) == (y & katrun.PARITY_MASK), (i, hex(x), hex(y))
 
 
+@pytest.mark.parametrize("switch_p,ops_p,n_events", [(0.15, 0.02, 700), (0.0008, 0.0003, 6000)])
+@pytest.mark.parametrize("seed", range(6))
+def test_random_streams_two_rings_gpu(seed, switch_p, ops_p, n_events, coracle_mod):
+    """Every sending endpoint's run goes to the device as two consecutive
+    rings of one usn_classify_multi launch (one tx grid), split at a seeded
+    random frame: learning, fragments, DHCP and the decision cache cross the
+    ring boundary inside the grid.  Long runs (about 1000 frames) span tiles."""
+    from gpu_backend import GpuBackend
+    stream = randtraffic.make_stream(500 + seed, n_events=n_events, tx_frac=0.7, switch_p=switch_p, ops_p=ops_p)
+    want = randtraffic.run_stream(stream, katrun.COracleBackend())
+    got = randtraffic.run_stream(stream, GpuBackend(split_tx_seed=seed))
+    assert len(want) == len(got)
+    for i, (x, y) in enumerate(zip(want, got)):
+        if isinstance(x, tuple):
+            assert x == y, (i, x, y)
+        else:
+            assert (x & katrun.PARITY_MASK) == (y & katrun.PARITY_MASK), (i, hex(x), hex(y))
+
+
 def _filler(n):
     """n rules no frame of randtraffic hits (dst 10.77.0.0/16): they push the
     image past LDS, so the rx kernel takes the projection table U."""

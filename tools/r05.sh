@@ -295,6 +295,16 @@ case $S in
       tail -1 $O/txb_prod_$rep.log; tail -1 $O/txb_tc4_$rep.log
     done
     ;;
+  r05af)
+    # the new two-ring random-stream parity tests, then a differential fuzz
+    # of two-ring tx launches (tools/fuzz_two_ring.py, 200 seeds in 4 chunks)
+    TESTS="tests/test_gpu_parity.py" bash tools/gpu.sh $S testsall || exit 1
+    for c in 0 1 2 3; do
+      timeout -k 10 240 python -u tools/fuzz_two_ring.py $((1000 + 50 * c)) 50 3000 > $O/fuzz_$c.log 2>&1 \
+        || { tail -3 $O/fuzz_$c.log; exit 1; }
+      tail -1 $O/fuzz_$c.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
