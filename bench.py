@@ -104,6 +104,8 @@ def parse_args(argv=None):
                          "while round i is queued)")
     ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
+    ap.add_argument("--tx-rings", type=int, default=4, choices=(1, 2, 3, 4),
+                    help="c4tx: consecutive rings of the sending endpoint per tx launch (one grid)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: ranks join the process group and report, no GPU")
     return ap.parse_args(argv)
@@ -478,7 +480,8 @@ def measure(run, args, dist, world):
 # (profiles/r03/r03r)
 EXTRA_QUEUES = {"c3": 8}
 EXTRA_MIN_STEPS = {"c3": 200}   # c3's poll round is ~55 us: 200 rounds time ~11 ms, not ~2
-TX_ROTATE = 6              # c4tx: the ring in 6 device buffers (384 MiB > the 256 MiB Infinity Cache)
+TX_ROTATE = 8              # c4tx: the ring in 8 device buffers (512 MiB > the 256 MiB Infinity Cache;
+                           # 7 others, 448 MiB, between two uses of one at 4 rings per launch)
 TX_RINGS = 100             # c4tx: timed rings (and device event pairs) at least
 
 
@@ -492,8 +495,8 @@ def measure_tx(ctx, args):
     j + 1 may be enqueued before launch j's rings are finalized (at most two
     launches in flight; launch j + 1 is decided again on the host when a
     finalize of launch j changed what it started from).  value = frames /
-    wall time of that pipelined loop with two consecutive rings per launch
-    (one tx grid, usn_classify_multi), one ring per launch beside it; the
+    wall time of that pipelined loop with --tx-rings (4) consecutive rings per
+    launch (one tx grid, usn_classify_multi), one ring per launch beside it; the
     device time of the call (tx kernel + per-endpoint scatter, HIP events)
     gives the roofline."""
     from usnetd_amd import lib, traffic
@@ -553,25 +556,26 @@ def measure_tx(ctx, args):
     wall_ev, nl = pipelined(True)
     learned += nl
     dev_ms = float(np.median([ctx.elapsed_ms(a, e) for a, e in evs]))
-    # two consecutive rings per usn_classify_multi launch (one tx grid: ring
-    # 2's header loads overlap ring 1's chain), launch j + 1 enqueued before
-    # launch j's rings are finalized
-    res2 = res + [lib.DeviceResult(ctx, n) for _ in range(2)]
-    K2 = K // 2
+    # P consecutive rings per usn_classify_multi launch (one tx grid: ring
+    # k's header loads overlap the chain of the rings before), launch j + 1
+    # enqueued before launch j's rings are finalized
+    P = args.tx_rings
+    res2 = res + [lib.DeviceResult(ctx, n) for _ in range(2 * P - 2)]
+    K2 = -(-K // P)
     evs2 = [(ctx.event(), ctx.event()) for _ in range(K2)]
 
     # the loop's ctypes arguments built once (the loop times the library, not
-    # the binding): launch j takes buffers 2j, 2j + 1 (mod TX_ROTATE) and
-    # results 2j, 2j + 1 (mod 4), a cycle of 6 launches
-    PER = 6
+    # the binding): launch j takes buffers Pj .. Pj + P - 1 (mod TX_ROTATE)
+    # and results Pj .. (mod 2P), a cycle of PER launches
+    PER = TX_ROTATE
     margs, fargs = [], []
     finfo = lib.FinalizeInfo()
     for j in range(PER):
-        ks = [2 * j, 2 * j + 1]
-        ba = (lib.Batch * 2)(*[bufs[k % TX_ROTATE].desc for k in ks])
-        ra = (lib.Result * 2)(*[res2[k % 4].desc for k in ks])
-        margs.append((ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), 2, s, ba, ra))
-        fargs.append([(ctx.h, C.byref(bufs[k % TX_ROTATE].desc), C.byref(res2[k % 4].desc), s,
+        ks = [P * j + q for q in range(P)]
+        ba = (lib.Batch * P)(*[bufs[k % TX_ROTATE].desc for k in ks])
+        ra = (lib.Result * P)(*[res2[k % (2 * P)].desc for k in ks])
+        margs.append((ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), P, s, ba, ra))
+        fargs.append([(ctx.h, C.byref(bufs[k % TX_ROTATE].desc), C.byref(res2[k % (2 * P)].desc), s,
                        C.byref(finfo)) for k in ks])
     multi, fin = ctx.L.usn_classify_multi, ctx.L.usn_finalize
 
@@ -597,22 +601,22 @@ def measure_tx(ctx, args):
                     lib.check(rc, "usn_finalize")
                 nl += finfo.n_learned
         return time.perf_counter() - t, nl
-    # untimed: the tx scratch grows to two rings' frames and tiles once
-    ctx.classify_multi([bufs[0], bufs[1]], [res2[0], res2[1]], s)
-    for q in range(2):
+    # untimed: the tx scratch grows to P rings' frames and tiles once
+    ctx.classify_multi(bufs[:P], res2[:P], s)
+    for q in range(P):
         learned += ctx.finalize(bufs[q], res2[q], s).n_learned
     wall2, nl = pipelined2(False)
     learned += nl
     wall2_ev, nl = pipelined2(True)
     learned += nl
     dev2_ms = float(np.median([ctx.elapsed_ms(a, e) for a, e in evs2]))
-    # the value: two rings per launch (its device time gives the roofline);
+    # the value: P rings per launch (its device time gives the roofline);
     # one ring per launch beside it
-    F2 = 2 * n
+    F2 = P * n
     achieved = ALGO_BYTES * F2 / (dev2_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "tx_kernel (two rings per grid) + per-endpoint scatter",
+            "kernel": "tx_kernel (%d rings per grid) + per-endpoint scatter" % P,
             "kernel_us_median": round(dev2_ms * 1e3, 3),
             "frames_per_launch": F2, "algo_bytes_per_frame": ALGO_BYTES}
     pmc = os.path.join(ROOT, "profiles", "pmc_c4tx.json")
@@ -627,13 +631,14 @@ def measure_tx(ctx, args):
                 roof["traffic_source"] = os.path.relpath(pmc, ROOT)
         except (OSError, ValueError):
             pass
-    x = {"value": round(2 * K2 * n / wall2 / 1e6, 2), "unit": "Mpkts/s",
-         "value_basis": "end to end: every ring classified and finalized; two consecutive rings "
+    x = {"value": round(P * K2 * n / wall2 / 1e6, 2), "unit": "Mpkts/s",
+         "value_basis": "end to end: every ring classified and finalized; %d consecutive rings "
                         "per usn_classify_multi launch (one tx grid), launch j + 1 enqueued "
-                        "before launch j's usn_finalize calls (no events in the timed loop)",
-         "ms_per_ring": round(wall2 * 1e3 / (2 * K2), 4),
+                        "before launch j's usn_finalize calls (no events in the timed loop)" % P,
+         "rings_per_launch": P,
+         "ms_per_ring": round(wall2 * 1e3 / (P * K2), 4),
          "device_mpps": round(F2 / (dev2_ms * 1e-3) / 1e6, 2),
-         "pipelined_with_events_mpps": round(2 * K2 * n / wall2_ev / 1e6, 2),
+         "pipelined_with_events_mpps": round(P * K2 * n / wall2_ev / 1e6, 2),
          "one_ring_launches": {"mpps": round(K * n / wall / 1e6, 2),
                                "sequential_mpps": round(K * n / wall_seq / 1e6, 2),
                                "ms_per_ring": round(wall * 1e3 / K, 4),
@@ -643,7 +648,7 @@ def measure_tx(ctx, args):
                                "basis": "one ring per launch, ring k + 1 enqueued before ring "
                                         "k's usn_finalize (sequential: each ring finalized "
                                         "before the next is enqueued)"},
-         "rings": K, "learned_in_timed_rings": int(learned),
+         "rings": P * K2, "learned_in_timed_rings": int(learned),
          "learning_ring_us": round(learn_us, 1), "learning_ring_learned": int(learn_n),
          "after_learning_ring_us": round(next_us, 1),
          "learning_ring_basis": "wall time of the first ring (classify call + usn_finalize, "

@@ -16,8 +16,8 @@ SLOT = 128
 class GpuBackend:
     def __init__(self, ctx: lib.Ctx | None = None, check_order=True, split_tx_seed=None):
         """split_tx_seed: a sending endpoint's run of frames goes to the
-        device as TWO consecutive rings in one usn_classify_multi launch (one
-        tx grid), split at a seeded random frame"""
+        device as 2-4 consecutive rings in one usn_classify_multi launch (one
+        tx grid), split at seeded random frames"""
         self.ctx = ctx or lib.Ctx(0)
         self.check_order = check_order
         self.stream = self.ctx.stream()
@@ -59,8 +59,9 @@ class GpuBackend:
     def forward_run(self, src, frames):
         n = len(frames)
         if self.split_rng is not None and self.kinds.get(src) != lib.EP_NIC and n >= 2:
-            k = self.split_rng.randrange(1, n)
-            parts = [self._batch(src, frames[:k]), self._batch(src, frames[k:])]
+            m = self.split_rng.randint(2, min(4, n))
+            cuts = [0] + sorted(self.split_rng.sample(range(1, n), m - 1)) + [n]
+            parts = [self._batch(src, frames[x:y]) for x, y in zip(cuts, cuts[1:])]
             try:
                 self.ctx.classify_multi([p[0] for p in parts], [p[1] for p in parts], self.stream)
                 out = []

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(L, n)]
     assert not missing, missing
     assert set(declared()) <= set(lib.EXPORTED)
-    assert L.usn_abi_version() == 4
+    assert L.usn_abi_version() == 5
 
 
 def test_device_code_is_gfx950():

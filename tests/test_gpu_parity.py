@@ -31,7 +31,7 @@ def _gpu():
 def test_library_is_native_and_gfx950():
     from usnetd_amd import lib
     ctx = lib.Ctx(0)
-    assert lib.load().usn_abi_version() == 4
+    assert lib.load().usn_abi_version() == 5
     ctx.close()
 
 
@@ -58,10 +58,10 @@ def test_random_streams_gpu(seed, tx_frac, coracle_mod):
 @pytest.mark.parametrize("switch_p,ops_p,n_events", [(0.15, 0.02, 700), (0.0008, 0.0003, 6000)])
 @pytest.mark.parametrize("seed", range(6))
 def test_random_streams_two_rings_gpu(seed, switch_p, ops_p, n_events, coracle_mod):
-    """Every sending endpoint's run goes to the device as two consecutive
-    rings of one usn_classify_multi launch (one tx grid), split at a seeded
-    random frame: learning, fragments, DHCP and the decision cache cross the
-    ring boundary inside the grid.  Long runs (about 1000 frames) span tiles."""
+    """Every sending endpoint's run goes to the device as 2-4 consecutive
+    rings of one usn_classify_multi launch (one tx grid), split at seeded
+    random frames: learning, fragments, DHCP and the decision cache cross the
+    ring boundaries inside the grid.  Long runs (about 1000 frames) span tiles."""
     from gpu_backend import GpuBackend
     stream = randtraffic.make_stream(500 + seed, n_events=n_events, tx_frac=0.7, switch_p=switch_p, ops_p=ops_p)
     want = randtraffic.run_stream(stream, katrun.COracleBackend())

@@ -326,10 +326,10 @@ def test_tx_pipeline_order_and_busy(coracle_mod):
     ctx.close()
 
 
-def _ring_launches(rings, coracle_mod, pipelined=False, src=None):
-    """Rings of one sending endpoint, two consecutive rings per
-    usn_classify_multi launch (one tx grid: ring 2's tiles order after ring
-    1's); with `pipelined`, launch j + 1 is enqueued before
+def _ring_launches(rings, coracle_mod, pipelined=False, src=None, per=2):
+    """Rings of one sending endpoint, `per` consecutive rings per
+    usn_classify_multi launch (one tx grid: ring k's tiles order after ring
+    k - 1's); with `pipelined`, launch j + 1 is enqueued before
     launch j's rings are finalized.  Every ring's decisions and lists, and
     the registry and bridge at the end, against the sequential oracle."""
     from usnetd_amd import lib, traffic
@@ -341,7 +341,7 @@ def _ring_launches(rings, coracle_mod, pipelined=False, src=None):
     s = ctx.stream()
     bs = [lib.DeviceBatch(ctx, c.frames, c.lens, src, stride=c.stride) for c in rings]
     rs = [lib.DeviceResult(ctx, c.n) for c in rings]
-    pairs = [list(range(k, min(k + 2, len(rings)))) for k in range(0, len(rings), 2)]
+    pairs = [list(range(k, min(k + per, len(rings)))) for k in range(0, len(rings), per)]
     infos = [None] * len(rings)
 
     def launch(p):
@@ -471,8 +471,10 @@ def test_tx_two_ring_launch_rules(coracle_mod):
         return ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(bb), s)
 
     assert multi([b, b2], rs[:2]) == lib.USN_EINVAL          # two sources
-    assert multi([b, b, b], rs[:3]) == lib.USN_EINVAL        # three rings
+    assert multi([b] * 5, rs[:5]) == lib.USN_EINVAL          # five rings
     assert multi([b, b], [rs[0], rs[0]]) == lib.USN_EINVAL   # one result twice
+    assert multi([b, b, b], [rs[0], rs[1], rs[0]]) == lib.USN_EINVAL
+    assert multi([b, b, b2], rs[:3]) == lib.USN_EINVAL       # a third ring of another source
     assert multi([b, b], rs[:2]) == 0
     assert multi([b], [rs[1]]) == lib.USN_EBUSY              # a result in flight
     assert multi([b, b], rs[2:4]) == 0                       # the second launch
@@ -519,3 +521,52 @@ def test_tx_two_rings_tile_edges(n1, n2, coracle_mod):
     r2 = traffic.c4tx(n=n2, seed=71)
     infos = _ring_launches([r1, r2, r1, r2], coracle_mod)
     assert [i.n_host for i in infos] == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_tx_four_rings_one_launch(n, coracle_mod):
+    """Four rings per grid: ring 0 learns, rings 1-3 (the same frames) saw
+    it inside the grid; then the same with launch 1 enqueued before launch
+    0's rings are finalized (all four decided again on the host)."""
+    from usnetd_amd import traffic
+    cfg = traffic.config("c4tx", n=n)
+    infos = _ring_launches([cfg] * 8, coracle_mod, per=4)
+    assert infos[0].n_learned > 0
+    assert [i.n_learned for i in infos[1:]] == [0] * 7
+    assert [i.n_host for i in infos] == [0] * 8
+    infos = _ring_launches([cfg] * 12, coracle_mod, pipelined=True, per=4)
+    assert [i.n_host for i in infos] == [0] * 4 + [n] * 4 + [0] * 4
+
+
+@pytest.mark.parametrize("per", [3, 4])
+def test_tx_multi_rings_all_learn(per, coracle_mod):
+    """Every ring brings new flows: each learns its own on the device, with
+    the earlier rings' items already visible to it."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=1 << 15, seed=80 + k) for k in range(2 * per)]
+    infos = _ring_launches(rings, coracle_mod, per=per)
+    assert all(i.n_learned > 0 for i in infos)
+    assert [i.n_host for i in infos] == [0] * (2 * per)
+
+
+@pytest.mark.parametrize("at", [0, 1, 3])
+def test_tx_four_rings_host_tail(at, coracle_mod):
+    """A DHCP request in ring `at` of four: the rest of that ring goes to the
+    host stage, and every later ring of the grid is decided again on the
+    host; the rings before stay final."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=5000, seed=90 + k) for k in range(4)]
+    rings[at] = traffic.c4tx(n=5000, host_at=[2500], seed=90 + at)
+    infos = _ring_launches(rings, coracle_mod, per=4)
+    assert [i.n_host for i in infos] == [0] * at + [2500] + [5000] * (3 - at)
+
+
+@pytest.mark.parametrize("ns", [(1, 1, 1, 1), (1023, 1, 1025, 3), (1024, 2049, 1, 5000), (3000, 1025)])
+def test_tx_multi_rings_tile_edges(ns, coracle_mod):
+    """Three and four rings in one grid at tile edges (rings of one frame,
+    rings ending inside a tile, full tiles); every launch twice."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=x, seed=100 + k) for k, x in enumerate(ns)]
+    per = len(ns) if len(ns) > 2 else 3
+    infos = _ring_launches(rings + rings, coracle_mod, per=per)
+    assert [i.n_host for i in infos] == [0] * len(infos)

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""Differential fuzz of the two-ring tx launch on the GPU: random streams
+"""Differential fuzz of multi-ring tx launches on the GPU: random streams
 (tests/randtraffic.py) through tests/gpu_backend.GpuBackend with every
-sending run split into two rings of one usn_classify_multi launch, against
+sending run split into 2-4 rings of one usn_classify_multi launch, against
 the C oracle.  Stops at the first mismatch.
-usage: fuzz_two_ring.py first_seed n_seeds [n_events=3000]"""
+usage: fuzz_multi_ring.py first_seed n_seeds [n_events=3000]"""
 import os
 import sys
 import time
@@ -42,4 +42,4 @@ for seed in range(s0, s0 + ns):
     frames += sum(1 for x in want if not isinstance(x, tuple))
     if seed % 10 == 9 or seed == s0 + ns - 1:
         print("seeds %d..%d ok, %d frames, %.0f s" % (s0, seed, frames, time.time() - t0), flush=True)
-print({"fuzz": "two_ring", "seeds": ns, "frames": frames, "mismatches": 0})
+print({"fuzz": "multi_ring", "seeds": ns, "frames": frames, "mismatches": 0})

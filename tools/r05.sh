@@ -297,12 +297,44 @@ case $S in
     ;;
   r05af)
     # the new two-ring random-stream parity tests, then a differential fuzz
-    # of two-ring tx launches (tools/fuzz_two_ring.py, 200 seeds in 4 chunks)
+    # of two-ring tx launches (tools/fuzz_two_ring.py, since renamed
+    # fuzz_multi_ring.py and splitting into 2-4 rings; 200 seeds in 4 chunks)
     TESTS="tests/test_gpu_parity.py" bash tools/gpu.sh $S testsall || exit 1
     for c in 0 1 2 3; do
-      timeout -k 10 240 python -u tools/fuzz_two_ring.py $((1000 + 50 * c)) 50 3000 > $O/fuzz_$c.log 2>&1 \
+      timeout -k 10 240 python -u tools/fuzz_multi_ring.py $((1000 + 50 * c)) 50 3000 > $O/fuzz_$c.log 2>&1 \
         || { tail -3 $O/fuzz_$c.log; exit 1; }
       tail -1 $O/fuzz_$c.log
+    done
+    ;;
+  r05ag)
+    # per-frame tx cost against the grid's size, same flows (--concat: a ring
+    # of K copies of the 1M c4tx ring): 1M x 2 rings (the product's launch),
+    # 2M x 1, 2M x 2 (a 4M grid, as four 1M rings would be), 4M x 1
+    for rep in 1 2; do
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 6 --rings 2 > $O/txb_1Mx2_$rep.log 2>&1 || exit 1
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 3 --concat 2 --rings 1 > $O/txb_2Mx1_$rep.log 2>&1 || exit 1
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 3 --concat 2 --rings 2 > $O/txb_2Mx2_$rep.log 2>&1 || exit 1
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 2 --concat 4 --rings 1 > $O/txb_4Mx1_$rep.log 2>&1 || exit 1
+      for v in 1Mx2 2Mx1 2Mx2 4Mx1; do echo "$v $(tail -1 $O/txb_${v}_$rep.log)"; done
+    done
+    ;;
+  r05ah)
+    # up to four consecutive rings per tx launch (one grid): the tx and
+    # random-stream GPU tests, a multi-ring fuzz, 2 vs 4 rings per launch
+    # (txbench, 8 rotating buffers), the bench's c4tx line at 2 and 4
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py tests/test_gpu_window.py tests/test_gpu_group.py" \
+      bash tools/gpu.sh $S testsall || exit 1
+    timeout -k 10 240 python -u tools/fuzz_multi_ring.py 2000 100 3000 > $O/fuzz.log 2>&1 || { tail -3 $O/fuzz.log; exit 1; }
+    tail -1 $O/fuzz.log
+    for rep in 1 2; do
+      for r in 2 4; do
+        timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 8 --rings $r > $O/txb_r${r}_$rep.log 2>&1 || exit 1
+        echo "rings=$r $(tail -1 $O/txb_r${r}_$rep.log)"
+      done
+    done
+    for r in 2 4; do
+      BENCH_ARGS="--steps 10 --warmup 3 --extras c4tx --no-cpu-baseline --tx-rings $r" bash tools/gpu.sh $S bench || exit 1
+      mv $O/bench.log $O/bench_tx$r.log
     done
     ;;
   *) echo "unknown session $S"; exit 2 ;;

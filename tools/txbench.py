@@ -12,8 +12,10 @@ Usage: python tools/txbench.py [n] [batches] [distinct] [libpath] [--rotate R] [
   (same flows, nothing new learned after the first batch, and R x the ring's
   bytes touched between two uses of a buffer: with R x 64 MiB > 256 MiB no
   batch is served from the Infinity Cache -- SURVEY §8d's anti-cache rule).
-  --rings 2: two consecutive rings per launch (one tx grid, usn_classify_multi);
-  a row is then one launch (2n frames).
+  --rings R: R consecutive rings per launch (one tx grid, usn_classify_multi);
+  a row is then one launch (R x n frames).
+  --concat K: each ring is K copies of the n generated frames (K x n frames,
+  the same flows: the per-frame work of an n-frame ring in a larger grid).
 """
 import argparse
 import ctypes as C
@@ -38,10 +40,16 @@ def main():
     ap.add_argument("distinct", nargs="?", type=int, default=1)
     ap.add_argument("libpath", nargs="?", default=None)
     ap.add_argument("--rotate", type=int, default=1)
-    ap.add_argument("--rings", type=int, default=1, choices=(1, 2))
+    ap.add_argument("--rings", type=int, default=1, choices=(1, 2, 3, 4))
+    ap.add_argument("--concat", type=int, default=1)
     a = ap.parse_args()
     n, nb, distinct = a.n, a.batches, a.distinct
     cfgs = [traffic.c4tx(n=n, seed=6 + k) for k in range(distinct)]
+    if a.concat > 1:
+        for c in cfgs:
+            c.frames = np.concatenate([c.frames[:n * c.stride]] * a.concat + [c.frames[n * c.stride:]])
+            c.lens = np.concatenate([c.lens[:n]] * a.concat)
+        n *= a.concat
     ctx = lib.Ctx(0, a.libpath) if a.libpath else lib.Ctx(0)
     traffic.install_ctx(ctx, cfgs[0])
     s = ctx.stream()

@@ -1680,7 +1680,7 @@ __device__ __forceinline__ uint32_t tx_learned_key1(const TxArgs &t, uint32_t x,
   if (ld_sc1(slot + 2) != (((unsigned long long)y << 32) | x) ||
       ld_sc1(slot + 3) != (((unsigned long long)meta << 32) | z))
     atomicOr(t.counters + 1, 2u);                      // fingerprint collision: host redoes
-  return USN_SLOT_VALID | (t.a.src << 16);
+  return USN_SLOT_VALID | (t.a[0].src << 16);
 }
 
 /* key2 = to_match_want_with_src(false) */
@@ -1707,7 +1707,7 @@ __device__ __forceinline__ uint32_t tx_lookup_dec(const ClassifyArgs &a, uint32_
 template <bool IN_LDS>
 __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 &r0,
                                    const uint4 &r1, uint32_t i, uint32_t ins) {
-  const ClassifyArgs &a = t.a;
+  const ClassifyArgs &a = t.a[0];
   const uint32_t fl = r0.x;
   if (!tx_dmac_in(t, fl, r1, i, ins)) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // :254-255
   uint32_t x, y, z, meta;
@@ -1898,12 +1898,14 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(NTHREA
 void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames all resident)
   extern __shared__ __align__(16) uint8_t smem[];
   /* tile: this workgroup's tile in the launch (the protocol's); rt: in its
-     ring (rings = 2: ring 2's tiles follow ring 1's, TxArgs) */
+     ring (rings > 1: ring k's tiles follow ring k - 1's, TxArgs) */
   const uint32_t tile = blockIdx.x;
-  const bool ring2 = tile >= t.a.ntiles;
-  const ClassifyArgs &a = ring2 ? t.a2 : t.a;
-  const uint32_t rt = ring2 ? tile - t.a.ntiles : tile;
-  const Lds L = carve(smem, t.a.nbins);
+  uint32_t ring = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < USN_TX_RINGS; ++k) ring += (k < t.rings && tile >= t.tile_base[k]) ? 1u : 0u;
+  const ClassifyArgs &a = t.a[ring];
+  const uint32_t rt = tile - t.tile_base[ring];
+  const Lds L = carve(smem, t.a[0].nbins);
   uint4 *srec = reinterpret_cast<uint4 *>(smem + lds_core_bytes(a.nbins));   // the tile's records
   uint32_t *sdec = reinterpret_cast<uint32_t *>(srec + TILE);               // its decisions
   uint4 *stab = reinterpret_cast<uint4 *>(smem + tx_lds_head(a.nbins));
@@ -1935,7 +1937,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     T = stab;
   }
   if (tile == 0) {   // carried-in cache of this source; counters for phase 2 (all wait for tile 0)
-    if (tid < 7 && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
+    if (tid < USN_TXC_WORDS && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
       __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     resolve_carry(a, s_carry, L.scratch);
     if (tid == 0) {
@@ -2413,7 +2415,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
         const uint64_t m = rec_smac(r1[r]);
         if (slot_first(set_find(t.macset, t.macset_mask, 2, t.epoch, m, usn_mac_hash(m)), t.epoch) == i) {
           const uint32_t pos = atomicAdd(t.counters, 1u);
-          if (ring2) atomicAdd(t.counters + 6, 1u);
+          if (ring) atomicAdd(t.counters + USN_TXC_LEARNED + ring, 1u);
           if (pos < t.learned_cap) {
             t.learned[2 * pos] = make_uint4(i, 0u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4((uint32_t)m, (uint32_t)(m >> 32), 0u, 0u);
@@ -2434,7 +2436,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
               ld_sc1(slot + 3) != (((unsigned long long)meta << 32) | z))
             atomicOr(t.counters + 1, 2u);
           const uint32_t pos = atomicAdd(t.counters, 1u);
-          if (ring2) atomicAdd(t.counters + 6, 1u);
+          if (ring) atomicAdd(t.counters + USN_TXC_LEARNED + ring, 1u);
           if (pos < t.learned_cap) {
             t.learned[2 * pos] = make_uint4(i, 1u, 0u, 0u);
             t.learned[2 * pos + 1] = make_uint4(x, y, z, meta);
@@ -2465,7 +2467,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       if (g_getn<1>(t.aux + (size_t)((hx - 1) / TILE) * TXA_GRANULES + TXG_HDEC, t, hv)) hd = hv[0];
     }
     s_head = hd;
-    if (ring2 && rt == 0) {   // ring 2's summary: the cache ring 1 hands on (state after its last frame)
+    if (ring && rt == 0) {   // ring k's summary: the cache ring k - 1 hands on (state after its last frame)
       usn_summary *S = a.summary;
       const uint32_t st = s_before ? (tx_touch(s_brec) == 1u && !(s_brec.x & TXR_HOST) ? USN_CS_VALID : 0u)
                                    : s_cin[0];
@@ -2541,7 +2543,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     H->class_count[3] = (uint16_t)fl;
     H->class_count[1] = (uint16_t)(nt - nic - fl - dr);
     if (!lastp) { H->last_state = 0; H->last_dst = 0; H->last_idx = 0xFFFFFFFFu; }
-    if (s_misc[1]) atomicAdd(t.counters + (ring2 ? 5 : 4), s_misc[1]);   // after phase 2: tile 0 zeroed it
+    if (s_misc[1]) atomicAdd(t.counters + USN_TXC_HOST + ring, s_misc[1]);   // after phase 2: tile 0 zeroed it
   }
   STAMP(11);
   STAMP_FLUSH_AT(tile);
@@ -2551,8 +2553,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
 static inline size_t table_lds_bytes(uint32_t table_units);
 
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream) {
-  const ClassifyArgs &a = t.a;
-  const uint32_t ntiles = a.ntiles + (t.rings == 2 ? t.a2.ntiles : 0u);
+  const ClassifyArgs &a = t.a[0];
+  const uint32_t ntiles = t.tile_base[t.rings];
   if (ntiles == 0) return hipSuccess;
   const dim3 g(ntiles), b(NTHREADS);
   const size_t head = tx_lds_head(a.nbins);
@@ -3029,8 +3031,11 @@ void scatter_kernel(ScatterArgs s) {
     };
     uint32_t v;
     if (tid == 0) v = B.summary->flags;
-    else if (tid == 1) v = bi == 0 ? ctr(0) - ctr(6) : ctr(6);   // the ring's learned items
-    else if (tid == 5) v = ctr(4 + bi);                           // ... frames for the host stage
+    else if (tid == 1) {                                          // the ring's learned items
+      v = bi ? ctr(USN_TXC_LEARNED + bi) : ctr(0);
+      if (bi == 0)
+        for (uint32_t k = 1; k < s.count; ++k) v -= ctr(USN_TXC_LEARNED + k);
+    } else if (tid == 5) v = ctr(USN_TXC_HOST + bi);              // ... frames for the host stage
     else v = ctr(tid - 1);                                        // flags, sets, timeout epoch
     uint32_t *to = s.txs_out + USN_TXS_WORDS * bi;
     to[tid] = v;

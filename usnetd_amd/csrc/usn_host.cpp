@@ -483,7 +483,7 @@ struct Replica {
 #ifndef USN_DONE_EV_FLAGS
 #define USN_DONE_EV_FLAGS hipEventDisableTiming
 #endif
-constexpr size_t TXSTATE_BYTES = 2 * USN_TXS_WORDS * 4;   // a tx launch's gathered state per slot
+constexpr size_t TXSTATE_BYTES = USN_TX_RINGS * USN_TXS_WORDS * 4;   // a tx launch's gathered state per slot
 
 struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
@@ -533,17 +533,18 @@ struct usn_ctx {
   uint32_t bridge_mask = 0;
   /* tx batches in flight: classified, not finalized, so the registry is not
    * final (every registry call returns USN_EBUSY).  At most two launches
-   * (each one ring, or two consecutive rings in one grid), of one source, on
+   * (each one ring, or up to USN_TX_RINGS consecutive rings in one grid), of one source, on
    * one stream and replica: launch k + 1 may be enqueued before launch k's
    * rings are finalized (the device is not left idle while the host
    * finalizes).  Launch k + 1 ran against the state launch k started from;
    * when a finalize of launch k's rings changed that state (it learned, or
    * ran a host tail), launch k + 1's first ring is decided again on the host
-   * from its first frame (tx_redo_next).  Ring 2 of a launch saw ring 1's
-   * learning on the device: it is redone only after ring 1 ran a host tail. */
+   * from its first frame (tx_redo_next).  Ring k of a launch saw ring k - 1's
+   * learning on the device: it is redone only after ring k - 1 ran a host
+   * tail (or was redone). */
   struct Tx {
     const uint32_t *decisions = nullptr;
-    const void *launch_dec = nullptr;   // ring 1's decisions (usn_ctx::txstate_for)
+    const void *launch_dec = nullptr;   // ring 0's decisions (usn_ctx::txstate_for)
     int src = -1;
     uint32_t replica = 0, slot = 0, epoch = 0;
     uint32_t ring = 0, rings = 1;       // this ring of the launch's
@@ -569,7 +570,7 @@ struct usn_ctx {
   size_t h_lists_cap = 0;
   uint4 *h_items = nullptr;      // pinned: a tx batch's learned list
   size_t h_items_cap = 0;
-  uint64_t h_items_for = 0;      // the launch whose list h_items holds (both rings read it)
+  uint64_t h_items_for = 0;      // the launch whose list h_items holds (every ring reads it)
   /* host frame reader: frames whose ports lie past the batch window */
   usn_frame_reader reader = nullptr;
   void *reader_user = nullptr;
@@ -2467,8 +2468,8 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bo
     T.aux_tiles = ntiles;
   }
   if (!X.counters) {
-    HIPCHK(hipMalloc(&X.counters, 8 * sizeof(uint32_t)));
-    HIPCHK(hipMemset(X.counters, 0, 8 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&X.counters, USN_TXC_WORDS * sizeof(uint32_t)));
+    HIPCHK(hipMemset(X.counters, 0, USN_TXC_WORDS * sizeof(uint32_t)));
   }
   bool clear = false;
   if (slots > T.set_slots) {
@@ -2592,15 +2593,16 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (st) return st;
     tx |= c->eps[b[k].src_endpoint].kind != USN_EP_NIC;
   }
-  if (tx) {   // a tx launch changes shared state: one ring of a source, or two consecutive rings
-    if (count > 2) return USN_EINVAL;
-    if (count == 2) {
-      if (b[1].src_endpoint != b[0].src_endpoint || r[1].decisions == r[0].decisions ||
-          r[1].scratch == r[0].scratch)
-        return USN_EINVAL;
-      // the launch's frame index (ring 2 after ring 1's tiles) stays below 2^32 - 1
-      if ((b[0].n + USN_TILE - 1) / USN_TILE * USN_TILE + b[1].n >= 0xFFFFFFFFull) return USN_ERANGE;
+  if (tx) {   // a tx launch changes shared state: one ring of a source, or up to 4 consecutive rings
+    if (count > USN_TX_RINGS) return USN_EINVAL;
+    uint64_t vend = 0;   // the launch's frame index (ring k after ring k - 1's tiles)
+    for (uint32_t k = 0; k < count; ++k) {
+      for (uint32_t j = 0; j < k; ++j)
+        if (r[j].decisions == r[k].decisions || r[j].scratch == r[k].scratch) return USN_EINVAL;
+      if (b[k].src_endpoint != b[0].src_endpoint) return USN_EINVAL;
+      vend += k + 1 < count ? (b[k].n + USN_TILE - 1) / USN_TILE * USN_TILE : b[k].n;
     }
+    if (vend >= 0xFFFFFFFFull) return USN_ERANGE;   // ... stays below 2^32 - 1
   } else {
     for (uint32_t k = 0; k < count; ++k)
       for (uint32_t j = 0; j < k; ++j)
@@ -2656,14 +2658,15 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
-    const uint64_t n_all = tb.n + (count == 2 ? b[1].n : 0);
+    uint64_t n_all = 0;
+    for (uint32_t k = 0; k < count; ++k) n_all += b[k].n;
     int st = tx_prepare(R, n_all, m.tile_base[count], slot, !c->txq.empty());
     if (st) return st;
     usn::TxArgs t;
     std::memset(&t, 0, sizeof t);
-    t.a = m.b[0];
     t.rings = count;
-    if (count == 2) t.a2 = m.b[1];
+    for (uint32_t k = 0; k < count; ++k) t.a[k] = m.b[k];
+    for (uint32_t k = 0; k <= count; ++k) t.tile_base[k] = m.tile_base[k];
     st = tx_listen(R, tb.src_endpoint, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
     t.aux = R.aux;
@@ -2677,7 +2680,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     t.bridge_set = R.d_bridge_set;
     t.bridge_mask = c->bridge_mask;
     t.listen = R.listen;
-    t.next_dhcp_set = t.a.next_dhcp_set;
+    t.next_dhcp_set = t.a[0].next_dhcp_set;
     if (c->tx512) HIPCHK(usn_t512::launch_tx(t, (hipStream_t)stream));
     else HIPCHK(usn::launch_tx(t, (hipStream_t)stream));   // tile 0 zeroes t.counters[0..2]
     const uint64_t launch = ++c->tx_launches;
@@ -2691,7 +2694,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       p.epoch = R.epoch;
       p.ring = k;
       p.rings = count;
-      p.voff = k ? m.b[0].ntiles * USN_TILE : 0u;
+      p.voff = m.tile_base[k] * USN_TILE;
       p.launch = launch;
       p.stream = (hipStream_t)stream;
       c->txq.push_back(p);
@@ -2914,7 +2917,8 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
                       usn_summary &sum, std::vector<usn_tile_hdr> &th, uint32_t *cnt,
                       const uint32_t *d_counters = nullptr, uint32_t *d_diag = nullptr) {
   const size_t tb = (size_t)ntiles * sizeof(usn_tile_hdr);
-  const size_t need = sizeof(usn_summary) + tb + 32 + 4;
+  constexpr size_t CB = USN_TXC_WORDS * 4;
+  const size_t need = sizeof(usn_summary) + tb + CB + 4;
   if (need > c->h_stage_cap) {
     if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
     c->h_stage = nullptr;
@@ -2927,16 +2931,16 @@ int fetch_batch_state(usn_ctx *c, const usn_result *r, uint32_t ntiles, hipStrea
   HIPCHK(hipMemcpyAsync(p, r->summary, sizeof(usn_summary), hipMemcpyDeviceToHost, s));
   if (tb) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary), r->tiles, tb, hipMemcpyDeviceToHost, s));
   if (cnt)
-    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, 32, hipMemcpyDeviceToHost, s));
-  if (d_diag) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb + 32, d_diag, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb, d_counters, CB, hipMemcpyDeviceToHost, s));
+  if (d_diag) HIPCHK(hipMemcpyAsync(p + sizeof(usn_summary) + tb + CB, d_diag, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   std::memcpy(&sum, p, sizeof sum);
   th.resize(ntiles);
   if (tb) std::memcpy(th.data(), p + sizeof(usn_summary), tb);
-  if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, 32);
+  if (cnt) std::memcpy(cnt, p + sizeof(usn_summary) + tb, CB);
   if (d_diag) {
     uint32_t dg;
-    std::memcpy(&dg, p + sizeof(usn_summary) + tb + 32, 4);
+    std::memcpy(&dg, p + sizeof(usn_summary) + tb + CB, 4);
     return lists_failed(dg, d_diag, s);
   }
   return USN_OK;
@@ -3071,7 +3075,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   const int nd_src0 = S.next_dhcp, nd_nic0 = S.for_nic >= 0 ? c->eps[S.for_nic].next_dhcp : -1;
   usn_summary sum;
   std::vector<usn_tile_hdr> th;
-  uint32_t cnt[8];
+  uint32_t cnt[USN_TXC_WORDS];
   if (c->txstate_for[txp.slot] == txp.launch_dec && X.txstate_ev) {   // gathered behind the launch
     HIPCHK(hipEventSynchronize(X.txstate_ev));
     if (txp.ring + 1 == txp.rings) c->txstate_for[txp.slot] = nullptr;
@@ -3079,7 +3083,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
         reinterpret_cast<const volatile uint32_t *>(c->h_txstate + txp.slot * TXSTATE_BYTES);
     uint32_t v[12];
     for (int k = 0; k < 11; ++k) v[k] = q[USN_TXS_WORDS * txp.ring + k];
-    v[11] = q[11];   // (ring 1's block: any chunk of the launch)
+    v[11] = q[11];   // (ring 0's block: any chunk of the launch)
     { const int e = lists_failed(v[10] | v[11], usn::scatter_diag(r->scratch, r->n, c->n_ep + 3), s); if (e) return e; }
     if (!redo && v[1] == 0 && v[2] == 0 && v[4] != txp.epoch && v[5] == 0) {
       // nothing learned, nothing for the host stage, no timeout: the
@@ -3104,7 +3108,10 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   // batch is redone: the whole batch goes to the host stage
   if (cnt[3] == txp.epoch) cnt[1] |= 8u;
   if (redo) cnt[1] |= 16u;
-  const uint32_t items_here = txp.ring ? cnt[6] : cnt[0] - cnt[6];   // learned by this ring's frames
+  uint32_t items_here = cnt[0];   // learned by this ring's frames
+  if (txp.ring) items_here = cnt[USN_TXC_LEARNED + txp.ring];
+  else
+    for (uint32_t k = 1; k < txp.rings; ++k) items_here -= cnt[USN_TXC_LEARNED + k];
   clk.mark("state");
   usn_finalize_info fi;
   std::memset(&fi, 0, sizeof fi);
@@ -3136,7 +3143,7 @@ static int finalize_tx(usn_ctx *c, const usn_batch *b, usn_result *r, hipStream_
   const uint32_t nl = items_here ? std::min(cnt[0], X.learned_cap) : 0u;
   const uint4 *items = nullptr;   // the learned list (the launch's), through pinned memory
   if (nl && c->h_items_for == txp.launch) {
-    items = c->h_items;           // ring 1 of this launch fetched it
+    items = c->h_items;           // an earlier ring of this launch fetched it
   } else if (nl) {
     c->h_items_for = 0;
     const size_t bytes = (size_t)nl * 2 * sizeof(uint4);
@@ -3388,7 +3395,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
       if (st == USN_EAGAIN_READER) return USN_EINVAL;
       c->txq.pop_front();
       c->tx_chg = c->tx_chg || changed || st != USN_OK;
-      // the next ring in flight: ring 2 of this launch saw this ring's device
+      // the next ring in flight: the next ring of this launch saw this ring's device
       // results (redone when the host decided part of this ring, or it
       // failed); a later launch started from the state before the finalizes
       // since it was enqueued (redone when one of them changed it)

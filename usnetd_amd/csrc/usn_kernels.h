@@ -90,15 +90,20 @@ static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
 #define TXR_WINDOW (1u << 30)    /* L4 ports lie past the batch window: the host reads the frame */
 #define TXR_I0_MASK 0x1FFFFu
 
-/* A tx launch takes one ring of the source, or two consecutive rings (a2,
- * rings = 2): workgroups [0, a.ntiles) take ring 1's tiles, the rest ring
- * 2's.  The cross-tile protocol (aux granules, the learning sets' first
- * learners, learned items) runs over the launch's frame index: ring 2's
- * frame j is a.ntiles * USN_TILE + j; decisions, host lists, count rows and
- * tile headers are each ring's own. */
+/* A tx launch takes one ring of the source, or up to USN_TX_RINGS consecutive
+ * rings (rings > 1): workgroups [tile_base[k], tile_base[k + 1]) take ring k's
+ * tiles.  The cross-tile protocol (aux granules, the learning sets' first
+ * learners, learned items) runs over the launch's frame index: ring k's frame
+ * j is tile_base[k] * USN_TILE + j; decisions, host lists, count rows and tile
+ * headers are each ring's own. */
+#define USN_TX_RINGS 4u
+#define USN_TXC_HOST 4u         /* counters: frames ring k listed for the host stage, [4 + k] */
+#define USN_TXC_LEARNED 8u      /* ... learned items of ring k's frames, [8 + k] (k >= 1) */
+#define USN_TXC_WORDS 12u
 struct TxArgs {
-  ClassifyArgs a;             /* batch, outputs, table, source, carried cache */
-  ClassifyArgs a2;            /* rings = 2: the second ring (same source; carry_mode unused) */
+  ClassifyArgs a[USN_TX_RINGS];  /* ring k's batch and outputs; ring 0's also the shared
+                                    fields: table, source, carried cache */
+  uint32_t tile_base[USN_TX_RINGS + 1];
   uint32_t rings;
   unsigned long long *aux;    /* per tile x TXA_GRANULES {epoch, value}: what crosses a tile boundary */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
@@ -107,10 +112,11 @@ struct TxArgs {
   uint32_t epoch;             /* 1..65535 */
   uint4 *learned;             /* items appended by tx_decide: {frame, kind 0 mac | 1 rule},
                                  {mac lo, mac hi} or the packed rule key {x, y, z, meta} */
-  uint32_t *counters;         /* [0] learned items, [1] overflow/collision flags, [2] sets with
-                                 items, [3] epoch of a batch whose tile waits timed out, [4] frames
-                                 of ring 1 listed for the host stage, [5] ring 2's, [6] learned
-                                 items of ring 2's frames */
+  uint32_t *counters;         /* USN_TXC_WORDS: [0] learned items, [1] overflow/collision flags,
+                                 [2] sets with items, [3] epoch of a batch whose tile waits timed
+                                 out, [USN_TXC_HOST + k] frames of ring k listed for the host
+                                 stage, [USN_TXC_LEARNED + k] learned items of ring k >= 1's
+                                 frames (ring 0's: [0] minus the others) */
   uint32_t learned_cap;
   const unsigned long long *bridge_set; /* open addressing, bit 63 = used */
   uint32_t bridge_mask;
@@ -182,7 +188,7 @@ struct ScatterArgs {
    * [1] the ring's learned items, [2] counters[1] (flags), [3] counters[2],
    * [4] counters[3] (timeout epoch), [5] the ring's host-stage frames,
    * [6..8] bin_off[n_ep .. n_ep + 2], [9] n, [10] the scan's diag; word 11 of
-   * ring 1's set by any chunk that finds inconsistent lists */
+   * ring 0's set by any chunk that finds inconsistent lists */
   uint32_t *txs_out;
   const uint32_t *txs_counters;
 };

@@ -377,8 +377,8 @@ class Ctx:
 
     def classify_multi(self, batches, results, stream=None):
         """One launch over several batches (usn_classify_multi): rx rings of
-        distinct NIC sources, or one or two consecutive rings of a sending
-        endpoint (the two in one tx grid)."""
+        distinct NIC sources, or up to four consecutive rings of a sending
+        endpoint (in one tx grid)."""
         n = len(batches)
         ba = (Batch * n)(*[b.desc for b in batches])
         ra = (Result * n)(*[r.desc for r in results])
