@@ -104,7 +104,7 @@ def parse_args(argv=None):
                          "while round i is queued)")
     ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
-    ap.add_argument("--tx-rings", type=int, default=4, choices=(1, 2, 3, 4),
+    ap.add_argument("--tx-rings", type=int, default=8, choices=range(1, 9),
                     help="c4tx: consecutive rings of the sending endpoint per tx launch (one grid)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: ranks join the process group and report, no GPU")
@@ -481,7 +481,7 @@ def measure(run, args, dist, world):
 EXTRA_QUEUES = {"c3": 8}
 EXTRA_MIN_STEPS = {"c3": 200}   # c3's poll round is ~55 us: 200 rounds time ~11 ms, not ~2
 TX_ROTATE = 8              # c4tx: the ring in 8 device buffers (512 MiB > the 256 MiB Infinity Cache;
-                           # 7 others, 448 MiB, between two uses of one at 4 rings per launch)
+                           # 7 others, 448 MiB, between two uses of one at 4 or 8 rings per launch)
 TX_RINGS = 100             # c4tx: timed rings (and device event pairs) at least
 
 
@@ -495,7 +495,7 @@ def measure_tx(ctx, args):
     j + 1 may be enqueued before launch j's rings are finalized (at most two
     launches in flight; launch j + 1 is decided again on the host when a
     finalize of launch j changed what it started from).  value = frames /
-    wall time of that pipelined loop with --tx-rings (4) consecutive rings per
+    wall time of that pipelined loop with --tx-rings (8) consecutive rings per
     launch (one tx grid, usn_classify_multi), one ring per launch beside it; the
     device time of the call (tx kernel + per-endpoint scatter, HIP events)
     gives the roofline."""

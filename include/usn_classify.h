@@ -35,7 +35,7 @@ extern "C" {
 
 /* 4: usn_result_release; two consecutive tx rings per usn_classify_multi;
  *    usn_finalize waits for the batch's own launch, not the stream
- * 5: up to four consecutive tx rings per usn_classify_multi */
+ * 5: up to eight consecutive tx rings per usn_classify_multi */
 #define USN_ABI_VERSION 5
 #define USN_WINDOW 64     /* default readable header bytes at every frame start (usn_batch.window) */
 #define USN_WINDOW_MAX 80 /* the most extract_pkt_info ever reads: L4 ports of IHL 15 end at byte 78 */
@@ -305,7 +305,7 @@ int usn_result_release(usn_ctx *ctx, const usn_result *r);
  * false) learns bridge MACs and answer rules; until its usn_finalize every
  * other call that reads or changes the registry returns USN_EBUSY, except
  * the source's next tx ring(s) on the same stream: at most two tx launches
- * (each one ring, or up to four rings through usn_classify_multi) are in flight,
+ * (each one ring, or up to eight rings through usn_classify_multi) are in flight,
  * and their rings are finalized in order (a later one first: USN_EBUSY).
  * A launch ran against the state the launch before it started from; when a
  * usn_finalize of the earlier launch's rings changed that state (it learned,
@@ -316,14 +316,13 @@ int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stre
 /* Several drained rings of DISTINCT sources (e.g. the rx queues of the NICs
  * polled in one poll() round, main.rs:1029-1046) in one launch: b[k] -> r[k],
  * count <= 8.  Same semantics as `count` usn_classify calls.
- * A sending endpoint's (tx) rings: one ring, or up to four CONSECUTIVE rings
- * of the same source (count <= 4, distinct results) in one grid, each ring's
+ * A sending endpoint's (tx) rings: one ring, or up to eight CONSECUTIVE rings
+ * of the same source (count <= 8, distinct results) in one grid, each ring's
  * frames following the ring before's: the same decisions, learning and
  * carried cache as `count` usn_classify calls finalized in turn (ring k sees
  * what the rings before it learned on the device, and is decided again on the
  * host only when ring k - 1's usn_finalize ran a host tail or redid it).
- * Finalize the rings in order.  tx rings of different sources, or more than
- * four: USN_EINVAL; the tiles of every ring but the last * USN_TILE + the last
+ * Finalize the rings in order.  tx rings of different sources: USN_EINVAL; the tiles of every ring but the last * USN_TILE + the last
  * ring's frames must stay below 2^32 - 1 (else USN_ERANGE). */
 int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
                        void *hip_stream);

@@ -16,7 +16,7 @@ SLOT = 128
 class GpuBackend:
     def __init__(self, ctx: lib.Ctx | None = None, check_order=True, split_tx_seed=None):
         """split_tx_seed: a sending endpoint's run of frames goes to the
-        device as 2-4 consecutive rings in one usn_classify_multi launch (one
+        device as 2-8 consecutive rings in one usn_classify_multi launch (one
         tx grid), split at seeded random frames"""
         self.ctx = ctx or lib.Ctx(0)
         self.check_order = check_order
@@ -59,7 +59,7 @@ class GpuBackend:
     def forward_run(self, src, frames):
         n = len(frames)
         if self.split_rng is not None and self.kinds.get(src) != lib.EP_NIC and n >= 2:
-            m = self.split_rng.randint(2, min(4, n))
+            m = self.split_rng.randint(2, min(8, n))
             cuts = [0] + sorted(self.split_rng.sample(range(1, n), m - 1)) + [n]
             parts = [self._batch(src, frames[x:y]) for x, y in zip(cuts, cuts[1:])]
             try:

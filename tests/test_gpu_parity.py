@@ -58,7 +58,7 @@ def test_random_streams_gpu(seed, tx_frac, coracle_mod):
 @pytest.mark.parametrize("switch_p,ops_p,n_events", [(0.15, 0.02, 700), (0.0008, 0.0003, 6000)])
 @pytest.mark.parametrize("seed", range(6))
 def test_random_streams_two_rings_gpu(seed, switch_p, ops_p, n_events, coracle_mod):
-    """Every sending endpoint's run goes to the device as 2-4 consecutive
+    """Every sending endpoint's run goes to the device as 2-8 consecutive
     rings of one usn_classify_multi launch (one tx grid), split at seeded
     random frames: learning, fragments, DHCP and the decision cache cross the
     ring boundaries inside the grid.  Long runs (about 1000 frames) span tiles."""

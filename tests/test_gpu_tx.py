@@ -453,8 +453,8 @@ def test_tx_two_rings_cache_across(coracle_mod):
 
 
 def test_tx_two_ring_launch_rules(coracle_mod):
-    """Two rings per tx launch: of one source, distinct results; at most two
-    launches in flight; rings finalized in order."""
+    """Up to eight rings per tx launch: of one source, distinct results; at
+    most two launches in flight; rings finalized in order."""
     import ctypes as C
     from usnetd_amd import lib, traffic
     cfg = traffic.config("c4tx", n=4096)
@@ -463,7 +463,7 @@ def test_tx_two_ring_launch_rules(coracle_mod):
     s = ctx.stream()
     b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
     b2 = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, 2, stride=cfg.stride)
-    rs = [lib.DeviceResult(ctx, cfg.n) for _ in range(6)]
+    rs = [lib.DeviceResult(ctx, cfg.n) for _ in range(9)]
 
     def multi(bb, rr):
         ba = (lib.Batch * len(bb))(*[x.desc for x in bb])
@@ -471,7 +471,7 @@ def test_tx_two_ring_launch_rules(coracle_mod):
         return ctx.L.usn_classify_multi(ctx.h, C.cast(ba, C.c_void_p), C.cast(ra, C.c_void_p), len(bb), s)
 
     assert multi([b, b2], rs[:2]) == lib.USN_EINVAL          # two sources
-    assert multi([b] * 5, rs[:5]) == lib.USN_EINVAL          # five rings
+    assert multi([b] * 9, rs[:9]) == lib.USN_EINVAL          # nine rings
     assert multi([b, b], [rs[0], rs[0]]) == lib.USN_EINVAL   # one result twice
     assert multi([b, b, b], [rs[0], rs[1], rs[0]]) == lib.USN_EINVAL
     assert multi([b, b, b2], rs[:3]) == lib.USN_EINVAL       # a third ring of another source
@@ -486,6 +486,9 @@ def test_tx_two_ring_launch_rules(coracle_mod):
     ctx.finalize(b, rs[1], s)
     assert multi([b], [rs[4]]) == 0
     for r in rs[2:5]:
+        ctx.finalize(b, r, s)
+    assert multi([b] * 8, rs[:8]) == 0                       # eight rings in one grid
+    for r in rs[:8]:
         ctx.finalize(b, r, s)
     ctx.close()
 
@@ -538,7 +541,7 @@ def test_tx_four_rings_one_launch(n, coracle_mod):
     assert [i.n_host for i in infos] == [0] * 4 + [n] * 4 + [0] * 4
 
 
-@pytest.mark.parametrize("per", [3, 4])
+@pytest.mark.parametrize("per", [3, 4, 8])
 def test_tx_multi_rings_all_learn(per, coracle_mod):
     """Every ring brings new flows: each learns its own on the device, with
     the earlier rings' items already visible to it."""
@@ -570,3 +573,26 @@ def test_tx_multi_rings_tile_edges(ns, coracle_mod):
     per = len(ns) if len(ns) > 2 else 3
     infos = _ring_launches(rings + rings, coracle_mod, per=per)
     assert [i.n_host for i in infos] == [0] * len(infos)
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 20])
+def test_tx_eight_rings_one_launch(n, coracle_mod):
+    """Eight rings per grid (the bench's c4tx launch): ring 0 learns, the
+    rest saw it inside the grid; pipelined, launch 1's rings are all decided
+    again on the host and launch 2's are final."""
+    from usnetd_amd import traffic
+    cfg = traffic.config("c4tx", n=n)
+    infos = _ring_launches([cfg] * 24, coracle_mod, pipelined=True, per=8)
+    assert infos[0].n_learned > 0
+    assert [i.n_host for i in infos] == [0] * 8 + [n] * 8 + [0] * 8
+
+
+@pytest.mark.parametrize("at", [0, 5, 7])
+def test_tx_eight_rings_host_tail(at, coracle_mod):
+    """A DHCP request in ring `at` of eight: that ring's rest and every later
+    ring go to the host stage."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=3000, seed=110 + k) for k in range(8)]
+    rings[at] = traffic.c4tx(n=3000, host_at=[1500], seed=110 + at)
+    infos = _ring_launches(rings, coracle_mod, per=8)
+    assert [i.n_host for i in infos] == [0] * at + [1500] + [3000] * (7 - at)

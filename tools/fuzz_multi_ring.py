@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Differential fuzz of multi-ring tx launches on the GPU: random streams
 (tests/randtraffic.py) through tests/gpu_backend.GpuBackend with every
-sending run split into 2-4 rings of one usn_classify_multi launch, against
+sending run split into 2-8 rings of one usn_classify_multi launch, against
 the C oracle.  Stops at the first mismatch.
 usage: fuzz_multi_ring.py first_seed n_seeds [n_events=3000]"""
 import os

@@ -337,6 +337,35 @@ case $S in
       mv $O/bench.log $O/bench_tx$r.log
     done
     ;;
+  r05ai)
+    # four-ring tx launches: kernel times (rocprof) and HBM traffic of one
+    # launch (8 rotating buffers), for the bench line's roofline; an 8M grid
+    # (4 rings of 2M, --concat 2: the same flows) against 4 x 1M
+    TXB_ARGS="1048576 24 1 --rotate 8 --rings 4" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 4194304 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
+    for rep in 1 2; do
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 8 --rings 4 > $O/txb_4x1M_$rep.log 2>&1 || exit 1
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 4 --concat 2 --rings 4 > $O/txb_4x2M_$rep.log 2>&1 || exit 1
+      for v in 4x1M 4x2M; do echo "$v $(tail -1 $O/txb_${v}_$rep.log)"; done
+    done
+    ;;
+  r05aj)
+    # up to eight consecutive rings per tx launch: the tx / parity / window /
+    # group GPU tests, a multi-ring fuzz (2-8 rings), txbench at 4 and 8 rings,
+    # the bench's c4tx line at 4 and 8, rocprof + PMC of the 8-ring launch
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py tests/test_gpu_window.py tests/test_gpu_group.py" \
+      bash tools/gpu.sh $S testsall || exit 1
+    timeout -k 10 240 python -u tools/fuzz_multi_ring.py 3000 100 3000 > $O/fuzz.log 2>&1 || { tail -3 $O/fuzz.log; exit 1; }
+    tail -1 $O/fuzz.log
+    for r in 4 8; do
+      timeout -k 10 200 python tools/txbench.py 1048576 24 1 --rotate 8 --rings $r > $O/txb_r$r.log 2>&1 || exit 1
+      echo "rings=$r $(tail -1 $O/txb_r$r.log)"
+      BENCH_ARGS="--steps 10 --warmup 3 --extras c4tx --no-cpu-baseline --tx-rings $r" bash tools/gpu.sh $S bench || exit 1
+      mv $O/bench.log $O/bench_tx$r.log
+    done
+    TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 8388608 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("distinct", nargs="?", type=int, default=1)
     ap.add_argument("libpath", nargs="?", default=None)
     ap.add_argument("--rotate", type=int, default=1)
-    ap.add_argument("--rings", type=int, default=1, choices=(1, 2, 3, 4))
+    ap.add_argument("--rings", type=int, default=1, choices=range(1, 9))
     ap.add_argument("--concat", type=int, default=1)
     a = ap.parse_args()
     n, nb, distinct = a.n, a.batches, a.distinct

@@ -2593,7 +2593,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (st) return st;
     tx |= c->eps[b[k].src_endpoint].kind != USN_EP_NIC;
   }
-  if (tx) {   // a tx launch changes shared state: one ring of a source, or up to 4 consecutive rings
+  if (tx) {   // a tx launch changes shared state: one ring of a source, or up to 8 consecutive rings
     if (count > USN_TX_RINGS) return USN_EINVAL;
     uint64_t vend = 0;   // the launch's frame index (ring k after ring k - 1's tiles)
     for (uint32_t k = 0; k < count; ++k) {

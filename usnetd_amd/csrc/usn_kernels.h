@@ -96,10 +96,10 @@ static_assert(sizeof(MultiArgs) <= 4096, "kernel argument block");
  * learners, learned items) runs over the launch's frame index: ring k's frame
  * j is tile_base[k] * USN_TILE + j; decisions, host lists, count rows and tile
  * headers are each ring's own. */
-#define USN_TX_RINGS 4u
+#define USN_TX_RINGS 8u
 #define USN_TXC_HOST 4u         /* counters: frames ring k listed for the host stage, [4 + k] */
-#define USN_TXC_LEARNED 8u      /* ... learned items of ring k's frames, [8 + k] (k >= 1) */
-#define USN_TXC_WORDS 12u
+#define USN_TXC_LEARNED (USN_TXC_HOST + USN_TX_RINGS)   /* ... ring k's learned items (k >= 1) */
+#define USN_TXC_WORDS (USN_TXC_LEARNED + USN_TX_RINGS)
 struct TxArgs {
   ClassifyArgs a[USN_TX_RINGS];  /* ring k's batch and outputs; ring 0's also the shared
                                     fields: table, source, carried cache */
@@ -128,6 +128,7 @@ struct TxArgs {
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
 static_assert(sizeof(TxArgs) <= 4096, "kernel argument block");
+static_assert(USN_TXC_WORDS <= 64, "tile 0's first wave zeroes the counters");
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
 
 /* LDS bytes a classify block needs (table staged in LDS when table_in_lds). */

@@ -377,7 +377,7 @@ class Ctx:
 
     def classify_multi(self, batches, results, stream=None):
         """One launch over several batches (usn_classify_multi): rx rings of
-        distinct NIC sources, or up to four consecutive rings of a sending
+        distinct NIC sources, or up to eight consecutive rings of a sending
         endpoint (in one tx grid)."""
         n = len(batches)
         ba = (Batch * n)(*[b.desc for b in batches])
