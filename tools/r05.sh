@@ -366,6 +366,30 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 8388608 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
     ;;
+  r05ak)
+    # what bounds the tx kernel at eight rings per launch (8192 tiles, eight
+    # generations at four workgroups per CU): SQ instruction mix, busy and
+    # wait cycles, LDS bank conflicts (two passes of txbench --rings 8)
+    TX="tools/txbench.py 1048576 12 1 --rotate 8 --rings 8"
+    sq_pass sq1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+      python3 $TX
+    sq_pass sq2 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA" \
+      python3 $TX
+    python3 tools/pmc_summary.py $O/sq1 $O/sq2 > $O/sq_summary.txt 2>&1 || true
+    cat $O/sq_summary.txt
+    ;;
+  r05al)
+    # final tree (eight tx rings per launch): the suite, smoke, the bench as
+    # the driver runs it, rocprof of the bench, PMC of c5 / c2 / c3 / c4 and
+    # of the 8-ring tx launch
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    PMC_CFGS="c5 c2 c3 c4" bash tools/gpu.sh $S pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 8388608 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
