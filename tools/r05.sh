@@ -390,6 +390,20 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py $O/txpmcf $O/txpmcw 8388608 $O/pmc_c4tx.json tx_kernel=1+33 > $O/pmct_c4tx.log 2>&1
     ;;
+  r05am)
+    # c3's launch shape (the poll round's 8 rings of 256K IMIX frames): calls
+    # of 4 on 2 streams (the bench's) against one call of 8 on 1 stream and
+    # calls of 8 on 2 streams, alternated
+    for rep in 1 2; do
+      for v in "4 2" "8 1" "8 2"; do
+        set -- $v
+        timeout -k 10 300 python bench.py --config c3 --no-extra --no-cpu-baseline --steps 40 --warmup 5 \
+          --rings-per-launch $1 --streams $2 > $O/c3_p$1_s$2_$rep.log 2>&1 || exit 1
+        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], d['value'], d.get('end_to_end_mpps'), r['frac'], r.get('kernel_us_median'), d['config'])" \
+          $O/c3_p$1_s$2_$rep.log "p=$1 s=$2" || exit 1
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
