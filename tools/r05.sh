@@ -404,6 +404,14 @@ case $S in
       done
     done
     ;;
+  r05an)
+    # more multi-ring tx fuzzing on the final tree: 200 seeds of 5000 events,
+    # and 100 over a table past LDS (3000 filler rules: U and X probes)
+    timeout -k 10 400 python -u tools/fuzz_multi_ring.py 5000 200 5000 > $O/fuzz.log 2>&1 || { tail -3 $O/fuzz.log; exit 1; }
+    tail -1 $O/fuzz.log
+    timeout -k 10 400 python -u tools/fuzz_multi_ring.py 6000 100 3000 3000 > $O/fuzz_filler.log 2>&1 || { tail -3 $O/fuzz_filler.log; exit 1; }
+    tail -1 $O/fuzz_filler.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
