@@ -412,6 +412,18 @@ case $S in
     timeout -k 10 400 python -u tools/fuzz_multi_ring.py 6000 100 3000 3000 > $O/fuzz_filler.log 2>&1 || { tail -3 $O/fuzz_filler.log; exit 1; }
     tail -1 $O/fuzz_filler.log
     ;;
+  r05ao)
+    # c5's scatter (2 x 8M per call: 2048 chunks of 8 tiles = 2.67 generations
+    # of 768 resident) at 4-tile chunks (4096 chunks, 5.3 generations: a
+    # finer tail), the test build's USN_SCATTER_TC, alternated
+    for rep in 1 2; do
+      for tc in 8 4; do
+        USN_SCATTER_TC=$tc timeout -k 10 300 python tools/scatter_bench.py --config c5 --frames 8388608 --multi 2 \
+          base testlib > $O/scb_c5_tc${tc}_$rep.log 2>&1 || exit 1
+        echo "tc=$tc"; grep scatter $O/scb_c5_tc${tc}_$rep.log
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
