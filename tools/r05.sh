@@ -424,6 +424,18 @@ case $S in
       done
     done
     ;;
+  r05ap)
+    # the share of the key1 / key2 probes (hashes + slot reads) in the 8-ring
+    # tx launch: build/abl/txnoprobe (no K1/K2 probes, wrong decisions)
+    # against build/abl/base, alternated
+    for rep in 1 2; do
+      for v in base txnoprobe; do
+        timeout -k 10 200 python tools/txbench.py 1048576 24 1 build/abl/$v/libusn.so --rotate 8 --rings 8 \
+          > $O/txb_${v}_$rep.log 2>&1 || exit 1
+        echo "$v $(tail -1 $O/txb_${v}_$rep.log)"
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
