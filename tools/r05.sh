@@ -436,6 +436,13 @@ case $S in
       done
     done
     ;;
+  r05aq)
+    # final tree again (product library rebuilt after the hash A/B was
+    # reverted; same sources as r05al): the suite, smoke, the driver's bench
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
