@@ -2180,7 +2180,8 @@ int usn_debug_image_stats(usn_ctx *c, int refresh, uint64_t *out4) {
 }
 
 /* Test hook: the tx scratch state of the selected replica: counters[0..7]
- * (learned, flags, sets used, timed-out epoch), epoch. */
+ * (learned, flags, sets used, timed-out epoch, host-stage frames of rings
+ * 0..3; usn_kernels.h USN_TXC_*), epoch. */
 int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
   if (!c || !out10 || c->reps.empty()) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
