@@ -596,3 +596,14 @@ def test_tx_eight_rings_host_tail(at, coracle_mod):
     rings[at] = traffic.c4tx(n=3000, host_at=[1500], seed=110 + at)
     infos = _ring_launches(rings, coracle_mod, per=8)
     assert [i.n_host for i in infos] == [0] * at + [1500] + [3000] * (7 - at)
+
+
+def test_tx_eight_rings_all_learn_1m(coracle_mod):
+    """The bench's launch shape with learning in every ring: eight 1M rings
+    of distinct flows in one grid (8192 tiles, eight generations), each
+    learning ~300K answer rules with the earlier rings' items visible."""
+    from usnetd_amd import traffic
+    rings = [traffic.c4tx(n=1 << 20, seed=200 + k) for k in range(8)]
+    infos = _ring_launches(rings, coracle_mod, per=8)
+    assert all(i.n_learned > 0 for i in infos)
+    assert [i.n_host for i in infos] == [0] * 8

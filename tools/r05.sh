@@ -443,6 +443,10 @@ case $S in
     bash tools/gpu.sh $S smoke || exit 1
     BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r05ar)
+    # eight 1M rings of distinct flows in one tx grid, every ring learning
+    TESTS=tests/test_gpu_tx.py TEST_K="eight_rings_all_learn" bash tools/gpu.sh $S testsall || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
