@@ -447,6 +447,16 @@ case $S in
     # eight 1M rings of distinct flows in one tx grid, every ring learning
     TESTS=tests/test_gpu_tx.py TEST_K="eight_rings_all_learn" bash tools/gpu.sh $S testsall || exit 1
     ;;
+  r05at)
+    # HEAD (r05as's tree): more multi-ring tx fuzz on new seeds (plain, and
+    # with an image past LDS so the rx kernel probes U and X), then c5's
+    # FETCH/WRITE passes on this tree
+    timeout -k 10 500 python -u tools/fuzz_multi_ring.py 7000 300 5000 > $O/fuzz.log 2>&1 || { tail -3 $O/fuzz.log; exit 1; }
+    tail -1 $O/fuzz.log
+    timeout -k 10 400 python -u tools/fuzz_multi_ring.py 8000 150 3000 3000 > $O/fuzz_filler.log 2>&1 || { tail -3 $O/fuzz_filler.log; exit 1; }
+    tail -1 $O/fuzz_filler.log
+    PMC_CFGS="c5" bash tools/gpu.sh $S pmc || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
