@@ -457,6 +457,24 @@ case $S in
     tail -1 $O/fuzz_filler.log
     PMC_CFGS="c5" bash tools/gpu.sh $S pmc || exit 1
     ;;
+  r05au)
+    # 16-tile scatter chunks (two consecutive tiles per wave, 2 workgroups per
+    # CU; the test build's USN_SCATTER_TC=16) against the product's 8: scan +
+    # scatter device time and lists equal to the product's, c5 2 x 8M, c4 and
+    # c2 8 x 1M; then the ballot fallback forced (USN_SCATTER_SLOW_RANK)
+    mkdir -p build/abl/testlib && cp build/test/libusn.so build/abl/testlib/libusn.so
+    for rep in 1 2; do
+      for c in c5 c4 c2; do
+        if [ $c = c5 ]; then A="--frames 8388608 --multi 2"; else A="--frames 1048576 --multi 8"; fi
+        USN_SCATTER_TC=16 timeout -k 10 300 python tools/scatter_bench.py --config $c $A \
+          --json $O/scb_${c}_$rep.json base testlib > $O/scb_${c}_$rep.log 2>&1 || { tail -3 $O/scb_${c}_$rep.log; exit 1; }
+        echo "$c rep $rep"; grep scatter $O/scb_${c}_$rep.log
+      done
+    done
+    USN_SCATTER_TC=16 USN_SCATTER_SLOW_RANK=1 timeout -k 10 300 python tools/scatter_bench.py --config c5 \
+      --frames 8388608 --multi 2 --launches 5 base testlib > $O/scb_c5_slow.log 2>&1 || { tail -3 $O/scb_c5_slow.log; exit 1; }
+    echo "c5 forced fallback"; grep scatter $O/scb_c5_slow.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

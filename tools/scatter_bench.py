@@ -29,6 +29,7 @@ def main():
     names = a.variants or ["base"]
     cfgs = [traffic.config(a.config, n=a.frames, seed=17 * k + 2) for k in range(a.multi)]
     out = {}
+    first_idx = None   # the first variant's lists: every other variant must equal them
     for nm in names:
         path = None if nm == "base" else os.path.join(ROOT, "build", "abl", nm, "libusn.so")
         ctx = lib.Ctx(0, libpath=path)
@@ -55,12 +56,17 @@ def main():
         ctx.sync(s)
         us = [ctx.elapsed_ms(x, y) * 1e3 for x, y in evs]
         same = all((r.index() == x).all() for r, x in zip(rs, ref))
+        idx = [r.index() for r in rs]
+        if first_idx is None:
+            first_idx = idx
+        same_first = all((x == y).all() for x, y in zip(idx, first_idx))
         med = statistics.median(us)
         out[nm] = dict(scatter_us=round(med, 2), min_us=round(min(us), 2), same_as_classify=same,
-                       frames=a.frames * a.multi)
+                       same_as_first_variant=same_first, frames=a.frames * a.multi)
         print("%-10s scatter %8.2f us (min %8.2f) per %d frames  %.1f GB/s of 12 B/frame  same=%s"
-              % (nm, med, min(us), a.frames * a.multi, 12 * a.frames * a.multi / med / 1e3, same),
-              flush=True)
+              " same_as_first=%s"
+              % (nm, med, min(us), a.frames * a.multi, 12 * a.frames * a.multi / med / 1e3, same,
+                 same_first), flush=True)
         if nm.startswith("stamps"):   # the diagnostic build: phase medians of the last launch
             import numpy as np
             buf = np.zeros(2 * 16384 * 16, np.uint64)   # the scatter's stamps: slots 16384..
