@@ -2706,7 +2706,7 @@ __device__ __forceinline__ void scan_put(unsigned long long *g, uint32_t epoch, 
  *     writes tot.  (Bin bases here too, handed on between bin blocks, cost
  *     the scan's last ranges one more round trip: 15.4 against 13.9 us for
  *     c5, more than the scatter's block scan they saved, profiles/r03.) */
-template <int CPT, int TCM>   // chunks per thread: a range is 16 * CPT chunks; TCM: the most tiles per chunk
+template <int CPT>   // chunks per thread: a range is 16 * CPT chunks
 __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   __shared__ uint32_t s_t[16][USN_SCAN_BLK];
   __shared__ uint32_t s_c[4][USN_SCAN_BLK];
@@ -2720,11 +2720,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   const bool binok = b0 < s.nbw;                            // nbw is a multiple of 8
   const uint32_t c0 = r * 16 * CPT + rg * CPT;              // this thread's CPT chunks
   // 1.
-  uint2 v[CPT][TCM];
+  uint2 v[CPT][8];
 #pragma unroll
   for (uint32_t j = 0; j < CPT; ++j)
 #pragma unroll
-    for (uint32_t w = 0; w < TCM; ++w) {
+    for (uint32_t w = 0; w < 8; ++w) {
       const uint32_t t = (c0 + j) * s.tc + w;
       const bool ok = binok && w < s.tc && t < B.ntiles;
       v[j][w] = ok ? *reinterpret_cast<const uint2 *>(B.cnt + (size_t)t * s.nbw + b0) : make_uint2(0, 0);
@@ -2734,7 +2734,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(ScatterArgs s) {
   for (uint32_t j = 0; j < CPT; ++j) {
     uint32_t a[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t w = 0; w < TCM; ++w) {
+    for (uint32_t w = 0; w < 8; ++w) {
       a[0] += v[j][w].x & 0xFFFFu; a[1] += v[j][w].x >> 16;
       a[2] += v[j][w].y & 0xFFFFu; a[3] += v[j][w].y >> 16;
     }
@@ -2847,24 +2847,15 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
 #endif
 template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
                                // registers for the row sums instead of occupancy)
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(
-    SELF ? 2 : TC > NTHREADS / 64 ? 4 : USN_SCATTER_WPE)))
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(SELF ? 2 : USN_SCATTER_WPE)))
 void scatter_kernel(ScatterArgs s) {
-  constexpr uint32_t NW = NTHREADS / 64;
-  constexpr uint32_t TPW = TC > NW ? TC / NW : 1;   // tiles per wave: 2 for 16-tile chunks
-  constexpr bool BIG = TPW > 1;
-  static_assert(TC >= 1 && (TC <= NW || TC == 2 * NW), "a wave per tile, or two consecutive tiles per wave");
-  static_assert(!(BIG && SELF), "16-tile chunks are scanned launches");
+  static_assert(TC >= 1 && TC <= NTHREADS / 64, "a wave per tile");
   constexpr uint32_t SEGS = TILE / 64;                               // 16 segments per tile
   extern __shared__ __align__(16) uint8_t smem[];
-  // 16-tile chunks: static LDS (stage | cursors, the offsets over the cursors after the ranking)
-  __shared__ __align__(16) uint8_t s_big[BIG ? TC * TILE * 4 + NW * USN_SC_BIG_NBW * 2 : 16];
-  __shared__ uint32_t s_scan_[BIG ? 1 : 16];
-  uint32_t *stage = reinterpret_cast<uint32_t *>(BIG ? s_big : smem);   // [TC * TILE]: bin << 16 | frame
-  // BIG: the block scans' scratch at the stage's start (step 2 ends before the stage is filled)
-  uint32_t *const s_scan = BIG ? stage : s_scan_;
-  uint32_t *off = stage + TC * TILE;                                 // [nbw] (BIG: over cur, after the ranking)
-  uint16_t *cur = reinterpret_cast<uint16_t *>(BIG ? off : off + s.nbw);   // [TC / TPW][nbw]: < TC * TILE
+  __shared__ uint32_t s_scan[16];
+  uint32_t *stage = reinterpret_cast<uint32_t *>(smem);              // [TC * TILE]: bin << 16 | frame
+  uint32_t *off = stage + TC * TILE;                                 // [nbw]
+  uint16_t *cur = reinterpret_cast<uint16_t *>(off + s.nbw);         // [TC][nbw]: < TC * TILE
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nwg = s.chunk_base[s.count];
@@ -2905,17 +2896,13 @@ void scatter_kernel(ScatterArgs s) {
     rc[w] = mine ? reinterpret_cast<const uint32_t *>(B.cnt + (size_t)t * s.nbw)[tid] : 0u;
     if (w >= ntc) rc[w] = 0;
   }
-  // 1. this wave's tile(s) (waves past the chunk's end re-read its last tile, unused)
-  uint64_t tbase[TPW];
-  uint32_t tn[TPW], d[TPW][SEGS];
+  // 1. this wave's tile (waves past the chunk's end re-read its last tile, unused)
+  const uint32_t wt = min(wave, ntc - 1);
+  const uint64_t tbase = first + (uint64_t)wt * TILE;
+  const uint32_t tn = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - tbase);
+  uint32_t d[SEGS];
 #pragma unroll
-  for (uint32_t j = 0; j < TPW; ++j) {
-    const uint32_t wt = min(wave * TPW + j, ntc - 1);
-    tbase[j] = first + (uint64_t)wt * TILE;
-    tn[j] = (uint32_t)min((uint64_t)TILE, (uint64_t)B.n - tbase[j]);
-#pragma unroll
-    for (uint32_t k = 0; k < SEGS; ++k) d[j][k] = B.decisions[tbase[j] + min(k * 64 + lane, tn[j] - 1)];
-  }
+  for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
   // 1b. (small launches) the scan's two sums for this chunk from the batch's
   // count rows: thread (g, q) adds bins 8q..8q+7 (one 16-byte load) of tiles
   // g, g + G, ... into the totals and, for the tiles before the chunk, into
@@ -2958,9 +2945,7 @@ void scatter_kernel(ScatterArgs s) {
       ve = make_uint2(sb[2 * tid], sb[2 * tid + 1]);
     }
   }
-  // 2. bases, the chunk's bin starts, the waves' cursors (BIG: one row per
-  // wave, its first tile's; the offsets stay in registers until the ranking is done)
-  uint2 offk = make_uint2(0, 0), pck = make_uint2(0, 0);
+  // 2. bases, the chunk's bin starts, the waves' cursors
   if (pair) {
     uint32_t c0 = 0, c1 = 0;
 #pragma unroll
@@ -2971,14 +2956,11 @@ void scatter_kernel(ScatterArgs s) {
     const uint32_t pc = block_excl_scan(c0 + c1, s_scan, &total);
     if (mine) {
       const uint32_t b = 2 * tid;
-      offk = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
-      pck = make_uint2(pc, pc + c0);
-      if (!BIG) *reinterpret_cast<uint2 *>(off + b) = offk;
+      *reinterpret_cast<uint2 *>(off + b) = make_uint2(pt + ve.x - pc, pt + vt.x + ve.y - (pc + c0));
       uint32_t s0 = pc, s1 = pc + c0;
 #pragma unroll
       for (uint32_t w = 0; w < TC; ++w) {
-        if (w % TPW == 0)
-          reinterpret_cast<uint32_t *>(cur + (size_t)(w / TPW) * s.nbw)[tid] = (s0 & 0xFFFFu) | (s1 << 16);
+        reinterpret_cast<uint32_t *>(cur + (size_t)w * s.nbw)[tid] = (s0 & 0xFFFFu) | (s1 << 16);
         s0 += rc[w] & 0xFFFFu;
         s1 += rc[w] >> 16;
       }
@@ -2996,8 +2978,7 @@ void scatter_kernel(ScatterArgs s) {
         }
       }
     }
-  } else if (!BIG) {   // more bins: per-thread contiguous runs of bins, the same sums
-    // (BIG launches have at most USN_SC_BIG_NBW bins: the host's plan)
+  } else {   // more bins: per-thread contiguous runs of bins, the same sums
     const uint32_t per = (s.nbw + NTHREADS - 1) / NTHREADS;
     const uint32_t b0 = tid * per;
     uint32_t st = 0, sc = 0;
@@ -3076,38 +3057,28 @@ void scatter_kernel(ScatterArgs s) {
   // chunk, an empty stage slot or a list position past n -- the count rows
   // and the decisions disagree.  Every access stays in bounds regardless, and
   // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
-  bool bad = BIG && !pair;   // (the host never plans that)
-  // BIG: the wave's second tile after its first, on the same cursors (a
-  // wave's LDS operations execute in order)
+  bool bad = false;
+  if (wave < ntc && USN_ABL_SC != 4) {
+    uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
+    uint32_t at[SEGS];   // (the bins are recomputed below: 16 VGPRs fewer while the atomics fly)
 #pragma unroll
-  for (uint32_t j = 0; j < TPW; ++j) {
-    const uint32_t ti = wave * TPW + j;   // the tile in the chunk (wave-uniform)
-    if (ti < ntc && USN_ABL_SC != 4) {
-      uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
-      uint32_t at[SEGS];   // (the bins are recomputed below: 16 VGPRs fewer while the atomics fly)
-#pragma unroll
-      for (uint32_t k = 0; k < SEGS; ++k) {
-        const uint32_t raw = dec_bin(d[j][k], s.n_ep);
-        const uint32_t b = min(raw, s.nbins - 1u);
-        const uint32_t sh = 16u * (b & 1u);
-        const bool v = k * 64 + lane < tn[j];
-        at[k] = v ? atomicAdd(&cw[b >> 1], 1u << sh) >> sh : 0u;
-        bad |= v && raw >= s.nbins;
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < SEGS; ++k)
-        if (k * 64 + lane < tn[j]) {
-          const uint32_t b = min(dec_bin(d[j][k], s.n_ep), s.nbins - 1u), q = at[k] & 0xFFFFu;
-          bad |= q >= nf;
-          stage[min(q, TC * TILE - 1u)] = (b << 16) | (ti * TILE + k * 64 + lane);
-        }
+    for (uint32_t k = 0; k < SEGS; ++k) {
+      const uint32_t raw = dec_bin(d[k], s.n_ep);
+      const uint32_t b = min(raw, s.nbins - 1u);
+      const uint32_t sh = 16u * (b & 1u);
+      const bool v = k * 64 + lane < tn;
+      at[k] = v ? atomicAdd(&cw[b >> 1], 1u << sh) >> sh : 0u;
+      bad |= v && raw >= s.nbins;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < SEGS; ++k)
+      if (k * 64 + lane < tn) {
+        const uint32_t b = min(dec_bin(d[k], s.n_ep), s.nbins - 1u), q = at[k] & 0xFFFFu;
+        bad |= q >= nf;
+        stage[min(q, TC * TILE - 1u)] = (b << 16) | (wave * TILE + k * 64 + lane);
+      }
   }
   __syncthreads();
-  if (BIG) {   // the cursors are done: the offsets over them
-    if (mine) *reinterpret_cast<uint2 *>(off + 2 * tid) = offk;
-    __syncthreads();
-  }
   STAMP(10);
   // 4. the stage out, in order (every address bounds-checked: counts that
   // disagree with the decisions, or an A/B build that skips a phase, cannot
@@ -3157,47 +3128,24 @@ void scatter_kernel(ScatterArgs s) {
     // 5. (not taken on gfx950 so far) the wave's cursors back to their
     // seeds (final value - the tile's count), the ranks from bit-sliced
     // ballots segment by segment, the stage out again
-    // BIG: the offsets hold the cursors' place: they go to this chunk's agg
-    // row (global, read by this chunk only) and the cursors are rebuilt
-    uint32_t *og = B.agg + (size_t)c * s.nbw;
-    if (BIG) {
-      if (mine) {
-        *reinterpret_cast<uint2 *>(og + 2 * tid) = offk;
-        uint32_t s0 = pck.x, s1 = pck.y;
-        for (uint32_t w = 0; w < ntc; ++w) {
-          if (w % TPW == 0)
-            reinterpret_cast<uint32_t *>(cur + (size_t)(w / TPW) * s.nbw)[tid] = (s0 & 0xFFFFu) | (s1 << 16);
-          const uint32_t rw = reinterpret_cast<const uint32_t *>(B.cnt + (size_t)(t0 + w) * s.nbw)[tid];
-          s0 += rw & 0xFFFFu;
-          s1 += rw >> 16;
-        }
-      }
-      __syncthreads();
-    } else if (wave < ntc) {
+    if (wave < ntc) {
       uint16_t *cw = cur + (size_t)wave * s.nbw;
       const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
       for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
-    }
 #pragma unroll
-    for (uint32_t j = 0; j < TPW; ++j) {
-      const uint32_t ti = wave * TPW + j;
-      if (ti < ntc) {
-        uint16_t *cw = cur + (size_t)wave * s.nbw;
-#pragma unroll
-        for (uint32_t k = 0; k < SEGS; ++k) {
-          const uint32_t local = k * 64 + lane;
-          const bool v = local < tn[j];
-          // the decision again from memory: keeping d[] live to here costs the
-          // common path VGPRs
-          const uint32_t dk = B.decisions[tbase[j] + min(local, tn[j] - 1)];
-          const uint32_t b = min(dec_bin(dk, s.n_ep), s.nbins - 1u);
-          const uint64_t same = match_bin(b, __ballot(v), s.nbits);
-          const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
-          const uint32_t at = cw[b];
-          if (v) {
-            stage[min(at + rank, TC * TILE - 1u)] = (b << 16) | (ti * TILE + local);
-            if (rank == 0) cw[b] = (uint16_t)(at + __popcll(same));
-          }
+      for (uint32_t k = 0; k < SEGS; ++k) {
+        const uint32_t local = k * 64 + lane;
+        const bool v = local < tn;
+        // the decision again from memory: keeping d[] live to here costs the
+        // common path VGPRs
+        const uint32_t dk = B.decisions[tbase + min(local, tn - 1)];
+        const uint32_t b = min(dec_bin(dk, s.n_ep), s.nbins - 1u);
+        const uint64_t same = match_bin(b, __ballot(v), s.nbits);
+        const uint32_t rank = (uint32_t)__popcll(same & lanemask_lt(lane));
+        const uint32_t at = cw[b];
+        if (v) {
+          stage[min(at + rank, TC * TILE - 1u)] = (b << 16) | (wave * TILE + local);
+          if (rank == 0) cw[b] = (uint16_t)(at + __popcll(same));
         }
       }
     }
@@ -3205,15 +3153,15 @@ void scatter_kernel(ScatterArgs s) {
     for (uint32_t q = tid; q < nf; q += NTHREADS) {
       const uint32_t e = stage[q];
       const uint32_t b = min(e >> 16, s.nbw - 1u);
-      const uint32_t pos = (BIG ? og[b] : off[b]) + q;
+      const uint32_t pos = off[b] + q;
       if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
     }
     if (tid == 0) atomicAdd(&usn_scatter_fallbacks, 1u);
   }
   STAMP_FLUSH_SCATTER(blockIdx.x);
 }
-static_assert(NTHREADS == 512, "scatter: 8 waves, one or two tiles each");
-static_assert(16 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
+static_assert(NTHREADS == 512, "scatter: 8 waves, a tile each");
+static_assert(8 * TILE <= 0x10000, "scatter: a stage entry holds a 16-bit frame offset");
 
 uint32_t scatter_fallbacks() {
   uint32_t v = 0;
@@ -3227,22 +3175,15 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
-  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.tc > 8 ? 16 + s.cpt : s.cpt) {
-    case 4: hipLaunchKernelGGL((scan_kernel<4, 8>), sg, sb, 0, stream, s); break;
-    case 2: hipLaunchKernelGGL((scan_kernel<2, 8>), sg, sb, 0, stream, s); break;
-    case 1: hipLaunchKernelGGL((scan_kernel<1, 8>), sg, sb, 0, stream, s); break;
-    case 18: hipLaunchKernelGGL((scan_kernel<2, 16>), sg, sb, 0, stream, s); break;   // 16-tile chunks
-    case 17: hipLaunchKernelGGL((scan_kernel<1, 16>), sg, sb, 0, stream, s); break;
+  if (!(s.flags & (USN_SCF_NOSCAN | USN_SCF_SELFSCAN))) switch (s.cpt) {
+    case 4: hipLaunchKernelGGL(scan_kernel<4>, sg, sb, 0, stream, s); break;
+    case 2: hipLaunchKernelGGL(scan_kernel<2>, sg, sb, 0, stream, s); break;
+    case 1: hipLaunchKernelGGL(scan_kernel<1>, sg, sb, 0, stream, s); break;
     default: return hipErrorInvalidValue;
   }
-  const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
-  if (s.tc == 16) {   // 16-tile chunks: static LDS, scanned launches of at most USN_SC_BIG_NBW bins only
-    if (self || (s.flags & USN_SCF_NOSCAN) || s.nbw > USN_SC_BIG_NBW) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((scatter_kernel<16, false>), dim3(chunks), dim3(NTHREADS), 0, stream, s);
-    return hipGetLastError();
-  }
-  const size_t lds = scatter_lds(s.nbins, s.tc, self);
+  const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0);
   const dim3 g(chunks), b(NTHREADS);
+  const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
 #define USN_SC_LAUNCH(TC_)                                                              \
   do {                                                                                  \
     if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);    \

@@ -1764,10 +1764,7 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
     launch_tiles += ntiles[k];
     max_tiles = std::max(max_tiles, ntiles[k]);
   }
-  // 16-tile chunks (A/B: tc_knob 16): scanned launches of at most
-  // USN_SC_BIG_NBW bins only, else the shape's
-  const bool big = tc_knob == 16 && nbw <= USN_SC_BIG_NBW && max_tiles > 16;
-  uint32_t tc = big ? 16u : tc_knob ? std::min(tc_knob, sh.tc) : sh.tc;
+  uint32_t tc = tc_knob ? std::min(tc_knob, sh.tc) : sh.tc;
   p.noscan = max_tiles <= tc;
   if (!p.noscan && !tc_knob) {
     const uint32_t per = std::max(1u, launch_tiles / std::max(cus, 1u));
@@ -1781,13 +1778,12 @@ ScatterPlan scatter_plan(const uint32_t *ntiles, uint32_t count, uint32_t nbins,
     chunks += ch;
     self_bytes += (size_t)ch * ntiles[k] * nbw * 2;
   }
-  p.selfscan = !big && !p.noscan && nbw <= 2 * 512 && chunks <= std::max(cus, 1u) &&
+  p.selfscan = !p.noscan && nbw <= 2 * 512 && chunks <= std::max(cus, 1u) &&
                self_bytes <= (size_t)selfscan_kb * 1024 && scatter_lds(nbins, tc, true) <= 64u * 1024u;
   const uint32_t nbb = (nbw + USN_SCAN_BLK - 1) / USN_SCAN_BLK;
   uint32_t cpt = 4;
   while (cpt > 1 && (chunks / (16 * cpt)) * nbb < 256) cpt /= 2;
   p.cpt = cpt_knob ? cpt_knob : cpt;
-  if (big) p.cpt = std::min(p.cpt, 2u);   // the scan's rows per thread: cpt x 16
   return p;
 }
 
@@ -2341,10 +2337,10 @@ static usn::ScatterPlan plan_lists(usn_ctx *c, const usn::ClassifyArgs *as, uint
         }
     }
   }
-  static const uint32_t tc_knob = [] {   // A/B: USN_SCATTER_TC=1|2|4|8 (at most the shape's), 16
+  static const uint32_t tc_knob = [] {   // A/B: USN_SCATTER_TC=1|2|4|8 (at most the shape's)
     const char *e = test_knob("USN_SCATTER_TC");
     const int v = e ? std::atoi(e) : 0;
-    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? (uint32_t)v : 0u;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? (uint32_t)v : 0u;
   }();
   static const uint32_t cpt_knob = [] {   // A/B: USN_SCAN_CPT=1|2|4
     const char *e = test_knob("USN_SCAN_CPT");

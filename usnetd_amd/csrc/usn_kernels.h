@@ -208,10 +208,6 @@ struct ScatterArgs {
  * tc x 4 KiB | offsets nbw x 4 | cursors tc x nbw x 2 (| self-scan sums
  * nbw x 8) -- fits 64 KiB. */
 struct ScatterShape { uint32_t tc; size_t lds; };
-/* 16-tile chunks (two consecutive tiles per wave, one cursor row per wave,
- * the offsets written over the cursors after the ranking): static LDS of
- * 64 KiB stage + 8 x USN_SC_BIG_NBW x 2 cursors, two workgroups per CU */
-#define USN_SC_BIG_NBW 1008u
 inline size_t scatter_lds(uint32_t nbins, uint32_t tc, bool selfscan = false) {
   const size_t nbw = (nbins + 7u) & ~7u;
   return (size_t)tc * USN_TILE * 4 + nbw * 4 + (size_t)tc * nbw * 2 + (selfscan ? nbw * 8 : 0);
