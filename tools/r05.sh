@@ -475,6 +475,20 @@ case $S in
       --frames 8388608 --multi 2 --launches 5 base testlib > $O/scb_c5_slow.log 2>&1 || { tail -3 $O/scb_c5_slow.log; exit 1; }
     echo "c5 forced fallback"; grep scatter $O/scb_c5_slow.log
     ;;
+  r05av)
+    # the scatter compiled for 8 waves per SIMD (64 VGPRs, 96 B of spills per
+    # lane; build/abl/scwpe8) against the product's 6 (80 VGPRs): launches of
+    # few bins (c2: 32.5 KiB of LDS) fit 4 workgroups per CU by LDS; c5 stays
+    # at 3 (52.9 KiB)
+    for rep in 1 2; do
+      for c in c2 c4 c5; do
+        if [ $c = c5 ]; then A="--frames 8388608 --multi 2"; else A="--frames 1048576 --multi 8"; fi
+        timeout -k 10 300 python tools/scatter_bench.py --config $c $A \
+          --json $O/scb_${c}_$rep.json base scwpe8 > $O/scb_${c}_$rep.log 2>&1 || { tail -3 $O/scb_${c}_$rep.log; exit 1; }
+        echo "$c rep $rep"; grep scatter $O/scb_${c}_$rep.log
+      done
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"
