@@ -489,6 +489,25 @@ case $S in
       done
     done
     ;;
+  r05ax)
+    # the scatter without spills (the fallback's lane opaque to the compiler:
+    # 71 VGPRs, no scratch, against 80 and 32 B of spill stores per lane):
+    # the scatter and volume GPU tests; scan + scatter time against HEAD~
+    # (build/abl/spill) and the spill-free build at 8 waves per SIMD
+    # (build/abl/scwpe8: 64 VGPRs, no scratch now); the ballot fallback forced
+    TESTS="tests/test_gpu_scatter.py tests/test_gpu_volume.py" bash tools/gpu.sh $S testsall || exit 1
+    for rep in 1 2; do
+      for c in c5 c4 c2; do
+        if [ $c = c5 ]; then A="--frames 8388608 --multi 2"; else A="--frames 1048576 --multi 8"; fi
+        timeout -k 10 300 python tools/scatter_bench.py --config $c $A \
+          --json $O/scb_${c}_$rep.json base spill scwpe8 > $O/scb_${c}_$rep.log 2>&1 || { tail -3 $O/scb_${c}_$rep.log; exit 1; }
+        echo "$c rep $rep"; grep scatter $O/scb_${c}_$rep.log
+      done
+    done
+    USN_SCATTER_SLOW_RANK=1 timeout -k 10 300 python tools/scatter_bench.py --config c5 \
+      --frames 8388608 --multi 2 --launches 5 base testlib > $O/scb_c5_slow.log 2>&1 || { tail -3 $O/scb_c5_slow.log; exit 1; }
+    echo "c5 forced fallback"; grep scatter $O/scb_c5_slow.log
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
 echo "== session $S done"

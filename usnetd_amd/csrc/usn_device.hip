@@ -2840,10 +2840,12 @@ __device__ uint32_t usn_scatter_fallbacks = 0;
                            (the bounds clamps stay) */
 #define USN_SC_CHECKS 1
 #endif
-#ifndef USN_SCATTER_WPE   /* waves per SIMD the scatter is compiled for: 6 = 3 workgroups per CU
-                             (80 VGPRs, a few spilled): c5 scan + scatter 57.5 vs 61.7 us per 16M
-                             frames at 4 (85 VGPRs, 2 per CU), c2 29.1 vs 29.9 (profiles/r04/r04b) */
-#define USN_SCATTER_WPE 6
+#ifndef USN_SCATTER_WPE   /* waves per SIMD the scatter is compiled for: 8 = 64 VGPRs, no spills
+                             (since the fallback's lane is opaque, step 5): 4 workgroups per CU
+                             where the LDS allows (c2's few bins: scan + scatter 27.5-27.6 vs
+                             28.4 us at 6), c5 (3 per CU by LDS) and c4 equal (profiles/r05/r05ax);
+                             round 4: 6 against 4, c5 57.5 vs 61.7 us (profiles/r04/r04b) */
+#define USN_SCATTER_WPE 8
 #endif
 template <int TC, bool SELF>   // SELF: USN_SCF_SELFSCAN launches (one workgroup per CU at most:
                                // registers for the row sums instead of occupancy)
@@ -3132,9 +3134,14 @@ void scatter_kernel(ScatterArgs s) {
       uint16_t *cw = cur + (size_t)wave * s.nbw;
       const uint16_t *row = B.cnt + (size_t)(t0 + wave) * s.nbw;
       for (uint32_t bb = lane; bb < s.nbw; bb += 64) cw[bb] = (uint16_t)(cw[bb] - row[bb]);
+      // the lane made opaque to the compiler: otherwise it keeps step 1's
+      // per-segment indices and addresses live for this rare path (spilled:
+      // 6-7 scratch stores per lane and chunk, ~25 MB per c5 call)
+      uint32_t lf = lane;
+      asm volatile("" : "+v"(lf));
 #pragma unroll
       for (uint32_t k = 0; k < SEGS; ++k) {
-        const uint32_t local = k * 64 + lane;
+        const uint32_t local = k * 64 + lf;
         const bool v = local < tn;
         // the decision again from memory: keeping d[] live to here costs the
         // common path VGPRs
