@@ -160,13 +160,7 @@ class Run:
         # streams, with no dependence on how two streams' launches overlap;
         # two 2-ring launches on two streams: 61.1-62.0)
         S = max(1, streams) if streams else (1 if P * n >= LAUNCH_FRAMES else 2)
-        if strong:
-            total_q = max(world, STRONG_FRAMES // n)
-            mine = shard.rank_queues(total_q, world, rank)
-        else:
-            q = queues or P * S
-            total_q = q * world
-            mine = shard.rank_queues(total_q, world, rank)
+        mine, _ = shard.step_queues(n, world, rank, strong, queues or P * S, STRONG_FRAMES)
         self.queues = mine                                # global queue ids of this rank
         Q = len(mine)
         S = min(S, Q)
@@ -199,13 +193,15 @@ class Run:
                 self.results.append(_result(ctx, n))
                 del cfg
         self.R = R
-        # results: the device-throughput loop (the value) writes round i into
-        # the same results as round i - R, as a round's results are consumed
-        # before the next round; the end-to-end loop finalizes round i - 1 after
-        # round i's calls, so it double-buffers them (as the daemon keeps two
-        # per source, daemon/usnetd.cpp).  Double-buffered outputs no longer
-        # stay in the Infinity Cache between rounds: the value loop would run
-        # 6-7 % slower with them (profiles/r05/r05q)
+        # results: RR >= 2 rounds of result sets per queue, as the daemon binds
+        # them (two per source, daemon/usnetd.cpp: round i - 1 is delivered
+        # while round i is classified; the reference writes each frame into its
+        # target's ring and never overwrites one in place,
+        # /root/reference/src/endpoint.rs:61-74).  The value loop, the launch
+        # probe and the end-to-end loop all rotate over them, so no round's
+        # outputs are still in the Infinity Cache when they are written again.
+        # value_single_result_set (one set per queue, rewritten every round:
+        # ~170 MB of c5 outputs stay MALL-resident) is reported beside it
         self.RR = max(R, result_rounds)
         for _ in range(self.RR - R):
             for j in range(Q):
@@ -230,15 +226,17 @@ class Run:
     def frames_per_step(self):
         return self.Q * self.n
 
-    def step(self, i, stream_override=None, e2e=False):
+    def step(self, i, stream_override=None, single=False):
+        """poll round i: its launches, into round i's result sets (i mod RR;
+        `single`: one result set per queue, i mod R)"""
         multi = self.L.usn_classify_multi
-        for s, ba, ra, cnt, _, _ in self.groups[i % (self.RR if e2e else self.R)]:
+        for s, ba, ra, cnt, _, _ in self.groups[i % (self.R if single else self.RR)]:
             st = self.streams[s] if stream_override is None else stream_override
             rc = multi(self.h, ba, ra, cnt, st)
             if rc:
                 _lib().check(rc, "usn_classify_multi")
 
-    def timed(self, steps, dist):
+    def timed(self, steps, dist, single=False):
         ctx = self.ctx
         for x in self.streams:
             ctx.sync(x)
@@ -251,7 +249,7 @@ class Run:
         for x in self.streams[1:]:
             ctx.wait_event(x, self.ev0)
         for i in range(steps):
-            self.step(i)
+            self.step(i, single=single)
         self.enqueue_s = time.perf_counter() - t0     # host time to enqueue the steps
         for x, ej in zip(self.streams[1:], self.joins[1:]):
             ctx.record(ej, x)
@@ -300,7 +298,7 @@ class Run:
         t0 = time.perf_counter()
         t1 = None
         for i in range(steps):
-            self.step(i, e2e=True)
+            self.step(i)
             if i:
                 self.finalize_round(i - 1, times)
                 if i == 1:
@@ -320,7 +318,7 @@ class Run:
         first, so the call waits for nothing"""
         times = []
         for i in range(rounds):
-            self.step(i, e2e=True)
+            self.step(i)
             for x in self.streams:
                 self.ctx.sync(x)
             self.finalize_round(i, times)
@@ -343,7 +341,7 @@ class Run:
         for x in self.streams:
             ctx.sync(x)
         for i, (ea, eb) in enumerate(evs):
-            _, ba, ra, cnt, _, ral = self.groups[i % self.R][0]
+            _, ba, ra, cnt, _, ral = self.groups[i % self.RR][0]
             ctx.record(ea, st)
             rc = self.L.usn_classify_multi(self.h, ba, ra, cnt, st)
             if rc:
@@ -356,17 +354,19 @@ class Run:
         return float(np.median(ms)), frames
 
     def finalize_all(self):
-        """usn_finalize of every batch of the last rotation: the ordered host
-        stage has nothing to do on these configs (no fragments, DHCP, stale
-        caches); counted and reported."""
+        """usn_finalize of every batch of the last rotation (result rounds
+        0 .. RR - 1): the ordered host stage has nothing to do on these configs
+        (no fragments, DHCP, stale caches); counted and reported."""
         host_frames, flags, cls = 0, 0, [0, 0, 0, 0]
         for x in self.streams:
             self.ctx.sync(x)
-        for k in range(len(self.batches)):   # the value loop's results (rounds 0 .. R - 1)
-            info = self.ctx.finalize(self.batches[k], self.results[k], self.streams[0])
-            host_frames += info.n_host
-            flags |= info.flags
-            cls = [x + y for x, y in zip(cls, info.class_count)]
+        for r in range(self.RR):
+            for j in range(self.Q):
+                info = self.ctx.finalize(self.batches[(r % self.R) * self.Q + j],
+                                         self.results[r * self.Q + j], self.streams[0])
+                host_frames += info.n_host
+                flags |= info.flags
+                cls = [x + y for x, y in zip(cls, info.class_count)]
         return host_frames, flags, cls
 
     def free(self):
@@ -408,6 +408,12 @@ def measure(run, args, dist, world):
         run.step(args.warmup + args.ramp + i)
     wall, ev_ms = run.timed(args.steps, dist)
     elapsed = shard.max_over_ranks(wall, dist)
+    enqueue_s = run.enqueue_s
+    # the same K rounds with one result set per queue rewritten every round
+    # (rounds 0 .. R - 1 only; round 5's value basis), reported beside the value
+    wall1, _ = run.timed(args.steps, dist, single=True)
+    elapsed1 = shard.max_over_ranks(wall1, dist)
+    run.enqueue_s = enqueue_s
     host_frames, flags, cls = run.finalize_all()
     # the same poll rounds with usn_finalize of every ring in the timed loop
     # (what the reference does per drain)
@@ -449,6 +455,9 @@ def measure(run, args, dist, world):
             pass
     return {
         "value": round(frames / elapsed / 1e6, 2),
+        "value_basis": "K poll rounds, round i into result set i mod %d of each queue (the daemon's "
+                       "double-buffered results), no usn_finalize in the loop" % run.RR,
+        "value_single_result_set": round(frames / elapsed1 / 1e6, 2),
         "end_to_end_mpps": round(frames / e2e_elapsed / 1e6, 2),
         "end_to_end": {
             "basis": "poll rounds with usn_finalize of every ring in the timed loop (round i-1's "
@@ -692,7 +701,7 @@ def main(argv=None):
                  % (args.gpus, world))
     if args.launch_check:
         return launch_check(rank, world)
-    from usnetd_amd import lib
+    from usnetd_amd import lib, shard
     L = lib.load()            # the HIP runtime is loaded here, before torch (if any)
     dist = None
     device = local
@@ -701,9 +710,9 @@ def main(argv=None):
         import torch.distributed as dist_mod
         dist_mod.init_process_group("gloo")
         dist = dist_mod
-        ndev = torch.cuda.device_count()   # counts without initialising the GPU
-        if ndev > 0:                       # more ranks than GPUs (a rehearsal): round-robin
-            device = local % ndev
+        # counts without initialising the GPU; more ranks than GPUs (a
+        # rehearsal): round-robin
+        device = shard.rank_device(local, torch.cuda.device_count())
     ctx = lib.Ctx(device)
     if args.lists_async:
         ctx.set_lists_async(True)
@@ -716,6 +725,8 @@ def main(argv=None):
         "metric": METRIC,
         "value": res["value"],
         "unit": "Mpkts/s",
+        "value_basis": res["value_basis"],
+        "value_single_result_set": res["value_single_result_set"],
         "end_to_end_mpps": res["end_to_end_mpps"],
         "end_to_end": res["end_to_end"],
         "n_gpus": len(joined),
@@ -734,6 +745,7 @@ def main(argv=None):
             "streams": run.S,
             "batches_per_launch": run.P,
             "rotating_bytes_per_gpu": run.rotating_bytes,
+            "result_rounds": run.RR,
             "parallelism": "replicas%d" % world,
             "rank_devices": [d for _, d in joined],
             "event_ms_per_step": res["event_ms_per_step"],

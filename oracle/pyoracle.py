@@ -150,7 +150,9 @@ class Switch:
         if not incoming:
             want = (src, sport, dst, dport, proto)  # to_want: reversed tuple
             if (want[0], want[4], want[1]) not in me.listening:
-                is_dhcp_req = (proto == 17 and src == 0 and sport == 68 and dport == 67
+                # src_addr.is_unspecified() (pkt.rs:46): smoltcp 0.7.0 tests the
+                # 0.0.0.0/8 range, self.0[0] == 0 (smoltcp-recall)
+                is_dhcp_req = (proto == 17 and (src >> 24) == 0 and sport == 68 and dport == 67
                                and (dst & 0xFF) == 255)
                 if is_dhcp_req:
                     if me.for_nic is not None:

@@ -328,8 +328,11 @@ static int extract(uso_ctx *c, const uint8_t *b, uint32_t len, info_t *info,
   return R_PARSE;                                       /* Ipv6 (pkt.rs:205) and Unknown */
 }
 
-static int is_dhcp_request(const info_t *i) {           /* pkt.rs:36-58 */
-  return i->kind == 1 && i->proto == 17 && i->src == 0 && i->has_ports &&
+/* pkt.rs:36-58.  src_addr.is_unspecified() (pkt.rs:46) is smoltcp 0.7.0's
+ * "falls into the unspecified range" test, self.0[0] == 0 (0.0.0.0/8), written
+ * like is_loopback's self.0[0] == 127 (recalled; tag smoltcp-recall). */
+static int is_dhcp_request(const info_t *i) {
+  return i->kind == 1 && i->proto == 17 && (i->src >> 24) == 0 && i->has_ports &&
          i->sport == 68 && i->dport == 67 && (i->dst & 0xFF) == 255;
 }
 static int is_dhcp_answer(const info_t *i) {            /* pkt.rs:59-76 */

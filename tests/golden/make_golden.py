@@ -295,8 +295,55 @@ def kat_bridge():
     return {"name": "bridge", "endpoints": endpoints, "bridge": [MAC3], "steps": s}
 
 
+def kat_dhcp():
+    """is_dhcp_request's source test (pkt.rs:36-58): src_addr.is_unspecified()
+    (pkt.rs:46) is smoltcp 0.7.0's range test self.0[0] == 0, i.e. 0.0.0.0/8
+    (recalled: tag smoltcp-recall).  A request sets the NIC's next_dhcp and
+    clears both caches (endpoint.rs:217-228) and learns NO answer rule; a frame
+    from outside 0/8 is an ordinary client flow and learns one (:229-249)."""
+    endpoints = [[0, K_NIC, -1], [1, K_HOST, 0], [2, K_PIPE, 0], [4, K_UDS, 0]]
+    s = [{"op": "add_match", "want": W(L, 17, 3333), "owner": 2, "sticky": False, "expect": 1}]
+    rec = ["smoltcp-recall"]
+
+    def req(src, dst="10.0.0.255"):
+        return eth(BCAST, MAC4, 0x0800, ipv4(src, dst, 17, udp(68, 67, bytes(40))))
+
+    def ans(to, frm="10.0.0.255"):
+        return eth(BCAST, REMMAC, 0x0800, ipv4(frm, to, 17, udp(67, 68, bytes(40))))
+
+    for k, src in enumerate(("0.1.2.3", "0.0.0.0")):
+        f = udp_rx(1000 + k, 3333)
+        s.append(rx(f, EP, 2, NONE, "NIC caches decision 2"))
+        s.append({"op": "remove_match", "want": W(L, 17, 3333), "requester": 2, "expect": 1})
+        s.append(rx(f, EP, 2, NONE, "RemoveMatch leaves the NIC cache: stale hit (main.rs:608-625)"))
+        s.append(tx(4, req(src), NIC, 0, NONE,
+                    "tx UDP 68->67 to x.x.x.255 from %s: is_unspecified (0/8) -> DHCP request: "
+                    "NIC.next_dhcp=4, caches cleared, no answer rule (endpoint.rs:217-228); "
+                    "dmac bcast not bridged -> NIC" % src, rec))
+        s.append(rx(f, DROP, NOEP, NOMATCH, "the request cleared the NIC cache (endpoint.rs:223)", rec))
+        s.append(rx(ans(src), EP, 4, NONE, "answer: no rule, next_dhcp.take() -> 4 (endpoint.rs:262-268)", rec))
+        s.append(rx(ans(src), DROP, NOEP, DHCP_NONE,
+                    "again: no answer rule was learned and next_dhcp is None "
+                    "(a learned rule would hit 4 via key1)", rec))
+        s.append({"op": "add_match", "want": W(L, 17, 3333), "owner": 2, "sticky": False, "expect": 1})
+    # 1.0.0.0 is outside 0/8: an ordinary client flow, the answer key is learned
+    s.append(tx(4, req("1.0.0.0"), NIC, 0, NONE,
+                "src 1.0.0.0 is not unspecified: auto-learn {1.0.0.0,68,10.0.0.255,67,UDP}->4 "
+                "(endpoint.rs:229-249)", rec))
+    s.append(rx(ans("1.0.0.0"), EP, 4, NONE, "key1 hits the learned answer rule (endpoint.rs:317-320)", rec))
+    s.append(rx(ans("1.0.0.0"), EP, 4, NONE, "cache hit (a steered answer would have cleared it)", rec))
+    s.append(rx(ans("0.9.9.9"), DROP, NOEP, DHCP_NONE,
+                "next_dhcp was not set by the 1.0.0.0 frame (endpoint.rs:269-272)", rec))
+    # 0/8 source but dst[3] != 255: not a request, the answer key is learned
+    s.append(tx(4, req("0.7.7.7", "10.0.0.1"), NIC, 0, NONE,
+                "0/8 source to 10.0.0.1 (dst[3]!=255): not a DHCP request -> learns", rec))
+    s.append(rx(ans("0.7.7.7", "10.0.0.1"), EP, 4, NONE, "the learned answer rule", rec))
+    s.append(rx(ans("0.7.7.7", "10.0.0.1"), EP, 4, NONE, "cache hit", rec))
+    return {"name": "dhcp", "endpoints": endpoints, "bridge": [], "steps": s}
+
+
 def main():
-    for kat in (kat_main(), kat_bridge()):
+    for kat in (kat_main(), kat_bridge(), kat_dhcp()):
         path = os.path.join(HERE, "kat_%s.json" % kat["name"])
         with open(path, "w") as fh:
             json.dump(kat, fh, indent=1)

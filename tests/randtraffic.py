@@ -11,7 +11,7 @@ import random
 import struct
 
 IPS = ["169.254.137.191", "10.0.0.2", "10.0.0.3", "10.0.0.4", "127.0.0.1",
-       "0.0.0.0", "255.255.255.255", "10.0.0.1"]
+       "0.0.0.0", "255.255.255.255", "10.0.0.1", "0.1.2.3", "1.0.0.0", "10.0.0.255"]
 PORTS = [22, 67, 68, 80, 443, 3333, 3334, 5555, 9999, 40000]
 PROTOS = [6, 17, 17, 1, 132, 33, 136, 50]
 MACS = ["00:1b:21:4b:50:8c", "00:1b:21:4b:50:8d", "02:00:00:00:00:02", "02:00:00:00:00:03",
@@ -92,9 +92,13 @@ def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, 
     idents = [1, 2, 3]
     src = 0
     last = None
-    dhcp_req = (macb("ff:ff:ff:ff:ff:ff") + macb("02:00:00:00:00:04") + b"\x08\x00" +
-                bytes([0x45, 0, 0, 48, 0, 9, 0x40, 0, 64, 17, 0, 0]) + ipb("0.0.0.0") +
-                ipb("255.255.255.255") + struct.pack(">HHHH", 68, 67, 28, 0) + bytes(20))
+    # DHCP requests from 0.0.0.0/8 (smoltcp 0.7.0's is_unspecified range,
+    # pkt.rs:46) and, as a near miss that is an ordinary flow, from 1.0.0.0
+    dhcp_reqs = [(macb("ff:ff:ff:ff:ff:ff") + macb("02:00:00:00:00:04") + b"\x08\x00" +
+                  bytes([0x45, 0, 0, 48, 0, 9, 0x40, 0, 64, 17, 0, 0]) + ipb(s) +
+                  ipb(d) + struct.pack(">HHHH", 68, 67, 28, 0) + bytes(20))
+                 for s, d in (("0.0.0.0", "255.255.255.255"), ("0.0.0.0", "255.255.255.255"),
+                              ("0.1.2.3", "10.0.0.255"), ("1.0.0.0", "255.255.255.255"))]
     dhcp_ans = (macb("ff:ff:ff:ff:ff:ff") + macb("00:1b:21:4b:50:8d") + b"\x08\x00" +
                 bytes([0x45, 0, 0, 48, 0, 9, 0x40, 0, 64, 17, 0, 0]) + ipb("10.0.0.1") +
                 ipb("255.255.255.255") + struct.pack(">HHHH", 67, 68, 28, 0) + bytes(20))
@@ -125,7 +129,7 @@ def make_stream(seed: int, n_events: int = 400, tx_frac: float = 0.3, ops=True, 
         if last is not None and q < 0.2:
             f = last                     # repeats exercise the decision cache
         elif q < 0.23:
-            f = dhcp_req if src not in (0, 5) else dhcp_ans
+            f = rng.choice(dhcp_reqs) if src not in (0, 5) else dhcp_ans
         else:
             f = rand_frame(rng, idents)
         last = f

@@ -89,3 +89,35 @@ def test_two_rank_replicas_match_single_process():
     for q in range(8):
         assert np.array_equal(np.array(merged[q]) & 0xFFFFFF, np.array(single[q]) & 0xFFFFFF), q
     assert ret["elapsed"] == 2.0      # max over ranks (rank 1 reported 2.0)
+
+
+def test_rank_device_mapping():
+    """bench.py's rank -> HIP device map (shard.rank_device): one GPU per rank
+    on an 8-GPU node, round-robin when ranks outnumber the visible GPUs."""
+    assert [shard.rank_device(r, 8) for r in range(8)] == list(range(8))
+    assert [shard.rank_device(r, 1) for r in range(8)] == [0] * 8
+    assert [shard.rank_device(r, 4) for r in range(8)] == [0, 1, 2, 3, 0, 1, 2, 3]
+    assert [shard.rank_device(r, 0) for r in range(3)] == [0, 1, 2]
+    with pytest.raises(ValueError):
+        shard.rank_device(-1, 8)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_strong_partition_covers_every_frame(world):
+    """--strong: the 64M-frame job of c5 (8M-frame queues) split into disjoint
+    per-rank queue sets that together cover every queue, hence every frame
+    exactly once; weak scaling gives every rank its own queues_per_rank."""
+    import bench
+    n = bench.DEFAULT_FRAMES["c5"]
+    owned, totals = [], set()
+    for r in range(world):
+        mine, total = shard.step_queues(n, world, r, True, 2, bench.STRONG_FRAMES)
+        assert mine, "every rank drains at least one queue"
+        owned += mine
+        totals.add(total)
+    assert totals == {max(world, bench.STRONG_FRAMES // n)}
+    assert sorted(owned) == list(range(totals.pop()))
+    assert max(world, 8) * n >= bench.STRONG_FRAMES and len(owned) * n == max(world, 8) * n
+    weak = [shard.step_queues(n, world, r, False, 2)[0] for r in range(world)]
+    assert sorted(q for m in weak for q in m) == list(range(2 * world))
+    assert all(len(m) == 2 for m in weak)

@@ -2100,7 +2100,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       typedef __attribute__((address_space(3))) const uint32_t lds_u32;
       const bool listening = listen_lds ? tx_listening((const lds_u32 *)s_listen, t.n_listen, p)
                                         : tx_listening(t.listen, t.n_listen, p);
-      const bool dhcp_req = p.proto == 17u && p.src == 0u && p.has_ports && p.sport == 68u &&
+      // is_unspecified() is smoltcp 0.7.0's 0.0.0.0/8 range test (src[0] == 0), pkt.rs:46
+      const bool dhcp_req = p.proto == 17u && (p.src >> 24) == 0u && p.has_ports && p.sport == 68u &&
                             p.dport == 67u && (p.dst & 0xFFu) == 255u;
       if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
       if (!listening && !dhcp_req && !repeat) {   // learned unless the table has the answer key

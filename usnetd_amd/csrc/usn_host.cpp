@@ -1632,7 +1632,8 @@ uint32_t host_step(usn_ctx *c, int src, const uint8_t *frame, uint32_t len, Cach
       if (l.dst == w.dst && l.proto == w.proto && l.has_port == (ports ? 1 : 0) &&
           (!ports || l.port == w.dport)) { listening = true; break; }
     if (!listening) {
-      const bool dhcp_req = proto == 17 && p.info.src() == 0 && ports && p.info.sport() == 68 &&
+      // is_unspecified(): smoltcp 0.7.0's 0.0.0.0/8 range test (src[0] == 0), pkt.rs:46
+      const bool dhcp_req = proto == 17 && (p.info.src() >> 24) == 0 && ports && p.info.sport() == 68 &&
                             p.info.dport() == 67 && (p.info.dst() & 0xFF) == 255;
       if (dhcp_req) {
         if (S.for_nic >= 0) {

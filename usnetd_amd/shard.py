@@ -19,6 +19,29 @@ def rank_queues(total_queues: int, world: int, rank: int) -> list[int]:
     return list(range(start, start + per + (1 if rank < extra else 0)))
 
 
+def step_queues(frames_per_queue: int, world: int, rank: int, strong: bool = False,
+                queues_per_rank: int = 1, strong_frames: int = 1 << 26) -> tuple[list[int], int]:
+    """The rx queues `rank` drains in every poll round, and the job's queue count.
+
+    Weak scaling: every rank owns `queues_per_rank` queues (the job grows with
+    the world).  Strong scaling: the job is `strong_frames` frames per round in
+    queues of `frames_per_queue`, split over the ranks (at least one each)."""
+    if strong:
+        total = max(world, strong_frames // frames_per_queue)
+    else:
+        total = queues_per_rank * world
+    return rank_queues(total, world, rank), total
+
+
+def rank_device(local_rank: int, ndev: int) -> int:
+    """HIP device of a rank: its local rank on a node with one GPU per rank;
+    round-robin when there are more ranks than visible GPUs (a rehearsal on
+    one GPU); the local rank itself when no GPU count is known (ndev 0)."""
+    if local_rank < 0:
+        raise ValueError("local rank must be >= 0")
+    return local_rank % ndev if ndev > 0 else local_rank
+
+
 def queue_seed(queue: int, rnd: int) -> int:
     """Seed of the synthetic traffic of global rx queue `queue` in rotation
     round `rnd` (distinct across queues, hence across ranks; the rule table of
