@@ -106,6 +106,8 @@ def parse_args(argv=None):
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
     ap.add_argument("--tx-rings", type=int, default=8, choices=range(1, 9),
                     help="c4tx: consecutive rings of the sending endpoint per tx launch (one grid)")
+    ap.add_argument("--host-inclusive", default="c5,c2",
+                    help="configs whose PCIe-inclusive rate is measured at N=1 ('' for none)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test: ranks join the process group and report, no GPU")
     return ap.parse_args(argv)
@@ -677,6 +679,123 @@ def measure_tx(ctx, args):
     return x
 
 
+HOST_INCLUSIVE = {"c5": (1 << 23, 4, 2, 3), "c2": (1 << 20, 8, 4, 4)}   # frames, batches, streams, rounds
+
+
+def measure_host_inclusive(ctx, name):
+    """The PCIe-inclusive rate (north_star): frames start and end
+    in pinned host memory.  Per drained ring: hipMemcpyAsync H2D of the header
+    windows + lengths, usn_classify, usn_finalize, D2H of the decisions and the
+    per-endpoint lists (index + bin_off).  Rings go round-robin over S
+    streams, one NIC rx queue each, two device buffer sets per stream; a
+    stream's previous ring is finalized and copied back right before its next
+    ring is enqueued, so one stream's copies overlap the others' kernels.
+    Every returned decision and list is checked against the same ring
+    classified device-resident before the timed rounds (the device path,
+    itself parity-tested against the oracle in tests/).  Never the value."""
+    from usnetd_amd import lib, shard, traffic
+    n, nb, S, rounds = HOST_INCLUSIVE[name]
+    L = ctx.L
+    cfgs = [traffic.config(name, n=n, seed=shard.queue_seed(100 + k, 0)) for k in range(nb)]
+    cfg0 = cfgs[0]
+    traffic.install_ctx(ctx, cfg0)
+    nics = [cfg0.src] + traffic.extra_nics(cfg0, S - 1, ctx)
+    W = cfg0.stride
+    fbytes, lbytes = n * W, n * 2
+    n_ep = max(max(e[0] for e in cfg0.endpoints), max(nics)) + 1
+    obytes = n * 8 + (n_ep + 4) * 4            # decisions | index | bin_off
+    host = []
+    for cfg in cfgs:
+        hp = C.c_void_p()
+        lib.check(L.usn_host_alloc_pinned(ctx.h, fbytes + lbytes + obytes, C.byref(hp)))
+        C.memmove(hp.value, cfg.frames.ctypes.data, fbytes)
+        C.memmove(hp.value + fbytes, cfg.lens.ctypes.data, lbytes)
+        host.append(hp.value)
+    streams = [ctx.stream() for _ in range(S)]
+    dev = [[(lib.DeviceBatch(ctx, cfg0.frames, cfg0.lens, nics[si], stride=W), lib.DeviceResult(ctx, n))
+            for _ in range(2)] for si in range(S)]
+    # the device-resident decisions and lists of every ring (the check)
+    ref = []
+    b0, r0 = dev[0][0]
+    for cfg in cfgs:
+        b0.buf.upload(cfg.frames)
+        b0.lbuf.upload(cfg.lens)
+        ctx.classify(b0, r0, streams[0])
+        ctx.finalize(b0, r0, streams[0])
+        ref.append((r0.decisions().copy(), r0.index().copy(), r0.bin_off(n_ep + 3).copy()))
+    pending = [None] * S
+    flip = [0] * S
+    host_frames = [0]
+    out_of = lambda k, off, cnt: np.frombuffer((C.c_uint8 * (cnt * 4)).from_address(host[k] + fbytes + lbytes + off),
+                                              np.uint32)
+
+    def drain(si):
+        if pending[si] is None:
+            return
+        k, j = pending[si]
+        b, r = dev[si][j]
+        s = streams[si]
+        host_frames[0] += ctx.finalize(b, r, s).n_host
+        hp = host[k] + fbytes + lbytes
+        lib.check(L.usn_memcpy_d2h(ctx.h, hp, r.desc.decisions, n * 4, s))
+        lib.check(L.usn_memcpy_d2h(ctx.h, hp + n * 4, r.desc.index, n * 4, s))
+        lib.check(L.usn_memcpy_d2h(ctx.h, hp + n * 8, r.desc.bin_off, (n_ep + 4) * 4, s))
+        pending[si] = None
+
+    def one(k, si):
+        drain(si)
+        j = flip[si] = flip[si] ^ 1
+        b, r = dev[si][j]
+        s = streams[si]
+        hp = host[k % nb]
+        lib.check(L.usn_memcpy_h2d(ctx.h, b.buf.ptr, hp, fbytes, s))
+        lib.check(L.usn_memcpy_h2d(ctx.h, b.lbuf.ptr, hp + fbytes, lbytes, s))
+        lib.check(L.usn_classify(ctx.h, C.byref(b.desc), C.byref(r.desc), s))
+        pending[si] = (k % nb, j)
+
+    def finish():
+        for si in range(S):
+            drain(si)
+        ctx.sync()
+
+    for k in range(2 * S):                   # warm-up: every stream and buffer set used
+        one(k, k % S)
+    finish()
+    rates = []
+    K = 2 * nb
+    for _ in range(rounds):
+        for k in range(nb):                  # poison the host copies: the check sees this round's
+            out_of(k, 0, n)[:] = 0xFFFFFFFF
+        t0 = time.perf_counter()
+        for k in range(K):
+            one(k, k % S)
+        finish()
+        rates.append(K * n / (time.perf_counter() - t0) / 1e6)
+    bad = bad_lists = 0
+    for k in range(nb):
+        d, idx, off = ref[k]
+        bad += int(((out_of(k, 0, n) ^ d) & lib.PARITY_MASK).astype(bool).sum())
+        bad_lists += int(not np.array_equal(out_of(k, n * 4, n), idx))
+        bad_lists += int(not np.array_equal(out_of(k, n * 8, n_ep + 4)[:n_ep + 4], off[:n_ep + 4]))
+    for si in range(S):
+        for b, r in dev[si]:
+            r.free()
+            b.free()
+    for hp in host:
+        L.usn_host_free_pinned(ctx.h, C.c_void_p(hp))
+    med = float(np.median(rates))
+    return {"mpps_median": round(med, 1), "mpps_all": [round(x, 1) for x in rates], "unit": "Mpkts/s",
+            "frames_per_ring": n, "rings_per_round": K, "streams": S,
+            "h2d_bytes_per_frame": W + 2, "d2h_bytes_per_frame": 8,
+            "pcie_gbs_equiv": round(med * (W + 10) / 1e3, 1),
+            "host_stage_frames": host_frames[0], "decisions_checked": nb * n,
+            "decisions_differing": bad, "rings_with_lists_differing": bad_lists,
+            "check": "each ring's round-tripped decisions and lists against the same ring "
+                     "classified device-resident before the timed rounds",
+            "loop": "pinned H2D windows+lens, usn_classify, usn_finalize, D2H decisions+index+bin_off; "
+                    "%d streams, a stream's previous ring finalized before its next" % S}
+
+
 def workload(run, strong):
     cfg = run.cfg0
     sizes = sorted(set(int(x) for x in np.unique(cfg.lens)))
@@ -796,6 +915,14 @@ def main(argv=None):
                     x["cpu_baseline"] = cpu_pinned_1core(name, min(args.cpu_seconds, 3.0))
                 rx.free()
             out[name] = x
+    if world == 1 and not args.no_extra and args.host_inclusive:
+        # the PCIe-inclusive rate of c5 and c2 (frames and results in pinned
+        # host memory), beside the device-resident value
+        out["host_inclusive"] = {}
+        for name in args.host_inclusive.split(","):
+            ctx.close()
+            ctx = lib.Ctx(device)
+            out["host_inclusive"][name] = measure_host_inclusive(ctx, name)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -322,8 +322,10 @@ int usn_classify(usn_ctx *ctx, const usn_batch *b, usn_result *r, void *hip_stre
  * carried cache as `count` usn_classify calls finalized in turn (ring k sees
  * what the rings before it learned on the device, and is decided again on the
  * host only when ring k - 1's usn_finalize ran a host tail or redid it).
- * Finalize the rings in order.  tx rings of different sources: USN_EINVAL; the tiles of every ring but the last * USN_TILE + the last
- * ring's frames must stay below 2^32 - 1 (else USN_ERANGE). */
+ * Finalize the rings in order.  tx rings of different sources: USN_EINVAL.
+ * The launch's frame index must fit 32 bits: the sum over rings k < count - 1
+ * of ceil(n_k / USN_TILE) * USN_TILE, plus n of the last ring, must be below
+ * 2^32 - 1, else USN_ERANGE. */
 int usn_classify_multi(usn_ctx *ctx, const usn_batch *b, usn_result *r, uint32_t count,
                        void *hip_stream);
 

@@ -47,7 +47,10 @@ def main():
         # "product": the in-tree library (usnetd_amd/libusn.so, always the tree
         # under test); other names: build/abl/<name>, built by `make abl` or
         # tools/abl_commit.sh (rebuild them with the tree they are to match)
-        path = None if build == "product" else os.path.join(ROOT, "build", "abl", build, "libusn.so")
+        # "testlib": the test build of the tree (build/test/libusn.so), which
+        # reads the context knobs after "@" (USN_RX_EV, USN_TIMING_EV, ...)
+        path = None if build == "product" else lib.TEST_LIB_PATH if build == "testlib" else \
+            os.path.join(ROOT, "build", "abl", build, "libusn.so")
         saved = {}
         for kv in filter(None, knobs.split(",")):
             k, v = kv.split("=", 1)

@@ -5,7 +5,8 @@ table; each round: one AddMatch of a new connected rule (a server accepting
 a connection, /root/reference/src/main.rs:266-298), then one 1M-frame rx
 batch classified and finalized.  Reports the wall time of AddMatch + classify
 + finalize per round, and the same rounds with no AddMatch.  USN_IMG_FULL=1
-makes every change rebuild the image (round 2's behaviour).
+makes every change rebuild the image (round 2's behaviour): only the test
+build (build/test/libusn.so) reads that knob, so it is loaded then.
 usage: python tools/addmatch_latency.py [rounds]"""
 import json
 import os
@@ -21,7 +22,9 @@ from usnetd_amd import lib, traffic  # noqa: E402
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     cfg = traffic.config("c5", n=1 << 20, seed=3)
-    ctx = lib.Ctx(0)
+    full = bool(os.environ.get("USN_IMG_FULL"))
+    libpath = lib.TEST_LIB_PATH if full else None   # the product library ignores USN_IMG_FULL
+    ctx = lib.Ctx(0, libpath=libpath)
     traffic.install_ctx(ctx, cfg)
     s = ctx.stream()
     b = lib.DeviceBatch(ctx, cfg.frames, cfg.lens, cfg.src, stride=cfg.stride)
@@ -42,7 +45,8 @@ def main():
             ctx.finalize(b, rs[k % 2], s)
             ms.append((time.perf_counter() - t0) * 1e3)
         out[mode] = {"median_ms": round(statistics.median(ms), 3), "max_ms": round(max(ms), 3)}
-    out["image_rebuild_every_change"] = bool(os.environ.get("USN_IMG_FULL"))
+    out["image_rebuild_every_change"] = full
+    out["library"] = os.path.relpath(libpath or lib.LIB_PATH, ROOT)
     out["rules"] = ctx.rule_count()
     print(json.dumps(out), flush=True)
 

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 6 GPU sessions (one tag per gpurun call; outputs under gpurun_out/<tag>/).
+#   tools/r06.sh TAG
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+S=${1:?tag}
+export TMPDIR=/tmp
+C3="--frames 262144 --multi 4 --batches 16 --streams 2 --rounds 5 --launches 60"
+C2="--frames 1048576 --multi 8 --batches 16 --streams 2 --rounds 5 --launches 40"
+C5="--frames 8388608 --multi 2 --batches 4 --rounds 5 --launches 30"
+case $S in
+  r06b)
+    # ADVICE r05 (release waits), then what a call's rx completion event and
+    # host-mapped state gather cost: one test-build binary,
+    # knobs per context, interleaved in one process, c3 / c2 / c5 call shapes
+    TESTS=tests/test_gpu_release.py bash tools/gpu.sh $S tests || exit 1
+    V="product testlib@USN_RX_EV=1 testlib@USN_RX_EV=0 testlib@USN_RX_EV=2 testlib@USN_RX_EV=3 testlib@USN_RX_STATE=0 testlib@USN_RX_EV=0,USN_RX_STATE=0"
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    BENCH_ARGS="--steps 20 --warmup 3 --extras c3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
+  *) echo "unknown session $S"; exit 2 ;;
+esac

@@ -113,45 +113,20 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #define STAMP_FLUSH_SCATTER(slot) do { } while (0)
 #endif
 
-/* A/B-only knobs below give WRONG results on purpose (ablations timed by
- * tools/abl.py).  Those builds define USN_AB_BUILD=1 (the Makefile's `abl`
- * target, tests/isa_check.py); a product build that sets one fails here. */
+/* The wrong-result ablations of rounds 2-5 (no probes, load floor, no X,
+ * one U line, scatter without ranks / write-out) were removed from this
+ * source in round 6; git history keeps them (tools/abl.py builds knobs that
+ * keep results exact).  The one knob left that breaks the kernel on purpose
+ * is the ISA test's: those builds define USN_AB_BUILD=1 (tests/isa_check.py);
+ * a product build that sets it fails here. */
 #ifndef USN_AB_BUILD
 #define USN_AB_BUILD 0
-#endif
-#ifndef USN_ABL_NOTAGS   /* A/B only: global-table probes without the tag array */
-#define USN_ABL_NOTAGS 0
-#endif
-#ifndef USN_ABL_TXNOPROBE   /* A/B only: tx kernels without rule-table probes (wrong results) */
-#define USN_ABL_TXNOPROBE 0
-#endif
-
-#ifndef USN_ABL_NOPROBE   /* A/B only: no rule-table probes (wrong results) */
-#define USN_ABL_NOPROBE 0
-#endif
-#ifndef USN_ABL_NODISPCOPY   /* A/B only: one 1 KiB chunk of the image copied to LDS (wrong results) */
-#define USN_ABL_NODISPCOPY 0
-#endif
-#ifndef USN_ABL_NOX   /* A/B only: the U path never probes X (wrong results) */
-#define USN_ABL_NOX 0
-#endif
-#ifndef USN_ABL_ULINE   /* A/B only: every slot read of a probe reads the table's first line (wrong results) */
-#define USN_ABL_ULINE 0
-#endif
-#ifndef USN_ABL_LOADONLY   /* A/B only: loads and stores, no parse/probe/decide */
-#define USN_ABL_LOADONLY 0
-#endif
-#ifndef USN_ABL_SC   /* A/B only: scatter_kernel 4 no rank walk, 5 no write-out */
-#define USN_ABL_SC 0
 #endif
 #ifndef USN_ISA_PERTURB   /* tests/test_isa_waits.py only: 1 an extra load, 2 a stale wait count */
 #define USN_ISA_PERTURB 0
 #endif
-static_assert(USN_AB_BUILD || !(USN_ABL_NOTAGS || USN_ABL_TXNOPROBE || USN_ABL_NOPROBE || USN_ABL_NOX ||
-                                USN_ABL_ULINE ||
-                                USN_ABL_NODISPCOPY || USN_ABL_LOADONLY || USN_ABL_SC ||
-                                USN_ISA_PERTURB),
-              "an A/B-only knob (wrong results) in a build without USN_AB_BUILD=1");
+static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
+              "the ISA test's perturbation in a build without USN_AB_BUILD=1");
 
 /* 16-byte header load, default cache policy (the `nt` hint was slower on
  * these per-lane loads: c3 and the tx kernel, profiles/r02cp, r04/r04at) */
@@ -389,7 +364,7 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
  * first slot, which every such lane of the wave shares: one L2 request */
 __device__ __forceinline__ void asm_slot1(const uint4 *T, const usn_ph_table &t, bool need,
                                           const PhKeyH &k, uint32_t d, v4u32 &s) {
-  const uint4 *p = T + t.slot_off + (need && !USN_ABL_ULINE ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
+  const uint4 *p = T + t.slot_off + (need ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
   asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(s) : "v"(p) : "memory");
 }
 
@@ -597,9 +572,6 @@ template <int TM>
 __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const uint16_t *Dl,
                                               const ClassifyArgs &a, const Parsed &p) {
   uint32_t w1 = 0, w2 = 0;
-#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
-  w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
-#else
   if (TM == TM_DISPLDS && (a.probe_mask & 4u)) {   // Dl holds U's and X's displacements
     u_probe_sync(T, Dl, a, p, w1, w2);
   } else {
@@ -608,7 +580,6 @@ __device__ __forceinline__ uint32_t decide_rx(const uint4 *T, const uint16_t *Dl
     ph_probe2<TM>(T, Dl, a, (a.probe_mask & 1u) != 0, (a.probe_mask & 2u) != 0, x1, y1, z1, m1, x2,
                   y2, z2, m2, w1, w2);
   }
-#endif
   return decide_rx_w(a, p, w1, w2);
 }
 
@@ -979,10 +950,9 @@ template <int TM, bool GLDS>
 __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
-  constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA && !USN_ABL_LOADONLY;
+  constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA;
   // both rounds' probes batched (two rounds per lane, global image)
-  constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1 &&
-                          !USN_ABL_LOADONLY && !USN_ABL_NOPROBE;
+  constexpr bool BATCH2 = GLDS && TM != TM_LDS && ROUNDS == 2 && GD == 1;
   constexpr uint32_t WSTAGE = GD * STAGE_ROUND_SLOTS;   // per wave
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint4 s_stage[GLDS ? NWAVES * WSTAGE : 1];
@@ -1001,7 +971,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     const bool um = TM == TM_DISPLDS && (m.b[0].probe_mask & 4u);
     const uint32_t u0 = TM == TM_LDS ? 0u : um ? m.b[0].u_disp_unit : m.b[0].disp_unit;
     const uint32_t uend = um ? m.b[0].u_end_unit : m.b[0].table_units;
-    const uint32_t units = USN_ABL_NODISPCOPY ? min(64u, uend - u0) : uend - u0;
+    const uint32_t units = uend - u0;
     for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
       const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
@@ -1125,7 +1095,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       x0 = x0 && n0;
       x1 = x1 && n1;
       STAMP(4);
-      if (!USN_ABL_NOX && __ballot(x0 || x1)) {
+      if (__ballot(x0 || x1)) {
         uint32_t wx0, wx1;   // both rounds' X reads in flight together
         x_probe2(T, Dl, a, pr[0], x0, pr[1], x1, wx0, wx1);
         if (x0) w01 = wx0;
@@ -1256,15 +1226,9 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
         lane_round(fp[r + 1], q[r + 1]);
         __builtin_amdgcn_sched_barrier(0);
       }
-#if USN_ABL_LOADONLY   /* ablation build only: load floor (tools/abl.py) */
-      dec[r] = usn_mkdec(USN_CLS_DROP, USN_R_PARSE,
-                         (q[r][0].w ^ q[r][1].y ^ q[r][2].x ^ q[r][2].y ^ len[r]) & 0xFFFFu);
-      pr[r] = Parsed{};   // defined (a parse failure): the touch pass below reads it
-      continue;
-#endif
       Parsed &p = pr[r];
       parse(q[r], local < nt ? len[r] : 0u, fp[r], a.window, p);
-      if (LATE_DMA && !USN_ABL_NOPROBE && TM == TM_DISPLDS && (a.probe_mask & 4u)) {
+      if (LATE_DMA && TM == TM_DISPLDS && (a.probe_mask & 4u)) {
         // U (rare here: the 512-thread build batches both rounds above);
         // synchronous, then the next round's header DMA
         uint32_t w1 = 0, w2 = 0;
@@ -1279,33 +1243,22 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       } else if (LATE_DMA) {
         // global probes: the slot loads first, then the next round's header DMA,
         // so the wait for the slots does not also wait for the DMA
-        uint32_t w1 = 0, w2 = 0;
-#if USN_ABL_NOPROBE   /* ablation build only: no table probes */
-        w2 = (p.dport & 0xF) ? usn_key_meta(p.proto, 1) | ((p.dport & 0xF) << 16) : 0u;
-#else
         uint32_t x1, y1, z1, m1, x2, y2, z2, m2;
         rx_keys(p, x1, y1, z1, m1, x2, y2, z2, m2);
         const bool use1 = (a.probe_mask & 1u) != 0, use2 = (a.probe_mask & 2u) != 0;
         v4u32 s1, s2;
         ph_issue<TM, true>(T, Dl, a, use1, use2, x1, y1, z1, m1, x2, y2, z2, m2, s1, s2);
-#endif
         if (r + GD < ROUNDS) {
           __builtin_amdgcn_sched_barrier(0);
           lgkm_wait0();
           glds_round(a, base, nt, r + GD, wave, lane, sb);
           __builtin_amdgcn_sched_barrier(0);
-#if !USN_ABL_NOPROBE
           ph_slots_wait<GLDS_PARTS>(s1, s2);   // the next round's header DMAs may still fly
-#endif
         } else {
-#if !USN_ABL_NOPROBE
           ph_slots_wait<0>(s1, s2);
-#endif
         }
-#if !USN_ABL_NOPROBE
-        w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
-        w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
-#endif
+        const uint32_t w1 = use1 ? ph_hitv(s1, x1, y1, z1, m1) : 0u;
+        const uint32_t w2 = use2 ? ph_hitv(s2, x2, y2, z2, m2) : 0u;
         dec[r] = decide_rx_w(a, p, w1, w2);
       } else {
         dec[r] = decide_rx<TM>(T, Dl, a, p);
@@ -1390,9 +1343,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
 
     STAMP(6);
     // ---- the tile's frames per bin: LDS histogram, then its count row
-#if !USN_ABL_LOADONLY
     tile_hist(bins, nt, a.nbits, L.hist);
-#endif
     __syncthreads();
     STAMP(10);
     hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
@@ -1712,7 +1663,6 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
   if (!tx_dmac_in(t, fl, r1, i, ins)) return usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // :254-255
   uint32_t x, y, z, meta;
   key1_of(r0, x, y, z, meta);
-  if (USN_ABL_TXNOPROBE) return usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);
   uint32_t w = ph_probe1<IN_LDS>(T, a, 0, x, y, z, meta);
   if (!w && (ins & 2u)) w = tx_learned_key1(t, x, y, z, meta, i);
   if (!w && (a.probe_mask & 2u)) {
@@ -2106,7 +2056,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       if (!listening && dhcp_req) f |= TXR_HOST;              // NIC.next_dhcp := S (cross-endpoint)
       if (!listening && !dhcp_req && !repeat) {   // learned unless the table has the answer key
         want_key(make_uint4(p.i0, p.src, p.dst, p.ports), ax[r], ay[r], az[r], am[r]);
-        need[r] = !USN_ABL_TXNOPROBE;
+        need[r] = true;
       }
       if (p.proto == 17u && p.has_ports && p.sport == 67u && p.dport == 68u) f |= TXR_DHCPANS;
     }
@@ -2116,7 +2066,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     if (local < nt && touch) last = local + 1;
     const uint32_t kind = i0 & 0xFFu;
     if (touch == 1u && !(f & TXR_HOST) && (f & TXR_DMAC_IN) && !repeat && kind != USN_INFO_ARP &&
-        kind != USN_INFO_EAPOL && !USN_ABL_TXNOPROBE) {
+        kind != USN_INFO_EAPOL) {
       need[ROUNDS + r] = need[2 * ROUNDS + r] = true;
       key1_of(r0, ax[ROUNDS + r], ay[ROUNDS + r], az[ROUNDS + r], am[ROUNDS + r]);
       key2_of(r0, ax[2 * ROUNDS + r], ay[2 * ROUNDS + r], az[2 * ROUNDS + r], am[2 * ROUNDS + r]);
@@ -2372,8 +2322,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     } else if (!tx_dmac_in(t, fl, r1[r], vbase + local, ins_d)) {
       d = usn_mkdec(USN_CLS_NIC, USN_R_NONE, a.for_nic);   // endpoint.rs:254-255
     } else {
-      d = usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);  // (the A/B no-probe build keeps it)
-      use[r] = !USN_ABL_TXNOPROBE;
+      d = usn_mkdec(USN_CLS_DROP, USN_R_NOMATCH, 0xFFFFu);
+      use[r] = true;
       use[ROUNDS + r] = use[r] && !pre[r];                   // not probed in phase 1
       key1_of(rec[r], kx[r], ky[r], kz[r], km[r]);
       key2_of(rec[r], kx[ROUNDS + r], ky[ROUNDS + r], kz[ROUNDS + r], km[ROUNDS + r]);
@@ -3055,13 +3005,13 @@ void scatter_kernel(ScatterArgs s) {
   // out of order).  That is not an ISA guarantee, so step 4 verifies the
   // stage and a chunk that is not stably sorted is ranked again the
   // ballot way (5).
-  const uint32_t nf = USN_ABL_SC == 5 ? 0u : (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
+  const uint32_t nf = (uint32_t)min((uint64_t)TC * TILE, (uint64_t)B.n - first);
   // bad: a decision naming a bin past the batch's bins, a rank past the
   // chunk, an empty stage slot or a list position past n -- the count rows
   // and the decisions disagree.  Every access stays in bounds regardless, and
   // the batch's diag word gets USN_DIAG_LISTS (usn_finalize: USN_ELIST).
   bool bad = false;
-  if (wave < ntc && USN_ABL_SC != 4) {
+  if (wave < ntc) {
     uint32_t *cw = reinterpret_cast<uint32_t *>(cur + (size_t)wave * s.nbw);
     uint32_t at[SEGS];   // (the bins are recomputed below: 16 VGPRs fewer while the atomics fly)
 #pragma unroll
@@ -3088,7 +3038,7 @@ void scatter_kernel(ScatterArgs s) {
   // write past index), checking that each bin's run is in frame order
   bool unsorted = false;
   uint32_t q0 = 0;
-  if (USN_ABL_SC != 4) {
+  {
     // groups of 8 entries per thread: every stage read of the group, then
     // every offset read, then the stores (the LDS round trips overlap)
     constexpr uint32_t G = 8;
@@ -3115,19 +3065,19 @@ void scatter_kernel(ScatterArgs s) {
   for (uint32_t q = q0 + tid; q < nf; q += NTHREADS) {
     const uint32_t e = stage[q];
     const uint32_t b = min(e >> 16, s.nbw - 1u);
-    const uint32_t pos = USN_ABL_SC == 4 ? (uint32_t)first + q : off[b] + q;
+    const uint32_t pos = off[b] + q;
     if (pos < B.n) B.index[pos] = (uint32_t)first + (e & 0xFFFFu);
     bad |= pos >= B.n || e == ~0u;
     const uint32_t p = q ? stage[q - 1] : 0u;
     unsorted |= q && (p >> 16) == (e >> 16) && (p & 0xFFFFu) >= (e & 0xFFFFu);
   }
   STAMP(11);
-  if (USN_ABL_SC == 0 && USN_SC_CHECKS && __ballot(bad) && lane == 0) {   // rare: one report per wave
+  if (USN_SC_CHECKS && __ballot(bad) && lane == 0) {   // rare: one report per wave
     atomicOr(B.diag, USN_DIAG_LISTS);
     if (s.txs_out) s.txs_out[11] = USN_DIAG_LISTS;   // tx: beside chunk 0's copy of the scan's word
     if (B.rx_state) B.rx_state[2] = USN_DIAG_LISTS;
   }
-  if (USN_ABL_SC == 0 && __syncthreads_or(unsorted || (s.flags & USN_SCF_SLOW_RANK))) {
+  if (__syncthreads_or(unsorted || (s.flags & USN_SCF_SLOW_RANK))) {
     // 5. (not taken on gfx950 so far) the wave's cursors back to their
     // seeds (final value - the tile's count), the ranks from bit-sliced
     // ballots segment by segment, the stage out again

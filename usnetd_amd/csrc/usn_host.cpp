@@ -467,9 +467,13 @@ struct Replica {
   /* rx launches' completion (recorded after their scatter on the caller's
    * stream): usn_finalize of an rx batch waits for its own launch, not for
    * the later batches queued behind it.  A ring of events: a slot reused by
-   * a later launch only makes that wait longer */
+   * a later launch on the same stream only makes that wait longer; one
+   * re-recorded on another stream no longer orders the batch's launch, so
+   * each slot keeps the generation and stream of its last record (rx_wait) */
   static constexpr uint32_t RX_EVS = 64;
   hipEvent_t rx_ev[RX_EVS] = {};
+  uint64_t rx_ev_gen[RX_EVS] = {};
+  hipStream_t rx_ev_stream[RX_EVS] = {};
   uint32_t rx_ev_next = 0;
 };
 
@@ -489,6 +493,14 @@ struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
   uint32_t sel = 0;      // selected replica (usn_replica_select)
   int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
+  /* rx completion (A/B, test build: USN_RX_EV 0 none -- usn_finalize syncs
+   * the stream --, 1 the product's, 2 without the system-scope fence, 3 a
+   * device-scope release; USN_RX_STATE=0: no host-mapped state gather, the
+   * finalize reads summary and tile headers), and usn_event_create's flags
+   * (USN_TIMING_EV: 0 default, 1 device-scope release, 2 no system fence) */
+  int rx_ev_mode = 1;
+  bool rx_state_on = true;
+  unsigned timing_ev_flags = hipEventDefault;
   int tx512 = 1;   // USN_TX_T512 env (A/B): the tx kernel at 512 threads per tile (c4tx 1M:
                    // 51.2 vs 53.2 us at 256; two rounds per lane, 64 VGPRs, 4 workgroups per CU)
   double ph_load = USN_PH_LOAD;   // perfect-hash image geometry (env knobs)
@@ -584,8 +596,12 @@ struct usn_ctx {
     uint32_t rep, nbins;
     uint32_t slot, epoch;   // its rx state slot (RX_SLOTS: none) and launch tag
     hipEvent_t done;        // rx: recorded after its launch's scatter (Replica::rx_ev), or null
+    uint32_t ev_idx;        // ... its slot in Replica::rx_ev
+    uint64_t ev_gen;        // ... and the record's generation (rx_wait)
+    hipStream_t stream;     // the stream the launch ran on
   };
   std::unordered_map<const void *, BatchRec> batch_rep;
+  uint64_t rx_ev_gen = 0;   // Replica::rx_ev records so far (their generations)
   /* usn_set_lists_async: lists built on the replica's side stream; each
    * result's `lists done` event (keyed by its decisions array, created on
    * its replica's device) */
@@ -1858,6 +1874,11 @@ int usn_ctx_create_group(const int *hip_devices, uint32_t n, usn_ctx **out) {
   if (const char *e = test_knob("USN_TX_T512")) c->tx512 = std::atoi(e) ? 1 : 0;
   c->ph_load = ph_load_knob();
   c->ph_group = ph_group_knob();
+  if (const char *e = test_knob("USN_RX_EV")) c->rx_ev_mode = std::atoi(e);
+  if (const char *e = test_knob("USN_RX_STATE")) c->rx_state_on = std::atoi(e) != 0;
+  if (const char *e = test_knob("USN_TIMING_EV"))
+    c->timing_ev_flags = std::atoi(e) == 1 ? hipEventReleaseToDevice
+                       : std::atoi(e) == 2 ? hipEventDisableSystemFence : hipEventDefault;
   *out = c;
   return USN_OK;
 }
@@ -2180,9 +2201,11 @@ int usn_debug_image_stats(usn_ctx *c, int refresh, uint64_t *out4) {
   return USN_OK;
 }
 
-/* Test hook: the tx scratch state of the selected replica: counters[0..7]
- * (learned, flags, sets used, timed-out epoch, host-stage frames of rings
- * 0..3; usn_kernels.h USN_TXC_*), epoch. */
+/* Test hook: the tx scratch state of the selected replica's latest launch:
+ * counters[0..7] (learned, flags, sets used, timed-out epoch, and the
+ * host-stage frames of rings 0..3 ONLY; a launch takes up to USN_TX_RINGS = 8
+ * rings, whose host-stage counters [4 + k] for k >= 4 and learned items
+ * [12 + k] (usn_kernels.h USN_TXC_*) this hook does not expose), epoch. */
 int usn_debug_tx_state(usn_ctx *c, uint32_t *out10) {
   if (!c || !out10 || c->reps.empty()) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -2558,22 +2581,43 @@ static int chain_to_host(usn_ctx *c, Chain &ch) {
   return USN_OK;
 }
 
+/* wait for an rx batch's own launch (classify + lists on its stream): its
+ * completion event, unless the event's slot has since been re-recorded on
+ * another stream (more than Replica::RX_EVS rx launches in flight over two or
+ * more streams), which no longer orders this launch: then the device drains */
+static int rx_wait(usn_ctx *c, const usn_ctx::BatchRec &rec) {
+  Replica &R = c->reps[rec.rep];
+  HIPCHK(hipSetDevice(R.device));
+  if (R.rx_ev_gen[rec.ev_idx] == rec.ev_gen || R.rx_ev_stream[rec.ev_idx] == rec.stream)
+    HIPCHK(hipEventSynchronize(rec.done));
+  else
+    HIPCHK(hipDeviceSynchronize());
+  return USN_OK;
+}
+
 int usn_result_release(usn_ctx *c, const usn_result *r) {
   if (!c || !r || !r->decisions) return USN_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   for (const usn_ctx::Tx &t : c->txq)
     if (t.decisions == r->decisions) return USN_EBUSY;
+  // an rx batch classified into r and not finalized: its kernels may still be
+  // writing r, and the carried cache below is read from them
+  const auto br = c->batch_rep.find(r->decisions);
+  if (br != c->batch_rep.end() && br->second.done) { int e = rx_wait(c, br->second); if (e) return e; }
+  const auto le = c->lists_ev.find(r->decisions);
+  if (le != c->lists_ev.end() && le->second.ev) {   // lists on the side stream (after the classify)
+    HIPCHK(hipSetDevice(le->second.device));
+    HIPCHK(hipEventSynchronize(le->second.ev));   // the lists may still be built into r
+  }
   for (Chain &ch : c->chains)   // a carried cache read from this result's tile headers
     if (ch.device_chain && ch.summary == r->summary) {
       const int s = chain_to_host(c, ch);
       if (s) return s;
     }
-  c->batch_rep.erase(r->decisions);
-  const auto le = c->lists_ev.find(r->decisions);
+  if (br != c->batch_rep.end()) c->batch_rep.erase(br);
   if (le != c->lists_ev.end()) {
     if (le->second.ev) {
       HIPCHK(hipSetDevice(le->second.device));
-      HIPCHK(hipEventSynchronize(le->second.ev));   // the lists may still be built into r
       HIPCHK(hipEventDestroy(le->second.ev));
     }
     c->lists_ev.erase(le);
@@ -2657,6 +2701,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
   uint32_t rx_slot[USN_MAX_MULTI];
   uint32_t *rx_state[USN_MAX_MULTI];
   hipEvent_t rx_done = nullptr;   // rx, lists on the caller's stream: the launch's completion
+  uint32_t rx_ev_idx = 0;
   if (tx) {
     const usn_batch &tb = b[0];
     slot = c->tx_next_slot;
@@ -2722,12 +2767,13 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_rx), c->h_rxstate, 0));
     epoch = next_epoch(c);
     for (uint32_t k = 0; k < count; ++k) {
+      m.b[k].epoch = epoch;
+      if (!c->rx_state_on) { rx_slot[k] = usn_ctx::RX_SLOTS; rx_state[k] = nullptr; continue; }
       rx_slot[k] = c->rx_next_slot++ % usn_ctx::RX_SLOTS;
       volatile uint32_t *h = c->h_rxstate + rx_slot[k] * 8;
       h[0] = 0;   // (the tag, until the scatter writes it)
       h[2] = 0;   // (set by any scatter chunk that finds inconsistent lists)
       rx_state[k] = d_rx + rx_slot[k] * 8;
-      m.b[k].epoch = epoch;
     }
     if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
       HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
@@ -2751,10 +2797,16 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
                             epoch, tx ? nullptr : rx_state);
     if (st) return st;
-    if (!tx) {
-      hipEvent_t &e = R.rx_ev[R.rx_ev_next++ % Replica::RX_EVS];
-      if (!e) HIPCHK(hipEventCreateWithFlags(&e, USN_DONE_EV_FLAGS));
+    if (!tx && c->rx_ev_mode) {
+      rx_ev_idx = R.rx_ev_next++ % Replica::RX_EVS;
+      hipEvent_t &e = R.rx_ev[rx_ev_idx];
+      if (!e)
+        HIPCHK(hipEventCreateWithFlags(&e, USN_DONE_EV_FLAGS |
+                                               (c->rx_ev_mode == 2 ? hipEventDisableSystemFence
+                                                : c->rx_ev_mode == 3 ? hipEventReleaseToDevice : 0u)));
       HIPCHK(hipEventRecord(e, (hipStream_t)stream));
+      R.rx_ev_gen[rx_ev_idx] = ++c->rx_ev_gen;
+      R.rx_ev_stream[rx_ev_idx] = (hipStream_t)stream;
       rx_done = e;
     }
     if (tx) {
@@ -2800,7 +2852,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       HIPCHK(hipEventRecord(ch.done[rep], (hipStream_t)stream));
     }
     c->batch_rep[r[k].decisions] =
-        usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch, rx_done};
+        usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch, rx_done,
+                          rx_ev_idx, rx_done ? c->rx_ev_gen : 0, (hipStream_t)stream};
   }
   return USN_OK;
 }
@@ -3374,7 +3427,7 @@ int usn_finalize(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream,
   // recorded its completion, and the host-stage path below orders its copies
   // on the stream itself)
   if (!txb) {
-    if (br != c->batch_rep.end() && br->second.done) HIPCHK(hipEventSynchronize(br->second.done));
+    if (br != c->batch_rep.end() && br->second.done) { int e = rx_wait(c, br->second); if (e) return e; }
     else HIPCHK(hipStreamSynchronize(s));
   }
   {  // lists built on the side stream (usn_set_lists_async)
@@ -3713,7 +3766,7 @@ int usn_event_create(usn_ctx *c, void **ev) {
   if (!c || !ev) return USN_EINVAL;
   if (c->device < 0) return USN_ENODEV;
   hipEvent_t e;
-  HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventCreateWithFlags(&e, c->timing_ev_flags));
   *ev = e;
   return USN_OK;
 }
