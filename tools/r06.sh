@@ -20,5 +20,18 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     BENCH_ARGS="--steps 20 --warmup 3 --extras c3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06c)
+    # the cheaper probe hash (24-bit multiplies, no h2 finaliser), 32-bit header
+    # addresses, branch-free pidx: the suite (new image hashes), then the
+    # product against the previous commit (build/abl/r06old) and the rx
+    # completion event bound to the scatter's dispatch (USN_RX_EV=4)
+    bash tools/gpu.sh $S tests || exit 1
+    V="product r06old testlib@USN_RX_EV=4 testlib@USN_RX_EV=0"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

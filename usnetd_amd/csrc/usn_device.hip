@@ -32,6 +32,7 @@
  * USN_F_HOST and are listed per tile for the ordered host stage (usn_finalize).
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "usn_internal.h"
 #include "usn_kernels.h"
@@ -225,7 +226,7 @@ __device__ __forceinline__ PhKeyH ph_hash(const usn_ph_table &t, uint32_t x, uin
   PhKeyH k;
   const uint32_t h1 = usn_ph_h1(x, y, z, meta, t.seed);
   k.grp = usn_ph_group(h1, t.shift, t.g);
-  k.sbase = usn_ph_shard(h1, t.shift) * t.m;
+  k.sbase = usn_ph_sbase(h1, t.shift, t.m);
   k.h2 = usn_key_hash2(x, y, z, meta, t.seed);
   return k;
 }
@@ -479,8 +480,11 @@ __device__ __forceinline__ void ph_probe_many(const uint4 *T, const ClassifyArgs
  * Both lookups of a frame from ONE U slot: U's displacement from the LDS
  * copy (Dl), its slot from L2.  X (the projection's further K1 rules) only
  * when the slot says MORE and its inline K1 rule is not the frame's key1. */
+/* E of a parsed frame.  A frame has ports only for the five protocols of
+ * protocol_has_ports, so pidx is usn_u_pidx_ports's branch-free form (hipcc
+ * turned usn_u_pidx's compare chain into divergent branches) */
 __device__ __forceinline__ uint32_t u_key_e(const Parsed &p) {
-  return usn_u_e(p.proto, p.has_ports, p.dport);
+  return p.has_ports ? (usn_u_pidx_ports(p.proto) << 16 | p.dport) : (5u << 16 | p.proto);
 }
 
 /* w1/w2 as a K1/K2 probe would return them, and whether key1 needs X */
@@ -864,7 +868,11 @@ __device__ __forceinline__ void glds_round(const ClassifyArgs &a, uint64_t base,
     const uint32_t f = u / GLDS_PARTS, p = u - GLDS_PARTS * f;
     uint32_t local = r * NTHREADS + wave * 64 + f;
     local = local < nt ? local : nt - 1;          // tail tile: re-read the last frame
-    const uint8_t *src = a.frames + (base + local) * a.stride + GLDS_OFF + p * 16;
+    // the tile's first frame (scalar) + a 32-bit lane offset: local < 1024 and
+    // a GLDS stride <= 128, so one full-rate 24-bit multiply (a 64-bit index
+    // times the stride was three quarter-rate multiplies per instruction)
+    const uint8_t *tf = a.frames + base * a.stride;
+    const uint8_t *src = tf + (__umul24(local, a.stride) + GLDS_OFF + p * 16);
     __builtin_amdgcn_global_load_lds(src, (lds_void_t *)(st + 64 * k), 16, 0, GLDS_NT);
   }
 }
@@ -1002,9 +1010,12 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       for (uint32_t r = 0; r < ROUNDS; ++r)
         fp[r] = a.frames + a.offsets[base + min(r * NTHREADS + tid, nt - 1)];
     } else {
+      const uint8_t *tf = a.frames + base * a.stride;   // the tile's first frame (scalar)
 #pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r)
-        fp[r] = a.frames + (base + min(r * NTHREADS + tid, nt - 1)) * a.stride;
+      for (uint32_t r = 0; r < ROUNDS; ++r) {
+        const uint32_t i = min(r * NTHREADS + tid, nt - 1);
+        fp[r] = tf + (GLDS ? (size_t)__umul24(i, a.stride) : (size_t)i * a.stride);
+      }
     }
 #pragma unroll
     for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
@@ -3129,7 +3140,7 @@ uint32_t scatter_fallbacks() {
   return v;
 }
 
-hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
+hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream, hipEvent_t done) {
   const uint32_t chunks = s.chunk_base[s.count];
   if (chunks == 0) return hipSuccess;
   const dim3 sg(s.range_base[s.count] * s.nbb), sb(SCAN_THREADS);
@@ -3142,10 +3153,16 @@ hipError_t launch_scatter(const ScatterArgs &s, hipStream_t stream) {
   const size_t lds = scatter_lds(s.nbins, s.tc, (s.flags & USN_SCF_SELFSCAN) != 0);
   const dim3 g(chunks), b(NTHREADS);
   const bool self = (s.flags & USN_SCF_SELFSCAN) != 0;
-#define USN_SC_LAUNCH(TC_)                                                              \
-  do {                                                                                  \
-    if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);    \
-    else hipLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, s);        \
+  // `done`: bound to the scatter's own dispatch (no marker packet between
+  // this launch and the next, as hipEventRecord would add)
+#define USN_SC_LAUNCH(TC_)                                                                       \
+  do {                                                                                           \
+    if (done && self)                                                                            \
+      hipExtLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, nullptr, done, 0, s); \
+    else if (done)                                                                               \
+      hipExtLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, nullptr, done, 0, s); \
+    else if (self) hipLaunchKernelGGL((scatter_kernel<TC_, true>), g, b, lds, stream, s);        \
+    else hipLaunchKernelGGL((scatter_kernel<TC_, false>), g, b, lds, stream, s);                 \
   } while (0)
   switch (s.tc) {
     case 8: USN_SC_LAUNCH(8); break;

@@ -857,6 +857,8 @@ bool ph_build(std::vector<PhKey> &keys, usn_ph_table &t, std::vector<uint4> &slo
     const uint32_t m = std::max<uint32_t>({maxc + 1, (uint32_t)((double)maxc / load) + 1, 64u});
     const uint32_t g = std::max<uint32_t>({1u, (maxc + group - 1) / group,
                                            (uint32_t)(m * load / group)});
+    // the probes multiply shard ids by m and g in 24 bits (usn_mul24)
+    if (m >= (1u << 24) || g >= (1u << 24) || S > (1u << 16)) return false;
     slots.resize((size_t)S * m);
     disp.resize((size_t)S * g);
     std::vector<uint8_t> ok(S, 0);
@@ -2386,7 +2388,7 @@ static usn::ScatterPlan plan_lists(usn_ctx *c, const usn::ClassifyArgs *as, uint
 static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_result *r,
                           uint32_t count, hipStream_t s, uint32_t *txs_out = nullptr,
                           const uint32_t *txs_counters = nullptr, uint32_t epoch = 0,
-                          uint32_t *const *rx_state = nullptr) {
+                          uint32_t *const *rx_state = nullptr, hipEvent_t done = nullptr) {
   usn::ScatterArgs x;
   std::memset(&x, 0, sizeof x);
   x.count = count;
@@ -2442,7 +2444,7 @@ static int launch_scatter(usn_ctx *c, const usn::ClassifyArgs *as, const usn_res
   if (corrupt == 1) HIPCHK(hipMemsetAsync(const_cast<uint16_t *>(x.b[0].cnt), 0x01, 2, s));
   if (corrupt == 2) HIPCHK(hipMemsetD32Async(r[0].decisions, (int)((1u << 16) | 0x0FF0u), 1, s));
 #endif
-  HIPCHK(usn_t512::launch_scatter(x, s));
+  HIPCHK(usn_t512::launch_scatter(x, s, done));
   return USN_OK;
 }
 
@@ -2794,9 +2796,6 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       // slot's previous batch is final: its usn_finalize synchronised)
       reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
     }
-    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
-                            epoch, tx ? nullptr : rx_state);
-    if (st) return st;
     if (!tx && c->rx_ev_mode) {
       rx_ev_idx = R.rx_ev_next++ % Replica::RX_EVS;
       hipEvent_t &e = R.rx_ev[rx_ev_idx];
@@ -2804,11 +2803,16 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         HIPCHK(hipEventCreateWithFlags(&e, USN_DONE_EV_FLAGS |
                                                (c->rx_ev_mode == 2 ? hipEventDisableSystemFence
                                                 : c->rx_ev_mode == 3 ? hipEventReleaseToDevice : 0u)));
-      HIPCHK(hipEventRecord(e, (hipStream_t)stream));
       R.rx_ev_gen[rx_ev_idx] = ++c->rx_ev_gen;
       R.rx_ev_stream[rx_ev_idx] = (hipStream_t)stream;
       rx_done = e;
     }
+    // rx: the completion event bound to the scatter's dispatch (mode 4), or
+    // recorded behind it (a marker packet between this launch and the next)
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
+                            epoch, tx ? nullptr : rx_state, c->rx_ev_mode == 4 ? rx_done : nullptr);
+    if (st) return st;
+    if (rx_done && c->rx_ev_mode != 4) HIPCHK(hipEventRecord(rx_done, (hipStream_t)stream));
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
       if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, USN_DONE_EV_FLAGS));

@@ -84,6 +84,16 @@ USN_HD uint32_t usn_key_hash(uint32_t x, uint32_t y, uint32_t z, uint32_t meta) 
 USN_HD uint32_t usn_mulhi32(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
 }
+/* the low 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24 /
+ * v_mad_u32_u24 on CDNA (a 32-bit v_mul_lo_u32 is quarter rate).  Callers
+ * keep both operands below 2^24 (shard ids < 2^16, m and g < 2^24: ph_build) */
+USN_HD uint32_t usn_mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
+#endif
+}
 USN_HD uint32_t usn_fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -92,27 +102,37 @@ USN_HD uint32_t usn_fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-/* second key hash, independent of usn_key_hash (other multipliers) */
+/* second key hash, independent of usn_key_hash (other multipliers).  Not
+ * finalised: usn_ph_slot mixes h2 + d * phi through usn_fmix32 anyway, so
+ * the probe spends two quarter-rate multiplies fewer (round 6); keys of one
+ * group only need distinct h2 values */
 USN_HD uint32_t usn_key_hash2(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uint32_t seed) {
   uint32_t h = (x ^ seed) * 0xCC9E2D51u;
   h = usn_rotl32(h, 15) ^ (y * 0x1B873593u);
-  h = usn_rotl32(h, 13) * 5u + 0xE6546B64u;
+  h = usn_rotl32(h, 13);
+  h = (h ^ (h << 5)) + 0xE6546B64u;   // (murmur's h * 5 + c became a quarter-rate 64-bit mad)
   h ^= usn_rotl32(z * 0x85EBCA77u, 17);
   h ^= (meta + seed) * 0x165667B1u;
-  return usn_fmix32(h);
+  return h ^ (h >> 16);
 }
 USN_HD uint32_t usn_ph_h1(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uint32_t seed) {
   return usn_key_hash(x, y ^ seed, z, meta);
 }
+/* d is a 16-bit displacement: d * phi with a 24-bit odd phi is one
+ * full-rate 24-bit multiply */
 USN_HD uint32_t usn_ph_slot(uint32_t h2, uint32_t d, uint32_t m) {
-  return usn_mulhi32(usn_fmix32(h2 + d * 0x9E3779B9u), m);
+  return usn_mulhi32(usn_fmix32(h2 + usn_mul24(d, 0x9E3779u)), m);
 }
 USN_HD uint32_t usn_ph_shard(uint32_t h1, uint32_t shift) {
   return shift ? h1 >> (32u - shift) : 0u;
 }
 /* index of the key's displacement within its table's displacements */
 USN_HD uint32_t usn_ph_group(uint32_t h1, uint32_t shift, uint32_t g) {
-  return usn_ph_shard(h1, shift) * g + usn_mulhi32(h1 << shift, g);
+  return usn_mul24(usn_ph_shard(h1, shift), g) + usn_mulhi32(h1 << shift, g);
+}
+/* the first slot of the key's shard */
+USN_HD uint32_t usn_ph_sbase(uint32_t h1, uint32_t shift, uint32_t m) {
+  return usn_mul24(usn_ph_shard(h1, shift), m);
 }
 
 /* one table of the image, in 16-byte units / u16 units from the image base */
@@ -152,6 +172,14 @@ USN_HD uint32_t usn_u_pidx(uint32_t proto) {
   return proto == 6u ? 0u : proto == 17u ? 1u : proto == 33u ? 2u : proto == 132u ? 3u
          : proto == 136u ? 4u : 7u;
 }
+/* usn_u_pidx of a protocol that has ports (6, 17, 33 -> p >> 4; 132, 136 ->
+ * 3 + bit 3), without compares (the rx kernel's form) */
+USN_HD constexpr uint32_t usn_u_pidx_ports(uint32_t proto) {
+  return (proto & 0x80u) ? 3u + ((proto >> 3) & 1u) : (proto >> 4);
+}
+static_assert(usn_u_pidx_ports(6) == 0 && usn_u_pidx_ports(17) == 1 && usn_u_pidx_ports(33) == 2 &&
+                  usn_u_pidx_ports(132) == 3 && usn_u_pidx_ports(136) == 4,
+              "usn_u_pidx_ports differs from usn_u_pidx on a protocol with ports");
 USN_HD uint32_t usn_u_e(uint32_t proto, uint32_t has_ports, uint32_t dport) {
   return has_ports ? (usn_u_pidx(proto) << 16 | (dport & 0xFFFFu)) : (5u << 16 | (proto & 0xFFu));
 }

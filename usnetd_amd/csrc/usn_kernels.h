@@ -239,7 +239,9 @@ uint32_t *scatter_diag(void *scratch, uint64_t cap, uint32_t nbins);
  * usn_device.hip); usn_host.cpp use_t512() picks the build per launch */
 namespace usn_t512 {
 hipError_t launch_classify(const usn::MultiArgs &m, hipStream_t stream);
-hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream);
+/* done (optional): an event bound to the scatter kernel's dispatch, complete
+ * when the lists are (hipExtLaunchKernel's stop event) */
+hipError_t launch_scatter(const usn::ScatterArgs &s, hipStream_t stream, hipEvent_t done = nullptr);
 uint32_t scatter_fallbacks();   /* chunks the scatter ranked again (current device) */
 hipError_t launch_tx(const usn::TxArgs &t, hipStream_t stream);
 bool table_fits_lds(uint32_t nbins, uint32_t table_units);
