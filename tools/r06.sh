@@ -31,6 +31,12 @@ case $S in
     ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS=c4 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    # the tx grid (8 rings per launch, 8 rotating buffers): previous commit, product, twice
+    for v in old new old new; do
+      L=""; [ $v = old ] && L=build/abl/r06old/libusn.so
+      TAILN=3 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
     BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
   *) echo "unknown session $S"; exit 2 ;;
