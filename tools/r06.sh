@@ -39,5 +39,20 @@ case $S in
     done
     BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06d)
+    # the completion event bound to the scatter's dispatch by default (rx and
+    # tx): the suite; the tx grid against the hash A/B builds (which of the
+    # two hash changes slowed r06c's tx grid); c3 / c2 calls against mode 1
+    bash tools/gpu.sh $S tests || exit 1
+    for v in new r06old oldkey oldmac oldboth new r06old oldkey oldmac oldboth; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    V="product testlib@USN_RX_EV=1 testlib@USN_RX_EV=0"
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -493,12 +493,13 @@ struct usn_ctx {
   int device = 0;        // the selected replica's device (plumbing calls)
   uint32_t sel = 0;      // selected replica (usn_replica_select)
   int t512 = -1;   // USN_T512 env (A/B): -1 by table size, 0 never, 1 always
-  /* rx completion (A/B, test build: USN_RX_EV 0 none -- usn_finalize syncs
-   * the stream --, 1 the product's, 2 without the system-scope fence, 3 a
-   * device-scope release; USN_RX_STATE=0: no host-mapped state gather, the
+  /* launch completion (A/B, test build: USN_RX_EV 0 none for rx --
+   * usn_finalize syncs the stream --, 1 recorded behind the scatter, 2 the
+   * same without the system-scope fence, 3 with a device-scope release, 4
+   * bound to the scatter's dispatch, the product's; USN_RX_STATE=0: no host-mapped state gather, the
    * finalize reads summary and tile headers), and usn_event_create's flags
    * (USN_TIMING_EV: 0 default, 1 device-scope release, 2 no system fence) */
-  int rx_ev_mode = 1;
+  int rx_ev_mode = 4;
   bool rx_state_on = true;
   unsigned timing_ev_flags = hipEventDefault;
   int tx512 = 1;   // USN_TX_T512 env (A/B): the tx kernel at 512 threads per tile (c4tx 1M:
@@ -2807,18 +2808,23 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       R.rx_ev_stream[rx_ev_idx] = (hipStream_t)stream;
       rx_done = e;
     }
-    // rx: the completion event bound to the scatter's dispatch (mode 4), or
-    // recorded behind it (a marker packet between this launch and the next)
-    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
-                            epoch, tx ? nullptr : rx_state, c->rx_ev_mode == 4 ? rx_done : nullptr);
-    if (st) return st;
-    if (rx_done && c->rx_ev_mode != 4) HIPCHK(hipEventRecord(rx_done, (hipStream_t)stream));
+    hipEvent_t done = rx_done;   // the launch's completion: rx_ev, or the tx slot's
     if (tx) {
       Replica::TxSlot &X = R.txs[slot];
       if (!X.txstate_ev) HIPCHK(hipEventCreateWithFlags(&X.txstate_ev, USN_DONE_EV_FLAGS));
-      HIPCHK(hipEventRecord(X.txstate_ev, (hipStream_t)stream));
-      c->txstate_for[slot] = r[0].decisions;
+      done = X.txstate_ev;
     }
+    /* The completion event bound to the scatter's own dispatch
+     * (hipExtLaunchKernel's stop event, mode 4, the product's): recorded
+     * behind it instead (hipEventRecord), it is a marker packet between this
+     * launch and the next, which cost c3's calls of 4 x 256K frames 3.6 % and
+     * their two-stream steps 5 % (profiles/r06/r06c) */
+    const bool bind = done && c->rx_ev_mode == 4;
+    int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
+                            epoch, tx ? nullptr : rx_state, bind ? done : nullptr);
+    if (st) return st;
+    if (done && !bind) HIPCHK(hipEventRecord(done, (hipStream_t)stream));
+    if (tx) c->txstate_for[slot] = r[0].decisions;
   } else {
     // the scatter on the side stream, after this launch; the caller's stream
     // goes on to the next batch (usn_finalize / usn_lists_wait join them)

@@ -28,6 +28,13 @@
 
 #include <stdint.h>
 
+#ifndef USN_AB_OLDKEYHASH
+#define USN_AB_OLDKEYHASH 0
+#endif
+#ifndef USN_AB_OLDMACHASH
+#define USN_AB_OLDMACHASH 0
+#endif
+
 #define USN_SLOT_VALID (1u << 11)
 #define USN_SLOT_NICOWNER (1u << 12)
 #define USN_KEY_META_MASK 0x0FFFu
@@ -113,7 +120,11 @@ USN_HD uint32_t usn_key_hash2(uint32_t x, uint32_t y, uint32_t z, uint32_t meta,
   h = (h ^ (h << 5)) + 0xE6546B64u;   // (murmur's h * 5 + c became a quarter-rate 64-bit mad)
   h ^= usn_rotl32(z * 0x85EBCA77u, 17);
   h ^= (meta + seed) * 0x165667B1u;
+#if USN_AB_OLDKEYHASH   /* A/B (tools/abl_flags.sh): round 5's finalised h2 */
+  return usn_fmix32(h);
+#else
   return h ^ (h >> 16);
+#endif
 }
 USN_HD uint32_t usn_ph_h1(uint32_t x, uint32_t y, uint32_t z, uint32_t meta, uint32_t seed) {
   return usn_key_hash(x, y ^ seed, z, meta);
@@ -203,6 +214,12 @@ USN_HD uint32_t usn_mul24_mid(uint32_t a, uint32_t k) {
  * probe (the tx kernel hashes two MACs per frame: round 6 replaced a 64-bit
  * multiply, four quarter-rate instructions, with 24-bit ones) */
 USN_HD uint32_t usn_mac_hash(uint64_t m) {
+#if USN_AB_OLDMACHASH   /* A/B (tools/abl_flags.sh): round 5's 64-bit multiply */
+  m ^= m >> 29;
+  m *= 0xBF58476D1CE4E5B9ull;
+  m ^= m >> 32;
+  return (uint32_t)m;
+#endif
   const uint32_t a = (uint32_t)m & 0xFFFFFFu, b = (uint32_t)(m >> 24) & 0xFFFFFFu;
   uint32_t h = usn_mul24_mid(a, 0xED5AD5u) ^ usn_mul24_mid(b ^ 0x5BD1E9u, 0x9E3779u);
   h ^= h >> 15;
