@@ -54,5 +54,21 @@ case $S in
     ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06e)
+    # MAC hash reverted, completion events bound for launches <= 2048 tiles:
+    # the suite; c5's U geometry (a smaller displacement copy per tile: lower
+    # slot load, larger groups); c3 / c2 against recorded events; the tx grid
+    bash tools/gpu.sh $S tests || exit 1
+    V="product testlib@USN_PH_LOAD=0.35,USN_PH_GROUP=16 testlib@USN_PH_LOAD=0.4,USN_PH_GROUP=14 testlib@USN_PH_LOAD=0.3,USN_PH_GROUP=20 testlib@USN_PH_LOAD=0.25,USN_PH_GROUP=26"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    V="product testlib@USN_RX_EV=1"
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    for v in new new; do
+      TAILN=1 TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

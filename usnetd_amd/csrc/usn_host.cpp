@@ -484,6 +484,9 @@ struct Replica {
  * without the system-scope fence it is the same within noise (r05v), so the
  * events keep it (the host reads what they order: the launch's state words,
  * then the results through copies). */
+#ifndef USN_BIND_MAX_TILES   /* 2M frames: c3's calls of 4 x 256K are bound, c2's 8 x 1M are not */
+#define USN_BIND_MAX_TILES 2048u
+#endif
 #ifndef USN_DONE_EV_FLAGS
 #define USN_DONE_EV_FLAGS hipEventDisableTiming
 #endif
@@ -496,10 +499,11 @@ struct usn_ctx {
   /* launch completion (A/B, test build: USN_RX_EV 0 none for rx --
    * usn_finalize syncs the stream --, 1 recorded behind the scatter, 2 the
    * same without the system-scope fence, 3 with a device-scope release, 4
-   * bound to the scatter's dispatch, the product's; USN_RX_STATE=0: no host-mapped state gather, the
+   * bound to the scatter's dispatch, 5 bound for launches of at most
+   * USN_BIND_MAX_TILES tiles, else recorded (the product's); USN_RX_STATE=0: no host-mapped state gather, the
    * finalize reads summary and tile headers), and usn_event_create's flags
    * (USN_TIMING_EV: 0 default, 1 device-scope release, 2 no system fence) */
-  int rx_ev_mode = 4;
+  int rx_ev_mode = 5;
   bool rx_state_on = true;
   unsigned timing_ev_flags = hipEventDefault;
   int tx512 = 1;   // USN_TX_T512 env (A/B): the tx kernel at 512 threads per tile (c4tx 1M:
@@ -2818,8 +2822,11 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
      * (hipExtLaunchKernel's stop event, mode 4, the product's): recorded
      * behind it instead (hipEventRecord), it is a marker packet between this
      * launch and the next, which cost c3's calls of 4 x 256K frames 3.6 % and
-     * their two-stream steps 5 % (profiles/r06/r06c) */
-    const bool bind = done && c->rx_ev_mode == 4;
+     * their two-stream steps 5 % (profiles/r06/r06c, r06d).  Bound, it cost
+     * the two-stream steps of c2's 8M-frame calls 1-1.5 % in the same A/Bs:
+     * so bound for launches of at most USN_BIND_MAX_TILES tiles (mode 5) */
+    const bool bind = done && (c->rx_ev_mode == 4 ||
+                               (c->rx_ev_mode == 5 && m.tile_base[count] <= USN_BIND_MAX_TILES));
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
                             epoch, tx ? nullptr : rx_state, bind ? done : nullptr);
     if (st) return st;

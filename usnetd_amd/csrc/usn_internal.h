@@ -31,9 +31,6 @@
 #ifndef USN_AB_OLDKEYHASH
 #define USN_AB_OLDKEYHASH 0
 #endif
-#ifndef USN_AB_OLDMACHASH
-#define USN_AB_OLDMACHASH 0
-#endif
 
 #define USN_SLOT_VALID (1u << 11)
 #define USN_SLOT_NICOWNER (1u << 12)
@@ -204,27 +201,14 @@ USN_HD uint32_t usn_u_meta(uint32_t o) {
 /* 32-bit tag of a key in the tag array of a global-memory table (0 = empty) */
 USN_HD uint32_t usn_key_tag(uint32_t h) { return h | 1u; }
 
-/* bits 16..47 of the 48-bit product a * k of two 24-bit values: on CDNA a
- * full-rate v_mul_u32_u24 + v_mul_hi_u32_u24 and an align (hipcc selects
- * them for a 64-bit product of operands known to fit 24 bits) */
-USN_HD uint32_t usn_mul24_mid(uint32_t a, uint32_t k) {
-  return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(k & 0xFFFFFFu)) >> 16);
-}
 /* MAC (48 bits) set hash, shared by the host bridge-set build and the device
- * probe (the tx kernel hashes two MACs per frame: round 6 replaced a 64-bit
- * multiply, four quarter-rate instructions, with 24-bit ones) */
+ * probe.  (Round 6 tried 24-bit multiplies here: the tx grid ran 9 % slower,
+ * longer probe runs on c4tx's MAC pattern, profiles/r06/r06d.) */
 USN_HD uint32_t usn_mac_hash(uint64_t m) {
-#if USN_AB_OLDMACHASH   /* A/B (tools/abl_flags.sh): round 5's 64-bit multiply */
   m ^= m >> 29;
   m *= 0xBF58476D1CE4E5B9ull;
   m ^= m >> 32;
   return (uint32_t)m;
-#endif
-  const uint32_t a = (uint32_t)m & 0xFFFFFFu, b = (uint32_t)(m >> 24) & 0xFFFFFFu;
-  uint32_t h = usn_mul24_mid(a, 0xED5AD5u) ^ usn_mul24_mid(b ^ 0x5BD1E9u, 0x9E3779u);
-  h ^= h >> 15;
-  h ^= usn_mul24_mid((h ^ (h >> 8)) & 0xFFFFFFu, 0xC2B2AFu);
-  return h ^ (h >> 13);
 }
 
 /* 48-bit fingerprint of a packed Want key (tx learned-rule set) */
