@@ -70,5 +70,22 @@ case $S in
     done
     BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06f)
+    # the tx EARLY look-back over packed words (one 16-byte load per thread
+    # instead of 2048 granule lines per tile): the tx tests, then the tx grid
+    # against HEAD~ (build/abl/r06prev), interleaved; the bench's new probe
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py" bash tools/gpu.sh $S tests || exit 1
+    for v in new r06prev new r06prev new r06prev; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    for v in new r06prev; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 1" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench1_${v}_$RANDOM.log
+    done
+    BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -1713,7 +1713,7 @@ __device__ uint32_t decide_tx_ipv4(const TxArgs &t, const uint4 *T, const uint4 
 #define TXG_PINS 11u   /* INS of every tile up to and including this one */
 #define TXG_PHEAD 12u  /* 1 + batch index of the last non-hit touching frame up to this tile, 0 none */
 #define TXG_CIN 13u    /* tile 0: 6 granules, the carried-in cache {state, dst, info[4]} */
-#define TXG_EARLY 19u  /* bit 0/1: the tile has frames flagged to learn a MAC / rule (before
+#define TXG_EARLY 19u  /* (unused since round 6: EARLY is packed, TxArgs::early) bit 0/1: the tile has frames flagged to learn a MAC / rule (before
                           the hit pass: a superset of what it inserts), out with LAST */
 #define TXG_PEARLY 20u /* EARLY of every tile up to and including this one */
 static_assert(TXG_CIN + 6 <= TXA_GRANULES, "aux granules");
@@ -1804,22 +1804,47 @@ __device__ bool tx_lookback(const TxArgs &t, uint32_t tile, uint32_t *ins_out, u
   return ok;
 }
 
-/* The OR of EARLY over tiles [0, tile), the same way as tx_lookback (EARLY
- * goes out long before INS: a tile whose predecessors flag nothing to learn
- * need not wait for their claims). */
+/* The OR of EARLY over tiles [0, tile) (EARLY goes out long before INS: a
+ * tile whose predecessors flag nothing to learn need not wait for their
+ * claims).  The last TX_LOOKBACK tiles' EARLY words are packed (TxArgs::
+ * early), four per 16-byte agent-scope load, so the look-back of a tile deep
+ * in an 8-ring grid is one load per thread instead of four loads of one line
+ * each (round 5: 2048 lines per tile); the tiles below are covered by the
+ * PEARLY prefix granule of tile tile - TX_LOOKBACK - 1. */
 __device__ bool tx_lookback_early(const TxArgs &t, uint32_t tile, uint32_t *early_out) {
   const uint32_t tid = threadIdx.x;
+  const int below = (int)tile - 1 - (int)TX_LOOKBACK;   // the prefix of [0, below]
+  const uint32_t lo = below >= 0 ? (uint32_t)below + 1u : 0u;   // words of [lo, tile)
   uint32_t e = 0;
   bool ok = true;
+  for (uint32_t g = (lo >> 2) + tid; (g << 2) < tile && ok; g += NTHREADS) {
+    uint64_t t0 = 0;
+    for (uint32_t it = 0;; ++it) {
+      v4u32 v;
+      asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)"
+                   : "=v"(v) : "v"(t.early + 4u * g) : "memory");
+      bool all = true;
+      uint32_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < TX_LB_PER_THREAD; ++k) {
-    const int u = (int)tile - 1 - (int)tid - k * (int)NTHREADS;
-    if (u < 0 || !ok) continue;
-    uint32_t v[1];
-    ok = g_getn<1>(t.aux + (size_t)u * TXA_GRANULES + TXG_EARLY, t, v);
-    if (ok) e |= v[0];
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t u = 4u * g + j, w = v[j];
+        if (u < lo || u >= tile) continue;
+        all &= (w >> 16) == t.epoch;
+        acc |= w & 3u;
+      }
+      if (all) { e |= acc; break; }
+      if (tx_timed_out(t)) { ok = false; break; }
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (it == 0) {
+        t0 = now;
+      } else if (now - t0 > TX_SPIN_TICKS) {
+        atomicMax(t.counters + 3, t.epoch);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
   }
-  const int below = (int)tile - 1 - (int)TX_LOOKBACK;
   if (ok && tid == 0 && below >= 0) {
     uint32_t v[1];
     ok = g_getn<1>(t.aux + (size_t)below * TXA_GRANULES + TXG_PEARLY, t, v);
@@ -2129,7 +2154,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     const uint32_t lt = s_last;
     g_put4(aux + TXG_LREC, t.epoch, lt ? srec[lt - 1] : make_uint4(0, 0, 0, 0));
     g_put(aux + TXG_LAST, t.epoch, lt);
-    g_put(aux + TXG_EARLY, t.epoch, s_early);
+    __hip_atomic_store((gu32 *)(t.early + tile), (t.epoch << 16) | s_early, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);   // EARLY, packed (tx_lookback_early)
   }
   STAMP(3);
   // ---- cache hits (endpoint.rs:186-191); what a frame really learns is

@@ -2495,8 +2495,9 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bo
   if (ntiles > T.aux_tiles) {   // zeroed: no flag holds an epoch yet
     if (T.aux) HIPCHK(hipFree(T.aux));
     T.aux = nullptr;
-    HIPCHK(hipMalloc(&T.aux, (size_t)ntiles * usn::TXA_WORDS_BYTES));
-    HIPCHK(hipMemset(T.aux, 0, (size_t)ntiles * usn::TXA_WORDS_BYTES));
+    // granules, then the packed EARLY words (TxArgs::early)
+    HIPCHK(hipMalloc(&T.aux, (size_t)ntiles * usn::TXA_TILE_BYTES));
+    HIPCHK(hipMemset(T.aux, 0, (size_t)ntiles * usn::TXA_TILE_BYTES));
     T.aux_tiles = ntiles;
   }
   if (!X.counters) {
@@ -2517,7 +2518,7 @@ static int tx_prepare(Replica &T, uint64_t n, uint32_t ntiles, uint32_t slot, bo
   if (clear) {
     HIPCHK(hipMemset(T.macset, 0, (size_t)T.set_slots * 2 * 8));
     HIPCHK(hipMemset(T.ruleset, 0, (size_t)T.set_slots * 4 * 8));
-    HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_WORDS_BYTES));   // epoch-tagged flags
+    HIPCHK(hipMemset(T.aux, 0, (size_t)T.aux_tiles * usn::TXA_TILE_BYTES));   // epoch-tagged flags
     // the slots' timeout marks (counters[3]: the epoch of a batch whose waits
     // timed out) hold epochs of the cycle that ends here (the device drained)
     for (auto &x : T.txs)
@@ -2724,6 +2725,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     st = tx_listen(R, tb.src_endpoint, c->eps[tb.src_endpoint], t.n_listen);
     if (st) return st;
     t.aux = R.aux;
+    t.early = reinterpret_cast<uint32_t *>(R.aux + (size_t)R.aux_tiles * TXA_GRANULES);
     t.macset = R.macset;
     t.ruleset = R.ruleset;
     t.macset_mask = t.ruleset_mask = R.set_slots - 1;

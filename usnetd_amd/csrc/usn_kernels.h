@@ -106,6 +106,8 @@ struct TxArgs {
   uint32_t tile_base[USN_TX_RINGS + 1];
   uint32_t rings;
   unsigned long long *aux;    /* per tile x TXA_GRANULES {epoch, value}: what crosses a tile boundary */
+  uint32_t *early;            /* per tile: epoch << 16 | EARLY, packed (the EARLY look-back reads
+                                 four tiles per 16-byte load; granules would take one line each) */
   unsigned long long *macset; /* slots x 2: {epoch<<48 | mac, epoch<<32 | ~first} */
   unsigned long long *ruleset;/* slots x 4: {epoch<<48 | fp48, epoch<<32 | ~first, key xy, key zw} */
   uint32_t macset_mask, ruleset_mask;
@@ -127,6 +129,7 @@ struct TxArgs {
 
 #define TXA_GRANULES 24u       /* aux granules (8 bytes) per tile */
 constexpr size_t TXA_WORDS_BYTES = TXA_GRANULES * 8;
+constexpr size_t TXA_TILE_BYTES = TXA_WORDS_BYTES + 4;   /* + the tile's packed EARLY word */
 static_assert(sizeof(TxArgs) <= 4096, "kernel argument block");
 static_assert(USN_TXC_WORDS <= 64, "tile 0's first wave zeroes the counters");
 hipError_t launch_tx(const TxArgs &t, hipStream_t stream);
