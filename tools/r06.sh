@@ -87,5 +87,16 @@ case $S in
     done
     BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06g)
+    # where an 8-ring tx grid's tile time goes now (stamps, the diagnostic
+    # build), and the kernels of the bench in rocprof
+    STAMP_ARGS="c4tx 1048576 8" bash tools/gpu.sh $S stamps || exit 1
+    mv gpurun_out/$S/stamps.log gpurun_out/$S/stamps_c4tx8.log
+    STAMP_ARGS="c4tx 1048576 1" bash tools/gpu.sh $S stamps || exit 1
+    mv gpurun_out/$S/stamps.log gpurun_out/$S/stamps_c4tx1.log
+    STAMP_ARGS="c5 8388608" bash tools/gpu.sh $S stamps || exit 1
+    mv gpurun_out/$S/stamps.log gpurun_out/$S/stamps_c5.log
+    bash tools/gpu.sh $S rocprof || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -27,22 +27,35 @@ TX_STEPS = [1, 2, 3, 4, 5, 6, 7, 10, 11]
 def main():
     cfgname = sys.argv[1] if len(sys.argv) > 1 else "c2"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+    rings = int(sys.argv[3]) if len(sys.argv) > 3 else 1   # c4tx: consecutive rings per grid
     path = os.path.join(ROOT, "build", "abl", os.environ.get("STAMPS_BUILD", "stamps"), "libusn.so")
     ctx = lib.Ctx(0, libpath=path)
     # tx: one ring replayed (steady state: its answer rules are learned by the first pass)
-    cfgs = [traffic.config(cfgname, n=n, seed=6 if cfgname == "c4tx" else 17 * k + 2)
-            for k in range(5)]
+    if cfgname == "c4tx":   # one ring's frames (seed 6) in 8 device buffers
+        cfgs = [traffic.config(cfgname, n=n, seed=6)] * 8
+    else:
+        cfgs = [traffic.config(cfgname, n=n, seed=17 * k + 2) for k in range(5)]
     traffic.install_ctx(ctx, cfgs[0])
     bs = [lib.DeviceBatch(ctx, c.frames, c.lens, c.src, stride=c.stride) for c in cfgs]
     rs = [lib.DeviceResult(ctx, n) for _ in cfgs]
     s = ctx.stream()
     tx = cfgname == "c4tx"
-    for i in range(40):
-        lib.check(ctx.L.usn_classify(ctx.h, C.byref(bs[i % 5].desc), C.byref(rs[i % 5].desc), s))
-        if tx:
-            ctx.finalize(bs[i % 5], rs[i % 5], s)
+    if rings > 1:   # c4tx: one grid of `rings` consecutive rings (one ring's frames in 5 buffers)
+        assert tx and rings <= 8
+        rs2 = [lib.DeviceResult(ctx, n) for _ in range(2 * rings)]
+        for i in range(12):
+            grp = [(i * rings + k) % 8 for k in range(rings)]
+            res = [rs2[(i % 2) * rings + k] for k in range(rings)]
+            ctx.classify_multi([bs[g] for g in grp], res, s)
+            for g, r in zip(grp, res):
+                ctx.finalize(bs[g], r, s)
+    else:
+        for i in range(40):
+            lib.check(ctx.L.usn_classify(ctx.h, C.byref(bs[i % 5].desc), C.byref(rs[i % 5].desc), s))
+            if tx:
+                ctx.finalize(bs[i % 5], rs[i % 5], s)
     ctx.sync(s)
-    ntiles = (n + 1023) // 1024
+    ntiles = rings * ((n + 1023) // 1024)
     buf = np.zeros(16384 * 16, np.uint64)
     # the build that ran: the 512-thread one (every config now) or the 256-thread
     # one (STAMPS512=0 forces it); the other's buffer is all zero
