@@ -1564,40 +1564,39 @@ __device__ __forceinline__ void key1_of(const uint4 &r0, uint32_t &x, uint32_t &
   meta = usn_key_meta(proto, USN_WANT_SRC | (has ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0u));
 }
 
-/* Exclusive prefix max, in tile-local frame order, of v[r] (frame r*256+tid).
- * Values are <= TILE.  Uses L.order as a u16 scratch row and L.scratch. */
+/* Exclusive prefix max, in tile-local frame order, of v[r] (frame
+ * r * NTHREADS + tid).  Each round's wave-inclusive max by DPP, the 16 wave
+ * totals through L.scratch, ONE barrier (which also publishes whatever the
+ * block wrote to LDS before the call), then each lane folds the totals of the
+ * waves before it.  (Round 5's version staged the values through L.order and
+ * took four barriers; two calls per tx tile.) */
 __device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t out[ROUNDS]) {
+  static_assert(ROUNDS * NWAVES <= 16, "L.scratch holds 16 wave totals");
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t inc[ROUNDS];
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) L.order[r * NTHREADS + tid] = (uint16_t)v[r];
-  __syncthreads();
-  const uint32_t p0 = tid * ROUNDS;                        // contiguous chunk of 4 frames
-  uint32_t e[ROUNDS], m = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) { e[k] = L.order[p0 + k]; m = max(m, e[k]); }
-  uint32_t inc = m;                                        // wave inclusive max scan (DPP)
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x111, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x112, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x114, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x118, 0xF, 0xF, true));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x142, 0xA, 0xF, false));
-  inc = max(inc, (uint32_t)__builtin_amdgcn_update_dpp(0u, inc, 0x143, 0xC, 0xF, false));
-  uint32_t exc = __shfl_up(inc, 1, 64);
-  if (lane == 0) exc = 0;
-  if (lane == 63) L.scratch[wave] = inc;
-  __syncthreads();
-  for (uint32_t w = 0; w < wave; ++w) exc = max(exc, L.scratch[w]);
-  uint32_t run = exc;
-#pragma unroll
-  for (uint32_t k = 0; k < ROUNDS; ++k) {
-    const uint32_t x = e[k];
-    L.order[p0 + k] = (uint16_t)run;
-    run = max(run, x);
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    uint32_t x = v[r];   // wave inclusive max scan (DPP row shifts, then row broadcasts)
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false));
+    inc[r] = x;
+    if (lane == 63) L.scratch[r * NWAVES + wave] = x;
   }
   __syncthreads();
+  uint32_t before = 0;   // every wave of the earlier rounds, then the earlier waves of round r
 #pragma unroll
-  for (uint32_t r = 0; r < ROUNDS; ++r) out[r] = L.order[r * NTHREADS + tid];
-  __syncthreads();
+  for (uint32_t r = 0; r < ROUNDS; ++r) {
+    uint32_t b = before;
+    for (uint32_t w = 0; w < wave; ++w) b = max(b, L.scratch[r * NWAVES + w]);
+    uint32_t exc = __shfl_up(inc[r], 1, 64);
+    if (lane == 0) exc = 0;
+    out[r] = max(b, exc);
+    for (uint32_t w = 0; w < NWAVES; ++w) before = max(before, L.scratch[r * NWAVES + w]);
+  }
 }
 
 #define TX_BRIDGE_LDS_SLOTS 2048u   /* bridge sets up to 16 KiB are staged in LDS */
