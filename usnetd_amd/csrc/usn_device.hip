@@ -628,15 +628,6 @@ __device__ __forceinline__ uint32_t dec_bin(uint32_t d, uint32_t n_ep) {
   return other ^ ((other ^ USN_DEC_EP(d)) & m);
 }
 
-/* threadIdx.x as a value of the point of use: an opaque copy, so that hipcc
- * does not hoist what is derived from it out of the classify kernel's tile
- * loop (classify_tpw) and keep it live, and spilled, across the loop */
-__device__ __forceinline__ uint32_t tid_now() {
-  uint32_t t = threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
 /* --------------------------------------------------------------------------- */
 /* LDS layout of a block                                                        */
 struct Lds {
@@ -688,7 +679,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
  * exclusive prefix, *total = block sum.  Uses scratch[0..4]. */
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch,
                                                     uint32_t *total) {
-  const uint32_t tid = tid_now(), lane = tid & 63, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t inc = wave_incl_scan(v, lane);
   if (lane == 63) scratch[wave] = inc;
   __syncthreads();
@@ -738,7 +729,7 @@ __device__ __forceinline__ uint64_t match_bin(uint32_t b, uint64_t valid, uint32
  * kernel. */
 __device__ __forceinline__ void tile_hist(const uint32_t bins[ROUNDS], uint32_t nt, uint32_t nbits,
                                           uint32_t *hist) {
-  const uint32_t tid = tid_now(), lane = tid & 63;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
     const uint32_t local = r * NTHREADS + tid;
@@ -761,10 +752,10 @@ __device__ __forceinline__ uint32_t hist_get(const uint32_t *hist, uint32_t b) {
 __device__ __forceinline__ void hist_out(const uint32_t *hist, uint32_t nbw, uint16_t *row) {
   const uint4 *h = reinterpret_cast<const uint4 *>(hist);
   uint4 *w = reinterpret_cast<uint4 *>(row);
-  for (uint32_t i = tid_now(); i < nbw / 8; i += NTHREADS) w[i] = h[i];
+  for (uint32_t i = threadIdx.x; i < nbw / 8; i += NTHREADS) w[i] = h[i];
 }
 __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw) {
-  for (uint32_t i = tid_now(); i < nbw / 2; i += NTHREADS) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < nbw / 2; i += NTHREADS) hist[i] = 0;
 }
 
 /* --------------------------------------------------------------------------- */
@@ -773,7 +764,7 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t nbw) {
  * batch (its tiles are scanned in parallel), or that batch's own carried-in
  * state when none of its frames touched the cache.  out[0..5] in LDS. */
 __device__ __forceinline__ void resolve_carry(const ClassifyArgs &a, uint32_t *out, uint32_t *scratch) {
-  const uint32_t tid = tid_now(), lane = tid & 63;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const bool chain = a.carry_mode == CARRY_CHAIN && !(a.prev_summary->flags & USN_S_COUT);
   uint32_t best = 0;   // 1 + index of the last previous tile with a touching frame
   if (chain) {
@@ -957,37 +948,14 @@ __device__ __forceinline__ uint32_t batch_of(const MultiArgs &m, uint32_t w) {
   return bi;
 }
 
-/* Tiles per workgroup of the classify kernel with LDS displacements and a
- * global image (TM_DISPLDS: c4, c5).  A workgroup takes tiles 2b and 2b + 1:
- * the displacement copy and the workgroup's dispatch serve two tiles, and
- * the second tile's lengths and first header round are loaded while the
- * first tile finishes (its stores, histogram and count row).  The hardware
- * still deals the pairs to CUs dynamically (the persistent grids of rounds 2
- * and 4, below, dealt tiles statically). */
-#ifndef USN_TPW
-#define USN_TPW 2u
-#endif
-template <int TM, bool GLDS>
-__host__ __device__ constexpr uint32_t classify_tpw() {
-  return (TM == TM_DISPLDS && GLDS && ROUNDS == 2 && GD == 1) ? USN_TPW : 1u;
-}
-
-/* an LDS-only workgroup barrier: global loads in flight stay in flight */
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 /* The 1024-frame tiles of a launch (several batches = drained rx rings may
- * share one launch), one workgroup each (classify_tpw: two).  (A persistent grid looping over
+ * share one launch), one workgroup each.  (A persistent grid looping over
  * tiles, copying the displacements once per workgroup, was slower in rounds
  * 2 and 4: c5 8M 185.5 vs 170.5 us, profiles/r02ah; with the next tile's
  * headers prefetched 175.4 vs 159.1, profiles/r04/r04ao.  Both rounds' header
  * DMA at the workgroup's start was a wash, r04l.) */
 template <int TM, bool GLDS>
-__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(NTHREADS == 512 ? 8 : 1)))
-void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 threads per CU)
+__global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
   // global-image probes: the next round's header DMA goes out after this
   // round's slot loads (USN_LATE_DMA=0: right after this round's stage reads)
   constexpr bool LATE_DMA = GLDS && TM != TM_LDS && USN_LATE_DMA;
@@ -998,8 +966,8 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
   __shared__ uint4 s_stage[GLDS ? NWAVES * WSTAGE : 1];
   __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] last touching frame + 1, [1] host-list fill, [3..5] NIC/FLOOD/DROP
-  const uint32_t tid_k = threadIdx.x, lane_k = tid_k & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid_k >> 6);
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // bins and table are shared by the batches.  GLDS: the order row and the
   // radix keys live in the header stage (carve)
   const Lds L = carve(smem, m.b[0].nbins, GLDS ? s_stage : nullptr);
@@ -1013,27 +981,15 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
     const uint32_t uend = um ? m.b[0].u_end_unit : m.b[0].table_units;
     const uint32_t units = uend - u0;
     for (uint32_t c = wave; c * 64 < units; c += NWAVES) {
-      const uint32_t sl = u0 + min(c * 64 + lane_k, units - 1);
+      const uint32_t sl = u0 + min(c * 64 + lane, units - 1);
       __builtin_amdgcn_global_load_lds(m.b[0].table + sl, (lds_void_t *)(L.table + c * 64), 16, 0, 0);
     }
     if (TM == TM_LDS) T = L.table;
     else Dl = reinterpret_cast<const uint16_t *>(L.table) - (size_t)u0 * 8;
   }
   // (the tile's first barrier also waits for the image copy)
-  constexpr uint32_t TPW = classify_tpw<TM, GLDS>();
-  const uint32_t all_tiles = m.tile_base[m.count];
-  uint32_t len[ROUNDS];
-  bool pre = false;   // this tile's lengths and round 0's headers are in flight already (uniform)
-#pragma unroll 1
-  for (uint32_t kt = 0; kt < TPW; ++kt) {
-    const uint32_t w = blockIdx.x * TPW + kt;
-    if (w >= all_tiles) break;
-    // the thread's ids as values of this iteration: otherwise hipcc hoists
-    // every lane-derived address and mask out of the loop, and keeping them
-    // live across it spilled (64 VGPRs + 44 bytes of scratch per lane)
-    uint32_t tid = tid_k, lane = lane_k;
-    if (TPW > 1) asm volatile("" : "+v"(tid), "+v"(lane));
-    if (kt) lds_barrier();   // the previous tile's reads of the histogram and s_misc are done
+  {
+    const uint32_t w = blockIdx.x;
     uint4 *const st1 = st;   // round 1's stage: round 0's, once its reads are done
     const uint32_t bi = batch_of(m, w);
     const ClassifyArgs &a = m.b[bi];
@@ -1047,6 +1003,7 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
     //      Unpredicated at a clamped index: a load under `local < nt` made the
     //      compiler wait for each before issuing the next; lanes past nt are
     //      masked at use.
+    uint32_t len[ROUNDS];
     const uint8_t *fp[ROUNDS];
     if (!GLDS && a.offsets) {   // uniform; GLDS launches have no offsets array
 #pragma unroll
@@ -1060,18 +1017,13 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
         fp[r] = tf + (GLDS ? (size_t)__umul24(i, a.stride) : (size_t)i * a.stride);
       }
     }
-    if (!pre) {
 #pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
-    }
+    for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = a.lens[base + min(r * NTHREADS + tid, nt - 1)];
     uint4 q[ROUNDS][4];
     if (GLDS) {
-      if (!pre) {
 #pragma unroll
-        for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
-          glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
-      }
-      pre = false;
+      for (uint32_t r = 0; r < GD && r < ROUNDS; ++r)
+        glds_round(a, base, nt, r, wave, lane, st + r * STAGE_ROUND_SLOTS);
     } else {
       lane_round(fp[0], q[0]);
     }
@@ -1341,19 +1293,6 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
         differs |= 1u << r;        // later fragments also stop the device prefix
     }
     STAMP(5);
-    // ---- the workgroup's next tile (classify_tpw): its lengths and round 0's
-    //      headers go out now, after every load this tile waited for, and land
-    //      while this tile stores its decisions, counts and writes its row
-    if (TPW > 1 && kt + 1 < TPW && w + 1 < all_tiles) {
-      const uint32_t wn = w + 1, bn = batch_of(m, wn);
-      const ClassifyArgs &an = m.b[bn];
-      const uint64_t basen = (uint64_t)(wn - m.tile_base[bn]) * TILE;
-      const uint32_t ntn = (uint32_t)min((uint64_t)TILE, an.n - basen);
-#pragma unroll
-      for (uint32_t r = 0; r < ROUNDS; ++r) len[r] = an.lens[basen + min(r * NTHREADS + tid, ntn - 1)];
-      glds_round(an, basen, ntn, 0, wave, lane, st);
-      pre = true;
-    }
 
     // ---- stale carried cache: frames before the first break take the cached
     //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
@@ -1414,10 +1353,9 @@ void classify_rx_kernel(MultiArgs m) {   // (8 waves per SIMD: 4 tiles of 512 th
     }
 
     STAMP(6);
-    // ---- the tile's frames per bin: LDS histogram, then its count row (an
-    //      LDS-only barrier: the next tile's prefetched loads stay in flight)
+    // ---- the tile's frames per bin: LDS histogram, then its count row
     tile_hist(bins, nt, a.nbits, L.hist);
-    lds_barrier();
+    __syncthreads();
     STAMP(10);
     hist_out(L.hist, a.nbw, a.cnt + (size_t)tile * a.nbw);
 
@@ -2678,10 +2616,8 @@ hipError_t launch_classify(const MultiArgs &m, hipStream_t stream) {
                      (tm == TM_LDS ? table_lds_bytes(a.table_units)
                       : tm == TM_DISPLDS ? table_lds_bytes(disp_lds_units(a)) : 0);
   const dim3 b(NTHREADS);
-#define USN_LAUNCH(T_, G_)                                                                     \
-  hipLaunchKernelGGL((classify_rx_kernel<T_, G_>),                                             \
-                     dim3((tiles + classify_tpw<T_, G_>() - 1) / classify_tpw<T_, G_>()), b, lds, \
-                     stream, m)
+#define USN_LAUNCH(T_, G_) \
+  hipLaunchKernelGGL((classify_rx_kernel<T_, G_>), dim3(tiles), b, lds, stream, m)
   if (tm == TM_LDS) { if (glds) USN_LAUNCH(TM_LDS, true); else USN_LAUNCH(TM_LDS, false); }
   else if (tm == TM_DISPLDS) { if (glds) USN_LAUNCH(TM_DISPLDS, true); else USN_LAUNCH(TM_DISPLDS, false); }
   else { if (glds) USN_LAUNCH(TM_GLOBAL, true); else USN_LAUNCH(TM_GLOBAL, false); }
