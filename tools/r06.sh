@@ -99,9 +99,14 @@ case $S in
     bash tools/gpu.sh $S rocprof || exit 1
     ;;
   r06h)
-    # tile_prefix_max with one barrier (two calls per tx tile): the tx and
-    # parity tests, then the tx grid against HEAD~ (build/abl/r06prev)
-    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py tests/test_gpu_group.py" bash tools/gpu.sh $S tests || exit 1
+    # tile_prefix_max with one barrier (two calls per tx tile) and the rx
+    # classify at two tiles per workgroup (TM_DISPLDS, the second tile's loads
+    # prefetched): the suite; c5 / c4 against one tile per workgroup
+    # (build/abl/tpw1, same tree); the tx grid against HEAD~ (build/abl/r06prev)
+    bash tools/gpu.sh $S tests || exit 1
+    V="product tpw1"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     for v in new r06prev new r06prev new r06prev; do
       L=""; [ $v != new ] && L=build/abl/$v/libusn.so
       TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
