@@ -113,5 +113,15 @@ case $S in
       mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
     done
     ;;
+  r06i)
+    # tx: tile - 1's LAST/LREC and HEAD granules loaded ahead of the walk back
+    # and the HEAD walk: tx tests, then the tx grid against HEAD~ (build/abl/r06prev)
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py" bash tools/gpu.sh $S tests || exit 1
+    for v in new r06prev new r06prev new r06prev; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -2156,6 +2156,15 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     __hip_atomic_store((gu32 *)(t.early + tile), (t.epoch << 16) | s_early, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);   // EARLY, packed (tx_lookback_early)
   }
+  // tid 0: tile - 1's LAST and LREC granules read now, under the hit pass
+  // (the walk back below takes them when they carry the epoch, else polls)
+  unsigned long long pl[5] = {0, 0, 0, 0, 0};
+  if (tid == 0 && tile > 0) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      pl[k] = __hip_atomic_load((gu64 *)(t.aux + (size_t)(tile - 1) * TXA_GRANULES + TXG_LAST + k),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   STAMP(3);
   // ---- cache hits (endpoint.rs:186-191); what a frame really learns is
   //      claimed in the epoch-tagged sets with its index (first occurrence wins).
@@ -2238,7 +2247,13 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     uint4 brec = make_uint4(0, 0, 0, 0);
     for (int u = (int)tile - 1; u >= 0; --u) {
       uint32_t v[5];   // LAST, LREC
-      if (!g_getn<5>(t.aux + (size_t)u * TXA_GRANULES + TXG_LAST, t, v)) break;
+      bool pre = u == (int)tile - 1;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        v[k] = (uint32_t)pl[k];
+        pre &= (uint32_t)(pl[k] >> 32) == t.epoch;
+      }
+      if (!pre && !g_getn<5>(t.aux + (size_t)u * TXA_GRANULES + TXG_LAST, t, v)) break;
       const uint32_t lu = min(v[0], (uint32_t)TILE);
       if (lu) {
         before = (uint32_t)u * TILE + lu;
@@ -2284,6 +2299,11 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   //      flagged anything to learn (EARLY, out with LAST), no earlier tile
   //      claims: only the nearest tiles' HEAD is waited for.  Otherwise, or
   //      when the head is further back, every earlier tile's INS (tx_lookback).
+  // tid 0: tile - 1's HEAD read now, under the EARLY look-back
+  unsigned long long ph = 0;
+  if (tid == 0 && tile > 0)
+    ph = __hip_atomic_load((gu64 *)(t.aux + (size_t)(tile - 1) * TXA_GRANULES + TXG_HEAD),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   tx_lookback_early(t, tile, &s_early_all);
   __syncthreads();
   if (tid == 0) {
@@ -2292,8 +2312,9 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       uint32_t hx = 0;
       int u = (int)tile - 1;
       for (int steps = 0; u >= 0 && steps < 8; --u, ++steps) {
-        uint32_t v[1];
-        if (!g_getn<1>(t.aux + (size_t)u * TXA_GRANULES + TXG_HEAD, t, v)) break;
+        uint32_t v[1] = {(uint32_t)ph};
+        const bool pre = steps == 0 && (uint32_t)(ph >> 32) == t.epoch;
+        if (!pre && !g_getn<1>(t.aux + (size_t)u * TXA_GRANULES + TXG_HEAD, t, v)) break;
         const uint32_t h = min(v[0], (uint32_t)TILE);
         if (h) { hx = (uint32_t)u * TILE + h; break; }
       }
