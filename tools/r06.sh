@@ -134,5 +134,16 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py gpurun_out/$S/txpmcf gpurun_out/$S/txpmcw 8388608 gpurun_out/$S/pmc_c4tx.json tx_kernel=1+33 > gpurun_out/$S/pmct_c4tx.log 2>&1
     ;;
+  r06k)
+    # tx: the probes' slot reads waited for after the records and the prefix
+    # max (LDS-only barriers), keys recomputed from the records: tx and
+    # parity tests, then the tx grid against HEAD~ (build/abl/r06prev)
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py tests/test_gpu_group.py tests/test_gpu_window.py" bash tools/gpu.sh $S tests || exit 1
+    for v in new r06prev new r06prev new r06prev; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
