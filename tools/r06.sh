@@ -145,5 +145,16 @@ case $S in
       mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
     done
     ;;
+  r06l)
+    # r06k's A/B built r06prev from the same commit (identical ISA): the
+    # order of the runs, not the code, measured?  reversed order plus a
+    # byte copy of the product library at another path
+    mkdir -p build/abl/copy && cp usnetd_amd/libusn.so build/abl/copy/libusn.so
+    for v in r06prev new r06prev new copy new copy; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
