@@ -435,23 +435,6 @@ __device__ __forceinline__ void ph_disp_issue(const uint4 *T, const ClassifyArgs
 /* The slot reads of N keys whose displacements were read (ph_disp_issue;
  * keys [0, N1) in K1, the rest in K2), then the hits. */
 template <bool IN_LDS, int N, int N1>
-__device__ __forceinline__ void ph_slots_issue(const uint4 *T, const ClassifyArgs &a,
-                                               const PhKeyH (&k)[N], const uint32_t (&d)[N],
-                                               const bool (&on)[N], uint4 (&sl)[N]) {
-  typedef __attribute__((address_space(3))) const v4u32 lds_v4;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const usn_ph_table &t = a.ph[i < N1 ? 0 : 1];
-    const uint32_t si = t.slot_off + (on[i] ? k[i].sbase + usn_ph_slot(k[i].h2, d[i], t.m) : 0u);
-    if (IN_LDS) {
-      const v4u32 v = ((lds_v4 *)T)[si];
-      sl[i] = make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-      sl[i] = T[si];
-    }
-  }
-}
-template <bool IN_LDS, int N, int N1>
 __device__ __forceinline__ void ph_slots_hit(const uint4 *T, const ClassifyArgs &a,
                                              const uint32_t (&x)[N], const uint32_t (&y)[N],
                                              const uint32_t (&z)[N], const uint32_t (&m)[N],
@@ -1581,14 +1564,6 @@ __device__ __forceinline__ void key1_of(const uint4 &r0, uint32_t &x, uint32_t &
   meta = usn_key_meta(proto, USN_WANT_SRC | (has ? (USN_WANT_DPORT | USN_WANT_SPORT) : 0u));
 }
 
-/* an LDS-only workgroup barrier: global loads in flight stay in flight
- * (__syncthreads() waits for every vector memory operation first) */
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 /* Exclusive prefix max, in tile-local frame order, of v[r] (frame
  * r * NTHREADS + tid).  Each round's wave-inclusive max by DPP, the 16 wave
  * totals through L.scratch, ONE barrier (which also publishes whatever the
@@ -1611,7 +1586,7 @@ __device__ void tile_prefix_max(const uint32_t v[ROUNDS], const Lds &L, uint32_t
     inc[r] = x;
     if (lane == 63) L.scratch[r * NWAVES + wave] = x;
   }
-  lds_barrier();   // (global loads in flight stay in flight)
+  __syncthreads();
   uint32_t before = 0;   // every wave of the earlier rounds, then the earlier waves of round r
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -2139,25 +2114,27 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
       }
     }
   }
-  // the probes' slot reads go out now; they are waited for after the
-  // records and the prefix max below, which need only the parse (round 5
-  // waited for every wave's slots at the records barrier first)
-  uint4 sl[R3];
-  if (USN_TX_PIPE) {
-    ph_slots_issue<LDS, R3, 2 * ROUNDS>(T, a, pk, pd, pon, sl);
-  } else {
+  uint32_t w1e[ROUNDS], w2e[ROUNDS];   // key1 / key2 results, valid where need[R + r]
+  bool pre[ROUNDS];
+  {
+    uint32_t w[R3];
+    if (USN_TX_PIPE) ph_slots_hit<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, pk, pd, pon, w);
+    else ph_probe_many<LDS, R3, 2 * ROUNDS>(T, a, ax, ay, az, am, need, w);
 #pragma unroll
-    for (int k = 0; k < R3; ++k)
-      ph_disp_issue<LDS>(T, a, k < 2 * ROUNDS ? 0 : 1, ax[k], ay[k], az[k], am[k], need[k], pk[k], pd[k], pon[k]);
-    ph_slots_issue<LDS, R3, 2 * ROUNDS>(T, a, pk, pd, pon, sl);
+    for (uint32_t r = 0; r < ROUNDS; ++r) {
+      if (need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
+      pre[r] = need[ROUNDS + r];
+      w1e[r] = w[ROUNDS + r];
+      w2e[r] = w[2 * ROUNDS + r];
+    }
   }
 
   STAMP(2);
   // every wave is done with its header scratch before the records overwrite it
-  lds_barrier();
-  // ---- the tile's records in LDS (the answer-key learn flag is not in them:
-  //      what reads them -- the hit pass, LREC -- does not use it); each
-  //      frame's previous touching frame
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  // ---- the tile's records in LDS; each frame's previous touching frame
   uint32_t vt[ROUNDS], prev[ROUNDS];
 #pragma unroll
   for (uint32_t r = 0; r < ROUNDS; ++r) {
@@ -2165,40 +2142,19 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     if (local >= nt) rec[r] = make_uint4(0, 0, 0, 0);
     srec[local] = rec[r];
     vt[r] = (local < nt && tx_touch(rec[r])) ? local + 1 : 0u;
+    if (local < nt && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE)))
+      atomicOr(&s_early, ((rec[r].x & TXR_LEARNMAC) ? 1u : 0u) | ((rec[r].x & TXR_LEARNRULE) ? 2u : 0u));
   }
+  // (publishing LAST before the probes instead: 52.9 -> 61 us per 1M frames,
+  // the probes' compiler-placed vmcnt(0) then also waits for the sc1 stores)
   if (last) atomicMax(&s_last, last);
-  tile_prefix_max(vt, L, prev);   // its (LDS-only) barrier also publishes srec and s_last
-  uint32_t w1e[ROUNDS], w2e[ROUNDS];   // key1 / key2 results, valid where need[R + r]
-  bool pre[ROUNDS];
-  {
-    // the keys again from the records (cheaper than keeping 24 registers of
-    // keys live across the prefix max): answer key, key1, key2 of each round
-    uint32_t w[R3];
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      uint32_t x, y, z, mt;
-      want_key(rec[r], x, y, z, mt);
-      w[r] = pon[r] ? ph_hit(sl[r], x, y, z, mt) : 0u;
-      key1_of(rec[r], x, y, z, mt);
-      w[ROUNDS + r] = pon[ROUNDS + r] ? ph_hit(sl[ROUNDS + r], x, y, z, mt) : 0u;
-      key2_of(rec[r], x, y, z, mt);
-      w[2 * ROUNDS + r] = pon[2 * ROUNDS + r] ? ph_hit(sl[2 * ROUNDS + r], x, y, z, mt) : 0u;
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < ROUNDS; ++r) {
-      const uint32_t local = r * NTHREADS + tid;
-      if (local < nt && need[r] && !w[r]) rec[r].x |= TXR_LEARNRULE;
-      pre[r] = need[ROUNDS + r];
-      w1e[r] = w[ROUNDS + r];
-      w2e[r] = w[2 * ROUNDS + r];
-      if (local < nt && (rec[r].x & (TXR_LEARNMAC | TXR_LEARNRULE)))
-        atomicOr(&s_early, ((rec[r].x & TXR_LEARNMAC) ? 1u : 0u) | ((rec[r].x & TXR_LEARNRULE) ? 2u : 0u));
-    }
-  }
+  tile_prefix_max(vt, L, prev);   // its barriers also publish srec, s_last and s_early
   if (tid == 0) {
     const uint32_t lt = s_last;
     g_put4(aux + TXG_LREC, t.epoch, lt ? srec[lt - 1] : make_uint4(0, 0, 0, 0));
     g_put(aux + TXG_LAST, t.epoch, lt);
+    __hip_atomic_store((gu32 *)(t.early + tile), (t.epoch << 16) | s_early, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);   // EARLY, packed (tx_lookback_early)
   }
   // tid 0: tile - 1's LAST and LREC granules read now, under the hit pass
   // (the walk back below takes them when they carry the epoch, else polls)
@@ -2278,12 +2234,10 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (last_nh) atomicMax(&s_lastnh, last_nh);
   if (ins) atomicOr(&s_ins, ins);
   vm_drain();                  // this wave's claims (atomics, sc1 stores) have landed
-  __syncthreads();             // (and every frame has read srec, and s_early is complete)
+  __syncthreads();             // (and every frame has read srec)
   // HEAD and INS now unless the first touching frame can change them
   const bool early_pub = s_lastnh != 0 && s_dlearn == 0;
   if (tid == 0) {
-    __hip_atomic_store((gu32 *)(t.early + tile), (t.epoch << 16) | s_early, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);   // EARLY, packed (tx_lookback_early)
     if (early_pub) {   // INS last: its arrival also says the claims above have landed (R1)
       g_put(aux + TXG_HEAD, t.epoch, s_lastnh);
       g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
