@@ -156,5 +156,17 @@ case $S in
       mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
     done
     ;;
+  r06m)
+    # wave priority A/Bs (s_setprio, USN_AB_TXPRIO / USN_AB_RXPRIO builds of
+    # tools/abl_flags.sh; build/abl/base = the same flags-free build): the tx
+    # grid per variant, twice; c5 / c2 classify calls interleaved in one process
+    for v in base txp1 txp2 txp3 base txp1 txp2 txp3; do
+      TAILN=1 TXB_ARGS="1048576 24 1 build/abl/$v/libusn.so --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    V="base rxp1 rxp2"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -128,6 +128,17 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #endif
 static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
               "the ISA test's perturbation in a build without USN_AB_BUILD=1");
+/* wave priority A/Bs (s_setprio; results unchanged).  tx: 1 wave 0 (the
+ * tile's serial parts) high throughout, 2 a tile's waves rise as it moves
+ * through its phases (older tiles first), 3 high while the header loads
+ * issue.  rx: 1 high while the loads issue, 2 rising by phase. */
+#ifndef USN_AB_TXPRIO
+#define USN_AB_TXPRIO 0
+#endif
+#ifndef USN_AB_RXPRIO
+#define USN_AB_RXPRIO 0
+#endif
+#define USN_PRIO(cond, p) do { if (cond) __builtin_amdgcn_s_setprio(p); } while (0)
 
 /* 16-byte header load, default cache policy (the `nt` hint was slower on
  * these per-lane loads: c3 and the tx kernel, profiles/r02cp, r04/r04at) */
@@ -998,6 +1009,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
     STAMP_DECL
     STAMP(0);
+    USN_PRIO(USN_AB_RXPRIO == 1, 3);
 
     // ---- loads, oldest first: lengths, headers.
     //      Unpredicated at a clamped index: a load under `local < nt` made the
@@ -1028,6 +1040,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       lane_round(fp[0], q[0]);
     }
     STAMP(1);
+    USN_PRIO(USN_AB_RXPRIO == 1, 0);
     // ---- while they fly: zero the bin histogram (the barrier also waits
     //      for every load: table and round 0 are in LDS / registers after it)
     hist_zero(L.hist, a.nbw);
@@ -1056,6 +1069,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     }
     const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
     STAMP(3);
+    USN_PRIO(USN_AB_RXPRIO == 2, 1);
 
     // ---- parse + decide, the next round's headers in flight meanwhile
     uint32_t dec[ROUNDS], bins[ROUNDS];
@@ -1293,6 +1307,7 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
         differs |= 1u << r;        // later fragments also stop the device prefix
     }
     STAMP(5);
+    USN_PRIO(USN_AB_RXPRIO == 2, 2);
 
     // ---- stale carried cache: frames before the first break take the cached
     //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
@@ -1912,6 +1927,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   __syncthreads();
   STAMP_DECL
   STAMP(0);   // tickets out of step with the host: the waits time out
+  USN_PRIO(USN_AB_TXPRIO == 1 && wave == 0, 2);
+  USN_PRIO(USN_AB_TXPRIO == 3, 3);
   const uint64_t base = (uint64_t)rt * TILE;      // the tile's first frame in its ring
   const uint32_t vbase = tile * TILE;             // ... in the launch
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
@@ -1997,6 +2014,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     }
     qq[r][3] = make_uint4(0, 0, 0, 0);
   }
+  USN_PRIO(USN_AB_TXPRIO == 3, 0);
   if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
   if (bridge_lds) {
     if (USN_TX_PIPE) {
@@ -2130,6 +2148,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   }
 
   STAMP(2);
+  USN_PRIO(USN_AB_TXPRIO == 2, 1);
   // every wave is done with its header scratch before the records overwrite it
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -2294,6 +2313,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
   }
   STAMP(4);
+  USN_PRIO(USN_AB_TXPRIO == 2, 2);
   // ---- phase 2: the sets as every earlier frame left them, and the last
   //      non-hit touching frame before the tile.  When no earlier tile
   //      flagged anything to learn (EARLY, out with LAST), no earlier tile
