@@ -168,5 +168,13 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ;;
+  r06n)
+    # r06m's best tx variant (txp3: high priority while the header loads
+    # issue) against base and two combinations, three times each
+    for v in base txp3 txp4 txp5 base txp3 txp4 txp5 base txp3 txp4 txp5; do
+      TAILN=1 TXB_ARGS="1048576 24 1 build/abl/$v/libusn.so --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -131,7 +131,7 @@ static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
 /* wave priority A/Bs (s_setprio; results unchanged).  tx: 1 wave 0 (the
  * tile's serial parts) high throughout, 2 a tile's waves rise as it moves
  * through its phases (older tiles first), 3 high while the header loads
- * issue.  rx: 1 high while the loads issue, 2 rising by phase. */
+ * issue, 4 = 3 then 2, 5 = 3 and the tile's phase 2 raised.  rx: 1 high while the loads issue, 2 rising by phase. */
 #ifndef USN_AB_TXPRIO
 #define USN_AB_TXPRIO 0
 #endif
@@ -1928,7 +1928,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   STAMP_DECL
   STAMP(0);   // tickets out of step with the host: the waits time out
   USN_PRIO(USN_AB_TXPRIO == 1 && wave == 0, 2);
-  USN_PRIO(USN_AB_TXPRIO == 3, 3);
+  USN_PRIO(USN_AB_TXPRIO >= 3, 3);
   const uint64_t base = (uint64_t)rt * TILE;      // the tile's first frame in its ring
   const uint32_t vbase = tile * TILE;             // ... in the launch
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
@@ -2014,7 +2014,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     }
     qq[r][3] = make_uint4(0, 0, 0, 0);
   }
-  USN_PRIO(USN_AB_TXPRIO == 3, 0);
+  USN_PRIO(USN_AB_TXPRIO >= 3, 0);
   if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
   if (bridge_lds) {
     if (USN_TX_PIPE) {
@@ -2148,7 +2148,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   }
 
   STAMP(2);
-  USN_PRIO(USN_AB_TXPRIO == 2, 1);
+  USN_PRIO(USN_AB_TXPRIO == 2 || USN_AB_TXPRIO == 4, 1);
   // every wave is done with its header scratch before the records overwrite it
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -2313,7 +2313,8 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
   }
   STAMP(4);
-  USN_PRIO(USN_AB_TXPRIO == 2, 2);
+  USN_PRIO(USN_AB_TXPRIO == 2 || USN_AB_TXPRIO == 4, 2);
+  USN_PRIO(USN_AB_TXPRIO == 5, 1);
   // ---- phase 2: the sets as every earlier frame left them, and the last
   //      non-hit touching frame before the tile.  When no earlier tile
   //      flagged anything to learn (EARLY, out with LAST), no earlier tile
