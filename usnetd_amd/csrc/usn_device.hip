@@ -128,12 +128,14 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #endif
 static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
               "the ISA test's perturbation in a build without USN_AB_BUILD=1");
-/* wave priority A/Bs (s_setprio; results unchanged).  tx: 1 wave 0 (the
- * tile's serial parts) high throughout, 2 a tile's waves rise as it moves
- * through its phases (older tiles first), 3 high while the header loads
- * issue, 4 = 3 then 2, 5 = 3 and the tile's phase 2 raised.  rx: 1 high while the loads issue, 2 rising by phase. */
+/* wave priority (s_setprio; results unchanged).  tx: 1 wave 0 (the tile's
+ * serial parts) high throughout, 2 a tile's waves rise as it moves through
+ * its phases (older tiles first), 3 high while the header loads issue, 4 = 3
+ * then 2, 5 (the product) = 3 and the tile's phase 2 raised: 8-ring grid
+ * 0.3177 -> 0.3115 ms (3 reps each, profiles/r06/r06m, r06n; 3 and 4 0.313).
+ * rx: 1 high while the loads issue, 2 rising by phase: no change (r06m). */
 #ifndef USN_AB_TXPRIO
-#define USN_AB_TXPRIO 0
+#define USN_AB_TXPRIO 5
 #endif
 #ifndef USN_AB_RXPRIO
 #define USN_AB_RXPRIO 0
