@@ -187,5 +187,18 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py gpurun_out/$S/txpmcf gpurun_out/$S/txpmcw 8388608 gpurun_out/$S/pmc_c4tx.json tx_kernel=1+33 > gpurun_out/$S/pmct_c4tx.log 2>&1
     ;;
+  r06p)
+    # tx priority 6 (phase 2 at 2) and the scatter's load-issue priority
+    # (USN_AB_SCPRIO) against base (= the product's priorities), tx grid
+    # three times each; rx calls of c5 / c2 / c3 interleaved in one process
+    for v in base txp6 scp1 base txp6 scp1 base txp6 scp1; do
+      TAILN=1 TXB_ARGS="1048576 24 1 build/abl/$v/libusn.so --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    V="base scp1"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

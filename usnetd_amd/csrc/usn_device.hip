@@ -140,6 +140,9 @@ static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
 #ifndef USN_AB_RXPRIO
 #define USN_AB_RXPRIO 0
 #endif
+#ifndef USN_AB_SCPRIO   /* scatter: 1 high while its count rows and decisions load */
+#define USN_AB_SCPRIO 0
+#endif
 #define USN_PRIO(cond, p) do { if (cond) __builtin_amdgcn_s_setprio(p); } while (0)
 
 /* 16-byte header load, default cache policy (the `nt` hint was slower on
@@ -2317,6 +2320,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   STAMP(4);
   USN_PRIO(USN_AB_TXPRIO == 2 || USN_AB_TXPRIO == 4, 2);
   USN_PRIO(USN_AB_TXPRIO == 5, 1);
+  USN_PRIO(USN_AB_TXPRIO == 6, 2);
   // ---- phase 2: the sets as every earlier frame left them, and the last
   //      non-hit touching frame before the tile.  When no earlier tile
   //      flagged anything to learn (EARLY, out with LAST), no earlier tile
@@ -2904,6 +2908,7 @@ void scatter_kernel(ScatterArgs s) {
   const uint64_t first = (uint64_t)t0 * TILE;                        // the chunk's first frame
   STAMP_DECL
   STAMP(0);
+  USN_PRIO(USN_AB_SCPRIO == 1, 3);
   const uint32_t *ex = B.agg + (size_t)c * s.nbw;             // frames of b in the chunks before
   // up to 1024 bins (a pair per thread): totals, chunk offsets and the
   // chunk's count rows are loaded first, then the decisions: waiting for the
@@ -2936,6 +2941,7 @@ void scatter_kernel(ScatterArgs s) {
   uint32_t d[SEGS];
 #pragma unroll
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
+  USN_PRIO(USN_AB_SCPRIO == 1, 0);
   // 1b. (small launches) the scan's two sums for this chunk from the batch's
   // count rows: thread (g, q) adds bins 8q..8q+7 (one 16-byte load) of tiles
   // g, g + G, ... into the totals and, for the tiles before the chunk, into
