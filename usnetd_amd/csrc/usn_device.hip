@@ -128,20 +128,15 @@ __device__ unsigned long long usn_stamp_buf[2 * 16384 * USN_NSTAMP];
 #endif
 static_assert(USN_AB_BUILD || !USN_ISA_PERTURB,
               "the ISA test's perturbation in a build without USN_AB_BUILD=1");
-/* wave priority (s_setprio; results unchanged).  tx: 1 wave 0 (the tile's
- * serial parts) high throughout, 2 a tile's waves rise as it moves through
- * its phases (older tiles first), 3 high while the header loads issue, 4 = 3
- * then 2, 5 (the product) = 3 and the tile's phase 2 raised: 8-ring grid
- * 0.3177 -> 0.3115 ms (3 reps each, profiles/r06/r06m, r06n; 3 and 4 0.313).
- * rx: 1 high while the loads issue, 2 rising by phase: no change (r06m). */
+/* tx wave priority (s_setprio; results unchanged): a tile's waves at the
+ * highest priority while they issue its header loads, then 0, and 1 from its
+ * phase 2 on.  8-ring grid 0.3177 -> 0.3115 ms (three runs each, one process
+ * per run, profiles/r06/r06m, r06n).  Measured and dropped:
+ * wave 0 alone raised, priority rising with every phase, phase 2 at 2, and
+ * the same ideas in the rx classify and the scatter (no change).
+ * USN_AB_TXPRIO=0 (tools/abl_flags.sh) builds the kernel without it. */
 #ifndef USN_AB_TXPRIO
-#define USN_AB_TXPRIO 5
-#endif
-#ifndef USN_AB_RXPRIO
-#define USN_AB_RXPRIO 0
-#endif
-#ifndef USN_AB_SCPRIO   /* scatter: 1 high while its count rows and decisions load */
-#define USN_AB_SCPRIO 0
+#define USN_AB_TXPRIO 1
 #endif
 #define USN_PRIO(cond, p) do { if (cond) __builtin_amdgcn_s_setprio(p); } while (0)
 
@@ -1014,7 +1009,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
     STAMP_DECL
     STAMP(0);
-    USN_PRIO(USN_AB_RXPRIO == 1, 3);
 
     // ---- loads, oldest first: lengths, headers.
     //      Unpredicated at a clamped index: a load under `local < nt` made the
@@ -1045,7 +1039,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
       lane_round(fp[0], q[0]);
     }
     STAMP(1);
-    USN_PRIO(USN_AB_RXPRIO == 1, 0);
     // ---- while they fly: zero the bin histogram (the barrier also waits
     //      for every load: table and round 0 are in LDS / registers after it)
     hist_zero(L.hist, a.nbw);
@@ -1074,7 +1067,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
     }
     const bool stale = tile == 0 && (s_carry[6] & USN_S_STALE);
     STAMP(3);
-    USN_PRIO(USN_AB_RXPRIO == 2, 1);
 
     // ---- parse + decide, the next round's headers in flight meanwhile
     uint32_t dec[ROUNDS], bins[ROUNDS];
@@ -1312,7 +1304,6 @@ __global__ __launch_bounds__(NTHREADS) void classify_rx_kernel(MultiArgs m) {
         differs |= 1u << r;        // later fragments also stop the device prefix
     }
     STAMP(5);
-    USN_PRIO(USN_AB_RXPRIO == 2, 2);
 
     // ---- stale carried cache: frames before the first break take the cached
     //      decision (endpoint.rs:186-191); only tile 0 is resolved here.
@@ -1932,8 +1923,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   __syncthreads();
   STAMP_DECL
   STAMP(0);   // tickets out of step with the host: the waits time out
-  USN_PRIO(USN_AB_TXPRIO == 1 && wave == 0, 2);
-  USN_PRIO(USN_AB_TXPRIO >= 3, 3);
+  USN_PRIO(USN_AB_TXPRIO, 3);   // while the tile's header loads issue
   const uint64_t base = (uint64_t)rt * TILE;      // the tile's first frame in its ring
   const uint32_t vbase = tile * TILE;             // ... in the launch
   const uint32_t nt = (uint32_t)min((uint64_t)TILE, a.n - base);
@@ -2019,7 +2009,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     }
     qq[r][3] = make_uint4(0, 0, 0, 0);
   }
-  USN_PRIO(USN_AB_TXPRIO >= 3, 0);
+  USN_PRIO(USN_AB_TXPRIO, 0);
   if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
   if (bridge_lds) {
     if (USN_TX_PIPE) {
@@ -2153,7 +2143,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   }
 
   STAMP(2);
-  USN_PRIO(USN_AB_TXPRIO == 2 || USN_AB_TXPRIO == 4, 1);
   // every wave is done with its header scratch before the records overwrite it
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -2318,9 +2307,7 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     g_put(aux + TXG_INS, t.epoch, s_ins | (s_ovf ? 4u : 0u));
   }
   STAMP(4);
-  USN_PRIO(USN_AB_TXPRIO == 2 || USN_AB_TXPRIO == 4, 2);
-  USN_PRIO(USN_AB_TXPRIO == 5, 1);
-  USN_PRIO(USN_AB_TXPRIO == 6, 2);
+  USN_PRIO(USN_AB_TXPRIO, 1);   // phase 2: ahead of the younger tiles' parse
   // ---- phase 2: the sets as every earlier frame left them, and the last
   //      non-hit touching frame before the tile.  When no earlier tile
   //      flagged anything to learn (EARLY, out with LAST), no earlier tile
@@ -2908,7 +2895,6 @@ void scatter_kernel(ScatterArgs s) {
   const uint64_t first = (uint64_t)t0 * TILE;                        // the chunk's first frame
   STAMP_DECL
   STAMP(0);
-  USN_PRIO(USN_AB_SCPRIO == 1, 3);
   const uint32_t *ex = B.agg + (size_t)c * s.nbw;             // frames of b in the chunks before
   // up to 1024 bins (a pair per thread): totals, chunk offsets and the
   // chunk's count rows are loaded first, then the decisions: waiting for the
@@ -2941,7 +2927,6 @@ void scatter_kernel(ScatterArgs s) {
   uint32_t d[SEGS];
 #pragma unroll
   for (uint32_t k = 0; k < SEGS; ++k) d[k] = B.decisions[tbase + min(k * 64 + lane, tn - 1)];
-  USN_PRIO(USN_AB_SCPRIO == 1, 0);
   // 1b. (small launches) the scan's two sums for this chunk from the batch's
   // count rows: thread (g, q) adds bins 8q..8q+7 (one 16-byte load) of tiles
   // g, g + G, ... into the totals and, for the tiles before the chunk, into
