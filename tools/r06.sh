@@ -200,5 +200,16 @@ case $S in
     ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     ;;
+  r06q)
+    # tx: the LDS state zeroed after the header loads issue (no full barrier
+    # ahead of them): tx and parity tests, then the tx grid against HEAD~
+    # (build/abl/r06prev), alternating, the previous build first
+    TESTS="tests/test_gpu_tx.py tests/test_gpu_parity.py tests/test_gpu_group.py tests/test_gpu_window.py" bash tools/gpu.sh $S tests || exit 1
+    for v in r06prev new r06prev new r06prev new r06prev new; do
+      L=""; [ $v != new ] && L=build/abl/$v/libusn.so
+      TAILN=1 TXB_ARGS="1048576 24 1 $L --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -1914,13 +1914,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   __shared__ uint32_t s_carry[8];
   __shared__ uint32_t s_misc[8];   // [0] 1+last touching, [1] host-list fill, [3..5] NIC/FLOOD/DROP
   __shared__ uint32_t s_listen[2 * TX_LISTEN_LDS];
-  if (tid == 0) {
-    s_last = 0; s_lastnh = 0; s_ins = 0; s_ovf = 0; s_insall = 0; s_hidx = 0; s_before = 0;
-    s_early = 0; s_early_all = 0; s_slow = 0; s_dlearn = 0;
-  }
-  if (tid < 8) s_misc[tid] = 0;
-  hist_zero(L.hist, a.nbw);
-  __syncthreads();
   STAMP_DECL
   STAMP(0);   // tickets out of step with the host: the waits time out
   USN_PRIO(USN_AB_TXPRIO, 3);   // while the tile's header loads issue
@@ -1932,23 +1925,6 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
   if (LDS) {
     for (uint32_t k = tid; k < a.table_units; k += NTHREADS) stab[k] = a.table[k];
     T = stab;
-  }
-  if (tile == 0) {   // carried-in cache of this source; counters for phase 2 (all wait for tile 0)
-    if (tid < USN_TXC_WORDS && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
-      __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    resolve_carry(a, s_carry, L.scratch);
-    if (tid == 0) {
-      for (int k = 0; k < 6; ++k) {
-        s_cin[k] = s_carry[k];
-        g_put(aux + TXG_CIN + k, t.epoch, s_carry[k]);
-      }
-      usn_summary *S = a.summary;
-      S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
-      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
-      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
-      S->n_ep = a.n_ep; S->n_bins = a.nbins;
-      S->flags = 0; S->first_break = 0xFFFFFFFFu;
-    }
   }
   /* the bridge snapshot set goes to LDS when small; its loads go out first
      (USN_TX_PIPE), so that its LDS copy and the barrier after it wait for
@@ -2010,6 +1986,33 @@ void tx_kernel(TxArgs t) {   // (4 workgroups per CU: 1024 tiles of 1M frames al
     qq[r][3] = make_uint4(0, 0, 0, 0);
   }
   USN_PRIO(USN_AB_TXPRIO, 0);
+  /* the LDS state's zeroing after the loads went out: the LDS barrier below
+     publishes it (a barrier before the loads held them for every wave) */
+  if (tid == 0) {
+    s_last = 0; s_lastnh = 0; s_ins = 0; s_ovf = 0; s_insall = 0; s_hidx = 0; s_before = 0;
+    s_early = 0; s_early_all = 0; s_slow = 0; s_dlearn = 0;
+  }
+  if (tid < 8) s_misc[tid] = 0;
+  hist_zero(L.hist, a.nbw);
+  // tile 0: the carried-in cache of this source; counters for phase 2 (all
+  // wait for tile 0; resolve_carry's barriers wait for its header loads)
+  if (tile == 0) {
+    if (tid < USN_TXC_WORDS && tid != 3)   // learned, flags, sets, host frames (3: the timeout epoch stays)
+      __hip_atomic_store((gu32 *)(t.counters + tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    resolve_carry(a, s_carry, L.scratch);
+    if (tid == 0) {
+      for (int k = 0; k < 6; ++k) {
+        s_cin[k] = s_carry[k];
+        g_put(aux + TXG_CIN + k, t.epoch, s_carry[k]);
+      }
+      usn_summary *S = a.summary;
+      S->cin_state = s_carry[0]; S->cin_dst = s_carry[1];
+      for (int k = 0; k < 4; ++k) S->cin_info[k] = s_carry[2 + k];
+      S->n_frames = (uint32_t)a.n; S->n_tiles = a.ntiles;
+      S->n_ep = a.n_ep; S->n_bins = a.nbins;
+      S->flags = 0; S->first_break = 0xFFFFFFFFu;
+    }
+  }
   if (listen_lds && tid < 2 * TX_LISTEN_LDS) s_listen[tid] = lv;
   if (bridge_lds) {
     if (USN_TX_PIPE) {
