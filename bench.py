@@ -105,6 +105,8 @@ def parse_args(argv=None):
                          "while round i is queued)")
     ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
+    ap.add_argument("--tx-launches", type=int, default=0,
+                    help="c4tx: timed multi-ring launches at least (default: the timed rings / --tx-rings)")
     ap.add_argument("--tx-rings", type=int, default=8, choices=range(1, 9),
                     help="c4tx: consecutive rings of the sending endpoint per tx launch (one grid)")
     ap.add_argument("--host-inclusive", default="c5,c2",
@@ -580,7 +582,7 @@ def measure_tx(ctx, args):
     # enqueued before launch j's rings are finalized
     P = args.tx_rings
     res2 = res + [lib.DeviceResult(ctx, n) for _ in range(2 * P - 2)]
-    K2 = -(-K // P)
+    K2 = max(-(-K // P), args.tx_launches)
     evs2 = [(ctx.event(), ctx.event()) for _ in range(K2)]
 
     # the loop's ctypes arguments built once (the loop times the library, not

@@ -211,5 +211,13 @@ case $S in
       mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
     done
     ;;
+  r06r)
+    # c4tx end to end: how much of the gap to the device rate is the timed
+    # loop's fill and drain (13 launches by default) -- 13, 50 and 100 launches
+    for L in 13 50 100 13 50 100; do
+      BENCH_ARGS="--steps 10 --warmup 2 --no-cpu-baseline --extras c4tx --host-inclusive= --tx-launches $L" bash tools/gpu.sh $S bench || exit 1
+      mv gpurun_out/$S/bench.log gpurun_out/$S/bench_tx${L}_$RANDOM.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
