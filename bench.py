@@ -105,8 +105,8 @@ def parse_args(argv=None):
                          "while round i is queued)")
     ap.add_argument("--rotate-mib", type=int, default=ROTATE_BYTES >> 20,
                     help="distinct batch bytes per rank (default 1024: past the 256 MiB Infinity Cache)")
-    ap.add_argument("--tx-launches", type=int, default=0,
-                    help="c4tx: timed multi-ring launches at least (default: the timed rings / --tx-rings)")
+    ap.add_argument("--tx-launches", type=int, default=TX_LAUNCHES,
+                    help="c4tx: timed multi-ring launches at least")
     ap.add_argument("--tx-rings", type=int, default=8, choices=range(1, 9),
                     help="c4tx: consecutive rings of the sending endpoint per tx launch (one grid)")
     ap.add_argument("--host-inclusive", default="c5,c2",
@@ -504,6 +504,8 @@ EXTRA_MIN_STEPS = {"c3": 200}   # c3's poll round is ~55 us: 200 rounds time ~11
 TX_ROTATE = 8              # c4tx: the ring in 8 device buffers (512 MiB > the 256 MiB Infinity Cache;
                            # 7 others, 448 MiB, between two uses of one at 4 or 8 rings per launch)
 TX_RINGS = 100             # c4tx: timed rings (and device event pairs) at least
+TX_LAUNCHES = 50           # c4tx: timed multi-ring launches at least (400 rings, ~15 ms: the
+                           # loop's fill and drain < 1 %; at 13 launches 5-10 %, profiles/r06/r06r)
 
 
 def measure_tx(ctx, args):
@@ -600,7 +602,7 @@ def measure_tx(ctx, args):
                        C.byref(finfo)) for k in ks])
     multi, fin = ctx.L.usn_classify_multi, ctx.L.usn_finalize
 
-    def pipelined2(with_events):
+    def pipelined2(with_events, K2=K2):
         def launch(j):
             if with_events:
                 ctx.record(evs2[j][0], s)
@@ -630,6 +632,12 @@ def measure_tx(ctx, args):
     learned += nl
     wall2_ev, nl = pipelined2(True)
     learned += nl
+    # the same loop over only the launches the timed rings fill (13 at the
+    # defaults): its fill (the first launch's enqueue) and drain (the last
+    # launch's finalizes) are a visible share of it (profiles/r06/r06r)
+    K2s = -(-K // P)
+    wall2s, nl = pipelined2(False, K2s)
+    learned += nl
     dev2_ms = float(np.median([ctx.elapsed_ms(a, e) for a, e in evs2]))
     # the value: P rings per launch (its device time gives the roofline);
     # one ring per launch beside it
@@ -655,8 +663,12 @@ def measure_tx(ctx, args):
     x = {"value": round(P * K2 * n / wall2 / 1e6, 2), "unit": "Mpkts/s",
          "value_basis": "end to end: every ring classified and finalized; %d consecutive rings "
                         "per usn_classify_multi launch (one tx grid), launch j + 1 enqueued "
-                        "before launch j's usn_finalize calls (no events in the timed loop)" % P,
+                        "before launch j's usn_finalize calls (no events in the timed loop), "
+                        "%d launches timed (the first one's enqueue and the last one's "
+                        "finalizes inside the timed region)" % (P, K2),
          "rings_per_launch": P,
+         "launches": K2,
+         "short_loop": {"launches": K2s, "mpps": round(P * K2s * n / wall2s / 1e6, 2)},
          "ms_per_ring": round(wall2 * 1e3 / (P * K2), 4),
          "device_mpps": round(F2 / (dev2_ms * 1e-3) / 1e6, 2),
          "pipelined_with_events_mpps": round(P * K2 * n / wall2_ev / 1e6, 2),
