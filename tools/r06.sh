@@ -219,5 +219,16 @@ case $S in
       mv gpurun_out/$S/bench.log gpurun_out/$S/bench_tx${L}_$RANDOM.log
     done
     ;;
+  r06s)
+    # the tree with the early tx loads and the 50-launch c4tx loop: the
+    # suite, smoke, the bench as the driver runs it, rocprof, PMC
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    PMC_CFGS="c5 c2" bash tools/gpu.sh $S pmc || exit 1
+    TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
+    python3 tools/pmc_traffic.py gpurun_out/$S/txpmcf gpurun_out/$S/txpmcw 8388608 gpurun_out/$S/pmc_c4tx.json tx_kernel=1+33 > gpurun_out/$S/pmct_c4tx.log 2>&1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
