@@ -230,5 +230,16 @@ case $S in
     TXB_ARGS="1048576 24 1 --rotate 8 --rings 8" bash tools/gpu.sh $S txprof txpmc || exit 1
     python3 tools/pmc_traffic.py gpurun_out/$S/txpmcf gpurun_out/$S/txpmcw 8388608 gpurun_out/$S/pmc_c4tx.json tx_kernel=1+33 > gpurun_out/$S/pmct_c4tx.log 2>&1
     ;;
+  r06t)
+    # the image's slot reads (one scattered 16-B read per frame) with an L1
+    # bypass policy (USN_SLOT_POL: sc1, nt, sc0 sc1) against the default:
+    # c5 / c4 / c3 classify calls interleaved in one process, twice
+    V="base polsc1 polnt polsc01"
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c4 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    mv gpurun_out/$S/abl_c5.log gpurun_out/$S/abl_c5_1.log
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="polnt polsc01 polsc1 base" bash tools/gpu.sh $S abl || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

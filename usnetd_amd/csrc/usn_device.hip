@@ -265,6 +265,11 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #else
 #define USN_U_WAIT0 "1"   /* round 0's U slot read: round 1's is the one younger load */
 #endif
+/* cache policy of the image's slot reads (one scattered 16-byte read per
+ * frame and key): A/B knob, "" = default policy */
+#ifndef USN_SLOT_POL
+#define USN_SLOT_POL ""
+#endif
 #ifndef USN_SEQ_K2    /* key2's slot read only where key1 missed (get_endpoint's order) */
 #define USN_SEQ_K2 1
 #endif
@@ -310,7 +315,7 @@ __device__ __forceinline__ void ph_issue(const uint4 *T, const uint16_t *Dl, con
   } else if (ASM_SLOTS) {
     // issued here, waited for by ph_slots_wait: hipcc's own wait before the
     // compare would be vmcnt(0), draining the header DMA issued after them
-    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
+    asm volatile("global_load_dwordx4 %0, %2, off" USN_SLOT_POL "\n\tglobal_load_dwordx4 %1, %3, off" USN_SLOT_POL
                  : "=&v"(s1), "=&v"(s2)
                  : "v"(T + si1), "v"(T + si2)
                  : "memory");
@@ -368,7 +373,7 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
                                           v4u32 &s1, v4u32 &s2) {
   const uint4 *p1 = T + a.ph[0].slot_off + (use1 ? k.k1.sbase + usn_ph_slot(k.k1.h2, d1, a.ph[0].m) : 0u);
   const uint4 *p2 = T + a.ph[1].slot_off + (use2 ? k.k2.sbase + usn_ph_slot(k.k2.h2, d2, a.ph[1].m) : 0u);
-  asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
+  asm volatile("global_load_dwordx4 %0, %2, off" USN_SLOT_POL "\n\tglobal_load_dwordx4 %1, %3, off" USN_SLOT_POL
                : "=&v"(s1), "=&v"(s2) : "v"(p1), "v"(p2) : "memory");
 }
 
@@ -377,7 +382,7 @@ __device__ __forceinline__ void asm_slot2(const uint4 *T, const ClassifyArgs &a,
 __device__ __forceinline__ void asm_slot1(const uint4 *T, const usn_ph_table &t, bool need,
                                           const PhKeyH &k, uint32_t d, v4u32 &s) {
   const uint4 *p = T + t.slot_off + (need ? k.sbase + usn_ph_slot(k.h2, d, t.m) : 0u);
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(s) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off" USN_SLOT_POL : "=&v"(s) : "v"(p) : "memory");
 }
 
 /* TM_DISPLDS: both displacements from the LDS copy (indexed like the image) */
