@@ -240,6 +240,12 @@ case $S in
     ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     mv gpurun_out/$S/abl_c5.log gpurun_out/$S/abl_c5_1.log
     ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="polnt polsc01 polsc1 base" bash tools/gpu.sh $S abl || exit 1
+    # tx: the probes' displacement and slot reads as buffer loads with a
+    # cache policy (USN_TX_AUX: 0 default, 2 nt, 16 sc1)
+    for v in base txaux0 txaux2 txaux16 txaux16 txaux2 txaux0 base; do
+      TAILN=1 TXB_ARGS="1048576 24 1 build/abl/$v/libusn.so --rotate 8 --rings 8" bash tools/gpu.sh $S txbench || exit 1
+      mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
+    done
     ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
