@@ -266,7 +266,10 @@ __device__ __forceinline__ uint32_t ph_hit(const uint4 &sl, uint32_t x, uint32_t
 #define USN_U_WAIT0 "1"   /* round 0's U slot read: round 1's is the one younger load */
 #endif
 /* cache policy of the image's slot reads (one scattered 16-byte read per
- * frame and key): A/B knob, "" = default policy */
+ * frame and key): A/B knob, "" = default policy.  L1 bypass (" sc1",
+ * " sc0 sc1") changed nothing and " nt" made c5's classify 157 -> 264 us per
+ * 8M (the U table then leaves L2), profiles/r06/r06t: the probes cost L2
+ * requests, one per frame, not L1 line fills. */
 #ifndef USN_SLOT_POL
 #define USN_SLOT_POL ""
 #endif
@@ -432,16 +435,6 @@ __device__ __forceinline__ uint32_t ph_probe1(const uint4 *T, const ClassifyArgs
   return ph_hit(T[t.slot_off + k.sbase + usn_ph_slot(k.h2, d, t.m)], x, y, z, meta);
 }
 
-/* tx probes from a global image: the displacement and slot reads as buffer
- * loads with this cache-policy aux (1 sc0, 2 nt, 16 sc1), or plain loads
- * (-1).  A/B knob. */
-#ifndef USN_TX_AUX
-#define USN_TX_AUX -1
-#endif
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const uint4 *T) {
-  return __builtin_amdgcn_make_buffer_rsrc((void *)T, (short)0, 0x7FFFFFFF, 0x00020000);
-}
-
 /* One key's displacement read of table `tb` (0 = K1, 1 = K2): its hash,
  * whether it is probed at all (use, and the table non-empty), and the read
  * (a key not probed reads the table's first displacement). */
@@ -455,9 +448,7 @@ __device__ __forceinline__ void ph_disp_issue(const uint4 *T, const ClassifyArgs
   on = use && ((a.probe_mask >> tb) & 1u);
   k = ph_hash(t, x, y, z, m);
   const uint32_t di = t.disp_off + (on ? k.grp : 0u);
-  if (IN_LDS) d = (uint32_t)((lds_u16 *)D)[di];
-  else if (USN_TX_AUX >= 0) d = __builtin_amdgcn_raw_buffer_load_b16(img_rsrc(T), di * 2u, 0, USN_TX_AUX);
-  else d = (uint32_t)D[di];
+  d = IN_LDS ? (uint32_t)((lds_u16 *)D)[di] : (uint32_t)D[di];
 }
 
 /* The slot reads of N keys whose displacements were read (ph_disp_issue;
@@ -476,9 +467,6 @@ __device__ __forceinline__ void ph_slots_hit(const uint4 *T, const ClassifyArgs 
     const uint32_t si = t.slot_off + (on[i] ? k[i].sbase + usn_ph_slot(k[i].h2, d[i], t.m) : 0u);
     if (IN_LDS) {
       const v4u32 v = ((lds_v4 *)T)[si];
-      sl[i] = make_uint4(v.x, v.y, v.z, v.w);
-    } else if (USN_TX_AUX >= 0) {
-      const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(img_rsrc(T), si * 16u, 0, USN_TX_AUX);
       sl[i] = make_uint4(v.x, v.y, v.z, v.w);
     } else {
       sl[i] = T[si];
