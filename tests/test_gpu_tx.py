@@ -64,13 +64,27 @@ def test_c4tx_parity(n, coracle_mod):
     assert [i.n_host for i in infos] == [0, 0, 0]
 
 
-@pytest.mark.parametrize("n,at", [(5000, [2500]), (1 << 16, [0]), (1 << 16, [40000, 40001, 60000])])
-def test_c4tx_host_tail(n, at, coracle_mod):
+@pytest.mark.parametrize("n,at,src", [(5000, [2500], 0), (1 << 16, [0], 0),
+                                      (1 << 16, [40000, 40001, 60000], 0),
+                                      (5000, [2500], 0x00010203), (1 << 16, [777], 0x00FFFFFF)])
+def test_c4tx_host_tail(n, at, src, coracle_mod):
     """A DHCP request (NIC.next_dhcp := S, endpoint.rs:214-226) sends the rest
-    of the batch through the ordered host stage from that frame on."""
+    of the batch through the ordered host stage from that frame on; its
+    source is unspecified anywhere in 0.0.0.0/8 (smoltcp 0.7.0, recalled:
+    tests/golden kat_dhcp)."""
     from usnetd_amd import traffic
-    infos = _run(traffic.c4tx(n=n, host_at=at), coracle_mod)
+    infos = _run(traffic.c4tx(n=n, host_at=at, host_src=src), coracle_mod)
     assert infos[0].n_host == n - at[0]
+
+
+@pytest.mark.parametrize("src", [0x01000000, 0x7F000001, 0x0A000001])
+def test_c4tx_dhcp_shaped_not_unspecified(src, coracle_mod):
+    """UDP 68 -> 67 to 255.255.255.255 from a source outside 0.0.0.0/8 is no
+    DHCP request: it is decided on the device (it learns its answer rule,
+    or is a loopback frame) and nothing goes to the host stage."""
+    from usnetd_amd import traffic
+    infos = _run(traffic.c4tx(n=5000, host_at=[100, 2500], host_src=src), coracle_mod)
+    assert [i.n_host for i in infos] == [0, 0]
 
 
 def test_tx_busy_until_finalize(coracle_mod):
@@ -587,13 +601,13 @@ def test_tx_eight_rings_one_launch(n, coracle_mod):
     assert [i.n_host for i in infos] == [0] * 8 + [n] * 8 + [0] * 8
 
 
-@pytest.mark.parametrize("at", [0, 5, 7])
-def test_tx_eight_rings_host_tail(at, coracle_mod):
+@pytest.mark.parametrize("at,src", [(0, 0), (5, 0), (7, 0), (3, 0x00070707)])
+def test_tx_eight_rings_host_tail(at, src, coracle_mod):
     """A DHCP request in ring `at` of eight: that ring's rest and every later
-    ring go to the host stage."""
+    ring go to the host stage (from 0.0.0.0, or another 0/8 source)."""
     from usnetd_amd import traffic
     rings = [traffic.c4tx(n=3000, seed=110 + k) for k in range(8)]
-    rings[at] = traffic.c4tx(n=3000, host_at=[1500], seed=110 + at)
+    rings[at] = traffic.c4tx(n=3000, host_at=[1500], seed=110 + at, host_src=src)
     infos = _ring_launches(rings, coracle_mod, per=8)
     assert [i.n_host for i in infos] == [0] * at + [1500] + [3000] * (7 - at)
 

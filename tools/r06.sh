@@ -247,5 +247,11 @@ case $S in
       mv gpurun_out/$S/txbench.log gpurun_out/$S/txbench_${v}_$RANDOM.log
     done
     ;;
+  r06u)
+    # DHCP requests from 0.0.0.0/8 sources other than 0.0.0.0 inside c4tx
+    # rings (one ring, eight rings per grid) and DHCP-shaped frames from
+    # outside 0/8, against the oracle
+    TESTS="tests/test_gpu_tx.py" TEST_K="host_tail or not_unspecified" bash tools/gpu.sh $S tests || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

@@ -243,7 +243,7 @@ def c5x(n=1 << 23, seed=5, n_ep=1000):
     return Config("c5x", n, _layout(H, lens, 64), lens, 64, 0, _base_endpoints(n_ep), rules)
 
 
-def c4tx(n=1 << 18, seed=6, host_at=None):
+def c4tx(n=1 << 18, seed=6, host_at=None, host_src=0):
     """c4's mix SENT by the host endpoint (tx: find_forward with incoming ==
     false, endpoint.rs:194-256), the "ADD_MACS learned-MAC path" of
     BASELINE.json configs[3]: the bridge is prefilled with 64 endpoint MACs
@@ -252,7 +252,9 @@ def c4tx(n=1 << 18, seed=6, host_at=None):
     bridged MAC (rule lookup), half to the gateway (Target::Nic); every new flow
     learns its answer rule (to_want); 30 % of frames repeat the previous one
     (decision cache).  host_at: frame indices replaced by a DHCP request (its
-    effect on the NIC is ordered host work)."""
+    effect on the NIC is ordered host work) from IPv4 source host_src (any
+    0.0.0.0/8 address is unspecified in smoltcp 0.7.0, pkt.rs:46; another
+    source makes the frame an ordinary one that learns its answer rule)."""
     cfg = c4(n, seed)
     rng = np.random.default_rng(seed + 100)
     stride = cfg.stride
@@ -289,7 +291,7 @@ def c4tx(n=1 << 18, seed=6, host_at=None):
     V[:] = V[idx]
     lens = cfg.lens[idx].copy()
     if host_at:
-        req = build_ipv4(1, 0xFFFFFFFF, 0, UDP, 68, 67, np.array([64], np.uint16),
+        req = build_ipv4(1, 0xFFFFFFFF, host_src, UDP, 68, 67, np.array([64], np.uint16),
                          dmac=b"\xff" * 6, smac=bytes(pool[3]))
         for i in host_at:
             V[i, :64] = req[0]
