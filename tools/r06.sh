@@ -253,5 +253,21 @@ case $S in
     # outside 0/8, against the oracle
     TESTS="tests/test_gpu_tx.py" TEST_K="host_tail or not_unspecified" bash tools/gpu.sh $S tests || exit 1
     ;;
+  r06v)
+    # differential fuzz of the final tree (random streams with 0/8 DHCP
+    # sources, sending runs split into 2-8 rings per launch) against the C
+    # oracle: small images (LDS) and images past LDS (U and X probes)
+    mkdir -p gpurun_out/$S
+    for c in 0 1 2; do
+      timeout -k 10 240 python -u tools/fuzz_multi_ring.py $((6000 + 100 * c)) 100 3000 > gpurun_out/$S/fuzz_$c.log 2>&1 \
+        || { tail -3 gpurun_out/$S/fuzz_$c.log; exit 1; }
+      tail -1 gpurun_out/$S/fuzz_$c.log
+    done
+    for c in 0 1; do
+      timeout -k 10 240 python -u tools/fuzz_multi_ring.py $((7000 + 50 * c)) 50 3000 3000 > gpurun_out/$S/fuzzf_$c.log 2>&1 \
+        || { tail -3 gpurun_out/$S/fuzzf_$c.log; exit 1; }
+      tail -1 gpurun_out/$S/fuzzf_$c.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
