@@ -269,5 +269,12 @@ case $S in
       tail -1 gpurun_out/$S/fuzzf_$c.log
     done
     ;;
+  r06w)
+    # the host-mapped state's device addresses cached per replica: the
+    # suite, smoke, the bench as the driver runs it
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

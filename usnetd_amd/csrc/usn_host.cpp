@@ -474,6 +474,9 @@ struct Replica {
   hipEvent_t rx_ev[RX_EVS] = {};
   uint64_t rx_ev_gen[RX_EVS] = {};
   hipStream_t rx_ev_stream[RX_EVS] = {};
+  // this device's addresses of the context's host-mapped rx / tx state
+  // (hipHostGetDevicePointer once, not per call)
+  uint32_t *d_rxstate = nullptr, *d_txstate = nullptr;
   uint32_t rx_ev_next = 0;
 };
 
@@ -2772,8 +2775,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (!c->h_rxstate)
       HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_rxstate), usn_ctx::RX_SLOTS * 32,
                            hipHostMallocMapped | hipHostMallocCoherent));
-    uint32_t *d_rx = nullptr;
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_rx), c->h_rxstate, 0));
+    if (!R.d_rxstate) HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&R.d_rxstate), c->h_rxstate, 0));
+    uint32_t *const d_rx = R.d_rxstate;
     epoch = next_epoch(c);
     for (uint32_t k = 0; k < count; ++k) {
       m.b[k].epoch = epoch;
@@ -2797,8 +2800,8 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
                              hipHostMallocMapped | hipHostMallocCoherent));
         c->h_txstate_cap = 2 * TXSTATE_BYTES;
       }
-      HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&txs), c->h_txstate, 0));
-      txs += slot * (TXSTATE_BYTES / 4);
+      if (!R.d_txstate) HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&R.d_txstate), c->h_txstate, 0));
+      txs = R.d_txstate + slot * (TXSTATE_BYTES / 4);
       // word 11: set by any scatter chunk that finds inconsistent lists (the
       // slot's previous batch is final: its usn_finalize synchronised)
       reinterpret_cast<volatile uint32_t *>(c->h_txstate + slot * TXSTATE_BYTES)[11] = 0;
