@@ -276,5 +276,14 @@ case $S in
     bash tools/gpu.sh $S smoke || exit 1
     BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
     ;;
+  r06x)
+    # the cached mapped-state addresses against HEAD~ (build/abl/r06prev),
+    # interleaved in one process: c3 / c2 / c5 calls; then rocprof of the bench
+    V="product r06prev"
+    ABL_CFGS=c3 ABL_ARGS="$C3" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c2 ABL_ARGS="$C2" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
+    bash tools/gpu.sh $S rocprof || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
