@@ -1,6 +1,9 @@
 #!/bin/bash
 # Round 6 GPU sessions (one tag per gpurun call; outputs under gpurun_out/<tag>/).
 #   tools/r06.sh TAG
+# The sessions are records: the A/B builds they time (build/abl/<name>) were
+# built for them at the time, and the knobs behind r06m-r06p's priority
+# variants and r06t's tx buffer loads have since left the source.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 S=${1:?tag}
