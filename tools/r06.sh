@@ -288,5 +288,13 @@ case $S in
     ABL_CFGS=c5 ABL_ARGS="$C5" ABL_VARIANTS="$V" bash tools/gpu.sh $S abl || exit 1
     bash tools/gpu.sh $S rocprof || exit 1
     ;;
+  r06y)
+    # host time of usn_classify_multi by checkpoint (test build, tools/hostprof.py)
+    mkdir -p gpurun_out/$S
+    for c in c3 c2 c5; do
+      timeout -k 10 240 python -u tools/hostprof.py $c 400 > gpurun_out/$S/hostprof_$c.log 2>&1 || { tail -3 gpurun_out/$S/hostprof_$c.log; exit 1; }
+      tail -1 gpurun_out/$S/hostprof_$c.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac

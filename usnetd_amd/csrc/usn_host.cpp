@@ -401,6 +401,21 @@ static const char *test_knob(const char *name) {
 #endif
 }
 
+/* host-time checkpoints of usn_classify_multi (test build only:
+ * tools/hostprof.py reads them through usn_debug_host_prof) */
+#if USN_TEST_HOOKS
+uint64_t g_hprof[16];
+inline uint64_t hprof_now() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define HPROF_DECL uint64_t hp_t_ = hprof_now();
+#define HPROF(k) do { const uint64_t t_ = hprof_now(); g_hprof[k] += t_ - hp_t_; hp_t_ = t_; } while (0)
+#else
+#define HPROF_DECL
+#define HPROF(k) do { } while (0)
+#endif
+
 struct Chain {
   bool device_chain = false;        // previous result on the device is authoritative
   uint32_t replica = 0;             // where the source's last batch was classified
@@ -2643,6 +2658,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
                        void *stream) {
   if (!c || !b || !r || count == 0 || count > USN_MAX_MULTI) return USN_EINVAL;
   if (c->reps.empty()) return USN_ENODEV;
+  HPROF_DECL
   std::lock_guard<std::mutex> g(c->mu);
   bool tx = false;
   for (uint32_t k = 0; k < count; ++k) {
@@ -2678,6 +2694,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         if (q.decisions == r[k].decisions) return USN_EBUSY;
   }
   Replica &R = c->reps[rep];
+  HPROF(1);
   /* the table-version fence: this replica sees every registry and bridge
    * change made before this call */
   { int s = upload_table(c, R); if (s) return s; }
@@ -2687,6 +2704,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (ch.device_chain && ch.replica != rep) { int s = chain_to_host(c, ch); if (s) return s; }
   }
   HIPCHK(hipSetDevice(R.device));
+  HPROF(2);
   usn::MultiArgs m;
   std::memset(&m, 0, sizeof m);
   m.count = count;
@@ -2707,6 +2725,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     }
     m.tile_base[k + 1] = m.tile_base[k] + a.ntiles;
   }
+  HPROF(3);
   uint32_t slot = 0;
   uint32_t epoch = 0;        // rx: the launch tag (classify and lists)
   uint32_t rx_slot[USN_MAX_MULTI];
@@ -2787,10 +2806,12 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
       h[2] = 0;   // (set by any scatter chunk that finds inconsistent lists)
       rx_state[k] = d_rx + rx_slot[k] * 8;
     }
+    HPROF(4);
     if (c->t512 == 1 || (c->t512 < 0 && use_t512(m.b[0].nbins, m.b[0].table_units)))
       HIPCHK(usn_t512::launch_classify(m, (hipStream_t)stream));   // large table in L2
     else
       HIPCHK(usn::launch_classify(m, (hipStream_t)stream));
+    HPROF(5);
   }
   if (tx || !c->lists_async) {
     uint32_t *txs = nullptr;
@@ -2830,6 +2851,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
      * their two-stream steps 5 % (profiles/r06/r06c, r06d).  Bound, it cost
      * the two-stream steps of c2's 8M-frame calls 1-1.5 % in the same A/Bs:
      * so bound for launches of at most USN_BIND_MAX_TILES tiles (mode 5) */
+    HPROF(6);
     const bool bind = done && (c->rx_ev_mode == 4 ||
                                (c->rx_ev_mode == 5 && m.tile_base[count] <= USN_BIND_MAX_TILES));
     int st = launch_scatter(c, m.b, r, count, (hipStream_t)stream, txs, tx ? R.txs[slot].counters : nullptr,
@@ -2837,6 +2859,7 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
     if (st) return st;
     if (done && !bind) HIPCHK(hipEventRecord(done, (hipStream_t)stream));
     if (tx) c->txstate_for[slot] = r[0].decisions;
+    HPROF(7);
   } else {
     // the scatter on the side stream, after this launch; the caller's stream
     // goes on to the next batch (usn_finalize / usn_lists_wait join them)
@@ -2877,8 +2900,22 @@ int usn_classify_multi(usn_ctx *c, const usn_batch *b, usn_result *r, uint32_t c
         usn_ctx::BatchRec{rep, m.b[k].nbins, tx ? usn_ctx::RX_SLOTS : rx_slot[k], epoch, rx_done,
                           rx_ev_idx, rx_done ? c->rx_ev_gen : 0, (hipStream_t)stream};
   }
+  HPROF(8);
+#if USN_TEST_HOOKS
+  g_hprof[15] += 1;
+#endif
   return USN_OK;
 }
+
+#if USN_TEST_HOOKS
+/* test build only (not in include/usn_classify.h): the accumulated host ns
+ * per checkpoint of usn_classify_multi, [15] = calls */
+int usn_debug_host_prof(uint64_t *out16, int reset) {
+  for (int k = 0; k < 16; ++k) out16[k] = g_hprof[k];
+  if (reset) std::memset(g_hprof, 0, sizeof g_hprof);
+  return USN_OK;
+}
+#endif
 
 int usn_classify(usn_ctx *c, const usn_batch *b, usn_result *r, void *stream) {
   return usn_classify_multi(c, b, r, 1, stream);
