@@ -296,5 +296,12 @@ case $S in
       tail -1 gpurun_out/$S/hostprof_$c.log
     done
     ;;
+  r06z)
+    # the final tree's bench three times on one box (run-to-run spread)
+    for k in 1 2 3; do
+      BENCH_ARGS="--steps 40 --warmup 5" bash tools/gpu.sh $S bench || exit 1
+      mv gpurun_out/$S/bench.log gpurun_out/$S/bench_$k.log
+    done
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
