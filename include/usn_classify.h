@@ -287,9 +287,12 @@ size_t usn_result_bytes_ep(uint64_t n, uint32_t max_endpoints);
 int usn_result_bind(void *dev_mem, size_t bytes, uint64_t n, usn_result *out);
 /* Drops what the context keeps per result (keyed by its arrays: the replica
  * and bins its last batch ran with, a side-stream lists event, the scan
- * scratch's zeroing tag) before the caller frees or re-binds its memory.  A
- * source whose carried decision cache lives in this result's tile headers
- * takes the cache to the host first (it stays valid).  USN_EBUSY while the
+ * scratch's zeroing tag) before the caller frees or re-binds its memory.  An
+ * rx batch classified into it and not finalized is waited for first (its
+ * launch's completion event, or the side-stream lists event), so nothing of
+ * it still writes the memory when this returns.  A source whose carried
+ * decision cache lives in this result's tile headers takes the cache to the
+ * host first (it stays valid).  USN_EBUSY while the
  * result belongs to a tx batch not yet finalized.  Bind a result once per
  * allocation and reuse it: results are meant to be long-lived, and a context
  * whose caller never releases them keeps one small record per result. */
