@@ -44,3 +44,17 @@ def test_world_size_mismatch_is_refused():
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0
     assert "WORLD_SIZE=1" in out.stderr
+
+
+def test_bench_defaults_match_the_driver_contract():
+    """With no flags: one GPU, a K/W that finishes in minutes, the headline on
+    two result sets per queue, and c4tx's end-to-end loop over at least
+    TX_LAUNCHES launches (its fill and drain under 1 %)."""
+    a = bench.parse_args([])
+    assert a.gpus == 1 and a.config == "c5"
+    assert a.steps == 40 and a.warmup == 5
+    assert a.result_rounds == 2
+    assert a.tx_launches == bench.TX_LAUNCHES >= 50
+    assert a.tx_rings == 8
+    assert set(a.host_inclusive.split(",")) == {"c5", "c2"}
+    assert bench.parse_args(["--tx-launches", "13"]).tx_launches == 13
