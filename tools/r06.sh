@@ -303,5 +303,10 @@ case $S in
       mv gpurun_out/$S/bench.log gpurun_out/$S/bench_$k.log
     done
     ;;
+  r06zz)
+    # the final tree (test build with the host checkpoints): the suite and smoke
+    bash tools/gpu.sh $S testsall || exit 1
+    bash tools/gpu.sh $S smoke || exit 1
+    ;;
   *) echo "unknown session $S"; exit 2 ;;
 esac
